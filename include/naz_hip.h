@@ -1,0 +1,137 @@
+/*
+ * naz_hip.h — C ABI of libnazhip.so, the MI355X (gfx950) implementation of naz's
+ * normalizing-flow log_prob / sample hot path.
+ *
+ * Conventions:
+ *   - every pointer is a DEVICE pointer owned by the caller, row-major fp32; no
+ *     allocation happens inside a call;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the default stream);
+ *   - return 0 on success, nonzero on error; naz_last_error() returns a
+ *     thread-local message describing the last failure;
+ *   - calls are stateless and thread-safe across streams.
+ *
+ * Each entry point names the reference interface it replaces.  In the reference
+ * those interfaces are Python calls into pyro-ppl (not vendored; semantics restated
+ * in SURVEY.md §8a); the call sites are in /root/reference/src/naz.
+ */
+#ifndef NAZ_HIP_H
+#define NAZ_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants ---------------------------------------------------------- */
+#define NAZ_LAYOUT_DENSE 0 /* DenseNN hypernet output: [w(Dt*K) | h(Dt*K) | d(Dt*(K-1))]  */
+#define NAZ_LAYOUT_ARN 1   /* AutoRegressiveNN output: column p*Dt + i, p in [0, 3K-1)    */
+
+#define NAZ_LD_PERDIM 0      /* ld is [B, Dt], per dimension                                */
+#define NAZ_LD_ROWSUM 1      /* ld is [B], ld[r]  = sum_i ld[r, i]                          */
+#define NAZ_LD_ROWSUM_ADD 2  /* ld is [B], ld[r] += sum_i ld[r, i]                          */
+#define NAZ_LD_ROWSUM_SUB 3  /* ld is [B], ld[r] -= sum_i ld[r, i]                          */
+
+#define NAZ_ACT_IDENTITY 0
+#define NAZ_ACT_TANH 1 /* naz default activation: flows/transforms.py:133,165,201 */
+#define NAZ_ACT_RELU 2
+#define NAZ_ACT_SOFTPLUS 3
+#define NAZ_ACT_SIGMOID 4
+
+/* ---- library ------------------------------------------------------------ */
+const char* naz_last_error(void);
+int naz_abi_version(void); /* bumps on any signature change */
+
+/* ---- a1+a2: conditional spline -------------------------------------------
+ * Replaces [pyro] ConditionedSpline._call / ._inverse over a conditioner output,
+ * i.e. ConditionalSpline._params (softmax, softmax, softplus) followed by
+ * _monotonic_rational_spline(order="quadratic"), reached from
+ * naz/flows/transforms.py:190 (ConditionalSplineAutoregressive) and :228
+ * (SplineCoupling's upper spline).
+ *   x   [B, Dt] (row stride ldx)       raw [B, Dt*(3K-1)] (row stride ldr, `layout`)
+ *   y   [B, Dt] (row stride ldy)       ld  per `ld_mode`; the log|det| of the map applied
+ *                                           (naz_rqs_inv: of the inverse map)            */
+int naz_rqs_fwd(const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy, float* ld,
+                int ld_mode, int64_t B, int Dt, int K, int layout, float bound, void* stream);
+int naz_rqs_inv(const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy, float* ld,
+                int ld_mode, int64_t B, int Dt, int K, int layout, float bound, void* stream);
+
+/* ---- a1: unconditional elementwise spline ([pyro] Spline, the coupling's lower
+ * spline, naz/flows/transforms.py:128 intent).  uw/uh [Dt,K], ud [Dt,K-1] are the
+ * UNNORMALISED parameters; ld is per-dim [B, Dt].                                   */
+int naz_spline_elementwise(int inverse, const float* x, int64_t ldx, const float* uw, const float* uh,
+                           const float* ud, float* y, int64_t ldy, float* ld, int64_t B, int Dt, int K, float bound,
+                           void* stream);
+
+/* ---- a6/a7: one conditioner layer ----------------------------------------
+ * Replaces torch F.linear(cat([ctx, x]), W ⊙ mask, b) + nonlinearity inside
+ * [pyro] ConditionalDenseNN / ConditionalAutoRegressiveNN._forward
+ * (naz/flows/transforms.py:142,180,223).  The concatenation is fused: input column
+ * k < C reads ctx[m*ldc + k] (ldc = 0 broadcasts one context row), k >= C reads
+ * x[m*ldx + k - C].  W is [N, C+Kx] row-major; mask (same shape) may be NULL.
+ *   y[m, n] = act( sum_k in[m,k] * (W[n,k]*mask[n,k]) + b[n] )                       */
+int naz_linear_act(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx, int Kx, const float* W,
+                   const float* mask, const float* b, float* y, int64_t ldy, int64_t M, int N, int act, void* stream);
+
+/* ---- a5: affine autoregressive elementwise step --------------------------
+ * Replaces the elementwise part of [pyro] AffineAutoregressive._call / ._inverse
+ * (naz/flows/transforms.py:159; JAX restatement bflow_jax_maf.py:169-194):
+ *   fwd: y = exp(clamp(ls,-5,3)) * x + mean       inv: y = (x - mean) * exp(-clamp(ls,-5,3))
+ * raw is the ARN output [B, 2*D] (mean = columns 0..D-1, log_scale = D..2D-1);
+ * ld (per ld_mode) is the FORWARD log|det| = clamp(ls) for both directions.         */
+int naz_affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
+                  float* ld, int ld_mode, int64_t B, int D, void* stream);
+
+/* ---- a8: base density and bounding ----------------------------------------
+ * out[r] (+)= sum_i (-z^2/2 - log sqrt(2 pi))   (Independent(Normal(0,1)), naz/flows/flow.py:37)
+ * accumulate = 1 adds into out, 0 overwrites.                                        */
+int naz_base_log_prob(const float* z, int64_t ldz, float* out, int64_t B, int D, int accumulate, void* stream);
+/* naz/flows/transforms.py:20-23: y = logit((x-low)/(high-low)); out_logjac[r] = -sum log u + log1p(-u) - sum log(high-low) */
+int naz_bounding_fwd(const float* x, int64_t ldx, const float* low, const float* high, float* y, int64_t ldy,
+                     float* out_logjac, int64_t B, int D, void* stream);
+/* naz/flows/transforms.py:25-27: x = sigmoid(y)*(high-low) + low */
+int naz_bounding_inv(const float* y, int64_t ldy, const float* low, const float* high, float* x, int64_t ldx,
+                     int64_t B, int D, void* stream);
+
+/* ---- a3+a8+a9: fused conditional spline-coupling flow ---------------------
+ * Replaces the whole of NormalizingFlow.log_prob / .sample (naz/flows/flow.py:45-79,
+ * 94-129) for flow_type "nsc" (naz/flows/transforms.py:201-236 intent = pyro
+ * SplineCoupling with a (Conditional)DenseNN hypernet), L layers in one launch.
+ *
+ * Parameters live in ONE flat fp32 buffer, per layer in this order:
+ *   nn.layers.0.weight [H, C+S]  nn.layers.0.bias [H]
+ *   nn.layers.1.weight [H, H]    nn.layers.1.bias [H]
+ *   nn.layers.2.weight [(D-S)(3K-1), H]  nn.layers.2.bias [(D-S)(3K-1)]
+ *   lower_spline.unnormalized_{widths [S,K], heights [S,K], derivatives [S,K-1]}   (if has_lower)
+ * naz_coupling_pack re-lays them (on the device) into the kernel's MFMA operand
+ * order; re-pack after every weight update.                                          */
+typedef struct naz_coupling_desc {
+  int D, C, S, K, L, H;   /* data dim, context dim, split dim, bins, layers, hidden width (2 hidden layers) */
+  int act;                /* NAZ_ACT_* */
+  int has_lower;          /* 1: lower (unconditional) spline on x1; 0: pyro identity=True */
+  float bound;            /* spline box half-width (pyro default 3.0) */
+  int reserved[7];
+} naz_coupling_desc;
+
+int naz_coupling_supported(const naz_coupling_desc* d); /* 1 if a fused instantiation exists */
+int64_t naz_coupling_param_count(const naz_coupling_desc* d);
+int64_t naz_coupling_packed_bytes(const naz_coupling_desc* d);
+int naz_coupling_pack(const naz_coupling_desc* d, const float* flat_params, void* packed, void* stream);
+/* out_lp[r] = log p(x_r | ctx_r); ctx may be NULL when C == 0; ldc = 0 broadcasts one
+ * context row.  low/high (length D) enable naz's logit bounding prologue (flow.py:70-73);
+ * pass NULL for bounds=None.                                                          */
+int naz_coupling_log_prob(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx,
+                          const float* ctx, int64_t ldc, const float* low, const float* high, float* out_lp,
+                          int64_t B, void* stream);
+/* y = T_L ∘ … ∘ T_1 (z) (TransformedDistribution.sample's transform chain);
+ * out_ld (may be NULL) receives sum_l log|det J_l| per row.  low/high as above apply
+ * inverse_bounding_transform to the output (flow.py:129).                             */
+int naz_coupling_sample(const naz_coupling_desc* d, const void* packed, const float* z, int64_t ldz,
+                        const float* ctx, int64_t ldc, const float* low, const float* high, float* y, int64_t ldy,
+                        float* out_ld, int64_t B, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NAZ_HIP_H */

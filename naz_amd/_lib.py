@@ -1,0 +1,76 @@
+"""ctypes binding of libnazhip.so (the C ABI in include/naz_hip.h).
+
+The library is the ONLY compute path of naz_amd: if it is missing, or a tensor is
+not on a HIP device, calls raise — there is no CPU or eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libnazhip.so"
+
+LAYOUT_DENSE, LAYOUT_ARN = 0, 1
+LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB = 0, 1, 2, 3
+ACT = {"identity": 0, "tanh": 1, "relu": 2, "softplus": 3, "sigmoid": 4}
+
+_f, _i, _i64, _vp = C.POINTER(C.c_float), C.c_int, C.c_int64, C.c_void_p
+
+
+class CouplingDesc(C.Structure):
+    _fields_ = [("D", C.c_int), ("C", C.c_int), ("S", C.c_int), ("K", C.c_int), ("L", C.c_int), ("H", C.c_int),
+                ("act", C.c_int), ("has_lower", C.c_int), ("bound", C.c_float), ("reserved", C.c_int * 7)]
+
+
+# name -> (restype, argtypes); every symbol declared in include/naz_hip.h
+SIGNATURES = {
+    "naz_last_error": (C.c_char_p, []),
+    "naz_abi_version": (C.c_int, []),
+    "naz_rqs_fwd": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _i64, _i, _i, _i, C.c_float, _vp]),
+    "naz_rqs_inv": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _i64, _i, _i, _i, C.c_float, _vp]),
+    "naz_spline_elementwise": (C.c_int, [_i, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i, _i, C.c_float,
+                                         _vp]),
+    "naz_linear_act": (C.c_int, [_vp, _i64, _i, _vp, _i64, _i, _vp, _vp, _vp, _vp, _i64, _i64, _i, _i, _vp]),
+    "naz_affine_ar": (C.c_int, [_i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _i64, _i, _vp]),
+    "naz_base_log_prob": (C.c_int, [_vp, _i64, _vp, _i64, _i, _i, _vp]),
+    "naz_bounding_fwd": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _i, _vp]),
+    "naz_bounding_inv": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i, _vp]),
+    "naz_coupling_supported": (C.c_int, [C.POINTER(CouplingDesc)]),
+    "naz_coupling_param_count": (C.c_int64, [C.POINTER(CouplingDesc)]),
+    "naz_coupling_packed_bytes": (C.c_int64, [C.POINTER(CouplingDesc)]),
+    "naz_coupling_pack": (C.c_int, [C.POINTER(CouplingDesc), _vp, _vp, _vp]),
+    "naz_coupling_log_prob": (C.c_int, [C.POINTER(CouplingDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64,
+                                        _vp]),
+    "naz_coupling_sample": (C.c_int, [C.POINTER(CouplingDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp,
+                                      _i64, _vp]),
+}
+
+_lib = None
+
+
+class NazLibraryError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the HIP library; raise if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise NazLibraryError(
+                f"naz_amd: HIP library {LIB_PATH} is missing — build it with `python -m naz_amd.build` "
+                "(there is no CPU fallback)")
+        L = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | getattr(os, "RTLD_LOCAL", 0))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().naz_last_error().decode(errors="replace")
+        raise RuntimeError(f"naz_amd {what}: {msg or f'error code {rc}'}")

@@ -1,0 +1,113 @@
+// extern "C" entry points of libnazhip.so (declared in include/naz_hip.h).
+// Thin argument validation + dispatch into the HIP translation units.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "naz_internal.h"
+
+namespace naz {
+
+static thread_local char g_err[1024] = "";
+
+int set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return -1;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error("%s launch failed: %s", what, hipGetErrorString(e));
+  return 0;
+}
+
+static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static int check_spline_args(const char* fn, const float* x, const float* y, int64_t B, int Dt, int K, float bound) {
+  if (B < 0 || Dt <= 0) return set_error("%s: bad shape B=%lld Dt=%d", fn, (long long)B, Dt);
+  if (B > 0 && (x == nullptr || y == nullptr)) return set_error("%s: null x/y", fn);
+  if (K < 2) return set_error("%s: count_bins must be >= 2 (got %d)", fn, K);
+  if (1e-3 * K > 1.0) return set_error("%s: Minimal bin width too large for the number of bins", fn);
+  if (!(bound > 0.f)) return set_error("%s: bound must be positive", fn);
+  return 0;
+}
+
+}  // namespace naz
+
+using namespace naz;
+
+extern "C" {
+
+const char* naz_last_error(void) { return g_err; }
+int naz_abi_version(void) { return 1; }
+
+int naz_rqs_fwd(const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy, float* ld,
+                int ld_mode, int64_t B, int Dt, int K, int layout, float bound, void* stream) {
+  if (int rc = check_spline_args("naz_rqs_fwd", x, y, B, Dt, K, bound)) return rc;
+  return rqs_cond(0, x, ldx, raw, ldr, y, ldy, ld, ld_mode, B, Dt, K, layout, bound, as_stream(stream));
+}
+
+int naz_rqs_inv(const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy, float* ld,
+                int ld_mode, int64_t B, int Dt, int K, int layout, float bound, void* stream) {
+  if (int rc = check_spline_args("naz_rqs_inv", x, y, B, Dt, K, bound)) return rc;
+  return rqs_cond(1, x, ldx, raw, ldr, y, ldy, ld, ld_mode, B, Dt, K, layout, bound, as_stream(stream));
+}
+
+int naz_spline_elementwise(int inverse, const float* x, int64_t ldx, const float* uw, const float* uh,
+                           const float* ud, float* y, int64_t ldy, float* ld, int64_t B, int Dt, int K, float bound,
+                           void* stream) {
+  if (int rc = check_spline_args("naz_spline_elementwise", x, y, B, Dt, K, bound)) return rc;
+  return rqs_uncond(inverse, x, ldx, uw, uh, ud, y, ldy, ld, B, Dt, K, bound, as_stream(stream));
+}
+
+int naz_linear_act(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx, int Kx, const float* W,
+                   const float* mask, const float* b, float* y, int64_t ldy, int64_t M, int N, int act, void* stream) {
+  if (M < 0 || N < 0 || C < 0 || Kx < 0) return set_error("naz_linear_act: negative shape");
+  return linear_act(ctx, ldc, C, x, ldx, Kx, W, mask, b, y, ldy, M, N, act, as_stream(stream));
+}
+
+int naz_affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
+                  float* ld, int ld_mode, int64_t B, int D, void* stream) {
+  if (B < 0 || D <= 0) return set_error("naz_affine_ar: bad shape");
+  return affine_ar(inverse, x, ldx, raw, ldr, y, ldy, ld, ld_mode, B, D, as_stream(stream));
+}
+
+int naz_base_log_prob(const float* z, int64_t ldz, float* out, int64_t B, int D, int accumulate, void* stream) {
+  return base_log_prob(z, ldz, out, B, D, accumulate, as_stream(stream));
+}
+
+int naz_bounding_fwd(const float* x, int64_t ldx, const float* low, const float* high, float* y, int64_t ldy,
+                     float* out_logjac, int64_t B, int D, void* stream) {
+  return bounding_fwd(x, ldx, low, high, y, ldy, out_logjac, B, D, as_stream(stream));
+}
+
+int naz_bounding_inv(const float* y, int64_t ldy, const float* low, const float* high, float* x, int64_t ldx,
+                     int64_t B, int D, void* stream) {
+  return bounding_inv(y, ldy, low, high, x, ldx, B, D, as_stream(stream));
+}
+
+int naz_coupling_supported(const naz_coupling_desc* d) { return coupling_supported(d); }
+int64_t naz_coupling_param_count(const naz_coupling_desc* d) { return coupling_param_count(d); }
+int64_t naz_coupling_packed_bytes(const naz_coupling_desc* d) { return coupling_packed_bytes(d); }
+
+int naz_coupling_pack(const naz_coupling_desc* d, const float* flat_params, void* packed, void* stream) {
+  return coupling_pack(d, flat_params, packed, as_stream(stream));
+}
+
+int naz_coupling_log_prob(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx,
+                          const float* ctx, int64_t ldc, const float* low, const float* high, float* out_lp,
+                          int64_t B, void* stream) {
+  if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_log_prob: conditional flow needs ctx");
+  return coupling_log_prob(d, packed, x, ldx, ctx, ldc, low, high, out_lp, B, as_stream(stream));
+}
+
+int naz_coupling_sample(const naz_coupling_desc* d, const void* packed, const float* z, int64_t ldz,
+                        const float* ctx, int64_t ldc, const float* low, const float* high, float* y, int64_t ldy,
+                        float* out_ld, int64_t B, void* stream) {
+  if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_sample: conditional flow needs ctx");
+  return coupling_sample(d, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, as_stream(stream));
+}
+
+}  // extern "C"

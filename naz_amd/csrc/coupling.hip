@@ -1,0 +1,565 @@
+// Fused conditional spline-coupling flow: log_prob and sample for all L layers in
+// ONE launch (§7 steps 4-5).
+//
+// Reference semantics: naz NormalizingFlow.log_prob (naz/flows/flow.py:45-79) over
+// flow_type "nsc" (naz/flows/transforms.py:201-236 intent = pyro SplineCoupling
+// with a ConditionalDenseNN hypernet, DenseNN input cat([ctx, x1]), tanh):
+//   for l = L-1 .. 0:  x1 = lower.inv(y1);  raw = MLP([ctx, x1]);  x2 = RQS^-1(y2; raw)
+//                      lp -= sum(ld_upper) + sum(ld_lower)
+//   lp += sum(-z^2/2 - log sqrt(2 pi))
+//
+// MI355X mapping (see DESIGN.md §Fused coupling kernel):
+//   * workgroup = 4 waves = 128 batch rows; wave = 32 rows; lane l owns batch row
+//     (l & 31) and lane-half h = l >> 5 owns half of that row's dims;
+//   * activations live TRANSPOSED in MFMA accumulators (feature = accumulator row,
+//     batch row = accumulator column = lane & 31).  v_mfma_f32_32x32x2_f32's B operand
+//     is B[k = l>>5][j = l&31], so accumulator register r of layer n IS the B operand
+//     of k-step r of layer n+1 — the three GEMMs chain with no LDS and no shuffles;
+//     the weight packer permutes W's columns to match (hid_feature below);
+//   * the last GEMM's output rows are permuted so that lane-half h receives all
+//     3K-1 spline parameters of its own Dt/2 upper dims in registers: the spline,
+//     log-det and base density run per lane with no cross-lane traffic until the
+//     final one-shuffle row reduction;
+//   * weights (the A operands, exact fp32 MFMA) are staged per GEMM into LDS as
+//     [block][k/4][lane][4] panels read by ds_read_b128; one stage <= 64 KB so two
+//     workgroups share a CU and overlap each other's VALU (spline/tanh) with MFMA.
+#include "naz_device.h"
+#include "naz_internal.h"
+
+#include <type_traits>
+
+namespace naz {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+NAZ_DEV floatx16 mfma32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// accumulator register r on lane-half h holds feature row (within a 32-block)
+__host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+// Feature (input column of the next GEMM) carried by k-step t on lane-half h.
+__host__ __device__ constexpr int hid_feature(int t, int h) { return 32 * (t >> 4) + acc_row(t & 15, h); }
+
+constexpr int kStageFloats = 16384;  // 64 KB per LDS stage
+constexpr int kRowsPerWG = 128;
+
+template <int D_, int C_, int S_, int K_, int H_, bool LOWER_>
+struct CouplingCfg {
+  static constexpr int D = D_, C = C_, S = S_, K = K_, H = H_;
+  static constexpr bool LOWER = LOWER_;
+  static constexpr int Dt = D - S;
+  static constexpr int P = 3 * K - 1;       // raw params per upper dim
+  static constexpr int DH = Dt / 2;         // upper dims per lane-half
+  static constexpr int SH = S / 2;          // lower dims per lane-half
+  static constexpr int CH = (C + 1) / 2;    // context features per lane-half
+  static constexpr int CHA = CH > 0 ? CH : 1;
+  static constexpr int KS0 = CH + SH;       // GEMM1 k-steps (2 features each)
+  static constexpr int KS0P = (KS0 + 3) / 4 * 4;
+  static constexpr int HB = H / 32;         // hidden 32-row blocks
+  static constexpr int KS1 = H / 2;         // GEMM2/3 k-steps
+  static constexpr int NO = (DH * P + 15) / 16;  // GEMM3 output blocks
+  static constexpr int TBL = 3 * (K + 1);   // lower-spline table floats per dim
+  static constexpr int PANEL0 = KS0P * 64;
+  static constexpr int PANEL1 = KS1 * 64;
+  static constexpr int PPS = kStageFloats / PANEL1;  // GEMM2/3 panels per stage
+  static constexpr int NSTG3 = (NO + PPS - 1) / PPS;
+  // stage A: [HB panels0][HB*32 bias][S*TBL tables]  (padded to 4 floats)
+  static constexpr int A_BIAS = HB * PANEL0;
+  static constexpr int A_TBL = A_BIAS + HB * 32;
+  static constexpr int A_SIZE = (A_TBL + S * TBL + 255) / 256 * 256;
+  // stage B: [HB panels1][HB*32 bias]
+  static constexpr int B_OFF = A_SIZE;
+  static constexpr int B_BIAS = HB * PANEL1;
+  static constexpr int B_SIZE = (B_BIAS + HB * 32 + 255) / 256 * 256;
+  // stages C_j: [n_j panels1][n_j*32 bias]
+  static constexpr int C_OFF = B_OFF + B_SIZE;
+  static constexpr int C_STRIDE = (PPS * PANEL1 + PPS * 32 + 255) / 256 * 256;
+  static constexpr __host__ __device__ int c_count(int j) { return (NO - j * PPS) < PPS ? (NO - j * PPS) : PPS; }
+  static constexpr __host__ __device__ int c_off(int j) { return C_OFF + j * C_STRIDE; }
+  static constexpr __host__ __device__ int c_size(int j) { return (c_count(j) * (PANEL1 + 32) + 255) / 256 * 256; }
+  static constexpr int LAYER = C_OFF + (NSTG3 - 1) * C_STRIDE + c_size(NSTG3 - 1);
+  static constexpr int MAX_AB = A_SIZE > B_SIZE ? A_SIZE : B_SIZE;
+  static constexpr int MAXSTAGE = MAX_AB > C_STRIDE ? MAX_AB : C_STRIDE;
+  // flat (natural) parameter layout per layer
+  static constexpr int N_W0 = H * (C + S), N_B0 = H, N_W1 = H * H, N_B1 = H, N_W2 = Dt * P * H, N_B2 = Dt * P;
+  static constexpr int N_LOW = LOWER ? S * (3 * K - 1) : 0;
+  static constexpr int FLAT = N_W0 + N_B0 + N_W1 + N_B1 + N_W2 + N_B2 + N_LOW;
+  static_assert(Dt % 2 == 0 && S % 2 == 0 && H % 32 == 0 && S > 0 && Dt > 0, "unsupported coupling shape");
+  static_assert(PPS >= 1, "hidden width too large for one LDS stage");
+  static_assert(MAXSTAGE * 4 <= 80 * 1024, "stage exceeds the per-workgroup LDS budget");
+  static_assert(A_SIZE % 256 == 0 && B_SIZE % 256 == 0 && C_STRIDE % 256 == 0 && LAYER % 256 == 0, "stage alignment");
+};
+
+// ---------------------------------------------------------------------------
+// Packing kernel: flat natural params -> MFMA panel order (+ lower-spline tables)
+// ---------------------------------------------------------------------------
+template <class CF>
+__global__ void coupling_pack_kernel(const float* __restrict__ flat, float* __restrict__ packed, int L, float bound) {
+  const int64_t n = (int64_t)L * CF::LAYER;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(e / CF::LAYER);
+    const int off = (int)(e - (int64_t)l * CF::LAYER);
+    const float* W0 = flat + (int64_t)l * CF::FLAT;
+    const float* b0 = W0 + CF::N_W0;
+    const float* W1 = b0 + CF::N_B0;
+    const float* b1 = W1 + CF::N_W1;
+    const float* W2 = b1 + CF::N_B1;
+    const float* b2 = W2 + CF::N_W2;
+    const float* low = b2 + CF::N_B2;  // unnormalized widths [S,K] | heights [S,K] | derivatives [S,K-1]
+    float v = 0.f;
+    if (off < CF::A_SIZE) {
+      if (off < CF::A_BIAS) {  // W0 panels: [o][t/4][lane][t%4]
+        const int o = off / CF::PANEL0, rem = off - o * CF::PANEL0;
+        const int t = (rem / 256) * 4 + (rem & 3), lane = (rem >> 2) & 63;
+        const int i = lane & 31, kh = lane >> 5;
+        int col = -1;
+        if (t < CF::CH) {
+          const int c = kh * CF::CH + t;
+          if (c < CF::C) col = c;
+        } else if (t < CF::KS0) {
+          col = CF::C + kh * CF::SH + (t - CF::CH);
+        }
+        if (col >= 0) v = W0[(32 * o + i) * (CF::C + CF::S) + col];
+      } else if (off < CF::A_TBL) {
+        const int q = off - CF::A_BIAS, o = q / 32, h = (q >> 4) & 1, r = q & 15;
+        v = b0[32 * o + acc_row(r, h)];
+      } else if (CF::LOWER && off < CF::A_TBL + CF::S * CF::TBL) {
+        const int q = off - CF::A_TBL, g = q / CF::TBL, w = q - g * CF::TBL;
+        float uw[CF::K], uh[CF::K], ud[CF::K - 1];
+        for (int k = 0; k < CF::K; ++k) {
+          uw[k] = low[g * CF::K + k];
+          uh[k] = low[CF::S * CF::K + g * CF::K + k];
+        }
+        for (int k = 0; k < CF::K - 1; ++k) ud[k] = low[2 * CF::S * CF::K + g * (CF::K - 1) + k];
+        SplineTables<CF::K> tb;
+        build_tables<CF::K>(uw, uh, ud, bound, tb);
+        const int which = w / (CF::K + 1), k = w - which * (CF::K + 1);
+        v = which == 0 ? tb.cw[k] : (which == 1 ? tb.ch[k] : tb.dv[k]);
+      }
+    } else if (off < CF::C_OFF) {
+      const int q = off - CF::B_OFF;
+      if (q < CF::B_BIAS) {
+        const int o = q / CF::PANEL1, rem = q - o * CF::PANEL1;
+        const int t = (rem / 256) * 4 + (rem & 3), lane = (rem >> 2) & 63;
+        v = W1[(32 * o + (lane & 31)) * CF::H + hid_feature(t, lane >> 5)];
+      } else {
+        const int qq = q - CF::B_BIAS, o = qq / 32, h = (qq >> 4) & 1, r = qq & 15;
+        v = b1[32 * o + acc_row(r, h)];
+      }
+    } else {
+      int j = (off - CF::C_OFF) / CF::C_STRIDE;
+      const int q = off - CF::c_off(j), cnt = CF::c_count(j);
+      const bool is_w = q < cnt * CF::PANEL1;
+      int o, h, r, col = 0;
+      if (is_w) {
+        const int ob = q / CF::PANEL1, rem = q - ob * CF::PANEL1;
+        const int t = (rem / 256) * 4 + (rem & 3), lane = (rem >> 2) & 63;
+        const int i = lane & 31;               // A row = output row within block
+        o = j * CF::PPS + ob;
+        h = (i >> 2) & 1;                      // which lane-half's accumulator holds row i
+        r = (i & 3) + 4 * (i >> 3);            // ... in which register
+        col = hid_feature(t, lane >> 5);       // A column = k-step feature
+      } else {
+        const int qq = q - cnt * CF::PANEL1, ob = qq / 32;
+        o = j * CF::PPS + ob;
+        h = (qq >> 4) & 1;
+        r = qq & 15;
+      }
+      // slot (o, r) on half h -> (upper dim, param) -> DenseNN output column
+      const int slot = 16 * o + r, qd = slot / CF::P, p = slot - qd * CF::P;
+      if (qd < CF::DH) {
+        const int dim = h * CF::DH + qd;
+        int orig;
+        if (p < CF::K) orig = dim * CF::K + p;
+        else if (p < 2 * CF::K) orig = CF::Dt * CF::K + dim * CF::K + (p - CF::K);
+        else orig = 2 * CF::Dt * CF::K + dim * (CF::K - 1) + (p - 2 * CF::K);
+        v = is_w ? W2[orig * CF::H + col] : b2[orig];
+      }
+    }
+    packed[e] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Stage copy HBM/L2 -> LDS (16-byte loads, all 256 threads)
+// ---------------------------------------------------------------------------
+// Asynchronous stage copy HBM/L2 -> LDS with LDS-DMA (global_load_lds_dwordx4): wave w
+// moves 1 KB chunks w, w+4, ...; no VGPRs hold the data.  Completion is awaited by the
+// next __syncthreads() (which waits vmcnt(0)).
+template <int NFLOATS>
+NAZ_DEV void stage_issue(float* lds, const float* __restrict__ src) {
+  static_assert(NFLOATS % 256 == 0, "stage must be whole 1 KB chunks");
+  constexpr int CHUNKS = NFLOATS / 256;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int c0 = 0; c0 < CHUNKS; c0 += 4) {
+    const int c = c0 + wave;
+    if (c0 + 3 < CHUNKS || c < CHUNKS) {
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(src + c * 256 + lane * 4),
+          (void __attribute__((address_space(3)))*)(lds + c * 256), 16, 0, 0);
+    }
+  }
+}
+
+// Accumulators init from the packed bias block [o][h][16]
+template <int NB>
+NAZ_DEV void init_bias(floatx16 (&acc)[NB], const float* __restrict__ bias, int h) {
+#pragma unroll
+  for (int o = 0; o < NB; ++o) {
+    const float4* b4 = reinterpret_cast<const float4*>(bias + (o * 2 + h) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = b4[q];
+      acc[o][4 * q + 0] = v.x;
+      acc[o][4 * q + 1] = v.y;
+      acc[o][4 * q + 2] = v.z;
+      acc[o][4 * q + 3] = v.w;
+    }
+  }
+}
+
+// acc[o] += W-panel(o) x B for all NT k-steps; B operand for k-step t is bop(t).
+// panels: [NB][NT/4][64][4] in LDS.
+template <int NB, int NT, class BOp>
+NAZ_DEV void gemm_panels(floatx16 (&acc)[NB], const float* __restrict__ panels, int lane, BOp bop) {
+  const float4* p4 = reinterpret_cast<const float4*>(panels);
+#pragma unroll
+  for (int t4 = 0; t4 < NT / 4; ++t4) {
+    float4 a[NB];
+#pragma unroll
+    for (int o = 0; o < NB; ++o) a[o] = p4[(o * (NT / 4) + t4) * 64 + lane];
+#pragma unroll
+    for (int o = 0; o < NB; ++o) acc[o] = mfma32(a[o].x, bop(4 * t4 + 0), acc[o]);
+#pragma unroll
+    for (int o = 0; o < NB; ++o) acc[o] = mfma32(a[o].y, bop(4 * t4 + 1), acc[o]);
+#pragma unroll
+    for (int o = 0; o < NB; ++o) acc[o] = mfma32(a[o].z, bop(4 * t4 + 2), acc[o]);
+#pragma unroll
+    for (int o = 0; o < NB; ++o) acc[o] = mfma32(a[o].w, bop(4 * t4 + 3), acc[o]);
+  }
+}
+
+template <int NB>
+NAZ_DEV void tanh_all(floatx16 (&acc)[NB]) {
+#pragma unroll
+  for (int o = 0; o < NB; ++o)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[o][r] = tanh_f(acc[o][r]);
+}
+
+template <int I, int N, class F>
+NAZ_DEV void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Main fused kernel.  DIR_INV = true: log_prob (layers reversed, inverse maps).
+//
+// Per layer the LDS buffer holds, in turn, stage A (W0 + b0 + lower tables), B (W1 + b1)
+// and C_j (W2 panel groups + b2).  Each stage's LDS-DMA copy is issued right after the
+// barrier that frees the buffer and lands while the waves run the VALU epilogue of the
+// GEMM just finished (tanh, or the spline), so copies hide behind VALU work and the
+// second co-resident workgroup keeps the matrix pipe busy meanwhile.
+// ---------------------------------------------------------------------------
+template <class CF>
+NAZ_DEV void load_tables(const float* tb, SplineTables<CF::K>& t) {
+#pragma unroll
+  for (int k = 0; k <= CF::K; ++k) {
+    t.cw[k] = tb[k];
+    t.ch[k] = tb[CF::K + 1 + k];
+    t.dv[k] = tb[2 * (CF::K + 1) + k];
+  }
+}
+
+template <class CF, bool DIR_INV>
+__global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
+    const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
+    const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
+    float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound) {
+  extern __shared__ float4 lds4[];
+  float* lds = reinterpret_cast<float*>(lds4);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int h = lane >> 5;
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerWG + wave * 32 + (lane & 31);
+  const bool valid = row < B;
+  const int64_t crow = valid ? row : 0;  // clamp so every lane can load unconditionally
+
+  // first layer's stage A goes out before anything else
+  stage_issue<CF::A_SIZE>(lds, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER);
+
+  // ---- per-lane state: lower dims {h*SH..}, upper dims {S + h*DH..}
+  float zl[CF::SH], zu[CF::DH];
+  float ldsum = 0.f;   // sum of per-dim FORWARD log-dets over this lane's dims
+  float logjac = 0.f;  // bounding prologue contribution (log_prob only)
+#pragma unroll
+  for (int q = 0; q < CF::SH; ++q) zl[q] = valid ? x[crow * ldx + h * CF::SH + q] : 0.f;
+#pragma unroll
+  for (int q = 0; q < CF::DH; ++q) zu[q] = valid ? x[crow * ldx + CF::S + h * CF::DH + q] : 0.f;
+
+  if (DIR_INV && low != nullptr) {  // naz bounding_transform (transforms.py:20-23)
+    auto bnd = [&](float& v, int dim) {
+      const float lo = low[dim], hi = high[dim];
+      const float u = (v - lo) / (hi - lo);
+      logjac -= logf(u) + log1pf(-u);
+      v = logf(u / (1.f - u));
+    };
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) bnd(zl[q], h * CF::SH + q);
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) bnd(zu[q], CF::S + h * CF::DH + q);
+    if (h == 0) {
+      float sl = 0.f;
+      for (int d = 0; d < CF::D; ++d) sl += logf(high[d] - low[d]);
+      logjac -= sl;
+    }
+  }
+  __syncthreads();  // stage A of the first layer has landed
+
+  for (int li = 0; li < L; ++li) {
+    const int l = DIR_INV ? (L - 1 - li) : li;
+    const float* lp = packed + (int64_t)l * CF::LAYER;
+
+    // context half-row for the conditioner input (re-read per layer: L1/L2-resident)
+    float cx[CF::CHA];
+#pragma unroll
+    for (int q = 0; q < CF::CHA; ++q) {
+      const int c = h * CF::CH + q;
+      cx[q] = (CF::CH > 0 && c < CF::C) ? ctx[crow * ldc + c] : 0.f;
+    }
+
+    // ---------------- stage A resident: lower spline (inverse dir), GEMM1
+    float x1[CF::SH];
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) {
+      if constexpr (DIR_INV && CF::LOWER) {
+        SplineTables<CF::K> t;
+        load_tables<CF>(lds + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
+        float ld;
+        zl[q] = rqs_apply<CF::K, true>(t, zl[q], bound, ld);
+        ldsum -= ld;  // forward ld = -(inverse ld)
+      }
+      x1[q] = zl[q];
+    }
+    floatx16 acc1[CF::HB];
+    init_bias<CF::HB>(acc1, lds + CF::A_BIAS, h);
+    gemm_panels<CF::HB, CF::KS0P>(acc1, lds, lane, [&](int t) -> float {
+      if (t < CF::CH) return cx[t < CF::CHA ? t : 0];
+      if (t < CF::KS0) return x1[(t - CF::CH) < CF::SH ? (t - CF::CH) : 0];
+      return 0.f;
+    });
+    if constexpr (!DIR_INV && CF::LOWER) {  // forward: y1 = lower(x1) after x1 fed the conditioner
+#pragma unroll
+      for (int q = 0; q < CF::SH; ++q) {
+        SplineTables<CF::K> t;
+        load_tables<CF>(lds + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
+        float ld;
+        zl[q] = rqs_apply<CF::K, false>(t, zl[q], bound, ld);
+        ldsum += ld;
+      }
+    }
+    __syncthreads();
+    stage_issue<CF::B_SIZE>(lds, lp + CF::B_OFF);
+    tanh_all<CF::HB>(acc1);
+    __syncthreads();
+
+    // ---------------- stage B resident: GEMM2
+    floatx16 acc2[CF::HB];
+    init_bias<CF::HB>(acc2, lds + CF::B_BIAS, h);
+    gemm_panels<CF::HB, CF::KS1>(acc2, lds, lane, [&](int t) -> float { return acc1[t >> 4][t & 15]; });
+    __syncthreads();
+    stage_issue<CF::c_size(0)>(lds, lp + CF::c_off(0));
+    tanh_all<CF::HB>(acc2);
+    __syncthreads();
+
+    // ---------------- stages C_j resident: GEMM3 -> raw spline params in registers
+    floatx16 acc3[CF::NO];
+    static_for<0, CF::NSTG3>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      constexpr int cnt = CF::c_count(j);
+      if constexpr (j > 0) {
+        __syncthreads();
+        stage_issue<CF::c_size(j)>(lds, lp + CF::c_off(j));
+        __syncthreads();
+      }
+      floatx16 part[cnt];
+      init_bias<cnt>(part, lds + cnt * CF::PANEL1, h);
+      gemm_panels<cnt, CF::KS1>(part, lds, lane, [&](int t) -> float { return acc2[t >> 4][t & 15]; });
+#pragma unroll
+      for (int o = 0; o < cnt; ++o) acc3[j * CF::PPS + o] = part[o];
+    });
+    __syncthreads();
+    if (li + 1 < L) stage_issue<CF::A_SIZE>(lds, packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER);
+
+    // ---------------- upper spline on this lane's DH dims (overlaps the next stage A copy)
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) {
+      float uw[CF::K], uh[CF::K], ud[CF::K - 1];
+#pragma unroll
+      for (int k = 0; k < CF::K; ++k) {
+        const int sw = q * CF::P + k, sh = q * CF::P + CF::K + k;
+        uw[k] = acc3[sw >> 4][sw & 15];
+        uh[k] = acc3[sh >> 4][sh & 15];
+      }
+#pragma unroll
+      for (int k = 0; k < CF::K - 1; ++k) {
+        const int sd = q * CF::P + 2 * CF::K + k;
+        ud[k] = acc3[sd >> 4][sd & 15];
+      }
+      SplineTables<CF::K> t;
+      build_tables<CF::K>(uw, uh, ud, bound, t);
+      float ld;
+      zu[q] = rqs_apply<CF::K, DIR_INV>(t, zu[q], bound, ld);
+      ldsum += DIR_INV ? -ld : ld;
+    }
+    __syncthreads();  // next layer's stage A has landed
+  }
+
+  if constexpr (DIR_INV) {
+    // base density Independent(Normal(0,1)) over this lane's dims, then combine halves
+    constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+    float base = 0.f;
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) base += -(zl[q] * zl[q]) / 2.f - kLogSqrt2Pi;
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) base += -(zu[q] * zu[q]) / 2.f - kLogSqrt2Pi;
+    float v = base - ldsum + logjac;
+    v += __shfl_xor(v, 32);
+    if (h == 0 && valid) out_lp[row] = v;
+  } else {
+    if (low != nullptr) {  // inverse_bounding_transform (transforms.py:25-27)
+#pragma unroll
+      for (int q = 0; q < CF::SH; ++q) {
+        const int d = h * CF::SH + q;
+        zl[q] = (1.f / (1.f + expf(-zl[q]))) * (high[d] - low[d]) + low[d];
+      }
+#pragma unroll
+      for (int q = 0; q < CF::DH; ++q) {
+        const int d = CF::S + h * CF::DH + q;
+        zu[q] = (1.f / (1.f + expf(-zu[q]))) * (high[d] - low[d]) + low[d];
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int q = 0; q < CF::SH; ++q) yout[row * ldy + h * CF::SH + q] = zl[q];
+#pragma unroll
+      for (int q = 0; q < CF::DH; ++q) yout[row * ldy + CF::S + h * CF::DH + q] = zu[q];
+    }
+    if (out_lp != nullptr) {
+      float v = ldsum + __shfl_xor(ldsum, 32);
+      if (h == 0 && valid) out_lp[row] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host dispatch over the compiled instantiations
+// ---------------------------------------------------------------------------
+template <class CF>
+struct CouplingOps {
+  static int64_t packed_bytes(int L) { return (int64_t)L * CF::LAYER * 4; }
+  static int64_t param_count(int L) { return (int64_t)L * CF::FLAT; }
+  static int pack(const float* flat, void* packed, int L, float bound, hipStream_t s) {
+    const int64_t n = (int64_t)L * CF::LAYER;
+    int64_t grid = (n + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL((coupling_pack_kernel<CF>), dim3((unsigned)grid), dim3(256), 0, s, flat,
+                       reinterpret_cast<float*>(packed), L, bound);
+    return check_launch("coupling_pack_kernel");
+  }
+  static int run(bool inv, const void* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
+                 const float* low, const float* high, float* out_lp, float* y, int64_t ldy, int64_t B, float bound,
+                 hipStream_t s) {
+    if (B == 0) return 0;
+    const int64_t grid = (B + kRowsPerWG - 1) / kRowsPerWG;
+    const size_t lds = (size_t)CF::MAXSTAGE * 4;
+    if (inv)
+      hipLaunchKernelGGL((coupling_flow_kernel<CF, true>), dim3((unsigned)grid), dim3(256), lds, s,
+                         reinterpret_cast<const float*>(packed), L, x, ldx, ctx, ldc, low, high, out_lp, y, ldy, B,
+                         bound);
+    else
+      hipLaunchKernelGGL((coupling_flow_kernel<CF, false>), dim3((unsigned)grid), dim3(256), lds, s,
+                         reinterpret_cast<const float*>(packed), L, x, ldx, ctx, ldc, low, high, out_lp, y, ldy, B,
+                         bound);
+    return check_launch("coupling_flow_kernel");
+  }
+};
+
+// Instantiation table: (D, C, S, K, H, lower).  Bench configs first (BASELINE.json
+// configs 2 and 3), then small shapes used by the parity tests.
+#ifndef NAZ_COUPLING_CONFIGS
+#define NAZ_COUPLING_CONFIGS(X)   \
+  X(16, 32, 8, 8, 128, true)      \
+  X(16, 32, 8, 8, 128, false)     \
+  X(8, 0, 4, 8, 128, true)        \
+  X(8, 0, 4, 8, 128, false)       \
+  X(16, 0, 8, 8, 128, true)       \
+  X(4, 3, 2, 8, 64, true)         \
+  X(6, 2, 2, 4, 32, true)         \
+  X(6, 2, 2, 4, 32, false)
+#endif
+
+template <class F>
+static int coupling_dispatch(const naz_coupling_desc* d, F&& f) {
+  if (d == nullptr) return set_error("naz_coupling: null descriptor");
+  if (d->act != NAZ_ACT_TANH) return -2;
+#define NAZ_TRY(D_, C_, S_, K_, H_, LOW_)                                                                  \
+  if (d->D == D_ && d->C == C_ && d->S == S_ && d->K == K_ && d->H == H_ && (d->has_lower != 0) == LOW_) \
+    return f(CouplingOps<CouplingCfg<D_, C_, S_, K_, H_, LOW_>>{});
+  NAZ_COUPLING_CONFIGS(NAZ_TRY)
+#undef NAZ_TRY
+  return -2;
+}
+
+int coupling_supported(const naz_coupling_desc* d) {
+  return coupling_dispatch(d, [](auto) { return 1; }) == 1 ? 1 : 0;
+}
+
+int64_t coupling_param_count(const naz_coupling_desc* d) {
+  int64_t v = -1;
+  coupling_dispatch(d, [&](auto ops) { v = decltype(ops)::param_count(d->L); return 0; });
+  return v;
+}
+
+int64_t coupling_packed_bytes(const naz_coupling_desc* d) {
+  int64_t v = -1;
+  coupling_dispatch(d, [&](auto ops) { v = decltype(ops)::packed_bytes(d->L); return 0; });
+  return v;
+}
+
+static int unsupported(const naz_coupling_desc* d) {
+  return set_error("naz_coupling: no fused instantiation for D=%d C=%d S=%d K=%d H=%d act=%d lower=%d", d->D, d->C,
+                   d->S, d->K, d->H, d->act, d->has_lower);
+}
+
+int coupling_pack(const naz_coupling_desc* d, const float* flat, void* packed, hipStream_t s) {
+  int rc = coupling_dispatch(d, [&](auto ops) { return decltype(ops)::pack(flat, packed, d->L, d->bound, s); });
+  return rc == -2 ? unsupported(d) : rc;
+}
+
+int coupling_log_prob(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                      int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s) {
+  if ((low == nullptr) != (high == nullptr)) return set_error("naz_coupling_log_prob: low/high must both be set");
+  int rc = coupling_dispatch(d, [&](auto ops) {
+    return decltype(ops)::run(true, packed, d->L, x, ldx, ctx, ldc, low, high, out_lp, nullptr, 0, B, d->bound, s);
+  });
+  return rc == -2 ? unsupported(d) : rc;
+}
+
+int coupling_sample(const naz_coupling_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx,
+                    int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B,
+                    hipStream_t s) {
+  if ((low == nullptr) != (high == nullptr)) return set_error("naz_coupling_sample: low/high must both be set");
+  int rc = coupling_dispatch(d, [&](auto ops) {
+    return decltype(ops)::run(false, packed, d->L, z, ldz, ctx, ldc, low, high, out_ld, y, ldy, B, d->bound, s);
+  });
+  return rc == -2 ? unsupported(d) : rc;
+}
+
+}  // namespace naz

@@ -1,0 +1,182 @@
+// Device-side building blocks shared by the naz_amd HIP kernels (gfx950 / CDNA4).
+//
+// The rational-quadratic spline below restates pyro-ppl 1.9's
+// distributions/transforms/spline.py::_monotonic_rational_spline (order="quadratic",
+// the naz default: naz/flows/transforms.py:165,201) one (row, dim) at a time, with the
+// K+1 knots held in registers instead of ~40 separate [B,Dt,K] tensors.
+//   * knot cumsum is accumulated in double and rounded per prefix, which is exactly what
+//     torch's CPU cumsum does for float32 (acc_type<float> == double on CPU), so knot
+//     positions match the CPU reference bit for bit given equal bin fractions;
+//   * knot affine map (2B·c − B) uses separately rounded mul/add like torch's eager ops;
+//   * bin search = count(x >= knot + eps) − 1, clamped — pyro's _searchsorted/_select_bins.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NAZ_DEV __device__ __forceinline__
+
+namespace naz {
+
+constexpr float kMinBinWidth = 1e-3f;
+constexpr float kMinBinHeight = 1e-3f;
+constexpr float kMinDerivative = 1e-3f;
+constexpr float kSearchEps = 1e-6f;
+
+enum Act : int { ACT_IDENTITY = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SOFTPLUS = 3, ACT_SIGMOID = 4 };
+
+// torch.nn.functional.softplus(beta=1, threshold=20)
+NAZ_DEV float softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+NAZ_DEV float tanh_f(float x) {
+  // tanh via one exp: |err| <= ~1e-7 absolute (the next layer consumes absolute values)
+  float ax = fabsf(x);
+  float t = expf(-2.f * ax);
+  float r = (1.f - t) / (1.f + t);
+  return copysignf(r, x);
+}
+
+template <int ACT>
+NAZ_DEV float activate(float x) {
+  if constexpr (ACT == ACT_TANH) return tanh_f(x);
+  else if constexpr (ACT == ACT_RELU) return fmaxf(x, 0.f);
+  else if constexpr (ACT == ACT_SOFTPLUS) return softplus(x);
+  else if constexpr (ACT == ACT_SIGMOID) return 1.f / (1.f + expf(-x));
+  else return x;
+}
+
+NAZ_DEV float activate_rt(int act, float x) {
+  switch (act) {
+    case ACT_TANH: return tanh_f(x);
+    case ACT_RELU: return fmaxf(x, 0.f);
+    case ACT_SOFTPLUS: return softplus(x);
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-x));
+    default: return x;
+  }
+}
+
+// d act / d pre expressed through the post-activation value y (all supported acts allow it)
+NAZ_DEV float activate_grad_from_out(int act, float y) {
+  switch (act) {
+    case ACT_TANH: return 1.f - y * y;
+    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    case ACT_SOFTPLUS: return -expm1f(-y);  // sigmoid(pre) = 1 - exp(-softplus(pre))
+    case ACT_SIGMOID: return y * (1.f - y);
+    default: return 1.f;
+  }
+}
+
+// Normalised spline tables for one dimension: K+1 knots in x and y, K+1 knot slopes.
+template <int K>
+struct SplineTables {
+  float cw[K + 1];  // x knots
+  float ch[K + 1];  // y knots
+  float dv[K + 1];  // slopes (edge slopes pinned to 1 - min_derivative)
+};
+
+// softmax over K register values, torch order: exp(x - max) then divide by the sum
+template <int K>
+NAZ_DEV void softmax_k(const float* u, float* out) {
+  float m = u[0];
+#pragma unroll
+  for (int k = 1; k < K; ++k) m = fmaxf(m, u[k]);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) { out[k] = expf(u[k] - m); s += out[k]; }
+#pragma unroll
+  for (int k = 0; k < K; ++k) out[k] = out[k] / s;
+}
+
+// [pyro] _calculate_knots applied to softmaxed fractions (min-width blend included)
+template <int K>
+NAZ_DEV void knots_from_fractions(const float* frac, float minw, float bound, float* knots) {
+  const float scale = 1.f - minw * (float)K;
+  double acc = 0.0;
+  knots[0] = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float wk = __fadd_rn(minw, __fmul_rn(scale, frac[k]));
+    acc += (double)wk;
+    knots[k + 1] = (float)acc;
+  }
+  const float two_b = 2.f * bound;
+#pragma unroll
+  for (int k = 0; k <= K; ++k) knots[k] = __fadd_rn(__fmul_rn(two_b, knots[k]), -bound);
+  knots[0] = -bound;
+  knots[K] = bound;
+}
+
+// Build tables from UNNORMALISED params (uw[K], uh[K], ud[K-1]).
+template <int K>
+NAZ_DEV void build_tables(const float* uw, const float* uh, const float* ud, float bound,
+                          SplineTables<K>& t) {
+  float f[K];
+  softmax_k<K>(uw, f);
+  knots_from_fractions<K>(f, kMinBinWidth, bound, t.cw);
+  softmax_k<K>(uh, f);
+  knots_from_fractions<K>(f, kMinBinHeight, bound, t.ch);
+  t.dv[0] = 1.f - kMinDerivative;
+  t.dv[K] = 1.f - kMinDerivative;
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k) t.dv[k + 1] = kMinDerivative + softplus(ud[k]);
+}
+
+// Evaluate the spline (forward or inverse) with the bin quantities selected in registers.
+// Returns ld of the map actually applied (inverse map's ld for INV), 0 outside [-B, B].
+template <int K, bool INV>
+NAZ_DEV float rqs_apply(const SplineTables<K>& t, float x, float bound, float& ld) {
+  if (!(x >= -bound && x <= bound)) {  // identity tails (NaN also falls through unchanged)
+    ld = 0.f;
+    return x;
+  }
+  // bin search on (knots + eps)
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k <= K; ++k) {
+    float knot = INV ? t.ch[k] : t.cw[k];
+    cnt += (x >= knot + kSearchEps) ? 1 : 0;
+  }
+  int idx = cnt - 1;
+  idx = idx < 0 ? 0 : (idx > K - 1 ? K - 1 : idx);
+  float cw0 = t.cw[0], cw1 = t.cw[1], ch0 = t.ch[0], ch1 = t.ch[1], d0 = t.dv[0], d1 = t.dv[1];
+#pragma unroll
+  for (int k = 1; k < K; ++k) {
+    bool s = (idx == k);
+    cw0 = s ? t.cw[k] : cw0;
+    cw1 = s ? t.cw[k + 1] : cw1;
+    ch0 = s ? t.ch[k] : ch0;
+    ch1 = s ? t.ch[k + 1] : ch1;
+    d0 = s ? t.dv[k] : d0;
+    d1 = s ? t.dv[k + 1] : d1;
+  }
+  const float w = cw1 - cw0;
+  const float h = ch1 - ch0;
+  const float delta = h / w;
+  const float t1 = (d0 + d1) - 2.f * delta;
+  float out, dnum, den;
+  if constexpr (INV) {
+    const float dy = x - ch0;
+    const float a = dy * t1 + h * (delta - d0);
+    const float b = h * d0 - dy * t1;
+    const float c = -delta * dy;
+    const float disc = b * b - 4.f * a * c;
+    const float root = (2.f * c) / (-b - sqrtf(disc));
+    out = root * w + cw0;
+    const float tomt = root * (1.f - root);
+    den = delta + t1 * tomt;
+    const float omr = 1.f - root;
+    dnum = delta * delta * (d1 * root * root + 2.f * delta * tomt + d0 * omr * omr);
+    ld = -(logf(dnum) - 2.f * logf(den));
+  } else {
+    const float th = (x - cw0) / w;
+    const float tomt = th * (1.f - th);
+    const float num = h * (delta * th * th + d0 * tomt);
+    den = delta + t1 * tomt;
+    out = ch0 + num / den;
+    const float omt = 1.f - th;
+    dnum = delta * delta * (d1 * th * th + 2.f * delta * tomt + d0 * omt * omt);
+    ld = logf(dnum) - 2.f * logf(den);
+  }
+  return out;
+}
+
+}  // namespace naz

@@ -1,0 +1,39 @@
+// Host-side internals shared by the naz_amd HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/naz_hip.h"
+
+namespace naz {
+
+// Thread-local last-error message (naz_last_error); returns -1 for `return set_error(...)`.
+int set_error(const char* fmt, ...);
+// Checks hipGetLastError after a launch; sets the message and returns nonzero on failure.
+int check_launch(const char* what);
+
+int rqs_cond(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
+             float* ld, int ld_mode, int64_t B, int Dt, int K, int layout, float bound, hipStream_t s);
+int rqs_uncond(int inverse, const float* x, int64_t ldx, const float* uw, const float* uh, const float* ud, float* y,
+               int64_t ldy, float* ld, int64_t B, int Dt, int K, float bound, hipStream_t s);
+int linear_act(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx, int Kx, const float* W,
+               const float* mask, const float* b, float* y, int64_t ldy, int64_t M, int N, int act, hipStream_t s);
+int affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
+              float* ld, int ld_mode, int64_t B, int D, hipStream_t s);
+int base_log_prob(const float* z, int64_t ldz, float* out, int64_t B, int D, int accumulate, hipStream_t s);
+int bounding_fwd(const float* x, int64_t ldx, const float* low, const float* high, float* y, int64_t ldy,
+                 float* out_logjac, int64_t B, int D, hipStream_t s);
+int bounding_inv(const float* y, int64_t ldy, const float* low, const float* high, float* x, int64_t ldx, int64_t B,
+                 int D, hipStream_t s);
+
+int coupling_supported(const naz_coupling_desc* d);
+int64_t coupling_param_count(const naz_coupling_desc* d);
+int64_t coupling_packed_bytes(const naz_coupling_desc* d);
+int coupling_pack(const naz_coupling_desc* d, const float* flat, void* packed, hipStream_t s);
+int coupling_log_prob(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                      int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s);
+int coupling_sample(const naz_coupling_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx,
+                    int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B,
+                    hipStream_t s);
+
+}  // namespace naz

@@ -1,0 +1,180 @@
+// Standalone rational-quadratic spline kernels (SURVEY.md §8a rows a1+a2).
+//
+// Replaces, for one ConditionedSpline call, pyro's ~40 eager kernels
+// (softmax/softplus in ConditionalSpline._params, pad, cumsum, searchsorted,
+// seven gathers, the rational evaluation and the logs) reached from
+// naz/flows/transforms.py:190 (nsa) and :228 (nsc intent).
+//
+// Layout: one workgroup owns R = 256 / Dt consecutive rows.  The rows' raw
+// conditioner outputs (R × Dt·(3K−1) floats, contiguous when the caller's row
+// stride equals the row length) are copied HBM→LDS with 16-byte loads, then each
+// thread evaluates one (row, dim) with its knots in registers.  The per-row
+// log-det sum is a fixed-order LDS reduction (dims 0..Dt−1, like torch's .sum(-1)).
+// HBM-bound: per (row, dim) 4·(3K−1) + 4 bytes in, 4 (+4) bytes out.
+#include "naz_device.h"
+#include "naz_internal.h"
+
+namespace naz {
+
+// Copy `n` floats starting at src[0] into lds[0..n) with 16-B loads where aligned.
+NAZ_DEV void block_copy_to_lds(float* lds, const float* __restrict__ src, int n, int tid, int nthreads) {
+  uintptr_t addr = reinterpret_cast<uintptr_t>(src);
+  int head = (int)(((16 - (addr & 15)) & 15) >> 2);
+  if ((addr & 3) != 0) head = n;  // not even 4-B aligned: scalar path
+  if (head > n) head = n;
+  for (int i = tid; i < head; i += nthreads) lds[i] = src[i];
+  int nvec = (n - head) >> 2;
+  const float4* s4 = reinterpret_cast<const float4*>(src + head);
+  for (int i = tid; i < nvec; i += nthreads) {
+    float4 v = s4[i];
+    int o = head + 4 * i;
+    lds[o + 0] = v.x; lds[o + 1] = v.y; lds[o + 2] = v.z; lds[o + 3] = v.w;
+  }
+  for (int i = head + 4 * nvec + tid; i < n; i += nthreads) lds[i] = src[i];
+}
+
+template <int K, bool INV>
+__global__ void __launch_bounds__(256) rqs_cond_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ raw, int64_t ldr,
+    float* __restrict__ y, int64_t ldy, float* __restrict__ ld_out, int ld_mode, int64_t B, int Dt,
+    int layout, float bound) {
+  extern __shared__ float lds[];
+  constexpr int PD = 3 * K - 1;
+  const int P = Dt * PD;
+  const int R = (Dt >= 256) ? 1 : 256 / Dt;
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int rows = (int)((B - r0) < R ? (B - r0) : R);
+  float* raw_s = lds;              // [R][P]
+  float* ld_s = lds + (size_t)R * P;  // [R][Dt]
+
+  if (ldr == P) {
+    block_copy_to_lds(raw_s, raw + r0 * ldr, rows * P, tid, blockDim.x);
+  } else {
+    for (int i = tid; i < rows * P; i += blockDim.x) {
+      int r = i / P, c = i - r * P;
+      raw_s[i] = raw[(r0 + r) * ldr + c];
+    }
+  }
+  __syncthreads();
+
+  for (int e = tid; e < rows * Dt; e += blockDim.x) {
+    const int r = e / Dt, i = e - r * Dt;
+    const float* pr = raw_s + (size_t)r * P;
+    float uw[K], uh[K], ud[K - 1];
+    if (layout == NAZ_LAYOUT_DENSE) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) { uw[k] = pr[i * K + k]; uh[k] = pr[Dt * K + i * K + k]; }
+#pragma unroll
+      for (int k = 0; k < K - 1; ++k) ud[k] = pr[2 * Dt * K + i * (K - 1) + k];
+    } else {  // ARN: raw column p*Dt + i
+#pragma unroll
+      for (int k = 0; k < K; ++k) { uw[k] = pr[k * Dt + i]; uh[k] = pr[(K + k) * Dt + i]; }
+#pragma unroll
+      for (int k = 0; k < K - 1; ++k) ud[k] = pr[(2 * K + k) * Dt + i];
+    }
+    SplineTables<K> t;
+    build_tables<K>(uw, uh, ud, bound, t);
+    const float xv = x[(r0 + r) * ldx + i];
+    float ld;
+    const float yv = rqs_apply<K, INV>(t, xv, bound, ld);
+    y[(r0 + r) * ldy + i] = yv;
+    if (ld_mode == NAZ_LD_PERDIM) ld_out[(r0 + r) * Dt + i] = ld;
+    else ld_s[r * Dt + i] = ld;
+  }
+  if (ld_mode == NAZ_LD_PERDIM) return;
+  __syncthreads();
+  for (int r = tid; r < rows; r += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < Dt; ++i) s += ld_s[r * Dt + i];
+    if (ld_mode == NAZ_LD_ROWSUM) ld_out[r0 + r] = s;
+    else if (ld_mode == NAZ_LD_ROWSUM_ADD) ld_out[r0 + r] += s;
+    else ld_out[r0 + r] -= s;
+  }
+}
+
+// Unconditional elementwise spline ([pyro] Spline, the coupling's lower spline):
+// params uw [Dt,K], uh [Dt,K], ud [Dt,K-1] shared by all rows.
+template <int K, bool INV>
+__global__ void __launch_bounds__(256) rqs_uncond_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ uwp, const float* __restrict__ uhp,
+    const float* __restrict__ udp, float* __restrict__ y, int64_t ldy, float* __restrict__ ld_out, int ld_mode,
+    int64_t B, int Dt, float bound) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * Dt) return;
+  const int64_t r = e / Dt;
+  const int i = (int)(e - r * Dt);
+  float uw[K], uh[K], ud[K - 1];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { uw[k] = uwp[i * K + k]; uh[k] = uhp[i * K + k]; }
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k) ud[k] = udp[i * (K - 1) + k];
+  SplineTables<K> t;
+  build_tables<K>(uw, uh, ud, bound, t);
+  float ld;
+  y[r * ldy + i] = rqs_apply<K, INV>(t, x[r * ldx + i], bound, ld);
+  ld_out[r * Dt + i] = ld;  // per-dim only (row sums are formed by the caller's layer)
+  (void)ld_mode;
+}
+
+template <int K, bool INV>
+static int launch_rqs_cond(const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
+                           float* ld, int ld_mode, int64_t B, int Dt, int layout, float bound, hipStream_t s) {
+  const int R = (Dt >= 256) ? 1 : 256 / Dt;
+  const size_t lds = ((size_t)R * Dt * (3 * K - 1) + (size_t)R * Dt) * sizeof(float);
+  if (lds > 160 * 1024) return set_error("naz_rqs: Dt*K too large for one LDS block (%zu bytes)", lds);
+  const int64_t grid = (B + R - 1) / R;
+  hipLaunchKernelGGL((rqs_cond_kernel<K, INV>), dim3((unsigned)grid), dim3(256), lds, s, x, ldx, raw, ldr, y, ldy,
+                     ld, ld_mode, B, Dt, layout, bound);
+  return check_launch("rqs_cond_kernel");
+}
+
+template <int K, bool INV>
+static int launch_rqs_uncond(const float* x, int64_t ldx, const float* uw, const float* uh, const float* ud, float* y,
+                             int64_t ldy, float* ld, int64_t B, int Dt, float bound, hipStream_t s) {
+  const int64_t n = B * Dt;
+  const int64_t grid = (n + 255) / 256;
+  hipLaunchKernelGGL((rqs_uncond_kernel<K, INV>), dim3((unsigned)grid), dim3(256), 0, s, x, ldx, uw, uh, ud, y, ldy,
+                     ld, NAZ_LD_PERDIM, B, Dt, bound);
+  return check_launch("rqs_uncond_kernel");
+}
+
+#define NAZ_K_DISPATCH(K_, CALL) \
+  switch (K_) {                  \
+    case 2: CALL(2); break;      \
+    case 3: CALL(3); break;      \
+    case 4: CALL(4); break;      \
+    case 5: CALL(5); break;      \
+    case 6: CALL(6); break;      \
+    case 8: CALL(8); break;      \
+    case 10: CALL(10); break;    \
+    case 12: CALL(12); break;    \
+    case 16: CALL(16); break;    \
+    default: return set_error("naz_rqs: count_bins=%d not instantiated (2,3,4,5,6,8,10,12,16)", K_); \
+  }
+
+int rqs_cond(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
+             float* ld, int ld_mode, int64_t B, int Dt, int K, int layout, float bound, hipStream_t s) {
+  if (B == 0) return 0;
+  int rc = 0;
+#define CALLC(KK)                                                                                              \
+  rc = inverse ? launch_rqs_cond<KK, true>(x, ldx, raw, ldr, y, ldy, ld, ld_mode, B, Dt, layout, bound, s) \
+               : launch_rqs_cond<KK, false>(x, ldx, raw, ldr, y, ldy, ld, ld_mode, B, Dt, layout, bound, s)
+  NAZ_K_DISPATCH(K, CALLC)
+#undef CALLC
+  return rc;
+}
+
+int rqs_uncond(int inverse, const float* x, int64_t ldx, const float* uw, const float* uh, const float* ud, float* y,
+               int64_t ldy, float* ld, int64_t B, int Dt, int K, float bound, hipStream_t s) {
+  if (B == 0) return 0;
+  int rc = 0;
+#define CALLU(KK)                                                                                   \
+  rc = inverse ? launch_rqs_uncond<KK, true>(x, ldx, uw, uh, ud, y, ldy, ld, B, Dt, bound, s) \
+               : launch_rqs_uncond<KK, false>(x, ldx, uw, uh, ud, y, ldy, ld, B, Dt, bound, s)
+  NAZ_K_DISPATCH(K, CALLU)
+#undef CALLU
+  return rc;
+}
+
+}  // namespace naz

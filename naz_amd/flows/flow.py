@@ -1,0 +1,193 @@
+"""``NormalizingFlow`` — naz's flow facade (naz/flows/flow.py:21-129), MI355X-native.
+
+Same constructor (``NormalizingFlow(flow_type, bounds, D, C, hidden, L, [K, [split]],
+embedding_net=None, **kw)``), same methods (``log_prob``, ``bounded_log_prob``,
+``average_log_prob``, ``sample``) and attributes (``flow``, ``transforms``, ``nets``,
+``flow_dist``, ``base_dist``, ``bounds``, ``conditional``, ``embedding_net``).
+
+For flow_type "nsc" with a compiled shape, log_prob / sample run as ONE fused HIP
+launch over all layers (``_FusedCoupling``); everything else runs the per-layer HIP
+kernels through the Transform objects.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+from torch import nn
+from torch.distributions import Normal
+
+from .. import ops
+from ..nn import activation_name
+from ..utils import device
+from .distributions import ConditionalTransformedDistribution, TransformedDistribution
+from .transforms import (ConditionalSplineCoupling, Permute, SplineCoupling, masked_affine_autoregressive,
+                         neural_spline_autoregressive, neural_spline_coupling)
+
+
+def continuous_free_form(*args, **kwargs):
+    """naz "cnf" (naz/flows/continuous_transforms.py:124-139) — SURVEY.md §8a row a11,
+    config 5: not built in this round."""
+    raise NotImplementedError("naz_amd: the FFJORD CNF (flow_type 'cnf') is not implemented yet")
+
+
+flow_makers = {"maf": masked_affine_autoregressive, "nsa": neural_spline_autoregressive,
+               "nsc": neural_spline_coupling, "cnf": continuous_free_form}
+
+
+class _FusedCoupling:
+    """All L spline-coupling layers as one HIP launch (naz_coupling_log_prob / _sample).
+
+    Parameters are gathered into the C ABI's flat per-layer order and re-laid into the
+    kernel's MFMA panel order by ``naz_coupling_pack`` — only when a parameter changed
+    (tracked by tensor version counters), so inference pays it once."""
+
+    def __init__(self, layers: List[nn.Module], D: int, C: int, S: int, K: int, H: int, act: str, lower: bool,
+                 bound: float):
+        self.layers = layers
+        self.desc = ops.coupling_desc(D, C, S, K, len(layers), H, act, lower, bound)
+        self._sig = None
+        self._packed = None
+
+    def params(self) -> List[torch.Tensor]:
+        out = []
+        for t in self.layers:
+            net = t.nn
+            for lin in net.layers:
+                out += [lin.weight, lin.bias]
+            low = t.lower_spline
+            if low is not None:
+                out += [low.unnormalized_widths, low.unnormalized_heights, low.unnormalized_derivatives]
+        return out
+
+    def packed(self) -> torch.Tensor:
+        ps = self.params()
+        sig = tuple((p.data_ptr(), p._version) for p in ps)
+        if sig != self._sig or self._packed is None:
+            flat = torch.cat([p.detach().reshape(-1) for p in ps])
+            self._packed = ops.coupling_pack(self.desc, flat, self._packed)
+            self._sig = sig
+        return self._packed
+
+    def log_prob(self, x, context=None, bounds=None, out=None):
+        low = high = None
+        if bounds is not None:
+            low, high = bounds["low"].to(x.device, torch.float32), bounds["high"].to(x.device, torch.float32)
+        return ops.coupling_log_prob(self.desc, self.packed(), x, context, low, high, out=out)
+
+    def sample(self, z, context=None, bounds=None, with_logdet=False):
+        low = high = None
+        if bounds is not None:
+            low, high = bounds["low"].to(z.device, torch.float32), bounds["high"].to(z.device, torch.float32)
+        return ops.coupling_sample(self.desc, self.packed(), z, context, low, high, with_logdet=with_logdet)
+
+
+def _fused_plan(flow_type, flow_args, flow_kwargs, transforms) -> Optional[_FusedCoupling]:
+    if flow_type != "nsc" or any(isinstance(t, Permute) for t in transforms):
+        return None
+    D, C, hidden, L, K, S = flow_args[:6]
+    hidden = list(hidden) if isinstance(hidden, (list, tuple)) else [hidden]
+    if len(hidden) != 2 or hidden[0] != hidden[1]:
+        return None
+    act = activation_name(flow_kwargs.get("activation", nn.Tanh()))
+    layers = list(transforms)
+    inner = [t.module if isinstance(t, SplineCoupling) else t for t in layers]
+    lower = all(t.lower_spline is not None for t in inner)
+    if not lower and any(t.lower_spline is not None for t in inner):
+        return None
+    try:
+        plan = _FusedCoupling(inner, D, C, S, K, hidden[0], act, lower, inner[0].bound)
+        return plan if ops.coupling_supported(plan.desc) else None
+    except Exception:
+        return None
+
+
+class NormalizingFlow(nn.Module):
+    """naz/flows/flow.py:24-129."""
+
+    def __init__(self, flow_type, bounds, *flow_maker_args, embedding_net=None, **flow_maker_kwargs):
+        super().__init__()
+        assert flow_type in list(flow_makers.keys())
+        flow_maker = flow_makers[flow_type]
+        self.flow_type = flow_type
+        self.conditional = True if flow_maker_args[1] > 0 else False
+        if embedding_net is not None:
+            assert self.conditional
+            self.embedding_net = embedding_net
+        else:
+            self.embedding_net = nn.Identity()
+        self.bounds = bounds
+        D = flow_maker_args[0]
+        self.register_buffer("_base_loc", torch.zeros(D))
+        self.register_buffer("_base_scale", torch.ones(D))
+        self.flow, self.transforms, self.nets = flow_maker(*flow_maker_args, **flow_maker_kwargs)
+        self._plan = _fused_plan(flow_type, flow_maker_args, flow_maker_kwargs, self.transforms)
+        self.to(device)
+        self._make_dist()
+
+    # -- distribution objects are rebuilt after device moves (the base Normal holds tensors)
+    def _make_dist(self):
+        self.base_dist = Normal(self._base_loc, self._base_scale)
+        if self.conditional:
+            self.flow_dist = ConditionalTransformedDistribution(self.base_dist, self.flow, fused=self._plan)
+        else:
+            self.flow_dist = TransformedDistribution(self.base_dist, self.flow, fused=self._plan)
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        if "_base_loc" in self._buffers and hasattr(self, "flow"):
+            self._make_dist()
+        return out
+
+    def set_fused(self, enabled: bool) -> None:
+        """Switch between the single fused launch and the per-layer kernels (testing aid)."""
+        if enabled and self._plan is None:
+            raise RuntimeError("no fused instantiation for this flow")
+        if not enabled:
+            self._plan_saved, self._plan = self._plan, None
+        elif getattr(self, "_plan_saved", None) is not None:
+            self._plan = self._plan_saved
+        self._make_dist()
+
+    @property
+    def fused(self) -> bool:
+        """True when log_prob/sample run as the single fused coupling launch."""
+        return self._plan is not None
+
+    def _bounds_dev(self, ref):
+        if self.bounds is None:
+            return None
+        return {k: torch.as_tensor(v, dtype=torch.float32, device=ref.device) for k, v in self.bounds.items()}
+
+    def _pdf(self, condition):
+        if self.conditional:
+            assert condition is not None
+            return self.flow_dist.condition(self.embedding_net(condition))
+        return self.flow_dist
+
+    def log_prob(self, x, *args, condition=None, **kwargs):
+        """log p(theta | lambda) for x [B, D] (naz/flows/flow.py:45-79)."""
+        pdf = self._pdf(condition)
+        return pdf.log_prob(x, bounds=self._bounds_dev(x))
+
+    def bounded_log_prob(self, x, *args, condition=None, **kwargs):
+        """naz/flows/flow.py:81-87: -inf outside the bounding box."""
+        if self.bounds is None:
+            return self.log_prob(x, *args, condition=condition, **kwargs)
+        b = self._bounds_dev(x)
+        lp = torch.full(x.shape[:1], float("-inf"), device=x.device, dtype=torch.float32)
+        valid = torch.prod((x > b["low"].expand(x.shape)) * (x < b["high"].expand(x.shape)), dim=1).to(torch.bool)
+        if bool(valid.any()):
+            lp[valid] = self.log_prob(x[valid, :], *args, condition=condition, **kwargs)
+        return lp
+
+    def average_log_prob(self, x, *args, condition=None, **kwargs):
+        """naz/flows/flow.py:90-91."""
+        return torch.mean(self.bounded_log_prob(x, *args, condition=condition, **kwargs))
+
+    def sample(self, *args, condition=None, **kwargs):
+        """theta ~ p(theta | lambda) (naz/flows/flow.py:94-129); ``args[0]`` is the sample shape."""
+        pdf = self._pdf(condition)
+        shape = args[0] if args else kwargs.get("sample_shape", ())
+        ref = self._base_loc
+        return pdf.sample(shape, bounds=self._bounds_dev(ref))

@@ -1,0 +1,206 @@
+"""Conditioner networks with pyro's module surface, executed by the HIP kernels.
+
+Mirrors the pyro-ppl 1.9 classes naz instantiates (naz/flows/transforms.py:142,180,223):
+``ConditionalDenseNN``/``DenseNN`` and ``ConditionalAutoRegressiveNN``/``AutoRegressiveNN``
+with ``layers.{i}.weight|bias`` parameter names, ``masks``, ``mask_skip``, ``permutation``
+and the pyro output shapes (so ``torch_to_jax`` in naz/flows/bflow_jax_maf.py:26-46 and
+``get_params``/``set_params`` in naz/trainers/train_flows.py:20-71 work unchanged).
+Every forward runs ``naz_linear_act`` (fused concat + mask + bias + activation).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+from torch import nn
+
+from . import ops
+
+
+def activation_name(f: nn.Module) -> str:
+    """Map a torch activation module to the kernel's activation code."""
+    if isinstance(f, nn.Tanh):
+        return "tanh"
+    if isinstance(f, nn.ReLU):
+        return "relu"
+    if isinstance(f, nn.Sigmoid):
+        return "sigmoid"
+    if isinstance(f, nn.Softplus) and f.beta == 1 and f.threshold == 20:
+        return "softplus"
+    if isinstance(f, nn.Identity):
+        return "identity"
+    raise NotImplementedError(f"naz_amd: activation {f!r} has no HIP kernel (tanh, relu, sigmoid, softplus)")
+
+
+# ----------------------------------------------------------------------------- MADE masks
+def sample_mask_indices(input_dim: int, hidden_dim: int) -> torch.Tensor:
+    """[pyro] auto_reg_nn.sample_mask_indices(simple=True): round-half-to-even of a float32 linspace."""
+    return torch.round(torch.linspace(1, input_dim, steps=hidden_dim, dtype=torch.float32))
+
+
+def create_mask(input_dim: int, context_dim: int, hidden_dims: Sequence[int], permutation: torch.Tensor,
+                output_dim_multiplier: int):
+    """[pyro] auto_reg_nn.create_mask: context inputs get index 0, variable perm[k] gets k+1."""
+    permutation = permutation.cpu()
+    var_index = torch.empty(permutation.shape, dtype=torch.float32)
+    var_index[permutation] = torch.arange(input_dim, dtype=torch.float32)
+    input_indices = torch.cat((torch.zeros(context_dim), 1 + var_index))
+    if context_dim > 0:
+        hidden_indices = [sample_mask_indices(input_dim, h) - 1 for h in hidden_dims]
+    else:
+        hidden_indices = [sample_mask_indices(input_dim - 1, h) for h in hidden_dims]
+    output_indices = (var_index + 1).repeat(output_dim_multiplier)
+    mask_skip = (output_indices.unsqueeze(-1) > input_indices.unsqueeze(0)).float()
+    masks = [(hidden_indices[0].unsqueeze(-1) >= input_indices.unsqueeze(0)).float()]
+    for i in range(1, len(hidden_dims)):
+        masks.append((hidden_indices[i].unsqueeze(-1) >= hidden_indices[i - 1].unsqueeze(0)).float())
+    masks.append((output_indices.unsqueeze(-1) > hidden_indices[-1].unsqueeze(0)).float())
+    return masks, mask_skip
+
+
+class MaskedLinear(nn.Linear):
+    """[pyro] nn.auto_reg_nn.MaskedLinear: F.linear(x, mask * W, b); mask is a buffer."""
+
+    def __init__(self, in_features: int, out_features: int, mask: torch.Tensor, bias: bool = True):
+        super().__init__(in_features, out_features, bias)
+        self.register_buffer("mask", mask.data.clone())
+
+    def forward(self, x):  # pragma: no cover - kept for API completeness; the nets call the fused kernel
+        return ops.linear_act(x, self.weight, self.bias, "identity", mask=self.mask)
+
+
+def _slices(param_dims: Sequence[int]):
+    ends = torch.cumsum(torch.tensor(param_dims), dim=0)
+    starts = torch.cat((torch.zeros(1).type_as(ends), ends[:-1]))
+    return [slice(int(s), int(e)) for s, e in zip(starts, ends)]
+
+
+def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Tensor], masked: bool) -> torch.Tensor:
+    n = len(layers)
+    h = None
+    for i, layer in enumerate(layers):
+        act = f_name if i < n - 1 else "identity"
+        m = layer.mask if masked else None
+        if i == 0:
+            h = ops.linear_act(x, layer.weight, layer.bias, act, context=context, mask=m)
+        else:
+            h = ops.linear_act(h, layer.weight, layer.bias, act, mask=m)
+    return h
+
+
+class ConditionalDenseNN(nn.Module):
+    """[pyro] nn/dense_nn.py::ConditionalDenseNN — input cat([context, x])."""
+
+    def __init__(self, input_dim: int, context_dim: int, hidden_dims: Sequence[int],
+                 param_dims: Sequence[int] = (1, 1), nonlinearity: nn.Module = nn.ReLU()):
+        super().__init__()
+        self.input_dim, self.context_dim = input_dim, context_dim
+        self.hidden_dims = list(hidden_dims)
+        self.param_dims = list(param_dims)
+        self.count_params = len(self.param_dims)
+        self.output_multiplier = sum(self.param_dims)
+        self.param_slices = _slices(self.param_dims)
+        dims = [input_dim + context_dim] + self.hidden_dims + [self.output_multiplier]
+        self.layers = nn.ModuleList([nn.Linear(dims[i], dims[i + 1]) for i in range(len(dims) - 1)])
+        self.f = nonlinearity
+        self.act = activation_name(nonlinearity)
+
+    def raw(self, x: torch.Tensor, context: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Flat conditioner output [B, sum(param_dims)] (what the spline kernels consume)."""
+        return _run_chain(self.layers, self.act, x, context, masked=False)
+
+    def _shape(self, h, lead):
+        if self.output_multiplier == 1:
+            return h
+        h = h.reshape(list(lead) + [self.output_multiplier])
+        if self.count_params == 1:
+            return h
+        return tuple(h[..., s] for s in self.param_slices)
+
+    def forward(self, x, context=None):
+        return self._shape(self.raw(x, context), x.shape[:-1])
+
+
+class DenseNN(ConditionalDenseNN):
+    """[pyro] nn/dense_nn.py::DenseNN."""
+
+    def __init__(self, input_dim, hidden_dims, param_dims=(1, 1), nonlinearity=nn.ReLU()):
+        super().__init__(input_dim, 0, hidden_dims, param_dims, nonlinearity)
+
+    def forward(self, x):
+        return self._shape(self.raw(x, None), x.shape[:-1])
+
+
+class ConditionalAutoRegressiveNN(nn.Module):
+    """[pyro] nn/auto_reg_nn.py::ConditionalAutoRegressiveNN (MADE, Germain et al. 2015)."""
+
+    def __init__(self, input_dim: int, context_dim: int, hidden_dims: Sequence[int],
+                 param_dims: Sequence[int] = (1, 1), permutation: Optional[torch.Tensor] = None,
+                 skip_connections: bool = False, nonlinearity: nn.Module = nn.ReLU()):
+        super().__init__()
+        if skip_connections:
+            raise NotImplementedError("naz_amd: MADE skip connections are not on naz's path (transforms.py:142,180)")
+        self.input_dim, self.context_dim = input_dim, context_dim
+        self.hidden_dims = list(hidden_dims)
+        self.param_dims = list(param_dims)
+        self.count_params = len(self.param_dims)
+        self.output_multiplier = sum(self.param_dims)
+        self.all_ones = all(p == 1 for p in self.param_dims)
+        self.param_slices = _slices(self.param_dims)
+        for h in self.hidden_dims:
+            if h < input_dim:
+                raise ValueError("Hidden dimension must not be less than input dimension.")
+        if permutation is None:
+            P = torch.randperm(input_dim, device="cpu")
+        else:
+            P = permutation.type(dtype=torch.int64).cpu()
+        self.register_buffer("permutation", P)
+        self.masks, self.mask_skip = create_mask(input_dim, context_dim, self.hidden_dims, P,
+                                                 self.output_multiplier)
+        dims = [input_dim + context_dim] + self.hidden_dims + [input_dim * self.output_multiplier]
+        self.layers = nn.ModuleList([MaskedLinear(dims[i], dims[i + 1], self.masks[i])
+                                     for i in range(len(dims) - 1)])
+        self.skip_layer = None
+        self.f = nonlinearity
+        self.act = activation_name(nonlinearity)
+
+    def get_permutation(self):
+        return self.permutation
+
+    def set_permutation(self, permutation: torch.Tensor) -> None:
+        """Replace the variable order and rebuild every MADE mask (e.g. when importing weights)."""
+        P = torch.as_tensor(permutation).to(torch.int64).cpu()
+        self.masks, self.mask_skip = create_mask(self.input_dim, self.context_dim, self.hidden_dims, P,
+                                                 self.output_multiplier)
+        dev = self.layers[0].weight.device
+        self.permutation = P.to(self.permutation.device)
+        for layer, m in zip(self.layers, self.masks):
+            layer.mask = m.to(dev)
+
+    def raw(self, x: torch.Tensor, context: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Flat MADE output [B, mult*D], column p*D + i (pyro's reshape to [mult, D])."""
+        return _run_chain(self.layers, self.act, x, context, masked=True)
+
+    def _shape(self, h, lead):
+        if self.output_multiplier == 1:
+            return h
+        h = h.reshape(list(lead) + [self.output_multiplier, self.input_dim])
+        if self.count_params == 1:
+            return h
+        if self.all_ones:
+            return torch.unbind(h, dim=-2)
+        return tuple(h[..., s, :] for s in self.param_slices)
+
+    def forward(self, x, context=None):
+        return self._shape(self.raw(x, context), x.shape[:-1])
+
+
+class AutoRegressiveNN(ConditionalAutoRegressiveNN):
+    """[pyro] nn/auto_reg_nn.py::AutoRegressiveNN."""
+
+    def __init__(self, input_dim, hidden_dims, param_dims=(1, 1), permutation=None, skip_connections=False,
+                 nonlinearity=nn.ReLU()):
+        super().__init__(input_dim, 0, hidden_dims, param_dims, permutation, skip_connections, nonlinearity)
+
+    def forward(self, x):
+        return self._shape(self.raw(x, None), x.shape[:-1])

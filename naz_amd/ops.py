@@ -1,0 +1,258 @@
+"""Torch-facing wrappers of the HIP kernels (the only compute path of naz_amd).
+
+Tensors must be fp32 on a HIP device (``torch.device("cuda")`` on PyTorch-ROCm);
+outputs are allocated here, kernels are launched on the current stream of the
+input's device.  Row strides are passed through, so contiguous-last-dim views work
+without copies.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB, CouplingDesc,
+                   check, lib)
+
+Tensor = torch.Tensor
+
+__all__ = ["rqs", "spline_elementwise", "linear_act", "affine_ar", "base_log_prob", "bounding_fwd", "bounding_inv",
+           "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
+           "coupling_sample", "LAYOUT_ARN", "LAYOUT_DENSE", "LD_PERDIM", "LD_ROWSUM", "LD_ROWSUM_ADD",
+           "LD_ROWSUM_SUB"]
+
+
+def _dev(*ts: Optional[Tensor]) -> torch.device:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(f"naz_amd kernels run on the GPU only; got a tensor on {t.device} "
+                               "(no CPU fallback exists)")
+        if t.dtype != torch.float32:
+            raise TypeError(f"naz_amd kernels compute in float32; got {t.dtype}")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError("naz_amd: tensors on different devices")
+    return dev
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _rows(t: Tensor) -> Tuple[Tensor, int]:
+    """2-D view with unit last-dim stride; returns (tensor, row stride)."""
+    if t.dim() != 2:
+        raise ValueError(f"expected a 2-D tensor, got shape {tuple(t.shape)}")
+    if t.stride(1) != 1:
+        t = t.contiguous()
+    return t, t.stride(0)
+
+
+def _p(t: Optional[Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+# ----------------------------------------------------------------------------- a1 + a2
+def rqs(x: Tensor, raw: Tensor, count_bins: int, layout: int = LAYOUT_DENSE, inverse: bool = False,
+        bound: float = 3.0, ld_mode: int = LD_PERDIM, ld_out: Optional[Tensor] = None,
+        out: Optional[Tensor] = None, broadcast_raw: bool = False) -> Tuple[Tensor, Tensor]:
+    """Conditional RQ spline over a conditioner output (naz_rqs_fwd / naz_rqs_inv).
+
+    ``out`` may be a strided 2-D view (unit last stride) to write into; ``broadcast_raw``
+    passes a single parameter row (row stride 0) shared by every batch row, which is how
+    the unconditional lower spline of a coupling layer runs."""
+    dev = _dev(x, raw, ld_out, out)
+    x, ldx = _rows(x)
+    B, Dt = x.shape
+    P = Dt * (3 * count_bins - 1)
+    if broadcast_raw:
+        raw = raw.reshape(1, -1).contiguous()
+        ldr = 0
+        if raw.shape[1] != P:
+            raise ValueError(f"broadcast raw must have {P} entries, got {raw.shape[1]}")
+    else:
+        raw, ldr = _rows(raw)
+        if raw.shape != (B, P):
+            raise ValueError(f"raw must be [B, Dt*(3K-1)] = {(B, P)}, got {tuple(raw.shape)}")
+    if out is None:
+        out = torch.empty_like(x)
+    elif out.shape != (B, Dt) or out.stride(1) != 1:
+        raise ValueError("out must be a [B, Dt] view with unit last stride")
+    if ld_out is None:
+        ld_out = torch.empty((B, Dt) if ld_mode == LD_PERDIM else (B,), device=dev, dtype=torch.float32)
+    fn = lib().naz_rqs_inv if inverse else lib().naz_rqs_fwd
+    check(fn(_p(x), ldx, _p(raw), ldr, _p(out), out.stride(0), _p(ld_out), ld_mode, B, Dt, count_bins, layout,
+             float(bound), _stream(dev)), "rqs")
+    return out, ld_out
+
+
+def spline_elementwise(x: Tensor, uw: Tensor, uh: Tensor, ud: Tensor, inverse: bool = False,
+                       bound: float = 3.0) -> Tuple[Tensor, Tensor]:
+    """Unconditional elementwise spline ([pyro] Spline); returns (y, per-dim ld)."""
+    dev = _dev(x, uw, uh, ud)
+    x, ldx = _rows(x)
+    B, Dt = x.shape
+    K = uw.shape[-1]
+    uw, uh, ud = uw.contiguous(), uh.contiguous(), ud.contiguous()
+    y = torch.empty_like(x)
+    ld = torch.empty((B, Dt), device=dev, dtype=torch.float32)
+    check(lib().naz_spline_elementwise(int(inverse), _p(x), ldx, _p(uw), _p(uh), _p(ud), _p(y), y.stride(0), _p(ld),
+                                       B, Dt, K, float(bound), _stream(dev)), "spline_elementwise")
+    return y, ld
+
+
+# ----------------------------------------------------------------------------- a6 / a7
+def linear_act(x: Optional[Tensor], weight: Tensor, bias: Optional[Tensor], act: str = "identity",
+               context: Optional[Tensor] = None, mask: Optional[Tensor] = None,
+               out: Optional[Tensor] = None) -> Tensor:
+    """act(cat([context, x]) @ (weight * mask)^T + bias) with the concat fused."""
+    dev = _dev(x, weight, bias, context, mask)
+    C = 0 if context is None else context.shape[-1]
+    Kx = 0 if x is None else x.shape[-1]
+    M = x.shape[0] if x is not None else context.shape[0]
+    ldc = 0
+    if context is not None:
+        if context.dim() == 1 or context.shape[0] == 1 and M != 1:
+            context = context.reshape(1, -1).contiguous()
+            ldc = 0  # broadcast one context row
+        else:
+            context, ldc = _rows(context)
+            if context.shape[0] != M:
+                raise ValueError("context rows must match x rows (or be a single row)")
+    ldx = 0
+    if x is not None:
+        x, ldx = _rows(x)
+    N = weight.shape[0]
+    if weight.shape[1] != C + Kx:
+        raise ValueError(f"weight must be [N, {C + Kx}], got {tuple(weight.shape)}")
+    weight = weight.contiguous()
+    if mask is not None:
+        mask = mask.to(torch.float32).contiguous()
+    if out is None:
+        out = torch.empty((M, N), device=dev, dtype=torch.float32)
+    check(lib().naz_linear_act(_p(context), ldc, C, _p(x), ldx, Kx, _p(weight), _p(mask), _p(bias), _p(out),
+                               out.stride(0), M, N, ACT[act], _stream(dev)), "linear_act")
+    return out
+
+
+# ----------------------------------------------------------------------------- a5
+def affine_ar(x: Tensor, raw: Tensor, inverse: bool, ld_mode: int = LD_PERDIM,
+              ld_out: Optional[Tensor] = None, out: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    dev = _dev(x, raw, ld_out, out)
+    x, ldx = _rows(x)
+    raw, ldr = _rows(raw)
+    B, D = x.shape
+    if raw.shape != (B, 2 * D):
+        raise ValueError(f"raw must be [B, 2D] = {(B, 2 * D)}, got {tuple(raw.shape)}")
+    if out is None:
+        out = torch.empty_like(x)
+    if ld_out is None:
+        ld_out = torch.empty((B, D) if ld_mode == LD_PERDIM else (B,), device=dev, dtype=torch.float32)
+    check(lib().naz_affine_ar(int(inverse), _p(x), ldx, _p(raw), ldr, _p(out), out.stride(0), _p(ld_out), ld_mode,
+                              B, D, _stream(dev)), "affine_ar")
+    return out, ld_out
+
+
+# ----------------------------------------------------------------------------- a8
+def base_log_prob(z: Tensor, out: Optional[Tensor] = None, accumulate: bool = False) -> Tensor:
+    dev = _dev(z, out)
+    z, ldz = _rows(z)
+    B, D = z.shape
+    if out is None:
+        out = torch.empty((B,), device=dev, dtype=torch.float32)
+        accumulate = False
+    check(lib().naz_base_log_prob(_p(z), ldz, _p(out), B, D, int(accumulate), _stream(dev)), "base_log_prob")
+    return out
+
+
+def bounding_fwd(x: Tensor, low: Tensor, high: Tensor) -> Tuple[Tensor, Tensor]:
+    dev = _dev(x, low, high)
+    x, ldx = _rows(x)
+    B, D = x.shape
+    y = torch.empty_like(x)
+    lj = torch.empty((B,), device=dev, dtype=torch.float32)
+    check(lib().naz_bounding_fwd(_p(x), ldx, _p(low.contiguous()), _p(high.contiguous()), _p(y), y.stride(0), _p(lj),
+                                 B, D, _stream(dev)), "bounding_fwd")
+    return y, lj
+
+
+def bounding_inv(y: Tensor, low: Tensor, high: Tensor) -> Tensor:
+    dev = _dev(y, low, high)
+    y, ldy = _rows(y)
+    B, D = y.shape
+    x = torch.empty_like(y)
+    check(lib().naz_bounding_inv(_p(y), ldy, _p(low.contiguous()), _p(high.contiguous()), _p(x), x.stride(0), B, D,
+                                 _stream(dev)), "bounding_inv")
+    return x
+
+
+# ----------------------------------------------------------------------------- a3 + a8 + a9 fused
+def coupling_desc(D: int, C: int, S: int, K: int, L: int, H: int, act: str = "tanh", has_lower: bool = True,
+                  bound: float = 3.0) -> CouplingDesc:
+    d = CouplingDesc()
+    d.D, d.C, d.S, d.K, d.L, d.H = D, C, S, K, L, H
+    d.act, d.has_lower, d.bound = ACT.get(act, -1), int(has_lower), float(bound)
+    return d
+
+
+def coupling_supported(d: CouplingDesc) -> bool:
+    return bool(lib().naz_coupling_supported(d))
+
+
+def coupling_param_count(d: CouplingDesc) -> int:
+    return int(lib().naz_coupling_param_count(d))
+
+
+def coupling_pack(d: CouplingDesc, flat: Tensor, packed: Optional[Tensor] = None) -> Tensor:
+    dev = _dev(flat)
+    n = coupling_param_count(d)
+    if flat.numel() != n or not flat.is_contiguous():
+        raise ValueError(f"flat params must be a contiguous [{n}] fp32 tensor")
+    nbytes = int(lib().naz_coupling_packed_bytes(d))
+    if packed is None or packed.numel() * 4 != nbytes:
+        packed = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
+    check(lib().naz_coupling_pack(d, _p(flat), _p(packed), _stream(dev)), "coupling_pack")
+    return packed
+
+
+def _ctx_arg(context: Optional[Tensor], B: int):
+    if context is None:
+        return None, 0
+    if context.dim() == 1 or (context.shape[0] == 1 and B != 1):
+        return context.reshape(1, -1).contiguous(), 0
+    context, ldc = _rows(context)
+    if context.shape[0] != B:
+        raise ValueError("condition rows must match x rows (or be a single row)")
+    return context, ldc
+
+
+def coupling_log_prob(d: CouplingDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,
+                      low: Optional[Tensor] = None, high: Optional[Tensor] = None,
+                      out: Optional[Tensor] = None) -> Tensor:
+    dev = _dev(packed, x, context, low, high, out)
+    x, ldx = _rows(x)
+    B = x.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    if out is None:
+        out = torch.empty((B,), device=dev, dtype=torch.float32)
+    check(lib().naz_coupling_log_prob(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out), B,
+                                      _stream(dev)), "coupling_log_prob")
+    return out
+
+
+def coupling_sample(d: CouplingDesc, packed: Tensor, z: Tensor, context: Optional[Tensor] = None,
+                    low: Optional[Tensor] = None, high: Optional[Tensor] = None,
+                    with_logdet: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
+    dev = _dev(packed, z, context, low, high)
+    z, ldz = _rows(z)
+    B = z.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    y = torch.empty_like(z)
+    ld = torch.empty((B,), device=dev, dtype=torch.float32) if with_logdet else None
+    check(lib().naz_coupling_sample(d, _p(packed), _p(z), ldz, _p(context), ldc, _p(low), _p(high), _p(y),
+                                    y.stride(0), _p(ld), B, _stream(dev)), "coupling_sample")
+    return y, ld

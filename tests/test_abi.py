@@ -1,0 +1,66 @@
+"""CPU: the C-ABI library loads and exports every symbol include/naz_hip.h declares
+(no compute calls: there is no GPU here); host-side argument errors surface as messages."""
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "naz_hip.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(naz_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("naz_rqs_fwd", "naz_rqs_inv", "naz_linear_act", "naz_affine_ar", "naz_coupling_log_prob",
+                 "naz_coupling_sample", "naz_coupling_pack", "naz_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from naz_amd import _lib
+    L = _lib.lib()
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(declared_functions()) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
+    assert L.naz_abi_version() == 1
+
+
+def test_host_side_errors_have_messages():
+    from naz_amd import _lib
+    L = _lib.lib()
+    rc = L.naz_rqs_fwd(None, 0, None, 0, None, 0, None, 0, 16, 0, 8, 0, 3.0, None)  # Dt = 0
+    assert rc != 0 and b"bad shape" in L.naz_last_error()
+    rc = L.naz_rqs_inv(None, 0, None, 0, None, 0, None, 0, 0, 4, 2000, 0, 3.0, None)  # K*1e-3 > 1
+    assert rc != 0 and b"Minimal bin width" in L.naz_last_error()
+    d = _lib.CouplingDesc()
+    d.D, d.C, d.S, d.K, d.L, d.H, d.act, d.has_lower, d.bound = 7, 0, 3, 8, 2, 64, 1, 1, 3.0
+    assert L.naz_coupling_supported(d) == 0
+    rc = L.naz_coupling_pack(d, None, None, None)
+    assert rc != 0 and b"no fused instantiation" in L.naz_last_error()
+
+
+def test_fused_descriptor_matches_flow_parameters():
+    from naz_amd import ops
+    from naz_amd.flows import NormalizingFlow
+    f = NormalizingFlow("nsc", None, 16, 32, [128, 128], 8, 8, 8)
+    assert f.fused
+    n = sum(p.numel() for p in f.parameters())
+    assert ops.coupling_param_count(f._plan.desc) == n == 365440
+
+
+def test_no_cpu_fallback():
+    import torch
+    from naz_amd import ops
+    x = torch.zeros(4, 2)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        ops.rqs(x, torch.zeros(4, 2 * 23), 8)
+    from naz_amd.flows import NormalizingFlow
+    f = NormalizingFlow("nsc", None, 4, 3, [64, 64], 2, 8, 2)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        f.log_prob(torch.zeros(3, 4), condition=torch.zeros(3, 3))

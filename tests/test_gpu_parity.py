@@ -1,0 +1,274 @@
+"""GPU: the HIP kernels against the oracle (tests/golden fixtures + live oracle runs on the host).
+
+Tolerance: tests/parity.py (1e-5 relative vs the float64 oracle wherever the reference's own
+fp32 path achieves it; <= 4x the reference fp32 deviation on ill-conditioned rows).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import naz_oracle as O
+from tests.conftest import load_golden, spec_state
+from tests.parity import assert_parity, rel_err
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _cuda(a):
+    return torch.as_tensor(np.asarray(a), dtype=torch.float32, device=DEV)
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from naz_amd import _lib
+    _lib.lib()
+
+
+def _product_flow(fx):
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    spec, state = spec_state(fx)
+    ft = spec["flow_type"]
+    if ft == "nsc":
+        f = NormalizingFlow("nsc", None, spec["D"], spec["C"], spec["hidden"], spec["L"], spec["K"], spec["split"])
+    elif ft == "nsa":
+        f = NormalizingFlow("nsa", None, spec["D"], spec["C"], spec["hidden"], spec["L"], spec["K"])
+    else:
+        f = NormalizingFlow("maf", None, spec["D"], spec["C"], spec["hidden"], spec["L"])
+    fio.load_state(f, state)
+    return f, spec, state
+
+
+# ------------------------------------------------------------------ a1 + a2 standalone spline
+@pytest.mark.parametrize("name", ["rqs_dense_k8.npz", "rqs_arn_k5.npz", "rqs_dense_k16.npz"])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_rqs_kernel_vs_golden(name, inverse):
+    from naz_amd import ops
+    fx = load_golden(name)
+    K, Dt, layout = int(fx["K"]), int(fx["Dt"]), int(fx["layout"])
+    x, raw = _cuda(fx["x"]), _cuda(fx["raw"])
+    y, ld = ops.rqs(x, raw, K, layout, inverse=inverse)
+    ky, kl = ("y_inv", "ld_inv") if inverse else ("y_fwd", "ld_fwd")
+    y32, ld32 = O.rqs_from_raw(torch.as_tensor(fx["x"]), torch.as_tensor(fx["raw"]), Dt, K, layout, inverse)
+    assert_parity(_np(y), fx[ky], _np(y32), what=f"{name} y")
+    assert_parity(_np(ld), fx[kl], _np(ld32), what=f"{name} ld")
+    # tails are exactly the identity with exactly zero log-det
+    tail = np.abs(fx["x"]) > 3.0
+    assert np.array_equal(_np(y)[tail], fx["x"][tail]) and np.all(_np(ld)[tail] == 0)
+
+
+def test_rqs_ld_modes_and_strides():
+    from naz_amd import ops
+    fx = load_golden("rqs_dense_k8.npz")
+    K, Dt = int(fx["K"]), int(fx["Dt"])
+    x, raw = _cuda(fx["x"]), _cuda(fx["raw"])
+    _, per = ops.rqs(x, raw, K, inverse=True, ld_mode=ops.LD_PERDIM)
+    _, rs = ops.rqs(x, raw, K, inverse=True, ld_mode=ops.LD_ROWSUM)
+    acc = torch.full((x.shape[0],), 2.0, device=DEV)
+    ops.rqs(x, raw, K, inverse=True, ld_mode=ops.LD_ROWSUM_ADD, ld_out=acc)
+    sub = torch.full((x.shape[0],), 2.0, device=DEV)
+    ops.rqs(x, raw, K, inverse=True, ld_mode=ops.LD_ROWSUM_SUB, ld_out=sub)
+    s = per.sum(-1)
+    torch.testing.assert_close(rs, s, rtol=1e-6, atol=1e-5)
+    torch.testing.assert_close(acc, s + 2.0, rtol=1e-6, atol=1e-5)
+    torch.testing.assert_close(sub, 2.0 - s, rtol=1e-6, atol=1e-5)
+    # strided views: x as a column slice of a wider tensor, output into a slice
+    wide = torch.zeros(x.shape[0], Dt + 3, device=DEV)
+    wide[:, 1:1 + Dt] = x
+    out = torch.zeros(x.shape[0], Dt + 5, device=DEV)
+    ops.rqs(wide[:, 1:1 + Dt], raw, K, inverse=True, out=out[:, 2:2 + Dt])
+    y_ref, _ = ops.rqs(x, raw, K, inverse=True)
+    torch.testing.assert_close(out[:, 2:2 + Dt], y_ref, rtol=0, atol=0)
+
+
+def test_rqs_edge_batches():
+    from naz_amd import ops
+    K, Dt = 8, 5
+    for B in (0, 1, 33, 257):
+        raw = torch.randn(B, Dt * (3 * K - 1), device=DEV) * 2
+        x = torch.randn(B, Dt, device=DEV) * 2
+        y, ld = ops.rqs(x, raw, K, inverse=False)
+        assert y.shape == (B, Dt)
+        if B:
+            y32, ld32 = O.rqs_from_raw(x.cpu(), raw.cpu(), Dt, K, O.LAYOUT_DENSE, False)
+            y64, ld64 = O.rqs_from_raw(x.cpu().double(), raw.cpu().double(), Dt, K, O.LAYOUT_DENSE, False)
+            assert_parity(_np(y), y64.numpy(), y32.numpy(), what=f"B={B}")
+
+
+# ------------------------------------------------------------------ a6/a7 conditioner layer
+@pytest.mark.parametrize("act", ["identity", "tanh", "relu", "softplus", "sigmoid"])
+def test_linear_act_vs_fp64(act):
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(3)
+    M, C, Kx, N = 300, 7, 13, 70
+    ctx = torch.randn(M, C, generator=g)
+    x = torch.randn(M, Kx, generator=g)
+    W = torch.randn(N, C + Kx, generator=g) * 0.3
+    b = torch.randn(N, generator=g)
+    mask = (torch.rand(N, C + Kx, generator=g) > 0.4).float()
+    y = ops.linear_act(_cuda(x), _cuda(W), _cuda(b), act, context=_cuda(ctx), mask=_cuda(mask))
+    pre = torch.cat([ctx, x], 1).double() @ (W * mask).double().T + b.double()
+    ref = O.ACTIVATIONS[act](pre)
+    np.testing.assert_allclose(_np(y), ref.numpy(), rtol=2e-6, atol=2e-6)
+    # broadcast single context row
+    y1 = ops.linear_act(_cuda(x), _cuda(W), _cuda(b), act, context=_cuda(ctx[0]), mask=_cuda(mask))
+    pre1 = torch.cat([ctx[:1].expand(M, C), x], 1).double() @ (W * mask).double().T + b.double()
+    np.testing.assert_allclose(_np(y1), O.ACTIVATIONS[act](pre1).numpy(), rtol=2e-6, atol=2e-6)
+
+
+def test_affine_kernel_vs_oracle():
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(4)
+    B, D = 500, 5
+    x = torch.randn(B, D, generator=g)
+    raw = torch.randn(B, 2 * D, generator=g) * 4  # exercises both clamps
+    for inv in (False, True):
+        y, ld = ops.affine_ar(_cuda(x), _cuda(raw), inv)
+        mean, ls = raw[:, :D].double(), raw[:, D:].double().clamp(-5, 3)
+        ref = (x.double() - mean) * torch.exp(-ls) if inv else torch.exp(ls) * x.double() + mean
+        np.testing.assert_allclose(_np(y), ref.numpy(), rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(_np(ld), ls.numpy(), rtol=0, atol=0)
+
+
+# ------------------------------------------------------------------ flows (a3-a9)
+FLOWS = ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz", "nsa_d4c2.npz", "maf_d3c2.npz",
+         "maf_twomoons.npz"]
+
+
+@pytest.mark.parametrize("name", FLOWS)
+@pytest.mark.parametrize("fused", [True, False])
+def test_flow_log_prob_vs_golden(name, fused):
+    fx = load_golden(name)
+    f, spec, _ = _product_flow(fx)
+    if spec["flow_type"] == "nsc":
+        assert f.fused, "the nsc fixture shapes must hit a fused instantiation"
+        f.set_fused(fused)
+    elif fused:
+        pytest.skip("no fused kernel for this flow type yet")
+    x = _cuda(fx["x"])
+    c = _cuda(fx["ctx"]) if "ctx" in fx else None
+    lp = f.log_prob(x, condition=c)
+    st = assert_parity(_np(lp), fx["lp64"], fx["lp32"], what=f"{name} fused={fused}")
+    print(name, fused, st)
+
+
+@pytest.mark.parametrize("name", ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz"])
+@pytest.mark.parametrize("fused", [True, False])
+def test_flow_sample_transform_vs_golden(name, fused):
+    from naz_amd import ops
+    fx = load_golden(name)
+    f, spec, _ = _product_flow(fx)
+    f.set_fused(fused)
+    z = _cuda(fx["z"])
+    c = _cuda(fx["ctx"]) if "ctx" in fx else None
+    pdf = f._pdf(c)
+    if fused:
+        y, ld = f._plan.sample(z, c, with_logdet=True)
+    else:
+        ld = torch.zeros(z.shape[0], device=DEV)
+        y = z
+        for t in pdf.transforms:
+            y = t._call_acc(y, ld)
+    f32 = O.build_flow(spec, spec_state(fx)[1], torch.float32)
+    y32, ld32 = f32.forward_with_logdet(torch.as_tensor(fx["z"]), None if c is None else torch.as_tensor(fx["ctx"]))
+    assert_parity(_np(y), fx["y_sample"], y32.numpy(), what=f"{name} sample y")
+    assert_parity(_np(ld), fx["ld_sample"], ld32.numpy(), what=f"{name} sample ld")
+
+
+def test_config3_full_flow_vs_live_oracle():
+    """The metric configuration (D16|C32, K8, H[128,128], L=8) at 8192 rows vs the oracle."""
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    spec = dict(flow_type="nsc", D=16, C=32, hidden=[128, 128], L=8, K=8, split=8)
+    state = {k: v.float() for k, v in O.random_state(spec, seed=1234).items()}
+    f = NormalizingFlow("nsc", None, 16, 32, [128, 128], 8, 8, 8)
+    fio.load_state(f, {k: v.numpy() for k, v in state.items()})
+    assert f.fused
+    n = 8192
+    x = torch.as_tensor(O.gaussian_mixture(n, 16, seed=0))
+    c = torch.as_tensor(O.context_normal(n, 32, seed=1))
+    lp = f.log_prob(x.to(DEV), condition=c.to(DEV))
+    lp64 = O.build_flow(spec, state, torch.float64).log_prob(x.double(), c.double()).numpy()
+    lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, c).numpy()
+    st = assert_parity(_np(lp), lp64, lp32, what="config3 L8")
+    print("config3", st)
+
+
+def test_full_size_density_round_trip():
+    """Size-independent property at BASELINE's full batch (2^20): log_prob(T(z)) = base(z) - ld(z)."""
+    from naz_amd import ops
+    from naz_amd.flows import NormalizingFlow
+    torch.manual_seed(0)
+    f = NormalizingFlow("nsc", None, 16, 32, [128, 128], 8, 8, 8)
+    with torch.no_grad():
+        for t in f.flow_dist.transforms:
+            t.nn.layers[-1].weight.mul_(3.0)
+            t.nn.layers[-1].bias.mul_(3.0)
+    B = 1 << 20
+    z = torch.randn(B, 16, device=DEV)
+    c = torch.randn(B, 32, device=DEV)
+    y, ld = f._plan.sample(z, c, with_logdet=True)
+    lp = f.log_prob(y, condition=c)
+    base = ops.base_log_prob(z)
+    r = rel_err(_np(lp), _np(base - ld))
+    assert np.all(np.isfinite(_np(lp)))
+    assert np.median(r) < 1e-6 and np.quantile(r, 0.999) < 1e-4, (np.median(r), np.quantile(r, 0.999), r.max())
+
+
+def test_bounds_and_broadcast_context():
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    spec = dict(flow_type="nsc", D=6, C=2, hidden=[32, 32], L=3, K=4, split=2)
+    state = {k: v.float() for k, v in O.random_state(spec, seed=5).items()}
+    low = torch.tensor([-4.0, -3, -2, -5, -1, -6])
+    high = torch.tensor([4.0, 3, 5, 5, 2, 6])
+    bounds = {"low": low, "high": high}
+    f = NormalizingFlow("nsc", bounds, 6, 2, [32, 32], 3, 4, 2)
+    fio.load_state(f, {k: v.numpy() for k, v in state.items()})
+    g = torch.Generator().manual_seed(8)
+    x = low + (high - low) * (0.02 + 0.96 * torch.rand(500, 6, generator=g))
+    c1 = torch.randn(2, generator=g)
+    ob = O.build_flow(dict(spec, bounds={"low": low, "high": high}), state, torch.float64)
+    ob32 = O.build_flow(dict(spec, bounds={"low": low, "high": high}), state, torch.float32)
+    ref64 = ob.log_prob(x.double(), c1.double()).numpy()
+    ref32 = ob32.log_prob(x, c1).numpy()
+    for fused in (True, False):
+        f.set_fused(fused)
+        lp = f.log_prob(x.to(DEV), condition=c1.to(DEV))
+        assert_parity(_np(lp), ref64, ref32, what=f"bounded fused={fused}")
+    # bounded_log_prob: -inf outside the box
+    xo = x.clone()
+    xo[:10, 0] = 10.0
+    blp = _np(f.bounded_log_prob(xo.to(DEV), condition=c1.to(DEV)))
+    assert np.all(np.isneginf(blp[:10])) and np.all(np.isfinite(blp[10:]))
+    # samples respect the box
+    s = f.sample([1000], condition=c1.to(DEV))
+    assert s.shape == (1000, 6) and bool(((s > low.to(DEV)) & (s < high.to(DEV))).all())
+
+
+@pytest.mark.parametrize("B", [1, 127, 129, 1000])
+def test_fused_ragged_batches(B):
+    fx = load_golden("nsc_d16c32_l2.npz")
+    f, spec, state = _product_flow(fx)
+    x = _cuda(fx["x"][:B] if B <= 256 else np.resize(fx["x"], (B, 16)))
+    c = _cuda(fx["ctx"][:B] if B <= 256 else np.resize(fx["ctx"], (B, 32)))
+    lp_f = f.log_prob(x, condition=c)
+    f.set_fused(False)
+    lp_l = f.log_prob(x, condition=c)
+    np.testing.assert_allclose(_np(lp_f), _np(lp_l), rtol=2e-5, atol=2e-5)
+
+
+def test_native_library_is_the_path():
+    """The compute path is the in-tree HIP library (naz_amd/lib/libnazhip.so)."""
+    import os
+    from naz_amd import _lib
+    maps = open(f"/proc/{os.getpid()}/maps").read()
+    assert str(_lib.LIB_PATH) in maps

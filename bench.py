@@ -30,7 +30,9 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "samples/sec through log_prob+log|detJ|, 16-dim RQ-spline flow, batch 2^20"
 D, C, S, K, L, H = 16, 32, 8, 8, 8, 128
-FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense FP32 (matrix == vector)
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 (matrix == vector)
+BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16 MFMA
+X6_PRODUCTS = 6            # bf16x6: every fp32 product costs six bf16 MFMA products
 HBM_PEAK_GBS = 8000.0
 
 
@@ -124,6 +126,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="rows per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mfma", choices=["bf16x6", "f32"], default="bf16x6",
+                    help="bf16x6: FP32 GEMMs as six exact-split bf16 products (default); f32: exact FP32 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,6 +149,7 @@ def main():
     c = torch.as_tensor(c_host, device=dev)
     out = torch.empty(B, device=dev)
     plan = flow._plan
+    plan.set_mfma(args.mfma)
     packed = plan.packed()
 
     from naz_amd import ops
@@ -184,6 +189,8 @@ def main():
         total_rows = B * world * args.steps
         flop_launch = flops_per_row() * B
         achieved = flop_launch / avg_kern_s / 1e12
+        # ceiling for algorithmic FP32 FLOPs on the pipe the kernel actually uses
+        peak = BF16_PEAK_TFLOPS / X6_PRODUCTS if args.mfma == "bf16x6" else FP32_PEAK_TFLOPS
         traffic, traffic_src = load_traffic()
         rec = {
             "metric": METRIC, "value": total_rows / elapsed, "unit": "samples/s", "n_gpus": world,

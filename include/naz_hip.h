@@ -39,6 +39,9 @@ extern "C" {
 #define NAZ_ACT_SOFTPLUS 3
 #define NAZ_ACT_SIGMOID 4
 
+#define NAZ_MFMA_BF16X6 0 /* default: FP32 GEMMs as 6 exact-split bf16 MFMA products (fp32-grade error) */
+#define NAZ_MFMA_F32 1    /* exact FP32 MFMA (v_mfma_f32_32x32x2_f32)                                  */
+
 /* ---- library ------------------------------------------------------------ */
 const char* naz_last_error(void);
 int naz_abi_version(void); /* bumps on any signature change */
@@ -111,7 +114,8 @@ typedef struct naz_coupling_desc {
   int act;                /* NAZ_ACT_* */
   int has_lower;          /* 1: lower (unconditional) spline on x1; 0: pyro identity=True */
   float bound;            /* spline box half-width (pyro default 3.0) */
-  int reserved[7];
+  int mfma_mode;          /* NAZ_MFMA_BF16X6 (default, 0) or NAZ_MFMA_F32; the packed layout depends on it */
+  int reserved[6];
 } naz_coupling_desc;
 
 int naz_coupling_supported(const naz_coupling_desc* d); /* 1 if a fused instantiation exists */

@@ -14,13 +14,15 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / "libnazhip.so"
 LAYOUT_DENSE, LAYOUT_ARN = 0, 1
 LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB = 0, 1, 2, 3
 ACT = {"identity": 0, "tanh": 1, "relu": 2, "softplus": 3, "sigmoid": 4}
+MFMA_BF16X6, MFMA_F32 = 0, 1
 
 _f, _i, _i64, _vp = C.POINTER(C.c_float), C.c_int, C.c_int64, C.c_void_p
 
 
 class CouplingDesc(C.Structure):
     _fields_ = [("D", C.c_int), ("C", C.c_int), ("S", C.c_int), ("K", C.c_int), ("L", C.c_int), ("H", C.c_int),
-                ("act", C.c_int), ("has_lower", C.c_int), ("bound", C.c_float), ("reserved", C.c_int * 7)]
+                ("act", C.c_int), ("has_lower", C.c_int), ("bound", C.c_float), ("mfma_mode", C.c_int),
+                ("reserved", C.c_int * 6)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/naz_hip.h

@@ -247,7 +247,7 @@ NAZ_DEV void tanh_all(floatx16 (&acc)[NB]) {
 #pragma unroll
   for (int o = 0; o < NB; ++o)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[o][r] = tanh_f(acc[o][r]);
+    for (int r = 0; r < 16; ++r) acc[o][r] = tanh_f<true>(acc[o][r]);
 }
 
 template <int I, int N, class F>
@@ -342,7 +342,7 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
         SplineTables<CF::K> t;
         load_tables<CF>(lds + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
         float ld;
-        zl[q] = rqs_apply<CF::K, true>(t, zl[q], bound, ld);
+        zl[q] = rqs_apply<CF::K, true, true>(t, zl[q], bound, ld);
         ldsum -= ld;  // forward ld = -(inverse ld)
       }
       x1[q] = zl[q];
@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
         SplineTables<CF::K> t;
         load_tables<CF>(lds + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
         float ld;
-        zl[q] = rqs_apply<CF::K, false>(t, zl[q], bound, ld);
+        zl[q] = rqs_apply<CF::K, false, true>(t, zl[q], bound, ld);
         ldsum += ld;
       }
     }
@@ -413,9 +413,9 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
         ud[k] = acc3[sd >> 4][sd & 15];
       }
       SplineTables<CF::K> t;
-      build_tables<CF::K>(uw, uh, ud, bound, t);
+      build_tables<CF::K, true>(uw, uh, ud, bound, t);
       float ld;
-      zu[q] = rqs_apply<CF::K, DIR_INV>(t, zu[q], bound, ld);
+      zu[q] = rqs_apply<CF::K, DIR_INV, true>(t, zu[q], bound, ld);
       ldsum += DIR_INV ? -ld : ld;
     }
     __syncthreads();  // next layer's stage A has landed
@@ -458,35 +458,513 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
   }
 }
 
+// ===========================================================================
+// bf16x6 variant: FP32 GEMMs emulated on the bf16 matrix pipe.
+//
+// Every fp32 operand v is split EXACTLY into three bf16 pieces by truncation
+// (hi = v & 0xffff0000, mid = (v - hi) & 0xffff0000, lo = v - hi - mid, which has at most
+// 8 significant bits), and each product W·X is formed from the six largest cross terms
+//   Wh·Xh + Wh·Xm + Wm·Xh + Wm·Xm + Wh·Xl + Wl·Xh        (dropped terms ~2^-24 relative)
+// with v_mfma_f32_32x32x16_bf16 (exact bf16 products, fp32 accumulate).  Six 32-cycle MFMAs
+// per K=16 step replace eight 64-cycle v_mfma_f32_32x32x2_f32: 2.67x the FP32 matrix rate.
+// On the oracle (config 3, 4096 rows) the log_prob error statistics vs fp64 are those of
+// exact FP32 (median 2.70e-7 vs 2.79e-7, q99 4.08e-6 vs 4.03e-6, max 4.46e-5 vs 4.48e-5);
+// dropping any of the six products is 3-5x worse.
+//
+// Operand mapping (v_mfma_f32_32x32x16_bf16): A[i = l&31][k = 8(l>>5) + j], B[k = 8(l>>5) + j]
+// [col = l&31], j = 0..7.  The previous GEMM's accumulator registers 8s..8s+7 of block b ARE
+// the B fragment of k-step 2b+s, element j carrying feature hid16_feature(2b+s, j, h); the
+// packer permutes W's columns to match.  GEMM1's B fragments are built from the context
+// half-row and the lane-half's x1 dims.
+// ===========================================================================
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+NAZ_DEV floatx16 mfma_bf16(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__host__ __device__ constexpr int hid16_feature(int t, int j, int h) {
+  return 32 * (t >> 1) + 16 * (t & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+
+// exact 3-way truncation split of one fp32 value: bit patterns whose upper halves are the bf16s
+NAZ_DEV void split3_bits(float v, unsigned& hb, unsigned& mb, unsigned& lb) {
+  hb = __float_as_uint(v);
+  const float r1 = v - __uint_as_float(hb & 0xffff0000u);
+  mb = __float_as_uint(r1);
+  const float r2 = r1 - __uint_as_float(mb & 0xffff0000u);
+  lb = __float_as_uint(r2);
+}
+
+__host__ __device__ inline unsigned bf16_hi_bits(float v, int piece) {
+  // host+device reference of the same split (used by the packer)
+  unsigned b;
+  float r = v;
+  for (int p = 0;; ++p) {
+    __builtin_memcpy(&b, &r, 4);
+    const unsigned t = b & 0xffff0000u;
+    if (p == piece) return t >> 16;
+    float tf;
+    __builtin_memcpy(&tf, &t, 4);
+    r = r - tf;
+  }
+}
+
+struct Frag3 {
+  bf16x8 h, m, l;
+};
+
+// 8 fp32 values -> three bf16x8 fragments (element j = v[j])
+NAZ_DEV Frag3 split8(const float (&v)[8]) {
+  u32x4 H, M, L;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split3_bits(v[2 * q], h0, m0, l0);
+    split3_bits(v[2 * q + 1], h1, m1, l1);
+    H[q] = __builtin_amdgcn_perm(h1, h0, 0x07060302u);
+    M[q] = __builtin_amdgcn_perm(m1, m0, 0x07060302u);
+    L[q] = __builtin_amdgcn_perm(l1, l0, 0x07060302u);
+  }
+  return Frag3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, M), __builtin_bit_cast(bf16x8, L)};
+}
+
+NAZ_DEV floatx16 mfma6(const Frag3& a, const Frag3& b, floatx16 acc) {
+  acc = mfma_bf16(a.l, b.h, acc);  // small terms first
+  acc = mfma_bf16(a.h, b.l, acc);
+  acc = mfma_bf16(a.m, b.m, acc);
+  acc = mfma_bf16(a.m, b.h, acc);
+  acc = mfma_bf16(a.h, b.m, acc);
+  acc = mfma_bf16(a.h, b.h, acc);
+  return acc;
+}
+
+constexpr int kX6StageFloats = 18432;  // 72 KB of operand chunks per stage (+ biases)
+constexpr int kChunk = 256;            // one (block, k-step, piece) A fragment set: 64 lanes x 16 B
+
+template <int D_, int C_, int S_, int K_, int H_, bool LOWER_>
+struct CfgX6 {
+  static constexpr int D = D_, C = C_, S = S_, K = K_, H = H_;
+  static constexpr bool LOWER = LOWER_;
+  static constexpr int Dt = D - S, P = 3 * K - 1, DH = Dt / 2, SH = S / 2;
+  static constexpr int HB = H / 32;
+  static constexpr int CT = (C + 15) / 16;          // GEMM1 k-steps over the context
+  static constexpr int XT = (SH + 7) / 8;           // GEMM1 k-steps over the lane-half's x1
+  static constexpr int KS0 = CT + XT;
+  static constexpr int KS1 = 2 * HB;                // GEMM2/3 k-steps (16 features each)
+  static constexpr int NO = (DH * P + 15) / 16;     // GEMM3 output blocks
+  static constexpr int TBL = 3 * (K + 1);
+  static constexpr int OT = 3 * kChunk;             // floats per (block, k-step)
+  static constexpr int pick_kb(int nb) {            // largest k-steps-per-stage dividing KS1
+    int best = 1;
+    for (int kb = 1; kb <= KS1; ++kb)
+      if (KS1 % kb == 0 && nb * kb * OT <= kX6StageFloats) best = kb;
+    return best;
+  }
+  static constexpr int KB2 = pick_kb(HB), NB2 = KS1 / KB2;
+  static constexpr int KB3 = pick_kb(NO), NB3 = KS1 / KB3;
+  static constexpr int pad(int n) { return (n + 255) / 256 * 256; }
+  // stage A: [HB][KS0][3][256] | bias [HB][2][16] | tables [S][TBL]
+  static constexpr int A_BIAS = HB * KS0 * OT;
+  static constexpr int A_TBL = A_BIAS + HB * 32;
+  static constexpr int A_SIZE = pad(A_TBL + S * TBL);
+  // stages B_q: [HB][KB2][3][256] | bias [HB][2][16]
+  static constexpr int B_OFF = A_SIZE;
+  static constexpr int B_BIAS = HB * KB2 * OT;
+  static constexpr int B_SIZE = pad(B_BIAS + HB * 32);
+  // stages C_q: [NO][KB3][3][256] | bias [NO][2][16]
+  static constexpr int C_OFF = B_OFF + NB2 * B_SIZE;
+  static constexpr int C_BIAS = NO * KB3 * OT;
+  static constexpr int C_SIZE = pad(C_BIAS + NO * 32);
+  static constexpr int LAYER = C_OFF + NB3 * C_SIZE;
+  static constexpr int MAXSTAGE = A_SIZE > B_SIZE ? (A_SIZE > C_SIZE ? A_SIZE : C_SIZE)
+                                                  : (B_SIZE > C_SIZE ? B_SIZE : C_SIZE);
+  // natural flat layout (same as the FP32 variant)
+  static constexpr int N_W0 = H * (C + S), N_B0 = H, N_W1 = H * H, N_B1 = H, N_W2 = Dt * P * H, N_B2 = Dt * P;
+  static constexpr int N_LOW = LOWER ? S * (3 * K - 1) : 0;
+  static constexpr int FLAT = N_W0 + N_B0 + N_W1 + N_B1 + N_W2 + N_B2 + N_LOW;
+  static_assert(Dt % 2 == 0 && S % 2 == 0 && H % 32 == 0 && S > 0 && Dt > 0, "unsupported coupling shape");
+  static_assert(MAXSTAGE * 4 <= 76 * 1024, "stage exceeds the per-workgroup LDS budget (2 WGs / CU)");
+};
+
+// GEMM1 input column (in cat([ctx, x1]) order) for k-step t, element j, lane-half h; -1 = zero pad
+template <class CF>
+__host__ __device__ constexpr int x6_in_col(int t, int j, int h) {
+  if (t < CF::CT) {
+    const int c = 16 * t + 8 * h + j;
+    return c < CF::C ? c : -1;
+  }
+  const int q = 8 * (t - CF::CT) + j;
+  return q < CF::SH ? CF::C + h * CF::SH + q : -1;
+}
+
+// DenseNN output column carried by GEMM3 accumulator (block o, register r) on lane-half h; -1 = pad
+template <class CF>
+__host__ __device__ constexpr int x6_out_row(int o, int r, int h) {
+  const int slot = 16 * o + r, qd = slot / CF::P, p = slot - qd * CF::P;
+  if (qd >= CF::DH) return -1;
+  const int dim = h * CF::DH + qd;
+  if (p < CF::K) return dim * CF::K + p;
+  if (p < 2 * CF::K) return CF::Dt * CF::K + dim * CF::K + (p - CF::K);
+  return 2 * CF::Dt * CF::K + dim * (CF::K - 1) + (p - 2 * CF::K);
+}
+
+template <class CF>
+__global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* __restrict__ packed, int L,
+                                        float bound) {
+  const int64_t n = (int64_t)L * CF::LAYER;
+  unsigned* pu = reinterpret_cast<unsigned*>(packed);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(e / CF::LAYER);
+    const int off = (int)(e - (int64_t)l * CF::LAYER);
+    const float* W0 = flat + (int64_t)l * CF::FLAT;
+    const float* b0 = W0 + CF::N_W0;
+    const float* W1 = b0 + CF::N_B0;
+    const float* b1 = W1 + CF::N_W1;
+    const float* W2 = b1 + CF::N_B1;
+    const float* b2 = W2 + CF::N_W2;
+    const float* low = b2 + CF::N_B2;
+    // operand chunk entry: (o, t, piece, lane, pair) -> two bf16 of W[row][col(j)], W[row][col(j+1)]
+    auto chunk_word = [&](int q, int nt, int t0, const float* W, int ldw, bool gemm1) -> unsigned {
+      const int o = q / (nt * CF::OT), r1 = q - o * nt * CF::OT;
+      const int tl = r1 / CF::OT, r2 = r1 - tl * CF::OT;
+      const int piece = r2 / kChunk, u = r2 - piece * kChunk;
+      const int lane = u >> 2, pair = u & 3, i = lane & 31, kh = lane >> 5;
+      const int t = t0 + tl;
+      unsigned out = 0;
+      for (int e2 = 0; e2 < 2; ++e2) {
+        const int j = 2 * pair + e2;
+        int col, row;
+        if (gemm1) {
+          col = x6_in_col<CF>(t, j, kh);
+          row = 32 * o + i;
+        } else {
+          col = hid16_feature(t, j, kh);
+          row = 32 * o + i;
+        }
+        float v = 0.f;
+        if (W == W2) {  // output rows permuted into lane-half spline slots
+          const int hh = (i >> 2) & 1, rr = (i & 3) + 4 * (i >> 3);
+          const int orow = x6_out_row<CF>(o, rr, hh);
+          v = orow >= 0 ? W[orow * ldw + col] : 0.f;
+        } else if (col >= 0) {
+          v = W[row * ldw + col];
+        }
+        out |= bf16_hi_bits(v, piece) << (16 * e2);
+      }
+      return out;
+    };
+    unsigned word = 0;
+    float fv = 0.f;
+    bool is_word = false;
+    if (off < CF::A_SIZE) {
+      if (off < CF::A_BIAS) {
+        word = chunk_word(off, CF::KS0, 0, W0, CF::C + CF::S, true);
+        is_word = true;
+      } else if (off < CF::A_TBL) {
+        const int q = off - CF::A_BIAS, o = q / 32, h = (q >> 4) & 1, r = q & 15;
+        fv = b0[32 * o + acc_row(r, h)];
+      } else if (CF::LOWER && off < CF::A_TBL + CF::S * CF::TBL) {
+        const int q = off - CF::A_TBL, g = q / CF::TBL, w = q - g * CF::TBL;
+        float uw[CF::K], uh[CF::K], ud[CF::K - 1];
+        for (int k = 0; k < CF::K; ++k) {
+          uw[k] = low[g * CF::K + k];
+          uh[k] = low[CF::S * CF::K + g * CF::K + k];
+        }
+        for (int k = 0; k < CF::K - 1; ++k) ud[k] = low[2 * CF::S * CF::K + g * (CF::K - 1) + k];
+        SplineTables<CF::K> tb;
+        build_tables<CF::K>(uw, uh, ud, bound, tb);
+        const int which = w / (CF::K + 1), k = w - which * (CF::K + 1);
+        fv = which == 0 ? tb.cw[k] : (which == 1 ? tb.ch[k] : tb.dv[k]);
+      }
+    } else if (off < CF::C_OFF) {
+      const int sq = (off - CF::B_OFF) / CF::B_SIZE, q = off - CF::B_OFF - sq * CF::B_SIZE;
+      if (q < CF::B_BIAS) {
+        word = chunk_word(q, CF::KB2, sq * CF::KB2, W1, CF::H, false);
+        is_word = true;
+      } else if (q < CF::B_BIAS + CF::HB * 32) {
+        const int qq = q - CF::B_BIAS, o = qq / 32, h = (qq >> 4) & 1, r = qq & 15;
+        fv = b1[32 * o + acc_row(r, h)];
+      }
+    } else {
+      const int sq = (off - CF::C_OFF) / CF::C_SIZE, q = off - CF::C_OFF - sq * CF::C_SIZE;
+      if (q < CF::C_BIAS) {
+        word = chunk_word(q, CF::KB3, sq * CF::KB3, W2, CF::H, false);
+        is_word = true;
+      } else if (q < CF::C_BIAS + CF::NO * 32) {
+        const int qq = q - CF::C_BIAS, o = qq / 32, h = (qq >> 4) & 1, r = qq & 15;
+        const int orow = x6_out_row<CF>(o, r, h);
+        fv = orow >= 0 ? b2[orow] : 0.f;
+      }
+    }
+    if (is_word) pu[e] = word;
+    else packed[e] = fv;
+  }
+}
+
+template <int NB, int KB>
+NAZ_DEV void gemm_x6_stage(floatx16 (&acc)[NB], const float* __restrict__ stage, int lane, const Frag3 (&bf)[KB]) {
+  const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
+#pragma unroll
+  for (int t = 0; t < KB; ++t) {
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const int base = ((o * KB + t) * 3) * 64 + lane;
+      Frag3 a{__builtin_bit_cast(bf16x8, c4[base]), __builtin_bit_cast(bf16x8, c4[base + 64]),
+              __builtin_bit_cast(bf16x8, c4[base + 128])};
+      acc[o] = mfma6(a, bf[t], acc[o]);
+    }
+  }
+}
+
+// B fragments of k-steps [T0, T0+KB) from an accumulator array (already activated)
+template <int T0, int KB, int NB>
+NAZ_DEV void frags_from_acc(const floatx16 (&x)[NB], Frag3 (&bf)[KB]) {
+#pragma unroll
+  for (int tl = 0; tl < KB; ++tl) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int t = T0 + tl;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[t >> 1][8 * (t & 1) + j];
+    bf[tl] = split8(v);
+  }
+}
+
+template <class CF, bool DIR_INV>
+__global__ void __launch_bounds__(256, 2) coupling_x6_kernel(
+    const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
+    const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
+    float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound) {
+  extern __shared__ float4 lds4[];
+  float* lds = reinterpret_cast<float*>(lds4);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int h = lane >> 5;
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerWG + wave * 32 + (lane & 31);
+  const bool valid = row < B;
+  const int64_t crow = valid ? row : 0;
+
+  stage_issue<CF::A_SIZE>(lds, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER);
+
+  float zl[CF::SH], zu[CF::DH];
+  float ldsum = 0.f, logjac = 0.f;
+#pragma unroll
+  for (int q = 0; q < CF::SH; ++q) zl[q] = valid ? x[crow * ldx + h * CF::SH + q] : 0.f;
+#pragma unroll
+  for (int q = 0; q < CF::DH; ++q) zu[q] = valid ? x[crow * ldx + CF::S + h * CF::DH + q] : 0.f;
+  if (DIR_INV && low != nullptr) {  // naz bounding_transform (transforms.py:20-23)
+    auto bnd = [&](float& v, int dim) {
+      const float lo = low[dim], hi = high[dim];
+      const float u = (v - lo) / (hi - lo);
+      logjac -= logf(u) + log1pf(-u);
+      v = logf(u / (1.f - u));
+    };
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) bnd(zl[q], h * CF::SH + q);
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) bnd(zu[q], CF::S + h * CF::DH + q);
+    if (h == 0) {
+      float sl = 0.f;
+      for (int d = 0; d < CF::D; ++d) sl += logf(high[d] - low[d]);
+      logjac -= sl;
+    }
+  }
+  __syncthreads();
+
+  for (int li = 0; li < L; ++li) {
+    const int l = DIR_INV ? (L - 1 - li) : li;
+    const float* lp = packed + (int64_t)l * CF::LAYER;
+
+    // ---------------- stage A: lower spline (inverse), GEMM1 over [ctx | x1]
+    float x1[CF::SH];
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) {
+      if constexpr (DIR_INV && CF::LOWER) {
+        SplineTables<CF::K> t;
+        load_tables<CF>(lds + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
+        float ld;
+        zl[q] = rqs_apply<CF::K, true, true>(t, zl[q], bound, ld);
+        ldsum -= ld;
+      }
+      x1[q] = zl[q];
+    }
+    floatx16 acc1[CF::HB];
+    {
+      Frag3 bf[CF::KS0];
+#pragma unroll
+      for (int t = 0; t < CF::KS0; ++t) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (t < CF::CT) {
+            const int c = 16 * t + 8 * h + j;
+            v[j] = (c < CF::C) ? ctx[crow * ldc + c] : 0.f;
+          } else {
+            const int q = 8 * (t - CF::CT) + j;
+            v[j] = q < CF::SH ? x1[q < CF::SH ? q : 0] : 0.f;
+          }
+        }
+        bf[t] = split8(v);
+      }
+      init_bias<CF::HB>(acc1, lds + CF::A_BIAS, h);
+      gemm_x6_stage<CF::HB, CF::KS0>(acc1, lds, lane, bf);
+    }
+    if constexpr (!DIR_INV && CF::LOWER) {
+#pragma unroll
+      for (int q = 0; q < CF::SH; ++q) {
+        SplineTables<CF::K> t;
+        load_tables<CF>(lds + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
+        float ld;
+        zl[q] = rqs_apply<CF::K, false, true>(t, zl[q], bound, ld);
+        ldsum += ld;
+      }
+    }
+
+    // ---------------- stages B_q: GEMM2, k-steps [q*KB2, (q+1)*KB2); tanh of the acc1 blocks a
+    // stage consumes runs while that stage's copy is in flight
+    floatx16 acc2[CF::HB];
+    static_for<0, CF::NB2>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int T0 = q * CF::KB2;
+      __syncthreads();
+      stage_issue<CF::B_SIZE>(lds, lp + CF::B_OFF + q * CF::B_SIZE);
+#pragma unroll
+      for (int b = (T0 + 1) / 2; b < (T0 + CF::KB2 + 1) / 2; ++b)  // blocks first consumed here
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc1[b][r] = tanh_f<true>(acc1[b][r]);
+      __syncthreads();
+      if constexpr (q == 0) init_bias<CF::HB>(acc2, lds + CF::B_BIAS, h);
+      Frag3 bf[CF::KB2];
+      frags_from_acc<T0, CF::KB2>(acc1, bf);
+      gemm_x6_stage<CF::HB, CF::KB2>(acc2, lds, lane, bf);
+    });
+
+    // ---------------- stages C_q: GEMM3 -> raw spline params in registers
+    floatx16 acc3[CF::NO];
+    static_for<0, CF::NB3>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int T0 = q * CF::KB3;
+      __syncthreads();
+      stage_issue<CF::C_SIZE>(lds, lp + CF::C_OFF + q * CF::C_SIZE);
+#pragma unroll
+      for (int b = (T0 + 1) / 2; b < (T0 + CF::KB3 + 1) / 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[b][r] = tanh_f<true>(acc2[b][r]);
+      __syncthreads();
+      if constexpr (q == 0) init_bias<CF::NO>(acc3, lds + CF::C_BIAS, h);
+      Frag3 bf[CF::KB3];
+      frags_from_acc<T0, CF::KB3>(acc2, bf);
+      gemm_x6_stage<CF::NO, CF::KB3>(acc3, lds, lane, bf);
+    });
+    __syncthreads();
+    if (li + 1 < L) stage_issue<CF::A_SIZE>(lds, packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER);
+
+    // ---------------- upper spline on this lane's DH dims (overlaps the next stage A copy)
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) {
+      float uw[CF::K], uh[CF::K], ud[CF::K - 1];
+#pragma unroll
+      for (int k = 0; k < CF::K; ++k) {
+        const int sw = q * CF::P + k, sh = q * CF::P + CF::K + k;
+        uw[k] = acc3[sw >> 4][sw & 15];
+        uh[k] = acc3[sh >> 4][sh & 15];
+      }
+#pragma unroll
+      for (int k = 0; k < CF::K - 1; ++k) {
+        const int sd = q * CF::P + 2 * CF::K + k;
+        ud[k] = acc3[sd >> 4][sd & 15];
+      }
+      SplineTables<CF::K> t;
+      build_tables<CF::K, true>(uw, uh, ud, bound, t);
+      float ld;
+      zu[q] = rqs_apply<CF::K, DIR_INV, true>(t, zu[q], bound, ld);
+      ldsum += DIR_INV ? -ld : ld;
+    }
+    __syncthreads();
+  }
+
+  if constexpr (DIR_INV) {
+    constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+    float base = 0.f;
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) base += -(zl[q] * zl[q]) / 2.f - kLogSqrt2Pi;
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) base += -(zu[q] * zu[q]) / 2.f - kLogSqrt2Pi;
+    float v = base - ldsum + logjac;
+    v += __shfl_xor(v, 32);
+    if (h == 0 && valid) out_lp[row] = v;
+  } else {
+    if (low != nullptr) {
+#pragma unroll
+      for (int q = 0; q < CF::SH; ++q) {
+        const int d = h * CF::SH + q;
+        zl[q] = (1.f / (1.f + expf(-zl[q]))) * (high[d] - low[d]) + low[d];
+      }
+#pragma unroll
+      for (int q = 0; q < CF::DH; ++q) {
+        const int d = CF::S + h * CF::DH + q;
+        zu[q] = (1.f / (1.f + expf(-zu[q]))) * (high[d] - low[d]) + low[d];
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int q = 0; q < CF::SH; ++q) yout[row * ldy + h * CF::SH + q] = zl[q];
+#pragma unroll
+      for (int q = 0; q < CF::DH; ++q) yout[row * ldy + CF::S + h * CF::DH + q] = zu[q];
+    }
+    if (out_lp != nullptr) {
+      float v = ldsum + __shfl_xor(ldsum, 32);
+      if (h == 0 && valid) out_lp[row] = v;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host dispatch over the compiled instantiations
 // ---------------------------------------------------------------------------
-template <class CF>
+template <class CF, class CX>
 struct CouplingOps {
-  static int64_t packed_bytes(int L) { return (int64_t)L * CF::LAYER * 4; }
+  static int64_t layer_floats(int mode) { return mode == NAZ_MFMA_F32 ? CF::LAYER : CX::LAYER; }
+  static int64_t packed_bytes(int L, int mode) { return (int64_t)L * layer_floats(mode) * 4; }
   static int64_t param_count(int L) { return (int64_t)L * CF::FLAT; }
-  static int pack(const float* flat, void* packed, int L, float bound, hipStream_t s) {
-    const int64_t n = (int64_t)L * CF::LAYER;
+  static int pack(const float* flat, void* packed, int L, float bound, int mode, hipStream_t s) {
+    const int64_t n = (int64_t)L * layer_floats(mode);
     int64_t grid = (n + 255) / 256;
     if (grid > 8192) grid = 8192;
-    hipLaunchKernelGGL((coupling_pack_kernel<CF>), dim3((unsigned)grid), dim3(256), 0, s, flat,
-                       reinterpret_cast<float*>(packed), L, bound);
+    if (mode == NAZ_MFMA_F32)
+      hipLaunchKernelGGL((coupling_pack_kernel<CF>), dim3((unsigned)grid), dim3(256), 0, s, flat,
+                         reinterpret_cast<float*>(packed), L, bound);
+    else
+      hipLaunchKernelGGL((coupling_pack_x6_kernel<CX>), dim3((unsigned)grid), dim3(256), 0, s, flat,
+                         reinterpret_cast<float*>(packed), L, bound);
     return check_launch("coupling_pack_kernel");
   }
-  static int run(bool inv, const void* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
-                 const float* low, const float* high, float* out_lp, float* y, int64_t ldy, int64_t B, float bound,
-                 hipStream_t s) {
+  static int run(bool inv, int mode, const void* packed, int L, const float* x, int64_t ldx, const float* ctx,
+                 int64_t ldc, const float* low, const float* high, float* out_lp, float* y, int64_t ldy, int64_t B,
+                 float bound, hipStream_t s) {
     if (B == 0) return 0;
     const int64_t grid = (B + kRowsPerWG - 1) / kRowsPerWG;
-    const size_t lds = (size_t)CF::MAXSTAGE * 4;
-    if (inv)
-      hipLaunchKernelGGL((coupling_flow_kernel<CF, true>), dim3((unsigned)grid), dim3(256), lds, s,
-                         reinterpret_cast<const float*>(packed), L, x, ldx, ctx, ldc, low, high, out_lp, y, ldy, B,
-                         bound);
-    else
-      hipLaunchKernelGGL((coupling_flow_kernel<CF, false>), dim3((unsigned)grid), dim3(256), lds, s,
-                         reinterpret_cast<const float*>(packed), L, x, ldx, ctx, ldc, low, high, out_lp, y, ldy, B,
-                         bound);
+    const float* pk = reinterpret_cast<const float*>(packed);
+    if (mode == NAZ_MFMA_F32) {
+      const size_t lds = (size_t)CF::MAXSTAGE * 4;
+      if (inv)
+        hipLaunchKernelGGL((coupling_flow_kernel<CF, true>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
+                           ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+      else
+        hipLaunchKernelGGL((coupling_flow_kernel<CF, false>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
+                           ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+    } else {
+      const size_t lds = (size_t)CX::MAXSTAGE * 4;
+      if (inv)
+        hipLaunchKernelGGL((coupling_x6_kernel<CX, true>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
+                           ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+      else
+        hipLaunchKernelGGL((coupling_x6_kernel<CX, false>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
+                           ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+    }
     return check_launch("coupling_flow_kernel");
   }
 };
@@ -509,9 +987,10 @@ template <class F>
 static int coupling_dispatch(const naz_coupling_desc* d, F&& f) {
   if (d == nullptr) return set_error("naz_coupling: null descriptor");
   if (d->act != NAZ_ACT_TANH) return -2;
+  if (d->mfma_mode != NAZ_MFMA_BF16X6 && d->mfma_mode != NAZ_MFMA_F32) return -2;
 #define NAZ_TRY(D_, C_, S_, K_, H_, LOW_)                                                                  \
   if (d->D == D_ && d->C == C_ && d->S == S_ && d->K == K_ && d->H == H_ && (d->has_lower != 0) == LOW_) \
-    return f(CouplingOps<CouplingCfg<D_, C_, S_, K_, H_, LOW_>>{});
+    return f(CouplingOps<CouplingCfg<D_, C_, S_, K_, H_, LOW_>, CfgX6<D_, C_, S_, K_, H_, LOW_>>{});
   NAZ_COUPLING_CONFIGS(NAZ_TRY)
 #undef NAZ_TRY
   return -2;
@@ -529,17 +1008,17 @@ int64_t coupling_param_count(const naz_coupling_desc* d) {
 
 int64_t coupling_packed_bytes(const naz_coupling_desc* d) {
   int64_t v = -1;
-  coupling_dispatch(d, [&](auto ops) { v = decltype(ops)::packed_bytes(d->L); return 0; });
+  coupling_dispatch(d, [&](auto ops) { v = decltype(ops)::packed_bytes(d->L, d->mfma_mode); return 0; });
   return v;
 }
 
 static int unsupported(const naz_coupling_desc* d) {
-  return set_error("naz_coupling: no fused instantiation for D=%d C=%d S=%d K=%d H=%d act=%d lower=%d", d->D, d->C,
-                   d->S, d->K, d->H, d->act, d->has_lower);
+  return set_error("naz_coupling: no fused instantiation for D=%d C=%d S=%d K=%d H=%d act=%d lower=%d mode=%d", d->D,
+                   d->C, d->S, d->K, d->H, d->act, d->has_lower, d->mfma_mode);
 }
 
 int coupling_pack(const naz_coupling_desc* d, const float* flat, void* packed, hipStream_t s) {
-  int rc = coupling_dispatch(d, [&](auto ops) { return decltype(ops)::pack(flat, packed, d->L, d->bound, s); });
+  int rc = coupling_dispatch(d, [&](auto ops) { return decltype(ops)::pack(flat, packed, d->L, d->bound, d->mfma_mode, s); });
   return rc == -2 ? unsupported(d) : rc;
 }
 
@@ -547,7 +1026,8 @@ int coupling_log_prob(const naz_coupling_desc* d, const void* packed, const floa
                       int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s) {
   if ((low == nullptr) != (high == nullptr)) return set_error("naz_coupling_log_prob: low/high must both be set");
   int rc = coupling_dispatch(d, [&](auto ops) {
-    return decltype(ops)::run(true, packed, d->L, x, ldx, ctx, ldc, low, high, out_lp, nullptr, 0, B, d->bound, s);
+    return decltype(ops)::run(true, d->mfma_mode, packed, d->L, x, ldx, ctx, ldc, low, high, out_lp, nullptr, 0, B,
+                              d->bound, s);
   });
   return rc == -2 ? unsupported(d) : rc;
 }
@@ -557,7 +1037,8 @@ int coupling_sample(const naz_coupling_desc* d, const void* packed, const float*
                     hipStream_t s) {
   if ((low == nullptr) != (high == nullptr)) return set_error("naz_coupling_sample: low/high must both be set");
   int rc = coupling_dispatch(d, [&](auto ops) {
-    return decltype(ops)::run(false, packed, d->L, z, ldz, ctx, ldc, low, high, out_ld, y, ldy, B, d->bound, s);
+    return decltype(ops)::run(false, d->mfma_mode, packed, d->L, z, ldz, ctx, ldc, low, high, out_ld, y, ldy, B,
+                              d->bound, s);
   });
   return rc == -2 ? unsupported(d) : rc;
 }

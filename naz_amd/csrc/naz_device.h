@@ -24,14 +24,54 @@ constexpr float kSearchEps = 1e-6f;
 
 enum Act : int { ACT_IDENTITY = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SOFTPLUS = 3, ACT_SIGMOID = 4 };
 
-// torch.nn.functional.softplus(beta=1, threshold=20)
-NAZ_DEV float softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+// Math policy.  ACCURATE = the ocml (libm-grade, ~1 ulp, many instructions) functions,
+// used by the HBM-bound kernels.  FAST = the hardware transcendentals (v_exp_f32, v_log_f32,
+// v_rcp_f32, v_sqrt_f32; ~1-2 ulp, one instruction each) used by the MFMA-bound fused
+// kernel, where the VALU instruction count competes with the matrix pipe for issue.
+template <bool FAST>
+struct Math;
 
+template <>
+struct Math<false> {
+  static NAZ_DEV float exp(float x) { return expf(x); }
+  static NAZ_DEV float log(float x) { return logf(x); }
+  static NAZ_DEV float log1p(float x) { return log1pf(x); }
+  static NAZ_DEV float div(float a, float b) { return a / b; }
+  static NAZ_DEV float sqrt(float x) { return sqrtf(x); }
+};
+
+template <>
+struct Math<true> {
+  static NAZ_DEV float exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+  static NAZ_DEV float log(float x) { return __builtin_amdgcn_logf(x) * 0.693147180559945309f; }
+  static NAZ_DEV float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+  static NAZ_DEV float div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+  static NAZ_DEV float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+  // log1p with full relative precision for small x (Kahan: log(u) * x / (u - 1), u = 1 + x)
+  static NAZ_DEV float log1p(float x) {
+    const float u = 1.f + x;
+    const float d = u - 1.f;
+    return d == 0.f ? x : log(u) * div(x, d);
+  }
+};
+
+// torch.nn.functional.softplus(beta=1, threshold=20)
+template <bool FAST = false>
+NAZ_DEV float softplus(float x) {
+  if constexpr (FAST) {
+    if (x > 20.f) return x;
+    return fmaxf(x, 0.f) + Math<true>::log1p(Math<true>::exp(-fabsf(x)));
+  } else {
+    return x > 20.f ? x : log1pf(expf(x));
+  }
+}
+
+template <bool FAST = false>
 NAZ_DEV float tanh_f(float x) {
   // tanh via one exp: |err| <= ~1e-7 absolute (the next layer consumes absolute values)
-  float ax = fabsf(x);
-  float t = expf(-2.f * ax);
-  float r = (1.f - t) / (1.f + t);
+  const float ax = fabsf(x);
+  const float t = Math<FAST>::exp(-2.f * ax);
+  const float r = Math<FAST>::div(1.f - t, 1.f + t);
   return copysignf(r, x);
 }
 
@@ -74,16 +114,25 @@ struct SplineTables {
 };
 
 // softmax over K register values, torch order: exp(x - max) then divide by the sum
-template <int K>
+template <int K, bool FAST = false>
 NAZ_DEV void softmax_k(const float* u, float* out) {
   float m = u[0];
 #pragma unroll
   for (int k = 1; k < K; ++k) m = fmaxf(m, u[k]);
   float s = 0.f;
 #pragma unroll
-  for (int k = 0; k < K; ++k) { out[k] = expf(u[k] - m); s += out[k]; }
+  for (int k = 0; k < K; ++k) {
+    out[k] = Math<FAST>::exp(u[k] - m);
+    s += out[k];
+  }
+  if constexpr (FAST) {
+    const float r = Math<true>::rcp(s);
 #pragma unroll
-  for (int k = 0; k < K; ++k) out[k] = out[k] / s;
+    for (int k = 0; k < K; ++k) out[k] = out[k] * r;
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[k] = out[k] / s;
+  }
 }
 
 // [pyro] _calculate_knots applied to softmaxed fractions (min-width blend included)
@@ -106,24 +155,25 @@ NAZ_DEV void knots_from_fractions(const float* frac, float minw, float bound, fl
 }
 
 // Build tables from UNNORMALISED params (uw[K], uh[K], ud[K-1]).
-template <int K>
+template <int K, bool FAST = false>
 NAZ_DEV void build_tables(const float* uw, const float* uh, const float* ud, float bound,
                           SplineTables<K>& t) {
   float f[K];
-  softmax_k<K>(uw, f);
+  softmax_k<K, FAST>(uw, f);
   knots_from_fractions<K>(f, kMinBinWidth, bound, t.cw);
-  softmax_k<K>(uh, f);
+  softmax_k<K, FAST>(uh, f);
   knots_from_fractions<K>(f, kMinBinHeight, bound, t.ch);
   t.dv[0] = 1.f - kMinDerivative;
   t.dv[K] = 1.f - kMinDerivative;
 #pragma unroll
-  for (int k = 0; k < K - 1; ++k) t.dv[k + 1] = kMinDerivative + softplus(ud[k]);
+  for (int k = 0; k < K - 1; ++k) t.dv[k + 1] = kMinDerivative + softplus<FAST>(ud[k]);
 }
 
 // Evaluate the spline (forward or inverse) with the bin quantities selected in registers.
 // Returns ld of the map actually applied (inverse map's ld for INV), 0 outside [-B, B].
-template <int K, bool INV>
+template <int K, bool INV, bool FAST = false>
 NAZ_DEV float rqs_apply(const SplineTables<K>& t, float x, float bound, float& ld) {
+  using M = Math<FAST>;
   if (!(x >= -bound && x <= bound)) {  // identity tails (NaN also falls through unchanged)
     ld = 0.f;
     return x;
@@ -150,7 +200,7 @@ NAZ_DEV float rqs_apply(const SplineTables<K>& t, float x, float bound, float& l
   }
   const float w = cw1 - cw0;
   const float h = ch1 - ch0;
-  const float delta = h / w;
+  const float delta = M::div(h, w);
   const float t1 = (d0 + d1) - 2.f * delta;
   float out, dnum, den;
   if constexpr (INV) {
@@ -159,22 +209,22 @@ NAZ_DEV float rqs_apply(const SplineTables<K>& t, float x, float bound, float& l
     const float b = h * d0 - dy * t1;
     const float c = -delta * dy;
     const float disc = b * b - 4.f * a * c;
-    const float root = (2.f * c) / (-b - sqrtf(disc));
+    const float root = M::div(2.f * c, -b - M::sqrt(disc));
     out = root * w + cw0;
     const float tomt = root * (1.f - root);
     den = delta + t1 * tomt;
     const float omr = 1.f - root;
     dnum = delta * delta * (d1 * root * root + 2.f * delta * tomt + d0 * omr * omr);
-    ld = -(logf(dnum) - 2.f * logf(den));
+    ld = -(M::log(dnum) - 2.f * M::log(den));
   } else {
-    const float th = (x - cw0) / w;
+    const float th = M::div(x - cw0, w);
     const float tomt = th * (1.f - th);
     const float num = h * (delta * th * th + d0 * tomt);
     den = delta + t1 * tomt;
-    out = ch0 + num / den;
+    out = ch0 + M::div(num, den);
     const float omt = 1.f - th;
     dnum = delta * delta * (d1 * th * th + 2.f * delta * tomt + d0 * omt * omt);
-    ld = logf(dnum) - 2.f * logf(den);
+    ld = M::log(dnum) - 2.f * M::log(den);
   }
   return out;
 }

@@ -43,11 +43,18 @@ class _FusedCoupling:
     (tracked by tensor version counters), so inference pays it once."""
 
     def __init__(self, layers: List[nn.Module], D: int, C: int, S: int, K: int, H: int, act: str, lower: bool,
-                 bound: float):
+                 bound: float, mfma: str = "bf16x6"):
         self.layers = layers
-        self.desc = ops.coupling_desc(D, C, S, K, len(layers), H, act, lower, bound)
+        self.shape = (D, C, S, K, H, act, lower, bound)
+        self.desc = ops.coupling_desc(D, C, S, K, len(layers), H, act, lower, bound, mfma)
         self._sig = None
         self._packed = None
+
+    def set_mfma(self, mfma: str) -> None:
+        """"bf16x6" (default) or "f32" (exact FP32 MFMA kernel); invalidates the packed weights."""
+        D, C, S, K, H, act, lower, bound = self.shape
+        self.desc = ops.coupling_desc(D, C, S, K, len(self.layers), H, act, lower, bound, mfma)
+        self._sig, self._packed = None, None
 
     def params(self) -> List[torch.Tensor]:
         out = []

@@ -192,10 +192,13 @@ def bounding_inv(y: Tensor, low: Tensor, high: Tensor) -> Tensor:
 
 # ----------------------------------------------------------------------------- a3 + a8 + a9 fused
 def coupling_desc(D: int, C: int, S: int, K: int, L: int, H: int, act: str = "tanh", has_lower: bool = True,
-                  bound: float = 3.0) -> CouplingDesc:
+                  bound: float = 3.0, mfma: str = "bf16x6") -> CouplingDesc:
+    """``mfma``: "bf16x6" (default; FP32 GEMMs as six exact-split bf16 products) or "f32"
+    (exact v_mfma_f32_32x32x2_f32)."""
     d = CouplingDesc()
     d.D, d.C, d.S, d.K, d.L, d.H = D, C, S, K, L, H
     d.act, d.has_lower, d.bound = ACT.get(act, -1), int(has_lower), float(bound)
+    d.mfma_mode = {"bf16x6": 0, "f32": 1}[mfma]
     return d
 
 

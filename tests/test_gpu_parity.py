@@ -144,13 +144,15 @@ FLOWS = ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz", "nsa_d4c2
 
 
 @pytest.mark.parametrize("name", FLOWS)
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", ["bf16x6", "f32", False])
 def test_flow_log_prob_vs_golden(name, fused):
     fx = load_golden(name)
     f, spec, _ = _product_flow(fx)
     if spec["flow_type"] == "nsc":
         assert f.fused, "the nsc fixture shapes must hit a fused instantiation"
-        f.set_fused(fused)
+        f.set_fused(bool(fused))
+        if fused:
+            f._plan.set_mfma(fused)
     elif fused:
         pytest.skip("no fused kernel for this flow type yet")
     x = _cuda(fx["x"])
@@ -161,12 +163,14 @@ def test_flow_log_prob_vs_golden(name, fused):
 
 
 @pytest.mark.parametrize("name", ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz"])
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", ["bf16x6", "f32", False])
 def test_flow_sample_transform_vs_golden(name, fused):
     from naz_amd import ops
     fx = load_golden(name)
     f, spec, _ = _product_flow(fx)
-    f.set_fused(fused)
+    f.set_fused(bool(fused))
+    if fused:
+        f._plan.set_mfma(fused)
     z = _cuda(fx["z"])
     c = _cuda(fx["ctx"]) if "ctx" in fx else None
     pdf = f._pdf(c)
@@ -183,7 +187,8 @@ def test_flow_sample_transform_vs_golden(name, fused):
     assert_parity(_np(ld), fx["ld_sample"], ld32.numpy(), what=f"{name} sample ld")
 
 
-def test_config3_full_flow_vs_live_oracle():
+@pytest.mark.parametrize("mfma", ["bf16x6", "f32"])
+def test_config3_full_flow_vs_live_oracle(mfma):
     """The metric configuration (D16|C32, K8, H[128,128], L=8) at 8192 rows vs the oracle."""
     from naz_amd.flows import NormalizingFlow
     from naz_amd.flows import io as fio
@@ -192,14 +197,15 @@ def test_config3_full_flow_vs_live_oracle():
     f = NormalizingFlow("nsc", None, 16, 32, [128, 128], 8, 8, 8)
     fio.load_state(f, {k: v.numpy() for k, v in state.items()})
     assert f.fused
+    f._plan.set_mfma(mfma)
     n = 8192
     x = torch.as_tensor(O.gaussian_mixture(n, 16, seed=0))
     c = torch.as_tensor(O.context_normal(n, 32, seed=1))
     lp = f.log_prob(x.to(DEV), condition=c.to(DEV))
     lp64 = O.build_flow(spec, state, torch.float64).log_prob(x.double(), c.double()).numpy()
     lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, c).numpy()
-    st = assert_parity(_np(lp), lp64, lp32, what="config3 L8")
-    print("config3", st)
+    st = assert_parity(_np(lp), lp64, lp32, what=f"config3 L8 {mfma}")
+    print("config3", mfma, st)
 
 
 def _config3_flow(seed=1234):

@@ -107,9 +107,10 @@ def cpu_baseline(flow, x_host: np.ndarray, c_host: np.ndarray, budget_rows: int 
         "gpu_rel_max": float(rel.max()), "ref_fp32_rel_max": float(rel32.max())}
 
 
-def load_traffic():
-    """HBM bytes per launch measured with rocprofv3 PMC passes (profiles/), if present."""
-    p = ROOT / "profiles" / "traffic_config3.json"
+def load_traffic(mode: str):
+    """HBM bytes per launch measured with rocprofv3 PMC passes for this kernel variant
+    (profiles/traffic_config3_<mode>.json, written by scripts/pmc_summary.py), if present."""
+    p = ROOT / "profiles" / f"traffic_config3_{mode}.json"
     if p.exists():
         try:
             d = json.loads(p.read_text())
@@ -126,8 +127,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="rows per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mfma", choices=["bf16x6", "f32"], default="bf16x6",
-                    help="bf16x6: FP32 GEMMs as six exact-split bf16 products (default); f32: exact FP32 MFMA")
+    ap.add_argument("--mfma", choices=["auto", "f16x3", "bf16x6", "f32"], default="auto",
+                    help="auto (default): f16x3 when the hidden-layer weights fit fp16 (GEMM1 bf16x6, GEMM2/3 as "
+                         "three exact-split fp16 products), else bf16x6; f32: exact FP32 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -151,6 +153,7 @@ def main():
     plan = flow._plan
     plan.set_mfma(args.mfma)
     packed = plan.packed()
+    mode = plan.mode
 
     from naz_amd import ops
 
@@ -189,9 +192,16 @@ def main():
         total_rows = B * world * args.steps
         flop_launch = flops_per_row() * B
         achieved = flop_launch / avg_kern_s / 1e12
-        # ceiling for algorithmic FP32 FLOPs on the pipe the kernel actually uses
-        peak = BF16_PEAK_TFLOPS / X6_PRODUCTS if args.mfma == "bf16x6" else FP32_PEAK_TFLOPS
-        traffic, traffic_src = load_traffic()
+        # ceiling for algorithmic FP32 FLOPs on the pipe the kernel actually uses: bf16/fp16 dense
+        # MFMA peak divided by the products per fp32 product, weighted by each GEMM's FLOP share
+        g1 = 2 * L * (C + S) * H / flops_per_row()  # GEMM1 share (always bf16x6 in the split modes)
+        if mode == "f32":
+            peak = FP32_PEAK_TFLOPS
+        elif mode == "bf16x6":
+            peak = BF16_PEAK_TFLOPS / X6_PRODUCTS
+        else:
+            peak = BF16_PEAK_TFLOPS / (g1 * X6_PRODUCTS + (1 - g1) * 3)
+        traffic, traffic_src = load_traffic(mode)
         rec = {
             "metric": METRIC, "value": total_rows / elapsed, "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -202,12 +212,17 @@ def main():
                                    "L=8, H=[128,128], split 8, tanh; fused log_prob (naz_coupling_log_prob)",
                        "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"dp{world} (independent row shards, no collective)"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": "coupling_flow_kernel<16,32,8,8,128,lower,inv>",
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
+                         "mfma_mode": mode,
+                         "peak_note": ("exact FP32 MFMA (v_mfma_f32_32x32x2_f32) peak" if mode == "f32" else
+                                       "algorithmic fp32 FLOP/s vs the dense bf16/fp16 MFMA peak (2.5 PF) divided by "
+                                       "the MFMA products per fp32 product (bf16x6: 6; f16x3: 3 on GEMM2/3, 6 on "
+                                       f"GEMM1); the exact-FP32 MFMA peak is {FP32_PEAK_TFLOPS}"),
+                         "kernel": ("coupling_flow_kernel" if mode == "f32" else "coupling_x6_kernel")
+                                   + f"<16,32,8,8,128,lower,inv,{mode}>",
                          "flop_per_row": flops_per_row(), "avg_kernel_ms": avg_kern_s * 1e3,
-                         "hbm_alg_GBps": bytes_per_row() * B / avg_kern_s / 1e9,
-                         "traffic_source": traffic_src},
+                         "hbm_alg_GBps": bytes_per_row() * B / avg_kern_s / 1e9},
         }
         if world == 1 and not args.no_cpu_baseline:
             base, parity = cpu_baseline(flow, x_host, c_host)

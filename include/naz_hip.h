@@ -41,6 +41,8 @@ extern "C" {
 
 #define NAZ_MFMA_BF16X6 0 /* default: FP32 GEMMs as 6 exact-split bf16 MFMA products (fp32-grade error) */
 #define NAZ_MFMA_F32 1    /* exact FP32 MFMA (v_mfma_f32_32x32x2_f32)                                  */
+#define NAZ_MFMA_F16X3 2  /* GEMM1 bf16x6, GEMM2/3 as 3 exact-split fp16 products (fp32-grade error;
+                             requires every |W1|, |W2| < 2^15 — the caller checks at pack time)       */
 
 /* ---- library ------------------------------------------------------------ */
 const char* naz_last_error(void);
@@ -114,7 +116,7 @@ typedef struct naz_coupling_desc {
   int act;                /* NAZ_ACT_* */
   int has_lower;          /* 1: lower (unconditional) spline on x1; 0: pyro identity=True */
   float bound;            /* spline box half-width (pyro default 3.0) */
-  int mfma_mode;          /* NAZ_MFMA_BF16X6 (default, 0) or NAZ_MFMA_F32; the packed layout depends on it */
+  int mfma_mode;          /* NAZ_MFMA_BF16X6 (0), NAZ_MFMA_F32 or NAZ_MFMA_F16X3; the packed layout depends on it */
   int reserved[6];
 } naz_coupling_desc;
 

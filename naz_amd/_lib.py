@@ -14,7 +14,7 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / "libnazhip.so"
 LAYOUT_DENSE, LAYOUT_ARN = 0, 1
 LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB = 0, 1, 2, 3
 ACT = {"identity": 0, "tanh": 1, "relu": 2, "softplus": 3, "sigmoid": 4}
-MFMA_BF16X6, MFMA_F32 = 0, 1
+MFMA_BF16X6, MFMA_F32, MFMA_F16X3 = 0, 1, 2
 
 _f, _i, _i64, _vp = C.POINTER(C.c_float), C.c_int, C.c_int64, C.c_void_p
 

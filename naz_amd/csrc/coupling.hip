@@ -540,13 +540,60 @@ NAZ_DEV floatx16 mfma6(const Frag3& a, const Frag3& b, floatx16 acc) {
   return acc;
 }
 
+// fp16x3 (GEMM2/GEMM3 only, whose B operands are tanh outputs in [-1, 1]): v = hi + lo with
+// hi = fp16(v), lo = fp16(v - hi) (v - hi is exact), products Wh·Xh + Wh·Xl + Wl·Xh, at half the
+// MFMAs of bf16x6.  Weight range is checked at pack time (|W| < 2^15).
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+NAZ_DEV floatx16 mfma_f16(half8 a, half8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+struct Frag2 {
+  half8 h, l;
+};
+
+NAZ_DEV Frag2 split8_f16(const float (&v)[8]) {
+  u32x4 H, Lo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const auto hp = __builtin_amdgcn_cvt_pkrtz(v[2 * q], v[2 * q + 1]);
+    const float r0 = v[2 * q] - (float)hp[0], r1 = v[2 * q + 1] - (float)hp[1];
+    const auto lp = __builtin_amdgcn_cvt_pkrtz(r0, r1);
+    H[q] = __builtin_bit_cast(unsigned, hp);
+    Lo[q] = __builtin_bit_cast(unsigned, lp);
+  }
+  return Frag2{__builtin_bit_cast(half8, H), __builtin_bit_cast(half8, Lo)};
+}
+
+NAZ_DEV floatx16 mfma3(const Frag2& a, const Frag2& b, floatx16 acc) {
+  acc = mfma_f16(a.l, b.h, acc);
+  acc = mfma_f16(a.h, b.l, acc);
+  acc = mfma_f16(a.h, b.h, acc);
+  return acc;
+}
+
+// fp16 piece (0 = hi, 1 = lo) of a WEIGHT as 16 bits.  Weights are split with round-to-nearest
+// (done once per pack): |lo| <= 2^-12 |W|, so the dropped Wl·Xl term and W's residual error are
+// ~2^-24 relative.  Activations use the cheaper truncating split (v_cvt_pkrtz) on the fly.
+// On the oracle this RNE(W)/RTZ(X) pairing matches exact FP32 (median 3.1e-7 vs 2.8e-7, q99
+// 4.1e-6 vs 4.0e-6); RTZ on both sides is measurably worse (median 3.6e-7, q99 5.1e-6).
+NAZ_DEV unsigned f16_piece_bits(float v, int piece) {
+  const _Float16 hi = (_Float16)v;
+  if (piece == 0) return (unsigned)__builtin_bit_cast(unsigned short, hi);
+  const _Float16 lo = (_Float16)(v - (float)hi);
+  return (unsigned)__builtin_bit_cast(unsigned short, lo);
+}
+
 constexpr int kX6StageFloats = 18432;  // 72 KB of operand chunks per stage (+ biases)
 constexpr int kChunk = 256;            // one (block, k-step, piece) A fragment set: 64 lanes x 16 B
 
-template <int D_, int C_, int S_, int K_, int H_, bool LOWER_>
+template <int D_, int C_, int S_, int K_, int H_, bool LOWER_, int P23_ = 3>
 struct CfgX6 {
   static constexpr int D = D_, C = C_, S = S_, K = K_, H = H_;
   static constexpr bool LOWER = LOWER_;
+  static constexpr int P23 = P23_;                  // operand pieces of GEMM2/3: 3 = bf16x6, 2 = fp16x3
+  static constexpr bool F16 = P23 == 2;
   static constexpr int Dt = D - S, P = 3 * K - 1, DH = Dt / 2, SH = S / 2;
   static constexpr int HB = H / 32;
   static constexpr int CT = (C + 15) / 16;          // GEMM1 k-steps over the context
@@ -555,11 +602,12 @@ struct CfgX6 {
   static constexpr int KS1 = 2 * HB;                // GEMM2/3 k-steps (16 features each)
   static constexpr int NO = (DH * P + 15) / 16;     // GEMM3 output blocks
   static constexpr int TBL = 3 * (K + 1);
-  static constexpr int OT = 3 * kChunk;             // floats per (block, k-step)
+  static constexpr int OT = 3 * kChunk;             // floats per (block, k-step), GEMM1
+  static constexpr int OT23 = P23 * kChunk;         // floats per (block, k-step), GEMM2/3
   static constexpr int pick_kb(int nb) {            // largest k-steps-per-stage dividing KS1
     int best = 1;
     for (int kb = 1; kb <= KS1; ++kb)
-      if (KS1 % kb == 0 && nb * kb * OT <= kX6StageFloats) best = kb;
+      if (KS1 % kb == 0 && nb * kb * OT23 <= kX6StageFloats) best = kb;
     return best;
   }
   static constexpr int KB2 = pick_kb(HB), NB2 = KS1 / KB2;
@@ -571,11 +619,11 @@ struct CfgX6 {
   static constexpr int A_SIZE = pad(A_TBL + S * TBL);
   // stages B_q: [HB][KB2][3][256] | bias [HB][2][16]
   static constexpr int B_OFF = A_SIZE;
-  static constexpr int B_BIAS = HB * KB2 * OT;
+  static constexpr int B_BIAS = HB * KB2 * OT23;
   static constexpr int B_SIZE = pad(B_BIAS + HB * 32);
   // stages C_q: [NO][KB3][3][256] | bias [NO][2][16]
   static constexpr int C_OFF = B_OFF + NB2 * B_SIZE;
-  static constexpr int C_BIAS = NO * KB3 * OT;
+  static constexpr int C_BIAS = NO * KB3 * OT23;
   static constexpr int C_SIZE = pad(C_BIAS + NO * 32);
   static constexpr int LAYER = C_OFF + NB3 * C_SIZE;
   static constexpr int MAXSTAGE = A_SIZE > B_SIZE ? (A_SIZE > C_SIZE ? A_SIZE : C_SIZE)
@@ -627,8 +675,10 @@ __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* _
     const float* low = b2 + CF::N_B2;
     // operand chunk entry: (o, t, piece, lane, pair) -> two bf16 of W[row][col(j)], W[row][col(j+1)]
     auto chunk_word = [&](int q, int nt, int t0, const float* W, int ldw, bool gemm1) -> unsigned {
-      const int o = q / (nt * CF::OT), r1 = q - o * nt * CF::OT;
-      const int tl = r1 / CF::OT, r2 = r1 - tl * CF::OT;
+      const int ot = gemm1 ? CF::OT : CF::OT23;
+      const bool f16 = !gemm1 && CF::F16;
+      const int o = q / (nt * ot), r1 = q - o * nt * ot;
+      const int tl = r1 / ot, r2 = r1 - tl * ot;
       const int piece = r2 / kChunk, u = r2 - piece * kChunk;
       const int lane = u >> 2, pair = u & 3, i = lane & 31, kh = lane >> 5;
       const int t = t0 + tl;
@@ -651,7 +701,7 @@ __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* _
         } else if (col >= 0) {
           v = W[row * ldw + col];
         }
-        out |= bf16_hi_bits(v, piece) << (16 * e2);
+        out |= (f16 ? f16_piece_bits(v, piece) : bf16_hi_bits(v, piece)) << (16 * e2);
       }
       return out;
     };
@@ -715,6 +765,32 @@ NAZ_DEV void gemm_x6_stage(floatx16 (&acc)[NB], const float* __restrict__ stage,
               __builtin_bit_cast(bf16x8, c4[base + 128])};
       acc[o] = mfma6(a, bf[t], acc[o]);
     }
+  }
+}
+
+template <int NB, int KB>
+NAZ_DEV void gemm_f16_stage(floatx16 (&acc)[NB], const float* __restrict__ stage, int lane, const Frag2 (&bf)[KB]) {
+  const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
+#pragma unroll
+  for (int t = 0; t < KB; ++t) {
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const int base = ((o * KB + t) * 2) * 64 + lane;
+      Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+      acc[o] = mfma3(a, bf[t], acc[o]);
+    }
+  }
+}
+
+template <int T0, int KB, int NB>
+NAZ_DEV void frags_from_acc(const floatx16 (&x)[NB], Frag2 (&bf)[KB]) {
+#pragma unroll
+  for (int tl = 0; tl < KB; ++tl) {
+    const int t = T0 + tl;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[t >> 1][8 * (t & 1) + j];
+    bf[tl] = split8_f16(v);
   }
 }
 
@@ -837,9 +913,15 @@ __global__ void __launch_bounds__(256, 2) coupling_x6_kernel(
         for (int r = 0; r < 16; ++r) acc1[b][r] = tanh_f<true>(acc1[b][r]);
       __syncthreads();
       if constexpr (q == 0) init_bias<CF::HB>(acc2, lds + CF::B_BIAS, h);
-      Frag3 bf[CF::KB2];
-      frags_from_acc<T0, CF::KB2>(acc1, bf);
-      gemm_x6_stage<CF::HB, CF::KB2>(acc2, lds, lane, bf);
+      if constexpr (CF::F16) {
+        Frag2 bf[CF::KB2];
+        frags_from_acc<T0, CF::KB2>(acc1, bf);
+        gemm_f16_stage<CF::HB, CF::KB2>(acc2, lds, lane, bf);
+      } else {
+        Frag3 bf[CF::KB2];
+        frags_from_acc<T0, CF::KB2>(acc1, bf);
+        gemm_x6_stage<CF::HB, CF::KB2>(acc2, lds, lane, bf);
+      }
     });
 
     // ---------------- stages C_q: GEMM3 -> raw spline params in registers
@@ -855,9 +937,15 @@ __global__ void __launch_bounds__(256, 2) coupling_x6_kernel(
         for (int r = 0; r < 16; ++r) acc2[b][r] = tanh_f<true>(acc2[b][r]);
       __syncthreads();
       if constexpr (q == 0) init_bias<CF::NO>(acc3, lds + CF::C_BIAS, h);
-      Frag3 bf[CF::KB3];
-      frags_from_acc<T0, CF::KB3>(acc2, bf);
-      gemm_x6_stage<CF::NO, CF::KB3>(acc3, lds, lane, bf);
+      if constexpr (CF::F16) {
+        Frag2 bf[CF::KB3];
+        frags_from_acc<T0, CF::KB3>(acc2, bf);
+        gemm_f16_stage<CF::NO, CF::KB3>(acc3, lds, lane, bf);
+      } else {
+        Frag3 bf[CF::KB3];
+        frags_from_acc<T0, CF::KB3>(acc2, bf);
+        gemm_x6_stage<CF::NO, CF::KB3>(acc3, lds, lane, bf);
+      }
     });
     __syncthreads();
     if (li + 1 < L) stage_issue<CF::A_SIZE>(lds, packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER);
@@ -925,46 +1013,51 @@ __global__ void __launch_bounds__(256, 2) coupling_x6_kernel(
 // ---------------------------------------------------------------------------
 // Host dispatch over the compiled instantiations
 // ---------------------------------------------------------------------------
-template <class CF, class CX>
+template <class CF, class CX, class CH>
 struct CouplingOps {
-  static int64_t layer_floats(int mode) { return mode == NAZ_MFMA_F32 ? CF::LAYER : CX::LAYER; }
+  static int64_t layer_floats(int mode) {
+    return mode == NAZ_MFMA_F32 ? CF::LAYER : (mode == NAZ_MFMA_BF16X6 ? CX::LAYER : CH::LAYER);
+  }
   static int64_t packed_bytes(int L, int mode) { return (int64_t)L * layer_floats(mode) * 4; }
   static int64_t param_count(int L) { return (int64_t)L * CF::FLAT; }
   static int pack(const float* flat, void* packed, int L, float bound, int mode, hipStream_t s) {
     const int64_t n = (int64_t)L * layer_floats(mode);
     int64_t grid = (n + 255) / 256;
     if (grid > 8192) grid = 8192;
+    float* pk = reinterpret_cast<float*>(packed);
     if (mode == NAZ_MFMA_F32)
-      hipLaunchKernelGGL((coupling_pack_kernel<CF>), dim3((unsigned)grid), dim3(256), 0, s, flat,
-                         reinterpret_cast<float*>(packed), L, bound);
+      hipLaunchKernelGGL((coupling_pack_kernel<CF>), dim3((unsigned)grid), dim3(256), 0, s, flat, pk, L, bound);
+    else if (mode == NAZ_MFMA_BF16X6)
+      hipLaunchKernelGGL((coupling_pack_x6_kernel<CX>), dim3((unsigned)grid), dim3(256), 0, s, flat, pk, L, bound);
     else
-      hipLaunchKernelGGL((coupling_pack_x6_kernel<CX>), dim3((unsigned)grid), dim3(256), 0, s, flat,
-                         reinterpret_cast<float*>(packed), L, bound);
+      hipLaunchKernelGGL((coupling_pack_x6_kernel<CH>), dim3((unsigned)grid), dim3(256), 0, s, flat, pk, L, bound);
     return check_launch("coupling_pack_kernel");
+  }
+  template <class G, bool INV, bool X6>
+  static void launch(const float* pk, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
+                     const float* low, const float* high, float* out_lp, float* y, int64_t ldy, int64_t B, float bound,
+                     hipStream_t s) {
+    const int64_t grid = (B + kRowsPerWG - 1) / kRowsPerWG;
+    const size_t lds = (size_t)G::MAXSTAGE * 4;
+    if constexpr (X6)
+      hipLaunchKernelGGL((coupling_x6_kernel<G, INV>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx, ctx,
+                         ldc, low, high, out_lp, y, ldy, B, bound);
+    else
+      hipLaunchKernelGGL((coupling_flow_kernel<G, INV>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
+                         ctx, ldc, low, high, out_lp, y, ldy, B, bound);
   }
   static int run(bool inv, int mode, const void* packed, int L, const float* x, int64_t ldx, const float* ctx,
                  int64_t ldc, const float* low, const float* high, float* out_lp, float* y, int64_t ldy, int64_t B,
                  float bound, hipStream_t s) {
     if (B == 0) return 0;
-    const int64_t grid = (B + kRowsPerWG - 1) / kRowsPerWG;
     const float* pk = reinterpret_cast<const float*>(packed);
-    if (mode == NAZ_MFMA_F32) {
-      const size_t lds = (size_t)CF::MAXSTAGE * 4;
-      if (inv)
-        hipLaunchKernelGGL((coupling_flow_kernel<CF, true>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
-                           ctx, ldc, low, high, out_lp, y, ldy, B, bound);
-      else
-        hipLaunchKernelGGL((coupling_flow_kernel<CF, false>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
-                           ctx, ldc, low, high, out_lp, y, ldy, B, bound);
-    } else {
-      const size_t lds = (size_t)CX::MAXSTAGE * 4;
-      if (inv)
-        hipLaunchKernelGGL((coupling_x6_kernel<CX, true>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
-                           ctx, ldc, low, high, out_lp, y, ldy, B, bound);
-      else
-        hipLaunchKernelGGL((coupling_x6_kernel<CX, false>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
-                           ctx, ldc, low, high, out_lp, y, ldy, B, bound);
-    }
+#define NAZ_RUN(G, X6)                                                                                   \
+  (inv ? launch<G, true, X6>(pk, L, x, ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound, s)            \
+       : launch<G, false, X6>(pk, L, x, ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound, s))
+    if (mode == NAZ_MFMA_F32) NAZ_RUN(CF, false);
+    else if (mode == NAZ_MFMA_BF16X6) NAZ_RUN(CX, true);
+    else NAZ_RUN(CH, true);
+#undef NAZ_RUN
     return check_launch("coupling_flow_kernel");
   }
 };
@@ -987,10 +1080,11 @@ template <class F>
 static int coupling_dispatch(const naz_coupling_desc* d, F&& f) {
   if (d == nullptr) return set_error("naz_coupling: null descriptor");
   if (d->act != NAZ_ACT_TANH) return -2;
-  if (d->mfma_mode != NAZ_MFMA_BF16X6 && d->mfma_mode != NAZ_MFMA_F32) return -2;
+  if (d->mfma_mode != NAZ_MFMA_BF16X6 && d->mfma_mode != NAZ_MFMA_F32 && d->mfma_mode != NAZ_MFMA_F16X3) return -2;
 #define NAZ_TRY(D_, C_, S_, K_, H_, LOW_)                                                                  \
   if (d->D == D_ && d->C == C_ && d->S == S_ && d->K == K_ && d->H == H_ && (d->has_lower != 0) == LOW_) \
-    return f(CouplingOps<CouplingCfg<D_, C_, S_, K_, H_, LOW_>, CfgX6<D_, C_, S_, K_, H_, LOW_>>{});
+    return f(CouplingOps<CouplingCfg<D_, C_, S_, K_, H_, LOW_>, CfgX6<D_, C_, S_, K_, H_, LOW_, 3>, \
+                         CfgX6<D_, C_, S_, K_, H_, LOW_, 2>>{});
   NAZ_COUPLING_CONFIGS(NAZ_TRY)
 #undef NAZ_TRY
   return -2;

@@ -42,19 +42,30 @@ class _FusedCoupling:
     kernel's MFMA panel order by ``naz_coupling_pack`` — only when a parameter changed
     (tracked by tensor version counters), so inference pays it once."""
 
+    # fp16 pieces of GEMM2/3 weights must stay finite with margin: |W| < 2^15
+    F16_WEIGHT_LIMIT = 32768.0
+
     def __init__(self, layers: List[nn.Module], D: int, C: int, S: int, K: int, H: int, act: str, lower: bool,
-                 bound: float, mfma: str = "bf16x6"):
+                 bound: float, mfma: str = "auto"):
         self.layers = layers
         self.shape = (D, C, S, K, H, act, lower, bound)
-        self.desc = ops.coupling_desc(D, C, S, K, len(layers), H, act, lower, bound, mfma)
+        self.mfma = mfma
+        self.mode = "f16x3" if mfma == "auto" else mfma
+        self.desc = ops.coupling_desc(D, C, S, K, len(layers), H, act, lower, bound, self.mode)
         self._sig = None
         self._packed = None
 
     def set_mfma(self, mfma: str) -> None:
-        """"bf16x6" (default) or "f32" (exact FP32 MFMA kernel); invalidates the packed weights."""
-        D, C, S, K, H, act, lower, bound = self.shape
-        self.desc = ops.coupling_desc(D, C, S, K, len(self.layers), H, act, lower, bound, mfma)
+        """"auto" (default: f16x3 when the GEMM2/3 weights fit fp16's range, else bf16x6),
+        "f16x3", "bf16x6" or "f32" (exact FP32 MFMA kernel); invalidates the packed weights."""
+        self.mfma = mfma
         self._sig, self._packed = None, None
+
+    def _resolve_mode(self) -> str:
+        if self.mfma != "auto":
+            return self.mfma
+        big = max(float(t.nn.layers[i].weight.detach().abs().max()) for t in self.layers for i in (1, 2))
+        return "f16x3" if big < self.F16_WEIGHT_LIMIT else "bf16x6"
 
     def params(self) -> List[torch.Tensor]:
         out = []
@@ -71,6 +82,9 @@ class _FusedCoupling:
         ps = self.params()
         sig = tuple((p.data_ptr(), p._version) for p in ps)
         if sig != self._sig or self._packed is None:
+            D, C, S, K, H, act, lower, bound = self.shape
+            self.mode = self._resolve_mode()
+            self.desc = ops.coupling_desc(D, C, S, K, len(self.layers), H, act, lower, bound, self.mode)
             flat = torch.cat([p.detach().reshape(-1) for p in ps])
             self._packed = ops.coupling_pack(self.desc, flat, self._packed)
             self._sig = sig
@@ -80,13 +94,15 @@ class _FusedCoupling:
         low = high = None
         if bounds is not None:
             low, high = bounds["low"].to(x.device, torch.float32), bounds["high"].to(x.device, torch.float32)
-        return ops.coupling_log_prob(self.desc, self.packed(), x, context, low, high, out=out)
+        packed = self.packed()  # may re-resolve the mode: read self.desc only after it
+        return ops.coupling_log_prob(self.desc, packed, x, context, low, high, out=out)
 
     def sample(self, z, context=None, bounds=None, with_logdet=False):
         low = high = None
         if bounds is not None:
             low, high = bounds["low"].to(z.device, torch.float32), bounds["high"].to(z.device, torch.float32)
-        return ops.coupling_sample(self.desc, self.packed(), z, context, low, high, with_logdet=with_logdet)
+        packed = self.packed()
+        return ops.coupling_sample(self.desc, packed, z, context, low, high, with_logdet=with_logdet)
 
 
 def _fused_plan(flow_type, flow_args, flow_kwargs, transforms) -> Optional[_FusedCoupling]:

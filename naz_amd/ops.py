@@ -193,12 +193,13 @@ def bounding_inv(y: Tensor, low: Tensor, high: Tensor) -> Tensor:
 # ----------------------------------------------------------------------------- a3 + a8 + a9 fused
 def coupling_desc(D: int, C: int, S: int, K: int, L: int, H: int, act: str = "tanh", has_lower: bool = True,
                   bound: float = 3.0, mfma: str = "bf16x6") -> CouplingDesc:
-    """``mfma``: "bf16x6" (default; FP32 GEMMs as six exact-split bf16 products) or "f32"
-    (exact v_mfma_f32_32x32x2_f32)."""
+    """``mfma``: "bf16x6" (FP32 GEMMs as six exact-split bf16 products), "f16x3" (GEMM1 bf16x6,
+    GEMM2/3 three exact-split fp16 products; needs |W1|,|W2| < 2^15) or "f32" (exact
+    v_mfma_f32_32x32x2_f32)."""
     d = CouplingDesc()
     d.D, d.C, d.S, d.K, d.L, d.H = D, C, S, K, L, H
     d.act, d.has_lower, d.bound = ACT.get(act, -1), int(has_lower), float(bound)
-    d.mfma_mode = {"bf16x6": 0, "f32": 1}[mfma]
+    d.mfma_mode = {"bf16x6": 0, "f32": 1, "f16x3": 2}[mfma]
     return d
 
 
@@ -216,6 +217,8 @@ def coupling_pack(d: CouplingDesc, flat: Tensor, packed: Optional[Tensor] = None
     if flat.numel() != n or not flat.is_contiguous():
         raise ValueError(f"flat params must be a contiguous [{n}] fp32 tensor")
     nbytes = int(lib().naz_coupling_packed_bytes(d))
+    if nbytes <= 0:
+        raise RuntimeError("naz_amd coupling_pack: unsupported descriptor")
     if packed is None or packed.numel() * 4 != nbytes:
         packed = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
     check(lib().naz_coupling_pack(d, _p(flat), _p(packed), _stream(dev)), "coupling_pack")

@@ -144,7 +144,7 @@ FLOWS = ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz", "nsa_d4c2
 
 
 @pytest.mark.parametrize("name", FLOWS)
-@pytest.mark.parametrize("fused", ["bf16x6", "f32", False])
+@pytest.mark.parametrize("fused", ["auto", "bf16x6", "f32", False])
 def test_flow_log_prob_vs_golden(name, fused):
     fx = load_golden(name)
     f, spec, _ = _product_flow(fx)
@@ -163,7 +163,7 @@ def test_flow_log_prob_vs_golden(name, fused):
 
 
 @pytest.mark.parametrize("name", ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz"])
-@pytest.mark.parametrize("fused", ["bf16x6", "f32", False])
+@pytest.mark.parametrize("fused", ["auto", "bf16x6", "f32", False])
 def test_flow_sample_transform_vs_golden(name, fused):
     from naz_amd import ops
     fx = load_golden(name)
@@ -187,7 +187,7 @@ def test_flow_sample_transform_vs_golden(name, fused):
     assert_parity(_np(ld), fx["ld_sample"], ld32.numpy(), what=f"{name} sample ld")
 
 
-@pytest.mark.parametrize("mfma", ["bf16x6", "f32"])
+@pytest.mark.parametrize("mfma", ["auto", "f16x3", "bf16x6", "f32"])
 def test_config3_full_flow_vs_live_oracle(mfma):
     """The metric configuration (D16|C32, K8, H[128,128], L=8) at 8192 rows vs the oracle."""
     from naz_amd.flows import NormalizingFlow
@@ -199,6 +199,9 @@ def test_config3_full_flow_vs_live_oracle(mfma):
     assert f.fused
     f._plan.set_mfma(mfma)
     n = 8192
+    if mfma == "auto":
+        f._plan.packed()
+        assert f._plan.mode == "f16x3"
     x = torch.as_tensor(O.gaussian_mixture(n, 16, seed=0))
     c = torch.as_tensor(O.context_normal(n, 32, seed=1))
     lp = f.log_prob(x.to(DEV), condition=c.to(DEV))

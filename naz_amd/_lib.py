@@ -9,7 +9,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libnazhip.so"
+LIB_PATH = Path(os.environ.get("NAZ_LIB", Path(__file__).resolve().parent / "lib" / "libnazhip.so"))
 
 LAYOUT_DENSE, LAYOUT_ARN = 0, 1
 LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB = 0, 1, 2, 3

@@ -187,16 +187,19 @@ __global__ void coupling_pack_kernel(const float* __restrict__ flat, float* __re
 // Asynchronous stage copy HBM/L2 -> LDS with LDS-DMA (global_load_lds_dwordx4): wave w
 // moves 1 KB chunks w, w+4, ...; no VGPRs hold the data.  Completion is awaited by the
 // next __syncthreads() (which waits vmcnt(0)).
-template <int NFLOATS>
+template <int NFLOATS, int NW = 4>
 NAZ_DEV void stage_issue(float* lds, const float* __restrict__ src) {
+#ifdef NAZ_ABL_NOCOPY
+  return;
+#endif
   static_assert(NFLOATS % 256 == 0, "stage must be whole 1 KB chunks");
   constexpr int CHUNKS = NFLOATS / 256;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-  for (int c0 = 0; c0 < CHUNKS; c0 += 4) {
+  for (int c0 = 0; c0 < CHUNKS; c0 += NW) {
     const int c = c0 + wave;
-    if (c0 + 3 < CHUNKS || c < CHUNKS) {
+    if (c0 + NW - 1 < CHUNKS || c < CHUNKS) {
       __builtin_amdgcn_global_load_lds(
           (const void __attribute__((address_space(1)))*)(src + c * 256 + lane * 4),
           (void __attribute__((address_space(3)))*)(lds + c * 256), 16, 0, 0);
@@ -585,7 +588,17 @@ NAZ_DEV unsigned f16_piece_bits(float v, int piece) {
   return (unsigned)__builtin_bit_cast(unsigned short, lo);
 }
 
-constexpr int kX6StageFloats = 18432;  // 72 KB of operand chunks per stage (+ biases)
+#ifdef NAZ_ABL_NOTANH
+#define NAZ_TANH(v) (v)
+#else
+#define NAZ_TANH(v) tanh_f<true>(v)
+#endif
+
+// LDS ring: two slots of 40 KB per 128-row workgroup (two workgroups per CU use all 160 KB).
+// Stage s+1's LDS-DMA copy lands in one slot while stage s computes from the other.
+constexpr int kX6Slot = 10240;     // 40 KB: two 256-thread workgroups per CU (2 x 2 slots = 160 KB)
+constexpr int kX6Waves = 4;        // 128 rows per workgroup (8-wave / 256-row workgroups measured no faster)
+constexpr int kX6Rows = 32 * kX6Waves;
 constexpr int kChunk = 256;            // one (block, k-step, piece) A fragment set: 64 lanes x 16 B
 
 template <int D_, int C_, int S_, int K_, int H_, bool LOWER_, int P23_ = 3>
@@ -604,15 +617,15 @@ struct CfgX6 {
   static constexpr int TBL = 3 * (K + 1);
   static constexpr int OT = 3 * kChunk;             // floats per (block, k-step), GEMM1
   static constexpr int OT23 = P23 * kChunk;         // floats per (block, k-step), GEMM2/3
+  static constexpr int pad(int n) { return (n + 255) / 256 * 256; }
   static constexpr int pick_kb(int nb) {            // largest k-steps-per-stage dividing KS1
     int best = 1;
     for (int kb = 1; kb <= KS1; ++kb)
-      if (KS1 % kb == 0 && nb * kb * OT23 <= kX6StageFloats) best = kb;
+      if (KS1 % kb == 0 && pad(nb * kb * OT23 + nb * 32) <= kX6Slot) best = kb;
     return best;
   }
   static constexpr int KB2 = pick_kb(HB), NB2 = KS1 / KB2;
   static constexpr int KB3 = pick_kb(NO), NB3 = KS1 / KB3;
-  static constexpr int pad(int n) { return (n + 255) / 256 * 256; }
   // stage A: [HB][KS0][3][256] | bias [HB][2][16] | tables [S][TBL]
   static constexpr int A_BIAS = HB * KS0 * OT;
   static constexpr int A_TBL = A_BIAS + HB * 32;
@@ -626,14 +639,18 @@ struct CfgX6 {
   static constexpr int C_BIAS = NO * KB3 * OT23;
   static constexpr int C_SIZE = pad(C_BIAS + NO * 32);
   static constexpr int LAYER = C_OFF + NB3 * C_SIZE;
-  static constexpr int MAXSTAGE = A_SIZE > B_SIZE ? (A_SIZE > C_SIZE ? A_SIZE : C_SIZE)
-                                                  : (B_SIZE > C_SIZE ? B_SIZE : C_SIZE);
+  static constexpr int NSTG = 1 + NB2 + NB3;       // stages per layer
+  static constexpr int MAXSTAGE = 2 * kX6Slot;      // LDS floats per workgroup (the ring)
+  static constexpr __host__ __device__ int stage_off(int j) {
+    return j == 0 ? 0 : (j <= NB2 ? B_OFF + (j - 1) * B_SIZE : C_OFF + (j - 1 - NB2) * C_SIZE);
+  }
+  static constexpr __host__ __device__ int stage_size(int j) { return j == 0 ? A_SIZE : (j <= NB2 ? B_SIZE : C_SIZE); }
   // natural flat layout (same as the FP32 variant)
   static constexpr int N_W0 = H * (C + S), N_B0 = H, N_W1 = H * H, N_B1 = H, N_W2 = Dt * P * H, N_B2 = Dt * P;
   static constexpr int N_LOW = LOWER ? S * (3 * K - 1) : 0;
   static constexpr int FLAT = N_W0 + N_B0 + N_W1 + N_B1 + N_W2 + N_B2 + N_LOW;
   static_assert(Dt % 2 == 0 && S % 2 == 0 && H % 32 == 0 && S > 0 && Dt > 0, "unsupported coupling shape");
-  static_assert(MAXSTAGE * 4 <= 76 * 1024, "stage exceeds the per-workgroup LDS budget (2 WGs / CU)");
+  static_assert(A_SIZE <= kX6Slot && B_SIZE <= kX6Slot && C_SIZE <= kX6Slot, "stage exceeds one LDS ring slot");
 };
 
 // GEMM1 input column (in cat([ctx, x1]) order) for k-step t, element j, lane-half h; -1 = zero pad
@@ -755,6 +772,10 @@ __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* _
 
 template <int NB, int KB>
 NAZ_DEV void gemm_x6_stage(floatx16 (&acc)[NB], const float* __restrict__ stage, int lane, const Frag3 (&bf)[KB]) {
+#ifdef NAZ_ABL_NOGEMM
+  for (int o = 0; o < NB; ++o) acc[o][0] += __builtin_bit_cast(float, (unsigned)bf[0].h[0]) * 1e-30f;
+  return;
+#endif
   const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
 #pragma unroll
   for (int t = 0; t < KB; ++t) {
@@ -770,6 +791,10 @@ NAZ_DEV void gemm_x6_stage(floatx16 (&acc)[NB], const float* __restrict__ stage,
 
 template <int NB, int KB>
 NAZ_DEV void gemm_f16_stage(floatx16 (&acc)[NB], const float* __restrict__ stage, int lane, const Frag2 (&bf)[KB]) {
+#ifdef NAZ_ABL_NOGEMM
+  for (int o = 0; o < NB; ++o) acc[o][0] += (float)bf[0].h[0] * 1e-30f;
+  return;
+#endif
   const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
 #pragma unroll
   for (int t = 0; t < KB; ++t) {
@@ -778,6 +803,53 @@ NAZ_DEV void gemm_f16_stage(floatx16 (&acc)[NB], const float* __restrict__ stage
       const int base = ((o * KB + t) * 2) * 64 + lane;
       Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
       acc[o] = mfma3(a, bf[t], acc[o]);
+    }
+  }
+}
+
+// GEMM over k-steps [T0, T0+KB) with each B fragment split from the activated accumulator
+// just before its MFMAs (keeps one fragment live instead of KB).
+template <int NB, int KB, int T0, int NX>
+NAZ_DEV void gemm_f16_lazy(floatx16 (&acc)[NB], const float* __restrict__ stage, int lane, const floatx16 (&x)[NX]) {
+  const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
+#pragma unroll
+  for (int t = 0; t < KB; ++t) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[(T0 + t) >> 1][8 * ((T0 + t) & 1) + j];
+    const Frag2 b = split8_f16(v);
+#ifdef NAZ_ABL_NOGEMM
+    for (int o = 0; o < NB; ++o) acc[o][0] += (float)b.h[0] * 1e-30f;
+    continue;
+#endif
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const int base = ((o * KB + t) * 2) * 64 + lane;
+      Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+      acc[o] = mfma3(a, b, acc[o]);
+    }
+  }
+}
+
+template <int NB, int KB, int T0, int NX>
+NAZ_DEV void gemm_x6_lazy(floatx16 (&acc)[NB], const float* __restrict__ stage, int lane, const floatx16 (&x)[NX]) {
+  const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
+#pragma unroll
+  for (int t = 0; t < KB; ++t) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[(T0 + t) >> 1][8 * ((T0 + t) & 1) + j];
+    const Frag3 b = split8(v);
+#ifdef NAZ_ABL_NOGEMM
+    for (int o = 0; o < NB; ++o) acc[o][0] += __builtin_bit_cast(float, (unsigned)b.h[0]) * 1e-30f;
+    continue;
+#endif
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const int base = ((o * KB + t) * 3) * 64 + lane;
+      Frag3 a{__builtin_bit_cast(bf16x8, c4[base]), __builtin_bit_cast(bf16x8, c4[base + 64]),
+              __builtin_bit_cast(bf16x8, c4[base + 128])};
+      acc[o] = mfma6(a, b, acc[o]);
     }
   }
 }
@@ -810,20 +882,21 @@ NAZ_DEV void frags_from_acc(const floatx16 (&x)[NB], Frag3 (&bf)[KB]) {
 }
 
 template <class CF, bool DIR_INV>
-__global__ void __launch_bounds__(256, 2) coupling_x6_kernel(
+__global__ void __launch_bounds__(kX6Rows * 2, 2) coupling_x6_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound) {
   extern __shared__ float4 lds4[];
-  float* lds = reinterpret_cast<float*>(lds4);
+  float* const slot0 = reinterpret_cast<float*>(lds4);
+  float* const slot1 = slot0 + kX6Slot;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int h = lane >> 5;
-  const int64_t row = (int64_t)blockIdx.x * kRowsPerWG + wave * 32 + (lane & 31);
+  const int64_t row = (int64_t)blockIdx.x * kX6Rows + wave * 32 + (lane & 31);
   const bool valid = row < B;
   const int64_t crow = valid ? row : 0;
 
-  stage_issue<CF::A_SIZE>(lds, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER);
+  stage_issue<CF::A_SIZE, kX6Waves>(slot0, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER);
 
   float zl[CF::SH], zu[CF::DH];
   float ldsum = 0.f, logjac = 0.f;
@@ -848,109 +921,108 @@ __global__ void __launch_bounds__(256, 2) coupling_x6_kernel(
       logjac -= sl;
     }
   }
-  __syncthreads();
 
+  int g = 0;  // global stage counter: stage g lives in slot (g & 1)
   for (int li = 0; li < L; ++li) {
     const int l = DIR_INV ? (L - 1 - li) : li;
     const float* lp = packed + (int64_t)l * CF::LAYER;
+    const float* lnext = packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER;
+    floatx16 acc1[CF::HB], acc2[CF::HB], acc3[CF::NO];
 
-    // ---------------- stage A: lower spline (inverse), GEMM1 over [ctx | x1]
-    float x1[CF::SH];
-#pragma unroll
-    for (int q = 0; q < CF::SH; ++q) {
-      if constexpr (DIR_INV && CF::LOWER) {
-        SplineTables<CF::K> t;
-        load_tables<CF>(lds + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
-        float ld;
-        zl[q] = rqs_apply<CF::K, true, true>(t, zl[q], bound, ld);
-        ldsum -= ld;
+    static_for<0, CF::NSTG>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+#ifndef NAZ_ABL_NOBARRIER
+      __syncthreads();  // stage j has landed in slot (g&1); every wave is done with the other slot
+#endif
+      const float* cur = (g & 1) ? slot1 : slot0;
+      float* nxt = (g & 1) ? slot0 : slot1;
+      if constexpr (j + 1 < CF::NSTG) {
+        stage_issue<CF::stage_size(j + 1), kX6Waves>(nxt, lp + CF::stage_off(j + 1));
+      } else {
+        if (li + 1 < L) stage_issue<CF::A_SIZE, kX6Waves>(nxt, lnext);
       }
-      x1[q] = zl[q];
-    }
-    floatx16 acc1[CF::HB];
-    {
-      Frag3 bf[CF::KS0];
+      ++g;
+
+      if constexpr (j == 0) {
+        // ---------------- stage A: lower spline (inverse), GEMM1 over [ctx | x1]
+        float x1[CF::SH];
 #pragma unroll
-      for (int t = 0; t < CF::KS0; ++t) {
-        float v[8];
+        for (int q = 0; q < CF::SH; ++q) {
+#ifdef NAZ_ABL_NOLOWER
+          if constexpr (false) {
+#else
+          if constexpr (DIR_INV && CF::LOWER) {
+#endif
+            SplineTables<CF::K> t;
+            load_tables<CF>(cur + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
+            float ld;
+            zl[q] = rqs_apply<CF::K, true, true>(t, zl[q], bound, ld);
+            ldsum -= ld;
+          }
+          x1[q] = zl[q];
+        }
+        Frag3 bf[CF::KS0];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (t < CF::CT) {
-            const int c = 16 * t + 8 * h + j;
-            v[j] = (c < CF::C) ? ctx[crow * ldc + c] : 0.f;
-          } else {
-            const int q = 8 * (t - CF::CT) + j;
-            v[j] = q < CF::SH ? x1[q < CF::SH ? q : 0] : 0.f;
+        for (int t = 0; t < CF::KS0; ++t) {
+          float v[8];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            if (t < CF::CT) {
+              const int c = 16 * t + 8 * h + jj;
+              v[jj] = (c < CF::C) ? ctx[crow * ldc + c] : 0.f;
+            } else {
+              const int q = 8 * (t - CF::CT) + jj;
+              v[jj] = q < CF::SH ? x1[q < CF::SH ? q : 0] : 0.f;
+            }
+          }
+          bf[t] = split8(v);
+        }
+        init_bias<CF::HB>(acc1, cur + CF::A_BIAS, h);
+        gemm_x6_stage<CF::HB, CF::KS0>(acc1, cur, lane, bf);
+        if constexpr (!DIR_INV && CF::LOWER) {
+#pragma unroll
+          for (int q = 0; q < CF::SH; ++q) {
+            SplineTables<CF::K> t;
+            load_tables<CF>(cur + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
+            float ld;
+            zl[q] = rqs_apply<CF::K, false, true>(t, zl[q], bound, ld);
+            ldsum += ld;
           }
         }
-        bf[t] = split8(v);
-      }
-      init_bias<CF::HB>(acc1, lds + CF::A_BIAS, h);
-      gemm_x6_stage<CF::HB, CF::KS0>(acc1, lds, lane, bf);
-    }
-    if constexpr (!DIR_INV && CF::LOWER) {
+      } else if constexpr (j <= CF::NB2) {
+        // ---------------- stage B_q: GEMM2 k-steps [T0, T0 + KB2)
+        constexpr int q = j - 1, T0 = q * CF::KB2;
 #pragma unroll
-      for (int q = 0; q < CF::SH; ++q) {
-        SplineTables<CF::K> t;
-        load_tables<CF>(lds + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
-        float ld;
-        zl[q] = rqs_apply<CF::K, false, true>(t, zl[q], bound, ld);
-        ldsum += ld;
-      }
-    }
-
-    // ---------------- stages B_q: GEMM2, k-steps [q*KB2, (q+1)*KB2); tanh of the acc1 blocks a
-    // stage consumes runs while that stage's copy is in flight
-    floatx16 acc2[CF::HB];
-    static_for<0, CF::NB2>([&](auto qc) {
-      constexpr int q = decltype(qc)::value;
-      constexpr int T0 = q * CF::KB2;
-      __syncthreads();
-      stage_issue<CF::B_SIZE>(lds, lp + CF::B_OFF + q * CF::B_SIZE);
+        for (int b = (T0 + 1) / 2; b < (T0 + CF::KB2 + 1) / 2; ++b)  // activate blocks first used here
 #pragma unroll
-      for (int b = (T0 + 1) / 2; b < (T0 + CF::KB2 + 1) / 2; ++b)  // blocks first consumed here
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc1[b][r] = tanh_f<true>(acc1[b][r]);
-      __syncthreads();
-      if constexpr (q == 0) init_bias<CF::HB>(acc2, lds + CF::B_BIAS, h);
-      if constexpr (CF::F16) {
-        Frag2 bf[CF::KB2];
-        frags_from_acc<T0, CF::KB2>(acc1, bf);
-        gemm_f16_stage<CF::HB, CF::KB2>(acc2, lds, lane, bf);
+          for (int r = 0; r < 16; ++r) acc1[b][r] = NAZ_TANH(acc1[b][r]);
+        if constexpr (q == 0) init_bias<CF::HB>(acc2, cur + CF::B_BIAS, h);
+        if constexpr (CF::F16) gemm_f16_lazy<CF::HB, CF::KB2, T0>(acc2, cur, lane, acc1);
+        else gemm_x6_lazy<CF::HB, CF::KB2, T0>(acc2, cur, lane, acc1);
       } else {
-        Frag3 bf[CF::KB2];
-        frags_from_acc<T0, CF::KB2>(acc1, bf);
-        gemm_x6_stage<CF::HB, CF::KB2>(acc2, lds, lane, bf);
+        // ---------------- stage C_q: GEMM3 k-steps [T0, T0 + KB3) -> raw spline params
+        constexpr int q = j - 1 - CF::NB2, T0 = q * CF::KB3;
+#pragma unroll
+        for (int b = (T0 + 1) / 2; b < (T0 + CF::KB3 + 1) / 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc2[b][r] = NAZ_TANH(acc2[b][r]);
+        if constexpr (q == 0) init_bias<CF::NO>(acc3, cur + CF::C_BIAS, h);
+        if constexpr (CF::F16) gemm_f16_lazy<CF::NO, CF::KB3, T0>(acc3, cur, lane, acc2);
+        else gemm_x6_lazy<CF::NO, CF::KB3, T0>(acc3, cur, lane, acc2);
       }
     });
 
-    // ---------------- stages C_q: GEMM3 -> raw spline params in registers
-    floatx16 acc3[CF::NO];
-    static_for<0, CF::NB3>([&](auto qc) {
-      constexpr int q = decltype(qc)::value;
-      constexpr int T0 = q * CF::KB3;
-      __syncthreads();
-      stage_issue<CF::C_SIZE>(lds, lp + CF::C_OFF + q * CF::C_SIZE);
+    // ---------------- upper spline on this lane's DH dims (the next layer's stage A is in flight)
+#ifdef NAZ_ABL_NOSPLINE
 #pragma unroll
-      for (int b = (T0 + 1) / 2; b < (T0 + CF::KB3 + 1) / 2; ++b)
+    for (int q = 0; q < CF::DH; ++q) {
+      float sacc = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc2[b][r] = tanh_f<true>(acc2[b][r]);
-      __syncthreads();
-      if constexpr (q == 0) init_bias<CF::NO>(acc3, lds + CF::C_BIAS, h);
-      if constexpr (CF::F16) {
-        Frag2 bf[CF::KB3];
-        frags_from_acc<T0, CF::KB3>(acc2, bf);
-        gemm_f16_stage<CF::NO, CF::KB3>(acc3, lds, lane, bf);
-      } else {
-        Frag3 bf[CF::KB3];
-        frags_from_acc<T0, CF::KB3>(acc2, bf);
-        gemm_x6_stage<CF::NO, CF::KB3>(acc3, lds, lane, bf);
-      }
-    });
-    __syncthreads();
-    if (li + 1 < L) stage_issue<CF::A_SIZE>(lds, packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER);
-
-    // ---------------- upper spline on this lane's DH dims (overlaps the next stage A copy)
+      for (int k = 0; k < CF::P; ++k) sacc += acc3[(q * CF::P + k) >> 4][(q * CF::P + k) & 15];
+      zu[q] += 1e-30f * sacc;
+    }
+    if (false)
+#endif
 #pragma unroll
     for (int q = 0; q < CF::DH; ++q) {
       float uw[CF::K], uh[CF::K], ud[CF::K - 1];
@@ -971,7 +1043,6 @@ __global__ void __launch_bounds__(256, 2) coupling_x6_kernel(
       zu[q] = rqs_apply<CF::K, DIR_INV, true>(t, zu[q], bound, ld);
       ldsum += DIR_INV ? -ld : ld;
     }
-    __syncthreads();
   }
 
   if constexpr (DIR_INV) {
@@ -1037,14 +1108,16 @@ struct CouplingOps {
   static void launch(const float* pk, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
                      const float* low, const float* high, float* out_lp, float* y, int64_t ldy, int64_t B, float bound,
                      hipStream_t s) {
-    const int64_t grid = (B + kRowsPerWG - 1) / kRowsPerWG;
     const size_t lds = (size_t)G::MAXSTAGE * 4;
-    if constexpr (X6)
-      hipLaunchKernelGGL((coupling_x6_kernel<G, INV>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx, ctx,
-                         ldc, low, high, out_lp, y, ldy, B, bound);
-    else
+    if constexpr (X6) {
+      const int64_t grid = (B + kX6Rows - 1) / kX6Rows;
+      hipLaunchKernelGGL((coupling_x6_kernel<G, INV>), dim3((unsigned)grid), dim3(kX6Rows * 2), lds, s, pk, L, x,
+                         ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+    } else {
+      const int64_t grid = (B + kRowsPerWG - 1) / kRowsPerWG;
       hipLaunchKernelGGL((coupling_flow_kernel<G, INV>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
                          ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+    }
   }
   static int run(bool inv, int mode, const void* packed, int L, const float* x, int64_t ldx, const float* ctx,
                  int64_t ldc, const float* low, const float* high, float* out_lp, float* y, int64_t ldy, int64_t B,

@@ -95,8 +95,9 @@ def cpu_baseline(flow, x_host: np.ndarray, c_host: np.ndarray, budget_rows: int 
     with torch.inference_mode():
         ref = of64.log_prob(xs[:n].double(), cs[:n].double()).numpy()
         ref32 = of.log_prob(xs[:n], cs[:n]).numpy()
-    gpu = flow.log_prob(torch.as_tensor(x_host[:n], device="cuda"),
-                        condition=torch.as_tensor(c_host[:n], device="cuda")).cpu().numpy()
+    with torch.no_grad():
+        gpu = flow.log_prob(torch.as_tensor(x_host[:n], device="cuda"),
+                            condition=torch.as_tensor(c_host[:n], device="cuda")).cpu().numpy()
     rel = np.abs(gpu - ref) / np.maximum(np.abs(ref), 1.0)
     rel32 = np.abs(ref32 - ref) / np.maximum(np.abs(ref), 1.0)
     return {

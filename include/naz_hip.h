@@ -99,6 +99,41 @@ int naz_bounding_fwd(const float* x, int64_t ldx, const float* low, const float*
 int naz_bounding_inv(const float* y, int64_t ldy, const float* low, const float* high, float* x, int64_t ldx,
                      int64_t B, int D, void* stream);
 
+/* ---- a10: backward of the NLL training step --------------------------------
+ * naz's `train` (naz/trainers/train_flows.py:194-213) calls loss.backward() through pyro's
+ * transforms; these are the VJPs of the kernels above.
+ *
+ * naz_rqs_bwd: x = the INPUT the forward/inverse map was applied to; g_out [B, Dt] (may be
+ * NULL) = dL/d(map output); g_ld = dL/d(the ld that naz_rqs_{fwd,inv} returned), per
+ * g_ld_mode 0 none / 1 [B] row-sum / 2 [B, Dt]; writes g_in [B, Dt] (may be NULL) and
+ * g_raw (same layout as raw).  ldr = 0 (one shared parameter row, e.g. a lower spline):
+ * g_raw is [Dt*(3K-1)] and is ACCUMULATED (+=) over the batch.                        */
+int naz_rqs_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* g_out,
+                int64_t ldgo, const float* g_ld, int g_ld_mode, float* g_in, int64_t ldgi, float* g_raw, int64_t ldgr,
+                int64_t B, int Dt, int K, int layout, float bound, void* stream);
+/* C[m,n] (+)= sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn]; exact fp32 MFMA.  With a mask:
+ * mask_b = 0 multiplies the OUTPUT by mask[m*smm + n*smn] (dW of a MADE layer), mask_b = 1
+ * multiplies the B OPERAND by mask[k*smm + n*smn] (dX through W*mask).
+ * split_k > 1 accumulates atomically (zero C first for an overwrite).                     */
+int naz_gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+             int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
+             int mask_b, int accumulate, int split_k, void* stream);
+/* VJP of naz_affine_ar (the kernel reports the FORWARD log-det sum(clamp(ls)) in both
+ * directions).  x = the map's input, y = its output, g_ld [B] = dL/d(row ld) (may be NULL).
+ * pyro clamps log_scale with clamp_preserve_gradients: the clamp passes gradients through.
+ * Writes g_x [B, D] (may be NULL) and g_raw [B, 2D].                                       */
+int naz_affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y,
+                      int64_t ldy, const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx,
+                      float* g_raw, int64_t ldgr, int64_t B, int D, void* stream);
+/* out[n] += sum_m A[m*lda + n]  (atomic; zero `out` first for a plain column sum)         */
+int naz_colsum(const float* A, int64_t lda, int64_t M, int N, float* out, void* stream);
+/* gpre = gy * act'(pre) computed from the post-activation y (tanh, relu, softplus, sigmoid) */
+int naz_act_bwd(const float* gy, int64_t ldg, const float* y, int64_t ldy, float* gpre, int64_t ldp, int64_t M, int N,
+                int act, void* stream);
+/* g_z[r, i] = -z[r, i] * g_lp[r]   (VJP of naz_base_log_prob)                             */
+int naz_base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float* g_z, int64_t ldgz, int64_t B, int D,
+                          void* stream);
+
 /* ---- a3+a8+a9: fused conditional spline-coupling flow ---------------------
  * Replaces the whole of NormalizingFlow.log_prob / .sample (naz/flows/flow.py:45-79,
  * 94-129) for flow_type "nsc" (naz/flows/transforms.py:201-236 intent = pyro

@@ -38,6 +38,15 @@ SIGNATURES = {
     "naz_base_log_prob": (C.c_int, [_vp, _i64, _vp, _i64, _i, _i, _vp]),
     "naz_bounding_fwd": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _i, _vp]),
     "naz_bounding_inv": (C.c_int, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i, _vp]),
+    "naz_rqs_bwd": (C.c_int, [_i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _vp, _i64, _vp, _i64, _i64, _i, _i, _i,
+                              C.c_float, _vp]),
+    "naz_gemm": (C.c_int, [_i, _i, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i, _i,
+                           _i, _vp]),
+    "naz_affine_ar_bwd": (C.c_int, [_i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64,
+                                    _i, _vp]),
+    "naz_colsum": (C.c_int, [_vp, _i64, _i64, _i, _vp, _vp]),
+    "naz_act_bwd": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i, _i, _vp]),
+    "naz_base_log_prob_bwd": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _i64, _i, _vp]),
     "naz_coupling_supported": (C.c_int, [C.POINTER(CouplingDesc)]),
     "naz_coupling_param_count": (C.c_int64, [C.POINTER(CouplingDesc)]),
     "naz_coupling_packed_bytes": (C.c_int64, [C.POINTER(CouplingDesc)]),

@@ -1,0 +1,157 @@
+"""Differentiable HIP ops for the NLL training step.
+
+naz's ``train`` (naz/trainers/train_flows.py:194-213) differentiates
+``-flow.log_prob(x, condition=y).mean()`` through pyro's transforms with torch autograd.
+Here every node of that graph is a ``torch.autograd.Function`` whose forward AND backward
+are HIP kernels:
+
+  LinearActFn   act(cat[ctx, x] @ (W*mask)^T + b)   bwd: naz_act_bwd, naz_gemm (dX, dW with the
+                                                     MADE mask fused), naz_colsum (db)
+  RqsFn         RQ spline, either direction          bwd: naz_rqs_bwd (implicit-function rule
+                                                     for the inverse)
+  AffineARFn    pyro AffineAutoregressive step       bwd: naz_affine_ar_bwd
+  BaseLogProbFn Normal(0, 1) log density              bwd: naz_base_log_prob_bwd
+
+Autograd only sequences the kernels; no torch arithmetic runs on the batch except the
+[B]-sized log-det sums and index copies (cat / permutation gathers).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch.autograd import Function
+
+from . import ops
+
+
+def _needs(ctx, i: int) -> bool:
+    return bool(ctx.needs_input_grad[i])
+
+
+class LinearActFn(Function):
+    """y = act(cat([context, x]) @ (weight * mask)^T + bias).  ``context`` may be one row
+    (broadcast to every row of x), as ``ops.linear_act`` allows."""
+
+    @staticmethod
+    def forward(ctx, x, context, weight, bias, mask, act: str):
+        y = ops.linear_act(x, weight, bias, act, context=context, mask=mask)
+        ctx.act = act
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, context, weight, mask, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        x, c, W, mask, y = ctx.saved_tensors
+        act = ctx.act
+        g_y = g_y.contiguous()
+        gpre = g_y if act == "identity" else ops.act_bwd(g_y, y, act)
+        M = y.shape[0]
+        Cd = 0 if c is None else c.shape[-1]
+        g_x = g_c = g_W = g_b = None
+        if _needs(ctx, 2):
+            g_W = torch.empty_like(W)
+            gT = gpre.t()  # [N, M] view
+            if Cd:
+                cc = c.reshape(1, -1).expand(M, Cd) if (c.dim() == 1 or c.shape[0] == 1) and M != 1 else c
+                ops.gemm(gT, cc, out=g_W[:, :Cd], mask=None if mask is None else mask[:, :Cd])
+            if x is not None:
+                ops.gemm(gT, x, out=g_W[:, Cd:], mask=None if mask is None else mask[:, Cd:])
+        if ctx.has_bias and _needs(ctx, 3):
+            g_b = ops.colsum(gpre)
+        if x is not None and _needs(ctx, 0):
+            g_x = ops.gemm(gpre, W[:, Cd:], mask=None if mask is None else mask[:, Cd:], mask_b=True)
+        if Cd and _needs(ctx, 1):
+            Wc, mc = W[:, :Cd], (None if mask is None else mask[:, :Cd])
+            if c.shape[0] == M and c.dim() == 2:
+                g_c = ops.gemm(gpre, Wc, mask=mc, mask_b=True)
+            else:  # one broadcast row: sum_m gpre[m] @ W = (sum_m gpre[m]) @ W
+                g_c = ops.gemm(ops.colsum(gpre).reshape(1, -1), Wc, mask=mc, mask_b=True).reshape(c.shape)
+        return g_x, g_c, g_W, g_b, None, None
+
+
+def linear_act(x, weight, bias, act="identity", context=None, mask=None):
+    return LinearActFn.apply(x, context, weight, bias, mask, act)
+
+
+class RqsFn(Function):
+    """(y, ld_row) = RQ spline of x over conditioner output ``raw`` (row-sum log-det of THIS
+    direction: the forward ldf, or the inverse's -ldf)."""
+
+    @staticmethod
+    def forward(ctx, x, raw, count_bins: int, layout: int, inverse: bool, bound: float, broadcast: bool):
+        y, ld = ops.rqs(x, raw, count_bins, layout, inverse, bound, ops.LD_ROWSUM, broadcast_raw=broadcast)
+        ctx.cfg = (count_bins, layout, inverse, bound, broadcast)
+        ctx.save_for_backward(x, raw)
+        return y, ld
+
+    @staticmethod
+    def backward(ctx, g_y, g_ld):
+        x, raw = ctx.saved_tensors
+        K, layout, inverse, bound, broadcast = ctx.cfg
+        g_x, g_raw = ops.rqs_bwd(x, raw, K, layout, inverse, bound, g_y, g_ld, need_g_in=_needs(ctx, 0),
+                                 broadcast_raw=broadcast)
+        return g_x, g_raw, None, None, None, None, None
+
+
+def rqs(x, raw, count_bins, layout=ops.LAYOUT_DENSE, inverse=False, bound=3.0, broadcast=False):
+    return RqsFn.apply(x, raw, count_bins, layout, inverse, bound, broadcast)
+
+
+class AffineARFn(Function):
+    """(y, forward ld_row) of pyro's AffineAutoregressive step over MADE output ``raw``."""
+
+    @staticmethod
+    def forward(ctx, x, raw, inverse: bool):
+        y, ld = ops.affine_ar(x, raw, inverse, ops.LD_ROWSUM)
+        ctx.inverse = inverse
+        ctx.save_for_backward(x, raw, y)
+        return y, ld
+
+    @staticmethod
+    def backward(ctx, g_y, g_ld):
+        x, raw, y = ctx.saved_tensors
+        if g_y is None:
+            g_y = torch.zeros_like(y)
+        g_x, g_raw = ops.affine_ar_bwd(x, raw, y, ctx.inverse, g_y, g_ld, need_g_x=_needs(ctx, 0))
+        return g_x, g_raw, None
+
+
+def affine_ar(x, raw, inverse):
+    return AffineARFn.apply(x, raw, inverse)
+
+
+class BaseLogProbFn(Function):
+    """sum_i log N(z_i; 0, 1) per row."""
+
+    @staticmethod
+    def forward(ctx, z):
+        ctx.save_for_backward(z)
+        return ops.base_log_prob(z)
+
+    @staticmethod
+    def backward(ctx, g_lp):
+        (z,) = ctx.saved_tensors
+        return ops.base_log_prob_bwd(z, g_lp.contiguous())
+
+
+def base_log_prob(z):
+    return BaseLogProbFn.apply(z)
+
+
+def params_require_grad(modules) -> bool:
+    """True when autograd must record the walk: grad mode on and some parameter trainable."""
+    if not torch.is_grad_enabled():
+        return False
+    for m in modules:
+        if m is None:
+            continue
+        for p in m.parameters():
+            if p.requires_grad:
+                return True
+    return False
+
+
+def tensor_requires_grad(*ts: Optional[torch.Tensor]) -> bool:
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)

@@ -88,6 +88,48 @@ int naz_bounding_inv(const float* y, int64_t ldy, const float* low, const float*
   return bounding_inv(y, ldy, low, high, x, ldx, B, D, as_stream(stream));
 }
 
+int naz_rqs_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* g_out,
+                int64_t ldgo, const float* g_ld, int g_ld_mode, float* g_in, int64_t ldgi, float* g_raw, int64_t ldgr,
+                int64_t B, int Dt, int K, int layout, float bound, void* stream) {
+  if (int rc = check_spline_args("naz_rqs_bwd", x, x, B, Dt, K, bound)) return rc;
+  if (B > 0 && g_raw == nullptr) return set_error("naz_rqs_bwd: g_raw is required");
+  if (g_ld_mode < 0 || g_ld_mode > 2 || (g_ld_mode != 0 && g_ld == nullptr))
+    return set_error("naz_rqs_bwd: bad g_ld / g_ld_mode");
+  return rqs_bwd(inverse, x, ldx, raw, ldr, g_out, ldgo, g_ld, g_ld_mode, g_in, ldgi, g_raw, ldgr, B, Dt, K, layout,
+                 bound, as_stream(stream));
+}
+
+int naz_gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+             int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
+             int mask_b, int accumulate, int split_k, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return set_error("naz_gemm: negative shape");
+  return gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, mask, smm, smn, mask_b, accumulate, split_k,
+              as_stream(stream));
+}
+
+int naz_affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y,
+                      int64_t ldy, const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx,
+                      float* g_raw, int64_t ldgr, int64_t B, int D, void* stream) {
+  if (B > 0 && (g_raw == nullptr || g_y == nullptr)) return set_error("naz_affine_ar_bwd: g_y and g_raw are required");
+  return affine_ar_bwd(inverse, x, ldx, raw, ldr, y, ldy, g_y, ldgy, g_ld, g_x, ldgx, g_raw, ldgr, B, D,
+                       as_stream(stream));
+}
+
+int naz_colsum(const float* A, int64_t lda, int64_t M, int N, float* out, void* stream) {
+  return colsum(A, lda, M, N, out, as_stream(stream));
+}
+
+int naz_act_bwd(const float* gy, int64_t ldg, const float* y, int64_t ldy, float* gpre, int64_t ldp, int64_t M, int N,
+                int act, void* stream) {
+  if (act < 0 || act > NAZ_ACT_SIGMOID) return set_error("naz_act_bwd: unknown activation %d", act);
+  return act_bwd(gy, ldg, y, ldy, gpre, ldp, M, N, act, as_stream(stream));
+}
+
+int naz_base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float* g_z, int64_t ldgz, int64_t B, int D,
+                          void* stream) {
+  return base_log_prob_bwd(z, ldz, g_lp, g_z, ldgz, B, D, as_stream(stream));
+}
+
 int naz_coupling_supported(const naz_coupling_desc* d) { return coupling_supported(d); }
 int64_t naz_coupling_param_count(const naz_coupling_desc* d) { return coupling_param_count(d); }
 int64_t naz_coupling_packed_bytes(const naz_coupling_desc* d) { return coupling_packed_bytes(d); }

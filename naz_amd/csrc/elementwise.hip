@@ -71,7 +71,68 @@ __global__ void bounding_inv_kernel(const float* __restrict__ yv, int64_t ldy, c
   x[r * ldx + i] = sg * (high[i] - low[i]) + low[i];
 }
 
+__global__ void base_log_prob_bwd_kernel(const float* __restrict__ z, int64_t ldz, const float* __restrict__ g_lp,
+                                         float* __restrict__ g_z, int64_t ldgz, int64_t B, int D) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * D) return;
+  const int64_t r = e / D;
+  const int i = (int)(e - r * D);
+  g_z[r * ldgz + i] = -z[r * ldz + i] * g_lp[r];
+}
+
+// VJP of affine_ar_kernel (clamp_preserve_gradients: the clamp is the identity for gradients)
+//   fwd  y = e^ls x + mean :  g_x = g_y e^ls,   g_mean = g_y,          g_ls = g_y (y - mean) + g_ld
+//   inv  y = (x - mean)e^-ls: g_x = g_y e^-ls,  g_mean = -g_y e^-ls,   g_ls = -g_y y + g_ld
+__global__ void affine_ar_bwd_kernel(int inverse, const float* __restrict__ x, int64_t ldx,
+                                     const float* __restrict__ raw, int64_t ldr, const float* __restrict__ y,
+                                     int64_t ldy, const float* __restrict__ g_y, int64_t ldgy,
+                                     const float* __restrict__ g_ld, float* __restrict__ g_x, int64_t ldgx,
+                                     float* __restrict__ g_raw, int64_t ldgr, int64_t B, int D) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * D) return;
+  const int64_t r = e / D;
+  const int i = (int)(e - r * D);
+  const float mean = raw[r * ldr + i];
+  const float ls = fminf(fmaxf(raw[r * ldr + D + i], -5.f), 3.f);
+  const float gy = g_y[r * ldgy + i], yv = y[r * ldy + i];
+  const float gl = g_ld != nullptr ? g_ld[r] : 0.f;
+  float gx, gm, gs;
+  if (inverse) {
+    const float sc = expf(-ls);
+    gx = gy * sc;
+    gm = -gx;
+    gs = -gy * yv + gl;
+  } else {
+    const float sc = expf(ls);
+    gx = gy * sc;
+    gm = gy;
+    gs = gy * (yv - mean) + gl;
+  }
+  (void)x;
+  (void)ldx;
+  if (g_x != nullptr) g_x[r * ldgx + i] = gx;
+  g_raw[r * ldgr + i] = gm;
+  g_raw[r * ldgr + D + i] = gs;
+}
+
 static unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+int affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y, int64_t ldy,
+                  const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx, float* g_raw,
+                  int64_t ldgr, int64_t B, int D, hipStream_t s) {
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(affine_ar_bwd_kernel, dim3(blocks_for(B * D)), dim3(256), 0, s, inverse, x, ldx, raw, ldr, y,
+                     ldy, g_y, ldgy, g_ld, g_x, ldgx, g_raw, ldgr, B, D);
+  return check_launch("affine_ar_bwd_kernel");
+}
+
+int base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float* g_z, int64_t ldgz, int64_t B, int D,
+                      hipStream_t s) {
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(base_log_prob_bwd_kernel, dim3(blocks_for(B * D)), dim3(256), 0, s, z, ldz, g_lp, g_z, ldgz, B,
+                     D);
+  return check_launch("base_log_prob_bwd_kernel");
+}
 
 int affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
               float* ld, int ld_mode, int64_t B, int D, hipStream_t s) {

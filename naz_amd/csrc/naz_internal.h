@@ -14,6 +14,9 @@ int check_launch(const char* what);
 
 int rqs_cond(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
              float* ld, int ld_mode, int64_t B, int Dt, int K, int layout, float bound, hipStream_t s);
+int rqs_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* g_out, int64_t ldgo,
+            const float* g_ld, int g_ld_mode, float* g_in, int64_t ldgi, float* g_raw, int64_t ldgr, int64_t B, int Dt,
+            int K, int layout, float bound, hipStream_t s);
 int rqs_uncond(int inverse, const float* x, int64_t ldx, const float* uw, const float* uh, const float* ud, float* y,
                int64_t ldy, float* ld, int64_t B, int Dt, int K, float bound, hipStream_t s);
 int linear_act(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx, int Kx, const float* W,
@@ -25,6 +28,18 @@ int bounding_fwd(const float* x, int64_t ldx, const float* low, const float* hig
                  float* out_logjac, int64_t B, int D, hipStream_t s);
 int bounding_inv(const float* y, int64_t ldy, const float* low, const float* high, float* x, int64_t ldx, int64_t B,
                  int D, hipStream_t s);
+
+int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+         float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn, int mask_b, int accumulate,
+         int split_k, hipStream_t s);
+int affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y, int64_t ldy,
+                  const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx, float* g_raw,
+                  int64_t ldgr, int64_t B, int D, hipStream_t s);
+int colsum(const float* A, int64_t lda, int64_t M, int N, float* out, hipStream_t s);
+int act_bwd(const float* gy, int64_t ldg, const float* y, int64_t ldy, float* gp, int64_t ldp, int64_t M, int N, int act,
+            hipStream_t s);
+int base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float* g_z, int64_t ldgz, int64_t B, int D,
+                      hipStream_t s);
 
 int coupling_supported(const naz_coupling_desc* d);
 int64_t coupling_param_count(const naz_coupling_desc* d);

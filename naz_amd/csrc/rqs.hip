@@ -13,6 +13,7 @@
 // HBM-bound: per (row, dim) 4·(3K−1) + 4 bytes in, 4 (+4) bytes out.
 #include "naz_device.h"
 #include "naz_internal.h"
+#include "spline_bwd.h"
 
 namespace naz {
 
@@ -139,6 +140,90 @@ static int launch_rqs_uncond(const float* x, int64_t ldx, const float* uw, const
   return check_launch("rqs_uncond_kernel");
 }
 
+// ---------------------------------------------------------------------------
+// Backward (a10): d(input) and d(raw) from upstream d(output) and d(ld).
+//   g_ld_mode: 0 none, 1 one value per row (the row-sum ld), 2 per (row, dim)
+//   BCAST:     raw is ONE row shared by all rows (ldr = 0, e.g. the coupling's lower spline):
+//              the block reduces d(raw) over its rows in LDS and adds it atomically to g_raw[P].
+// ---------------------------------------------------------------------------
+template <int K, bool INV, bool BCAST>
+__global__ void __launch_bounds__(256) rqs_bwd_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ raw, int64_t ldr,
+    const float* __restrict__ g_out, int64_t ldgo, const float* __restrict__ g_ld, int g_ld_mode,
+    float* __restrict__ g_in, int64_t ldgi, float* __restrict__ g_raw, int64_t ldgr, int64_t B, int Dt, int layout,
+    float bound) {
+  extern __shared__ float lds[];
+  constexpr int PD = 3 * K - 1;
+  const int P = Dt * PD;
+  const int R = (Dt >= 256) ? 1 : 256 / Dt;
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int rows = (int)((B - r0) < R ? (B - r0) : R);
+  float* raw_s = lds;  // [R][P] (BCAST: [1][P]) then, for BCAST, grads [R][P]
+  float* gr_s = lds + (BCAST ? P : (size_t)R * P);
+  if (BCAST) {
+    for (int i = tid; i < P; i += blockDim.x) raw_s[i] = raw[i];
+    for (int i = tid; i < R * P; i += blockDim.x) gr_s[i] = 0.f;
+  } else if (ldr == P) {
+    block_copy_to_lds(raw_s, raw + r0 * ldr, rows * P, tid, blockDim.x);
+  } else {
+    for (int i = tid; i < rows * P; i += blockDim.x) {
+      const int r = i / P, c = i - r * P;
+      raw_s[i] = raw[(r0 + r) * ldr + c];
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < rows * Dt; e += blockDim.x) {
+    const int r = e / Dt, i = e - r * Dt;
+    const float* pr = raw_s + (BCAST ? 0 : (size_t)r * P);
+    float uw[K], uh[K], ud[K - 1];
+    auto col_w = [&](int k) { return layout == NAZ_LAYOUT_DENSE ? i * K + k : k * Dt + i; };
+    auto col_h = [&](int k) { return layout == NAZ_LAYOUT_DENSE ? Dt * K + i * K + k : (K + k) * Dt + i; };
+    auto col_d = [&](int k) { return layout == NAZ_LAYOUT_DENSE ? 2 * Dt * K + i * (K - 1) + k : (2 * K + k) * Dt + i; };
+#pragma unroll
+    for (int k = 0; k < K; ++k) { uw[k] = pr[col_w(k)]; uh[k] = pr[col_h(k)]; }
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) ud[k] = pr[col_d(k)];
+    const int64_t row = r0 + r;
+    const float go = g_out != nullptr ? g_out[row * ldgo + i] : 0.f;
+    const float gl = g_ld_mode == 1 ? g_ld[row] : (g_ld_mode == 2 ? g_ld[row * Dt + i] : 0.f);
+    float gw[K], gh[K], gd[K - 1];
+    const float gi = rqs_vjp<K, INV>(uw, uh, ud, bound, x[row * ldx + i], go, gl, gw, gh, gd);
+    if (g_in != nullptr) g_in[row * ldgi + i] = gi;
+    float* dst = BCAST ? gr_s + (size_t)r * P : g_raw + row * ldgr;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { dst[col_w(k)] = gw[k]; dst[col_h(k)] = gh[k]; }
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) dst[col_d(k)] = gd[k];
+  }
+  if (BCAST) {
+    __syncthreads();
+    for (int c = tid; c < P; c += blockDim.x) {
+      float s = 0.f;
+      for (int r = 0; r < rows; ++r) s += gr_s[(size_t)r * P + c];
+      atomicAdd(g_raw + c, s);
+    }
+  }
+}
+
+template <int K, bool INV>
+static int launch_rqs_bwd(const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* g_out,
+                          int64_t ldgo, const float* g_ld, int g_ld_mode, float* g_in, int64_t ldgi, float* g_raw,
+                          int64_t ldgr, int64_t B, int Dt, int layout, float bound, bool bcast, hipStream_t s) {
+  const int R = (Dt >= 256) ? 1 : 256 / Dt;
+  const size_t P = (size_t)Dt * (3 * K - 1);
+  const size_t lds = (bcast ? (P + (size_t)R * P) : (size_t)R * P) * sizeof(float);
+  if (lds > 160 * 1024) return set_error("naz_rqs_bwd: Dt*K too large for one LDS block (%zu bytes)", lds);
+  const int64_t grid = (B + R - 1) / R;
+  if (bcast)
+    hipLaunchKernelGGL((rqs_bwd_kernel<K, INV, true>), dim3((unsigned)grid), dim3(256), lds, s, x, ldx, raw, ldr, g_out,
+                       ldgo, g_ld, g_ld_mode, g_in, ldgi, g_raw, ldgr, B, Dt, layout, bound);
+  else
+    hipLaunchKernelGGL((rqs_bwd_kernel<K, INV, false>), dim3((unsigned)grid), dim3(256), lds, s, x, ldx, raw, ldr,
+                       g_out, ldgo, g_ld, g_ld_mode, g_in, ldgi, g_raw, ldgr, B, Dt, layout, bound);
+  return check_launch("rqs_bwd_kernel");
+}
+
 #define NAZ_K_DISPATCH(K_, CALL) \
   switch (K_) {                  \
     case 2: CALL(2); break;      \
@@ -162,6 +247,22 @@ int rqs_cond(int inverse, const float* x, int64_t ldx, const float* raw, int64_t
                : launch_rqs_cond<KK, false>(x, ldx, raw, ldr, y, ldy, ld, ld_mode, B, Dt, layout, bound, s)
   NAZ_K_DISPATCH(K, CALLC)
 #undef CALLC
+  return rc;
+}
+
+int rqs_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* g_out, int64_t ldgo,
+            const float* g_ld, int g_ld_mode, float* g_in, int64_t ldgi, float* g_raw, int64_t ldgr, int64_t B, int Dt,
+            int K, int layout, float bound, hipStream_t s) {
+  if (B == 0) return 0;
+  const bool bcast = ldr == 0;
+  int rc = 0;
+#define CALLB(KK)                                                                                                 \
+  rc = inverse ? launch_rqs_bwd<KK, true>(x, ldx, raw, ldr, g_out, ldgo, g_ld, g_ld_mode, g_in, ldgi, g_raw, ldgr, \
+                                          B, Dt, layout, bound, bcast, s)                                       \
+               : launch_rqs_bwd<KK, false>(x, ldx, raw, ldr, g_out, ldgo, g_ld, g_ld_mode, g_in, ldgi, g_raw,    \
+                                           ldgr, B, Dt, layout, bound, bcast, s)
+  NAZ_K_DISPATCH(K, CALLB)
+#undef CALLB
   return rc;
 }
 

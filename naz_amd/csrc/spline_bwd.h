@@ -1,0 +1,157 @@
+// Vector-Jacobian product of the rational-quadratic spline (SURVEY.md §8a a1+a2, backward for
+// the NLL training step a10).
+//
+// Both directions share the per-bin parameterisation  x = cw0 + W·θ,  y = F(θ) with
+//   F(θ)  = ch0 + H·N/Dn,   N = δθ² + d0·θ(1-θ),   Dn = δ + (d0 + d1 − 2δ)·θ(1-θ),   δ = H/W
+//   ldf(θ) = log δ² + log G − 2 log Dn,   G = d1θ² + 2δθ(1-θ) + d0(1-θ)²      (= log dy/dx)
+// forward:  θ = (x − cw0)/W, outputs (y, ldf);   inverse: θ solves F(θ) = y (pyro's root formula),
+// outputs (x, −ldf).  The inverse's parameter gradient uses the implicit-function rule
+// dθ/dp = −F_p / F_θ (equal to differentiating pyro's closed-form root in exact arithmetic).
+// Then: bin quantities -> knots (pinned ends carry no gradient, like pyro's in-place
+// knots[...,0] = lower) -> cumsum -> min-width blend -> softmax, and slopes -> softplus.
+#pragma once
+#include "naz_device.h"
+
+namespace naz {
+
+// Returns dL/d(input); accumulates nothing else — writes dL/d(unnormalised params) into
+// gw[K], gh[K], gd[K-1].  g_out: upstream gradient on the map's output; g_ld: upstream gradient on
+// the log-det the kernel returns for this direction (forward ld, or the inverse map's ld).
+template <int K, bool INV>
+NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float bound, float v, float g_out,
+                      float g_ld, float* gw, float* gh, float* gd) {
+  using M = Math<false>;
+#pragma unroll
+  for (int k = 0; k < K; ++k) { gw[k] = 0.f; gh[k] = 0.f; }
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k) gd[k] = 0.f;
+  if (!(v >= -bound && v <= bound)) return g_out;  // identity tails
+
+  float fw[K], fh[K];
+  softmax_k<K>(uw, fw);
+  softmax_k<K>(uh, fh);
+  SplineTables<K> t;
+  knots_from_fractions<K>(fw, kMinBinWidth, bound, t.cw);
+  knots_from_fractions<K>(fh, kMinBinHeight, bound, t.ch);
+  t.dv[0] = 1.f - kMinDerivative;
+  t.dv[K] = 1.f - kMinDerivative;
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k) t.dv[k + 1] = kMinDerivative + softplus(ud[k]);
+
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k <= K; ++k) cnt += (v >= (INV ? t.ch[k] : t.cw[k]) + kSearchEps) ? 1 : 0;
+  int idx = cnt - 1;
+  idx = idx < 0 ? 0 : (idx > K - 1 ? K - 1 : idx);
+  float cw0 = t.cw[0], cw1 = t.cw[1], ch0 = t.ch[0], ch1 = t.ch[1], d0 = t.dv[0], d1 = t.dv[1];
+#pragma unroll
+  for (int k = 1; k < K; ++k) {
+    const bool s = idx == k;
+    cw0 = s ? t.cw[k] : cw0;
+    cw1 = s ? t.cw[k + 1] : cw1;
+    ch0 = s ? t.ch[k] : ch0;
+    ch1 = s ? t.ch[k + 1] : ch1;
+    d0 = s ? t.dv[k] : d0;
+    d1 = s ? t.dv[k + 1] : d1;
+  }
+  const float W = cw1 - cw0, H = ch1 - ch0, delta = H / W;
+  const float T1 = (d0 + d1) - 2.f * delta;
+  float th;
+  if constexpr (INV) {
+    const float dy = v - ch0;
+    const float a = dy * T1 + H * (delta - d0);
+    const float b = H * d0 - dy * T1;
+    const float c = -delta * dy;
+    th = (2.f * c) / (-b - M::sqrt(b * b - 4.f * a * c));
+  } else {
+    th = (v - cw0) / W;
+  }
+  const float om = 1.f - th, tt = th * om;
+  const float N = delta * th * th + d0 * tt;
+  const float Dn = delta + T1 * tt;
+  const float G = d1 * th * th + 2.f * delta * tt + d0 * om * om;
+  const float iDn = 1.f / Dn, iG = 1.f / G;
+  // dF/dθ and the other partials of F and ldf
+  const float Np = 2.f * delta * th + d0 * (1.f - 2.f * th);
+  const float Dp = T1 * (1.f - 2.f * th);
+  const float F_th = H * (Np * Dn - N * Dp) * iDn * iDn;
+  const float F_H = N * iDn;
+  const float F_dl = H * (th * th * Dn - N * (1.f - 2.f * tt)) * iDn * iDn;
+  const float F_d0 = H * tt * (Dn - N) * iDn * iDn;
+  const float F_d1 = -H * N * tt * iDn * iDn;
+  const float Gp = 2.f * d1 * th + 2.f * delta * (1.f - 2.f * th) - 2.f * d0 * om;
+  const float L_th = Gp * iG - 2.f * Dp * iDn;
+  const float L_dl = 2.f / delta + 2.f * tt * iG - 2.f * (1.f - 2.f * tt) * iDn;
+  const float L_d0 = om * om * iG - 2.f * tt * iDn;
+  const float L_d1 = th * th * iG - 2.f * tt * iDn;
+
+  float g_in, gch0, gH, gdl, gd0, gd1, gcw0, gW;
+  if constexpr (!INV) {
+    const float gth = g_out * F_th + g_ld * L_th;
+    gch0 = g_out;
+    gH = g_out * F_H;
+    gdl = g_out * F_dl + g_ld * L_dl;
+    gd0 = g_out * F_d0 + g_ld * L_d0;
+    gd1 = g_out * F_d1 + g_ld * L_d1;
+    g_in = gth / W;
+    gcw0 = -gth / W;
+    gW = -gth * th / W;
+  } else {
+    // outputs x = cw0 + W·θ and ld_inv = −ldf(θ)
+    const float gth = g_out * W - g_ld * L_th;
+    gcw0 = g_out;
+    gW = g_out * th;
+    gdl = -g_ld * L_dl;
+    gd0 = -g_ld * L_d0;
+    gd1 = -g_ld * L_d1;
+    // implicit θ(y, p): dθ/dy = 1/F_θ, dθ/dp = −F_p/F_θ
+    const float r = gth / F_th;
+    g_in = r;
+    gch0 = -r;
+    gH = -r * F_H;
+    gdl += -r * F_dl;
+    gd0 += -r * F_d0;
+    gd1 += -r * F_d1;
+  }
+  // δ = H / W
+  gH += gdl / W;
+  gW += -gdl * delta / W;
+  // bin quantities -> knot / slope arrays
+  float gcw[K + 1], gch[K + 1], gdv[K + 1];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) {
+    const float a0 = (k == idx) ? 1.f : 0.f, a1 = (k == idx + 1) ? 1.f : 0.f;
+    gcw[k] = a0 * (gcw0 - gW) + a1 * gW;
+    gch[k] = a0 * (gch0 - gH) + a1 * gH;
+    gdv[k] = a0 * gd0 + a1 * gd1;
+  }
+  // knots j = 1..K-1 (ends pinned): cw_j = 2B·Σ_{i<j} w_i − B  ->  g_w_i = 2B Σ_{j=i+1}^{K-1} g_cw_j
+  const float s_w = 1.f - kMinBinWidth * (float)K, s_h = 1.f - kMinBinHeight * (float)K;
+  float gfw[K], gfh[K];
+  float accw = 0.f, acch = 0.f;
+#pragma unroll
+  for (int i = K - 1; i >= 0; --i) {
+    gfw[i] = 2.f * bound * accw * s_w;
+    gfh[i] = 2.f * bound * acch * s_h;
+    if (i >= 1) {
+      accw += gcw[i];
+      acch += gch[i];
+    }
+  }
+  float dotw = 0.f, doth = 0.f;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    dotw += fw[i] * gfw[i];
+    doth += fh[i] * gfh[i];
+  }
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    gw[i] = fw[i] * (gfw[i] - dotw);
+    gh[i] = fh[i] * (gfh[i] - doth);
+  }
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k) gd[k] = gdv[k + 1] / (1.f + M::exp(-ud[k]));  // softplus' = sigmoid
+  return g_in;
+}
+
+}  // namespace naz

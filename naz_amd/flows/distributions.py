@@ -14,6 +14,7 @@ from typing import List, Optional
 
 import torch
 
+from .. import autograd as ag
 from .. import ops
 
 
@@ -38,6 +39,35 @@ class TransformedDistribution:
     def event_dim(self):
         return 1
 
+    def _trainable_modules(self):
+        mods = []
+        for t in self.transforms:
+            for attr in ("module", "arn", "inner", "arn_module"):
+                m = getattr(t, attr, None)
+                if isinstance(m, torch.nn.Module):
+                    mods.append(m)
+            if isinstance(t, torch.nn.Module):
+                mods.append(t)
+        return mods
+
+    def _needs_graph(self, y) -> bool:
+        return ag.params_require_grad(self._trainable_modules()) or ag.tensor_requires_grad(y, self._context)
+
+    def _log_prob_graph(self, y: torch.Tensor, bounds=None) -> torch.Tensor:
+        """Autograd-recorded walk (training, a10): same order as torch's TransformedDistribution,
+        every node a HIP kernel with a HIP backward.  The bounding map (naz/flows/flow.py:52-70)
+        acts on the data only and is evaluated outside the graph."""
+        acc = None
+        if bounds is not None:
+            with torch.no_grad():
+                y, acc = ops.bounding_fwd(y.detach(), bounds["low"], bounds["high"])
+        for t in reversed(self.transforms):
+            y, ld = t._inv_ld(y)
+            if ld is not None:
+                acc = -ld if acc is None else acc - ld
+        lp = ag.base_log_prob(y)
+        return lp if acc is None else lp + acc
+
     def _log_prob_into(self, y: torch.Tensor, lp: torch.Tensor, bounds=None) -> torch.Tensor:
         if self._fused is not None:
             return self._fused.log_prob(y, self._context, bounds=bounds, out=lp)
@@ -51,6 +81,8 @@ class TransformedDistribution:
 
     def log_prob(self, value: torch.Tensor, bounds=None) -> torch.Tensor:
         y, lead = _rows2d(value)
+        if self._needs_graph(y):
+            return self._log_prob_graph(y, bounds).reshape(lead)
         lp = torch.zeros(y.shape[0], device=y.device, dtype=torch.float32)
         return self._log_prob_into(y, lp, bounds).reshape(lead)
 

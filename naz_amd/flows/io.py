@@ -29,6 +29,22 @@ def _lower(t):
     return getattr(t, "lower_spline", None)
 
 
+def named_state_params(flow) -> Dict[str, torch.nn.Parameter]:
+    """Canonical key -> the live trainable tensor (what get_params/set_params in
+    naz/trainers/train_flows.py:20-71 walk; gradients are read back by the same keys)."""
+    out = {}
+    for l, t in enumerate(_layers(flow)):
+        p = f"layers.{l}."
+        for i, lin in enumerate(t.nn.layers):
+            out[p + f"nn.layers.{i}.weight"] = lin.weight
+            out[p + f"nn.layers.{i}.bias"] = lin.bias
+        low = _lower(t)
+        if low is not None:
+            for n in ("widths", "heights", "derivatives"):
+                out[p + "lower_spline.unnormalized_" + n] = getattr(low, "unnormalized_" + n)
+    return out
+
+
 def export_state(flow) -> Dict[str, np.ndarray]:
     out = {}
     for l, t in enumerate(_layers(flow)):

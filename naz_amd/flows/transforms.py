@@ -22,6 +22,7 @@ from torch import nn
 from torch.distributions import Transform, constraints
 import torch.nn.functional as F
 
+from .. import autograd as ag
 from .. import ops
 from ..nn import (AutoRegressiveNN, ConditionalAutoRegressiveNN, ConditionalDenseNN, DenseNN)
 from ..utils import device, set_device
@@ -97,6 +98,14 @@ class ComposeTransformModule(TransformModule):
         for p in self._all:
             x = p._call_acc(x, ld)
         return x
+
+    def _inv_ld(self, y):
+        total = None
+        for p in reversed(self._all):
+            y, ld = p._inv_ld(y)
+            if ld is not None:
+                total = ld if total is None else total + ld
+        return y, total
 
 
 class ConditionalComposeTransformModule(ConditionalTransformModule):
@@ -246,6 +255,22 @@ class _ConditionedSplineCoupling(_LDCache, Transform):
     def _call_acc(self, x, ld):
         return self._map(x, False, ld, ops.LD_ROWSUM_ADD)
 
+    def _inv_ld(self, y):
+        """Differentiable x = T^-1(y) and the FORWARD row log-det (training walk, a10)."""
+        m = self.module
+        s = m.split_dim
+        y1, y2 = y[:, :s], y[:, s:]
+        ld_inv = None
+        if m.lower_spline is not None:
+            x1, ld_inv = ag.rqs(y1, m.lower_spline.flat_raw(), m.count_bins, ops.LAYOUT_DENSE, True, m.bound,
+                                broadcast=True)
+        else:
+            x1 = y1
+        raw = m.nn.raw(x1, self.context)
+        x2, ld2 = ag.rqs(y2, raw, m.count_bins, ops.LAYOUT_DENSE, True, m.bound)
+        ld_inv = ld2 if ld_inv is None else ld_inv + ld2
+        return torch.cat([x1, x2], dim=1), -ld_inv
+
 
 class ConditionalSplineCoupling(ConditionalTransformModule):
     """naz ``ConditionalSplineCoupling`` (naz/flows/transforms.py:113-129), made runnable:
@@ -344,6 +369,15 @@ class _ConditionedSplineAutoregressive(_LDCache, Transform):
     def _call_acc(self, x, ld):
         return self._map(x, False, ld, ops.LD_ROWSUM_ADD)
 
+    def _inv_ld(self, y):
+        """Differentiable D-pass inverse; autograd runs back through every pass, as pyro's does."""
+        x = torch.zeros_like(y)
+        ld = None
+        for _ in range(y.shape[-1]):
+            raw = self.arn.raw(x, self.context)
+            x, ld = ag.rqs(y, raw, self.count_bins, ops.LAYOUT_ARN, True, self.bound)
+        return x, -ld
+
 
 class ConditionalSplineAutoregressive(ConditionalTransformModule):
     """[pyro] ConditionalSplineAutoregressive (naz/flows/transforms.py:190)."""
@@ -436,6 +470,15 @@ class _ConditionedAffineAutoregressive(_LDCache, Transform):
     def _call_acc(self, x, ld):
         return self._map(x, False, ld, ops.LD_ROWSUM_ADD)
 
+    def _inv_ld(self, y):
+        """Differentiable D-pass inverse; the affine kernel reports the forward log-det."""
+        x = torch.zeros_like(y)
+        ld = None
+        for _ in range(y.shape[-1]):
+            raw = self.arn.raw(x, self.context)
+            x, ld = ag.affine_ar(y, raw, True)
+        return x, ld
+
 
 class ConditionalAffineAutoregressive(ConditionalTransformModule):
     """[pyro] ConditionalAffineAutoregressive (naz/flows/transforms.py:159)."""
@@ -497,6 +540,9 @@ class Permute(Transform):
 
     def _call_acc(self, x, ld):
         return self._call(x)
+
+    def _inv_ld(self, y):
+        return self._inverse(y), None
 
 
 # ----------------------------------------------------------------------------- factories

@@ -14,6 +14,7 @@ from typing import List, Optional, Sequence
 import torch
 from torch import nn
 
+from . import autograd as ag
 from . import ops
 
 
@@ -76,15 +77,19 @@ def _slices(param_dims: Sequence[int]):
 
 
 def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Tensor], masked: bool) -> torch.Tensor:
+    """The conditioner pass; recorded for autograd (HIP backward kernels) when grad mode is on
+    and a weight, the input or the context requires grad."""
     n = len(layers)
+    grad = ag.params_require_grad(layers) or ag.tensor_requires_grad(x, context)
+    lin = ag.linear_act if grad else ops.linear_act
     h = None
     for i, layer in enumerate(layers):
         act = f_name if i < n - 1 else "identity"
         m = layer.mask if masked else None
         if i == 0:
-            h = ops.linear_act(x, layer.weight, layer.bias, act, context=context, mask=m)
+            h = lin(x, layer.weight, layer.bias, act, context=context, mask=m)
         else:
-            h = ops.linear_act(h, layer.weight, layer.bias, act, mask=m)
+            h = lin(h, layer.weight, layer.bias, act, mask=m)
     return h
 
 

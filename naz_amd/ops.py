@@ -16,7 +16,8 @@ from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, LD_PERDIM, LD_ROWSUM, LD_ROWSU
 
 Tensor = torch.Tensor
 
-__all__ = ["rqs", "spline_elementwise", "linear_act", "affine_ar", "base_log_prob", "bounding_fwd", "bounding_inv",
+__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "affine_ar", "affine_ar_bwd", "base_log_prob",
+           "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
            "coupling_sample", "LAYOUT_ARN", "LAYOUT_DENSE", "LD_PERDIM", "LD_ROWSUM", "LD_ROWSUM_ADD",
            "LD_ROWSUM_SUB"]
@@ -188,6 +189,120 @@ def bounding_inv(y: Tensor, low: Tensor, high: Tensor) -> Tensor:
     check(lib().naz_bounding_inv(_p(y), ldy, _p(low.contiguous()), _p(high.contiguous()), _p(x), x.stride(0), B, D,
                                  _stream(dev)), "bounding_inv")
     return x
+
+
+# ----------------------------------------------------------------------------- a10 backward
+def rqs_bwd(x: Tensor, raw: Tensor, count_bins: int, layout: int, inverse: bool, bound: float,
+            g_out: Optional[Tensor], g_ld: Optional[Tensor], need_g_in: bool = True,
+            broadcast_raw: bool = False) -> Tuple[Optional[Tensor], Tensor]:
+    """VJP of ``rqs`` (naz_rqs_bwd).  ``g_ld``: [B] (gradient of the row-sum ld) or [B, Dt]
+    (per-dim ld) or None.  Returns (g_x or None, g_raw shaped like ``raw``)."""
+    dev = _dev(x, raw, g_out, g_ld)
+    x, ldx = _rows(x)
+    B, Dt = x.shape
+    P = Dt * (3 * count_bins - 1)
+    if broadcast_raw:
+        raw_c = raw.reshape(1, -1).contiguous()
+        ldr = 0
+        g_raw = torch.zeros(P, device=dev, dtype=torch.float32)
+        ldgr = 0
+    else:
+        raw_c, ldr = _rows(raw)
+        g_raw = torch.empty((B, P), device=dev, dtype=torch.float32)
+        ldgr = P
+    ldgo = 0
+    if g_out is not None:
+        g_out, ldgo = _rows(g_out)
+    mode = 0
+    if g_ld is not None:
+        g_ld = g_ld.contiguous()
+        mode = 1 if g_ld.dim() == 1 else 2
+    g_in = torch.empty((B, Dt), device=dev, dtype=torch.float32) if need_g_in else None
+    check(lib().naz_rqs_bwd(int(inverse), _p(x), ldx, _p(raw_c), ldr, _p(g_out), ldgo, _p(g_ld), mode, _p(g_in), Dt,
+                            _p(g_raw), ldgr, B, Dt, count_bins, layout, float(bound), _stream(dev)), "rqs_bwd")
+    return g_in, (g_raw.reshape(raw.shape) if broadcast_raw else g_raw)
+
+
+def affine_ar_bwd(x: Tensor, raw: Tensor, y: Tensor, inverse: bool, g_y: Tensor, g_ld: Optional[Tensor],
+                  need_g_x: bool = True) -> Tuple[Optional[Tensor], Tensor]:
+    """VJP of ``affine_ar`` with a row-sum ld (naz_affine_ar_bwd)."""
+    dev = _dev(x, raw, y, g_y, g_ld)
+    x, ldx = _rows(x)
+    raw, ldr = _rows(raw)
+    y, ldy = _rows(y)
+    g_y, ldgy = _rows(g_y)
+    B, D = x.shape
+    g_ld = None if g_ld is None else g_ld.contiguous()
+    g_x = torch.empty((B, D), device=dev, dtype=torch.float32) if need_g_x else None
+    g_raw = torch.empty((B, 2 * D), device=dev, dtype=torch.float32)
+    check(lib().naz_affine_ar_bwd(int(inverse), _p(x), ldx, _p(raw), ldr, _p(y), ldy, _p(g_y), ldgy, _p(g_ld),
+                                  _p(g_x), D, _p(g_raw), 2 * D, B, D, _stream(dev)), "affine_ar_bwd")
+    return g_x, g_raw
+
+
+def base_log_prob_bwd(z: Tensor, g_lp: Tensor) -> Tensor:
+    dev = _dev(z, g_lp)
+    z, ldz = _rows(z)
+    B, D = z.shape
+    g_z = torch.empty((B, D), device=dev, dtype=torch.float32)
+    check(lib().naz_base_log_prob_bwd(_p(z), ldz, _p(g_lp.contiguous()), _p(g_z), D, B, D, _stream(dev)),
+          "base_log_prob_bwd")
+    return g_z
+
+
+def _split_k(M: int, N: int, K: int) -> int:
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    want = max(1, 2048 // tiles)
+    return int(max(1, min(want, K // 512)))
+
+
+def gemm(a: Tensor, b: Tensor, out: Optional[Tensor] = None, mask: Optional[Tensor] = None, mask_b: bool = False,
+         accumulate: bool = False, split_k: Optional[int] = None) -> Tensor:
+    """out (+)= a @ b for arbitrary-strided 2-D views (transposes / stride-0 broadcasts are
+    free); ``mask`` multiplies the output (mask_b False) or ``b`` (mask_b True).  Exact fp32
+    MFMA (naz_gemm); long reductions are split over the grid with atomic accumulation."""
+    dev = _dev(a, b, out, mask)
+    M, K = a.shape
+    K2, N = b.shape
+    if K2 != K:
+        raise ValueError(f"gemm: inner dims differ ({K} vs {K2})")
+    if out is None:
+        out = torch.empty((M, N), device=dev, dtype=torch.float32)
+        accumulate = False
+    if out.shape != (M, N):
+        raise ValueError(f"gemm: out must be {(M, N)}")
+    if mask is not None and mask.shape != ((K, N) if mask_b else (M, N)):
+        raise ValueError("gemm: mask shape mismatch")
+    sk = _split_k(M, N, K) if split_k is None else int(split_k)
+    if sk > 1 and not accumulate:
+        out.zero_()
+    smm, smn = (0, 0) if mask is None else mask.stride()
+    check(lib().naz_gemm(M, N, K, _p(a), a.stride(0), a.stride(1), _p(b), b.stride(0), b.stride(1), _p(out),
+                         out.stride(0), out.stride(1), _p(mask), smm, smn, int(mask_b), int(accumulate), sk,
+                         _stream(dev)), "gemm")
+    return out
+
+
+def colsum(a: Tensor, out: Optional[Tensor] = None) -> Tensor:
+    """out (+)= a.sum(0) (naz_colsum; ``out`` is zeroed when allocated here)."""
+    dev = _dev(a, out)
+    a, lda = _rows(a)
+    M, N = a.shape
+    if out is None:
+        out = torch.zeros(N, device=dev, dtype=torch.float32)
+    check(lib().naz_colsum(_p(a), lda, M, N, _p(out), _stream(dev)), "colsum")
+    return out
+
+
+def act_bwd(g_y: Tensor, y: Tensor, act: str) -> Tensor:
+    """dL/d(pre-activation) from dL/dy and the post-activation y (naz_act_bwd)."""
+    dev = _dev(g_y, y)
+    g_y, ldg = _rows(g_y)
+    y, ldy = _rows(y)
+    M, N = y.shape
+    gp = torch.empty((M, N), device=dev, dtype=torch.float32)
+    check(lib().naz_act_bwd(_p(g_y), ldg, _p(y), ldy, _p(gp), N, M, N, ACT[act], _stream(dev)), "act_bwd")
+    return gp
 
 
 # ----------------------------------------------------------------------------- a3 + a8 + a9 fused

@@ -307,7 +307,9 @@ class SplineAutoregressive:
 
 
 def _clamp(t: Tensor, lo: float, hi: float) -> Tensor:
-    return t.clamp(min=lo, max=hi)
+    """[pyro] distributions/transforms/utils.py::clamp_preserve_gradients, which
+    AffineAutoregressive applies to log_scale: clamped value, identity gradient."""
+    return t + (t.clamp(min=lo, max=hi) - t).detach()
 
 
 class AffineAutoregressive:

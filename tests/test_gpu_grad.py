@@ -1,0 +1,252 @@
+"""GPU: the NLL training step's backward kernels against the oracle's
+float64 torch autograd (the gradient pyro's eager transforms produce, restated in
+oracle/naz_oracle.py), with the oracle's float32 autograd as the reference-precision yardstick.
+
+Criterion: tests/parity.py statistics with the gradient floor max(|g64|, rms(g64)) and the
+4x exceedance-count factor (see tests/parity.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import naz_oracle as O
+from tests.conftest import load_golden, spec_state
+from tests.parity import assert_parity, grad_floor
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _cuda(a):
+    return torch.as_tensor(np.asarray(a), dtype=torch.float32, device=DEV)
+
+
+def _np(t):
+    return t.detach().double().cpu().numpy()
+
+
+def _check(v, g64, g32, what):
+    g64 = _np(g64) if torch.is_tensor(g64) else g64
+    g32 = _np(g32) if torch.is_tensor(g32) else g32
+    return assert_parity(_np(v), g64, g32, what=what, floor=grad_floor(g64), count_factor=4.0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from naz_amd import _lib
+    _lib.lib()
+
+
+def _oracle_rqs_grads(x, raw, Dt, K, layout, inverse, g_out, g_ld, dtype, per_dim):
+    xo = torch.as_tensor(x).to(dtype).requires_grad_(True)
+    ro = torch.as_tensor(raw).to(dtype).requires_grad_(True)
+    y, ld = O.rqs_from_raw(xo, ro, Dt, K, layout, inverse)
+    gl = torch.as_tensor(g_ld).to(dtype)
+    loss = (y * torch.as_tensor(g_out).to(dtype)).sum()
+    loss = loss + ((ld * gl).sum() if per_dim else (ld.sum(-1) * gl).sum())
+    gx, gr = torch.autograd.grad(loss, [xo, ro])
+    return gx, gr
+
+
+# ------------------------------------------------------------------ a1+a2 spline VJP
+@pytest.mark.parametrize("name", ["rqs_dense_k8.npz", "rqs_arn_k5.npz", "rqs_dense_k16.npz"])
+@pytest.mark.parametrize("inverse", [False, True])
+@pytest.mark.parametrize("per_dim", [False, True])
+def test_rqs_bwd_vs_oracle(name, inverse, per_dim):
+    from naz_amd import ops
+    fx = load_golden(name)
+    K, Dt, layout = int(fx["K"]), int(fx["Dt"]), int(fx["layout"])
+    x, raw = fx["x"], fx["raw"]
+    B = x.shape[0]
+    rng = np.random.default_rng(7)
+    g_out = rng.standard_normal((B, Dt)).astype(np.float32)
+    g_ld = rng.standard_normal((B, Dt) if per_dim else (B,)).astype(np.float32)
+    gx, gr = ops.rqs_bwd(_cuda(x), _cuda(raw), K, layout, inverse, 3.0, _cuda(g_out), _cuda(g_ld))
+    gx64, gr64 = _oracle_rqs_grads(x, raw, Dt, K, layout, inverse, g_out, g_ld, torch.float64, per_dim)
+    gx32, gr32 = _oracle_rqs_grads(x, raw, Dt, K, layout, inverse, g_out, g_ld, torch.float32, per_dim)
+    _check(gx, gx64, gx32, f"{name} inv={inverse} d/dx")
+    _check(gr, gr64, gr32, f"{name} inv={inverse} d/draw")
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_rqs_bwd_broadcast_params(inverse):
+    """The coupling's lower spline: ONE parameter row for every batch row (ldr = 0); the
+    parameter gradient is reduced over the batch in-kernel."""
+    from naz_amd import ops
+    K, Dt, B = 8, 8, 3000
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal((B, Dt)) * 1.5).astype(np.float32)
+    raw = (rng.standard_normal(Dt * (3 * K - 1)) * 0.7).astype(np.float32)
+    g_out = rng.standard_normal((B, Dt)).astype(np.float32)
+    g_ld = rng.standard_normal(B).astype(np.float32)
+    gx, gr = ops.rqs_bwd(_cuda(x), _cuda(raw), K, O.LAYOUT_DENSE, inverse, 3.0, _cuda(g_out), _cuda(g_ld),
+                         broadcast_raw=True)
+    refs = []
+    for dt in (torch.float64, torch.float32):
+        ro = torch.as_tensor(raw).to(dt).requires_grad_(True)
+        xo = torch.as_tensor(x).to(dt).requires_grad_(True)
+        y, ld = O.rqs_from_raw(xo, ro.expand(B, -1), Dt, K, O.LAYOUT_DENSE, inverse)
+        loss = (y * torch.as_tensor(g_out).to(dt)).sum() + (ld.sum(-1) * torch.as_tensor(g_ld).to(dt)).sum()
+        refs.append(torch.autograd.grad(loss, [xo, ro]))
+    _check(gx, refs[0][0], refs[1][0], "broadcast d/dx")
+    _check(gr, refs[0][1], refs[1][1], "broadcast d/draw (batch-reduced)")
+
+
+# ------------------------------------------------------------------ a6/a7 conditioner VJP
+@pytest.mark.parametrize("act", ["identity", "tanh", "relu", "softplus", "sigmoid"])
+@pytest.mark.parametrize("ctx_kind", ["none", "rows", "one_row"])
+@pytest.mark.parametrize("masked", [False, True])
+def test_linear_act_grad(act, ctx_kind, masked):
+    from naz_amd import autograd as ag
+    rng = np.random.default_rng(11)
+    M, Kx, C, N = 1000, 24, (0 if ctx_kind == "none" else 13), 70
+    x = rng.standard_normal((M, Kx)).astype(np.float32)
+    W = (rng.standard_normal((N, C + Kx)) / np.sqrt(C + Kx)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32) * 0.1
+    mask = (rng.random((N, C + Kx)) > 0.4).astype(np.float32) if masked else None
+    ctx = None
+    if ctx_kind == "rows":
+        ctx = rng.standard_normal((M, C)).astype(np.float32)
+    elif ctx_kind == "one_row":
+        ctx = rng.standard_normal((1, C)).astype(np.float32)
+    gy = rng.standard_normal((M, N)).astype(np.float32)
+
+    def run(dev, dt, kernel):
+        ts = {"x": torch.as_tensor(x, device=dev, dtype=dt), "W": torch.as_tensor(W, device=dev, dtype=dt),
+              "b": torch.as_tensor(b, device=dev, dtype=dt)}
+        if ctx is not None:
+            ts["c"] = torch.as_tensor(ctx, device=dev, dtype=dt)
+        for t in ts.values():
+            t.requires_grad_(True)
+        m = None if mask is None else torch.as_tensor(mask, device=dev, dtype=dt)
+        if kernel:
+            y = ag.linear_act(ts["x"], ts["W"], ts["b"], act, context=ts.get("c"), mask=m)
+        else:
+            inp = ts["x"] if ctx is None else torch.cat([ts["c"].expand(M, C), ts["x"]], 1)
+            Wm = ts["W"] if m is None else ts["W"] * m
+            y = O.ACTIVATIONS[act](inp @ Wm.t() + ts["b"])
+        keys = list(ts)
+        gs = torch.autograd.grad((y * torch.as_tensor(gy, device=dev, dtype=dt)).sum(), [ts[k] for k in keys])
+        return dict(zip(keys, gs))
+
+    got = run(DEV, torch.float32, True)
+    r64 = run("cpu", torch.float64, False)
+    r32 = run("cpu", torch.float32, False)
+    for k in got:
+        _check(got[k], r64[k], r32[k], f"linear_act[{act},{ctx_kind},mask={masked}] d/d{k}")
+
+
+@pytest.mark.parametrize("M,N,K,split", [(128, 40, 50000, None), (184, 128, 4097, 7), (3, 5, 1, None),
+                                         (1000, 24, 70, None), (65, 130, 200000, None)])
+def test_gemm_strided_split_k(M, N, K, split):
+    """naz_gemm over transposed views (the dW = dPre^T X case) with split-K atomics."""
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(M * 7 + N)
+    a = torch.randn(K, M, generator=g)  # used transposed
+    b = torch.randn(K, N, generator=g)
+    mask = (torch.rand(M, N, generator=g) > 0.5).float()
+    out = ops.gemm(_cuda(a).t(), _cuda(b), mask=_cuda(mask), split_k=split)
+    ref64 = (a.double().t() @ b.double()) * mask.double()
+    ref32 = (a.t() @ b) * mask
+    _check(out, ref64, ref32, f"gemm {M}x{N}x{K}")
+
+
+# ------------------------------------------------------------------ a5 affine step VJP
+@pytest.mark.parametrize("inverse", [False, True])
+def test_affine_ar_grad(inverse):
+    from naz_amd import autograd as ag
+    rng = np.random.default_rng(5)
+    B, D = 2000, 5
+    x = rng.standard_normal((B, D)).astype(np.float32)
+    raw = (rng.standard_normal((B, 2 * D)) * 3).astype(np.float32)  # exercises both clip ends
+    gy = rng.standard_normal((B, D)).astype(np.float32)
+    gl = rng.standard_normal(B).astype(np.float32)
+
+    def ref(dt):
+        xo = torch.as_tensor(x, dtype=dt).requires_grad_(True)
+        ro = torch.as_tensor(raw, dtype=dt).requires_grad_(True)
+        mean, ls = ro[:, :D], O._clamp(ro[:, D:], -5.0, 3.0)
+        y = (xo - mean) * torch.exp(-ls) if inverse else torch.exp(ls) * xo + mean
+        loss = (y * torch.as_tensor(gy, dtype=dt)).sum() + (ls.sum(-1) * torch.as_tensor(gl, dtype=dt)).sum()
+        return torch.autograd.grad(loss, [xo, ro])
+
+    xg = _cuda(x).requires_grad_(True)
+    rg = _cuda(raw).requires_grad_(True)
+    y, ld = ag.affine_ar(xg, rg, inverse)
+    gx, gr = torch.autograd.grad((y * _cuda(gy)).sum() + (ld * _cuda(gl)).sum(), [xg, rg])
+    (x64, r64), (x32, r32) = ref(torch.float64), ref(torch.float32)
+    _check(gx, x64, x32, f"affine inv={inverse} d/dx")
+    _check(gr, r64, r32, f"affine inv={inverse} d/draw")
+
+
+# ------------------------------------------------------------------ a10: whole-flow NLL gradient
+def _product_flow(spec, state):
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    ft = spec["flow_type"]
+    if ft == "nsc":
+        f = NormalizingFlow("nsc", None, spec["D"], spec["C"], spec["hidden"], spec["L"], spec["K"], spec["split"])
+    elif ft == "nsa":
+        f = NormalizingFlow("nsa", None, spec["D"], spec["C"], spec["hidden"], spec["L"], spec["K"])
+    else:
+        f = NormalizingFlow("maf", None, spec["D"], spec["C"], spec["hidden"], spec["L"])
+    fio.load_state(f, state)
+    return f
+
+
+def _oracle_nll_grads(spec, state, x, ctx, dt):
+    st = {}
+    for k, v in state.items():
+        v = np.asarray(v)
+        st[k] = (torch.as_tensor(v) if v.dtype.kind in "iu" else
+                 torch.as_tensor(v).to(dt).requires_grad_(True))
+    of = O.build_flow(spec, st, dt)
+    c = None if ctx is None else torch.as_tensor(ctx).to(dt)
+    lp = of.log_prob(torch.as_tensor(x).to(dt), c)
+    loss = -lp.mean()
+    keys = [k for k in st if st[k].requires_grad]
+    gs = torch.autograd.grad(loss, [st[k] for k in keys])
+    return lp.detach(), dict(zip(keys, gs))
+
+
+@pytest.mark.parametrize("name", ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz", "nsa_d4c2.npz",
+                                  "maf_d3c2.npz", "maf_twomoons.npz"])
+def test_flow_nll_gradient_vs_oracle(name):
+    """loss = -log_prob(x | ctx).mean() -> backward (naz/trainers/train_flows.py:195,208):
+    every parameter's gradient against the oracle's float64 autograd."""
+    from naz_amd.flows import io as fio
+    fx = load_golden(name)
+    spec, state = spec_state(fx)
+    x, ctx = fx["x"], fx.get("ctx")
+    if name == "maf_twomoons.npz":
+        x = x[:512]
+    f = _product_flow(spec, state)
+    lp = f.log_prob(_cuda(x), condition=None if ctx is None else _cuda(ctx))
+    assert lp.requires_grad, "grad mode with trainable weights must record the autograd walk"
+    (-lp.mean()).backward()
+    lp64, g64 = _oracle_nll_grads(spec, state, x, ctx, torch.float64)
+    lp32, g32 = _oracle_nll_grads(spec, state, x, ctx, torch.float32)
+    assert_parity(_np(lp), _np(lp64), _np(lp32), what=f"{name} graph-walk log_prob")
+    params = fio.named_state_params(f)
+    assert set(params) == set(g64), "canonical parameter sets differ"
+    for k, p in params.items():
+        assert p.grad is not None, f"{k}: no gradient"
+        _check(p.grad, g64[k], g32[k], f"{name} d/d{k}")
+
+
+def test_graph_walk_matches_fused_inference():
+    """The autograd walk and the fused inference launch evaluate the same density."""
+    fx = load_golden("nsc_d16c32_l2.npz")
+    spec, state = spec_state(fx)
+    f = _product_flow(spec, state)
+    assert f.fused
+    x, c = _cuda(fx["x"]), _cuda(fx["ctx"])
+    lp_graph = f.log_prob(x, condition=c)
+    with torch.no_grad():
+        lp_fused = f.log_prob(x, condition=c)
+    assert lp_graph.requires_grad and not lp_fused.requires_grad
+    assert_parity(_np(lp_graph), fx["lp64"], fx["lp32"], what="graph walk")
+    assert_parity(_np(lp_fused), fx["lp64"], fx["lp32"], what="fused")

@@ -32,6 +32,14 @@ def _gpu():
     _lib.lib()
 
 
+@pytest.fixture(autouse=True)
+def _inference():
+    """Inference semantics (naz evaluates log_prob under no_grad, train_flows.py:220): the fused
+    / in-kernel-accumulating paths.  The autograd walk is covered by tests/test_gpu_grad.py."""
+    with torch.no_grad():
+        yield
+
+
 def _product_flow(fx):
     from naz_amd.flows import NormalizingFlow
     from naz_amd.flows import io as fio

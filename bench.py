@@ -121,6 +121,155 @@ def load_traffic(mode: str):
     return None, None
 
 
+def run_train(args, dev, rank, world, dist):
+    """configs[3]: the NLL step of naz's train (train_flows.py:194-213), 2^20 rows per GPU,
+    one process per GPU, gradients all-reduced over RCCL in one flat bucket."""
+    from naz_amd.trainers import DataParallel, nll_step
+    from naz_amd.trainers.train_flows import _flow_parameters
+    flow = build_flow()
+    flow.set_fused(False)
+    B = args.batch
+    x = torch.as_tensor(gaussian_mixture(B, D, seed=rank), device=dev)
+    c = torch.as_tensor(np.random.default_rng(1 + 1000 * rank).standard_normal(size=(B, C)).astype(np.float32),
+                        device=dev)
+    dp = DataParallel()
+    params = _flow_parameters(flow)
+    dp.broadcast_params(params)
+    opt = torch.optim.Adam(params, lr=1e-4)
+
+    def step():
+        return nll_step(flow, x, c, opt, params, dp, B * world, clip_val=1.0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    if rank == 0:
+        step_s = elapsed / args.steps
+        flop = 3 * flops_per_row() * B  # fwd GEMMs + dX + dW
+        achieved = flop / step_s / 1e12
+        rec = {
+            "metric": "samples/sec through the NLL training step (log_prob fwd + backward + grad all-reduce + "
+                      "clip + Adam), 16-dim RQ-spline flow",
+            "value": B * world / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
+            "config": {"workload": "BASELINE configs[3]: the configs[2] flow's NLL step, data parallel",
+                       "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world} (RCCL all-reduce)"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "whole step",
+                         "flop_per_row": 3 * flops_per_row()},
+            "final_loss": float(loss),
+        }
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+CNF_D, CNF_H, CNF_STEPS = 16, [128, 128, 128], 8
+
+
+def cnf_flops_per_row() -> int:
+    """Algorithmic FLOPs per row of one config-5 solve: per RHS the MLP forward plus the
+    Hutchinson product eps^T J eps, which needs J eps = one more pass of the same GEMMs (the
+    JVP; the reference's reverse-mode VJP costs the same), times 4 RHS per RK4 step."""
+    dims = [CNF_D] + CNF_H + [CNF_D]
+    fwd = sum(2 * a * b for a, b in zip(dims[:-1], dims[1:]))
+    return 2 * fwd * 4 * CNF_STEPS
+
+
+def run_cnf(args, dev, rank, world, dist):
+    """configs[4]: naz 'cnf' log_prob (FFJORD block, t 0 -> 1) through naz_cnf_integrate."""
+    from naz_amd import ops
+    from naz_amd.flows import NormalizingFlow
+    torch.manual_seed(1234)
+    f = NormalizingFlow("cnf", None, CNF_D, 0, CNF_H, 1, steps=CNF_STEPS)
+    B = args.batch if args.batch != (1 << 20) else (1 << 18)
+    x = torch.as_tensor(gaussian_mixture(B, CNF_D, seed=rank), device=dev) * 0.5
+    t = f.transforms[0]
+    plan = t._plan
+    packed = plan.packed()
+    eps = torch.randn(B, CNF_D, device=dev)
+    lp = torch.empty(B, device=dev)
+
+    def step():
+        # one log_prob: fresh Hutchinson probe, the solve (ld accumulated into lp), base density
+        torch.randn(B, CNF_D, device=dev, out=eps)
+        lp.zero_()
+        z, _ = ops.cnf_integrate(plan.desc, packed, x, eps, 0.0, 1.0, CNF_STEPS, ld_out=lp,
+                                 ld_mode=ops.LD_ROWSUM_SUB)
+        ops.base_log_prob(z, out=lp, accumulate=True)
+
+    stream = torch.cuda.current_stream(dev)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        evs = []
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            torch.randn(B, CNF_D, device=dev, out=eps)
+            lp.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            z, _ = ops.cnf_integrate(plan.desc, packed, x, eps, 0.0, 1.0, CNF_STEPS, ld_out=lp,
+                                     ld_mode=ops.LD_ROWSUM_SUB)
+            e1.record(stream)
+            ops.base_log_prob(z, out=lp, accumulate=True)
+            evs.append((e0, e1))
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+    kern_s = sum(a.elapsed_time(b) for a, b in evs) / len(evs) / 1e3
+    if dist is not None:
+        tt = torch.tensor([elapsed, kern_s], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_s = float(tt[0]), float(tt[1])
+    if rank == 0:
+        achieved = cnf_flops_per_row() * B / kern_s / 1e12
+        rec = {
+            "metric": "samples/sec through log_prob+log|detJ|, 16-dim CNF (FFJORD, Hutchinson trace)",
+            "value": B * world * args.steps / elapsed, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: x ~ 0.5 x 8-component Gaussian mixture; random-init weights (nn.Linear default, "
+                    "torch seed 1234); eps ~ N(0, I) redrawn per step",
+            "config": {"workload": "BASELINE configs[4]: FFJORD block D=16, H=[128,128,128], softplus, fixed-step "
+                                   "RK4 x 8 (NFE 32, SURVEY.md §8d pin), log_prob (naz_cnf_integrate t 0->1)",
+                       "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"dp{world} (independent row shards, no collective)"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "cnf_kernel<16,0,128,128,128,0,softplus>", "flop_per_row": cnf_flops_per_row(),
+                         "avg_kernel_ms": kern_s * 1e3},
+        }
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,6 +277,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 20, help="rows per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train", action="store_true",
+                    help="time the data-parallel NLL training step instead (BASELINE configs[3]: fwd + HIP "
+                         "backward + flat-bucket RCCL all-reduce + clip + Adam) on the same flow and batch")
+    ap.add_argument("--cnf", action="store_true",
+                    help="BASELINE configs[4]: 16-dim FFJORD CNF (H=[128]*3, softplus, Hutchinson trace, RK4 x 8 "
+                         "steps) log_prob at 2^18 rows per GPU")
     ap.add_argument("--mfma", choices=["auto", "f16x3", "bf16x6", "f32"], default="auto",
                     help="auto (default): f16x3 when the hidden-layer weights fit fp16 (GEMM1 bf16x6, GEMM2/3 as "
                          "three exact-split fp16 products), else bf16x6; f32: exact FP32 MFMA")
@@ -143,6 +298,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
+
+    if args.train:
+        return run_train(args, dev, rank, world, dist)
+    if args.cnf:
+        return run_cnf(args, dev, rank, world, dist)
 
     flow = build_flow()
     B = args.batch

@@ -172,6 +172,30 @@ int naz_coupling_sample(const naz_coupling_desc* d, const void* packed, const fl
                         const float* ctx, int64_t ldc, const float* low, const float* high, float* y, int64_t ldy,
                         float* out_ld, int64_t B, void* stream);
 
+/* ---- a11: continuous normalizing flow (FFJORD block, Hutchinson trace) --------
+ * naz FFJORDTransform (naz/flows/continuous_transforms.py:70-106) over ConditionalFCNN
+ * (:38-60, input cat([x, ctx]), Softplus default).  One call integrates ONE block
+ *     d[a, x]/dt = [-eps^T (df/dx) eps, f(x, ctx)],  a(t0) = 0
+ * from t0 to t1 with `steps` fixed classical RK4 steps (naz odeint.py:12-19,46-52; SURVEY.md
+ * §8d pins config 5 to 8 steps).  log_prob direction = t 0 -> 1 (`_inverse`), sampling
+ * = 1 -> 0 (`_call`).  eps [B, D] is the solve's Hutchinson probe.  ld receives a(t1) per
+ * ld_mode (ROWSUM write / ROWSUM_ADD / ROWSUM_SUB).  ctx may be NULL (C = 0) or one
+ * broadcast row (ldc = 0).  Flat params: W0 [H0, D+C], b0, ..., W_out [D, H_last], b_out.  */
+typedef struct naz_cnf_desc {
+  int D, C;
+  int n_hidden;
+  int H[4];
+  int act; /* NAZ_ACT_* (softplus = naz default) */
+  int reserved[8];
+} naz_cnf_desc;
+int naz_cnf_supported(const naz_cnf_desc* d);
+int64_t naz_cnf_param_count(const naz_cnf_desc* d);
+int64_t naz_cnf_packed_bytes(const naz_cnf_desc* d);
+int naz_cnf_pack(const naz_cnf_desc* d, const float* flat, void* packed, void* stream);
+int naz_cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                      int64_t ldc, const float* eps, int64_t lde, float t0, float t1, int steps, float* y,
+                      int64_t ldy, float* ld, int ld_mode, int64_t B, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

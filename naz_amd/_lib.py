@@ -25,6 +25,11 @@ class CouplingDesc(C.Structure):
                 ("reserved", C.c_int * 6)]
 
 
+class CnfDesc(C.Structure):
+    _fields_ = [("D", C.c_int), ("C", C.c_int), ("n_hidden", C.c_int), ("H", C.c_int * 4), ("act", C.c_int),
+                ("reserved", C.c_int * 8)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/naz_hip.h
 SIGNATURES = {
     "naz_last_error": (C.c_char_p, []),
@@ -47,6 +52,12 @@ SIGNATURES = {
     "naz_colsum": (C.c_int, [_vp, _i64, _i64, _i, _vp, _vp]),
     "naz_act_bwd": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i, _i, _vp]),
     "naz_base_log_prob_bwd": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _i64, _i, _vp]),
+    "naz_cnf_supported": (C.c_int, [C.POINTER(CnfDesc)]),
+    "naz_cnf_param_count": (C.c_int64, [C.POINTER(CnfDesc)]),
+    "naz_cnf_packed_bytes": (C.c_int64, [C.POINTER(CnfDesc)]),
+    "naz_cnf_pack": (C.c_int, [C.POINTER(CnfDesc), _vp, _vp, _vp]),
+    "naz_cnf_integrate": (C.c_int, [C.POINTER(CnfDesc), _vp, _vp, _i64, _vp, _i64, _vp, _i64, C.c_float, C.c_float,
+                                    _i, _vp, _i64, _vp, _i, _i64, _vp]),
     "naz_coupling_supported": (C.c_int, [C.POINTER(CouplingDesc)]),
     "naz_coupling_param_count": (C.c_int64, [C.POINTER(CouplingDesc)]),
     "naz_coupling_packed_bytes": (C.c_int64, [C.POINTER(CouplingDesc)]),

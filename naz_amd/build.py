@@ -18,7 +18,7 @@ OBJ = PKG / "build"
 LIB = PKG / "lib" / "libnazhip.so"
 INCLUDE = PKG.parent / "include"
 ARCH = os.environ.get("NAZ_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "elementwise.hip", "coupling.hip", "capi.cpp"]
+SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "elementwise.hip", "coupling.hip", "cnf.hip", "capi.cpp"]
 
 
 def hipcc() -> str:

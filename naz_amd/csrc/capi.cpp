@@ -130,6 +130,24 @@ int naz_base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float*
   return base_log_prob_bwd(z, ldz, g_lp, g_z, ldgz, B, D, as_stream(stream));
 }
 
+int naz_cnf_supported(const naz_cnf_desc* d) { return cnf_supported(d); }
+int64_t naz_cnf_param_count(const naz_cnf_desc* d) { return cnf_param_count(d); }
+int64_t naz_cnf_packed_bytes(const naz_cnf_desc* d) { return cnf_packed_bytes(d); }
+int naz_cnf_pack(const naz_cnf_desc* d, const float* flat, void* packed, void* stream) {
+  if (flat == nullptr || packed == nullptr) return set_error("naz_cnf_pack: null pointer");
+  return cnf_pack(d, flat, packed, as_stream(stream));
+}
+int naz_cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                      int64_t ldc, const float* eps, int64_t lde, float t0, float t1, int steps, float* y,
+                      int64_t ldy, float* ld, int ld_mode, int64_t B, void* stream) {
+  if (B < 0) return set_error("naz_cnf_integrate: negative batch");
+  if (B > 0 && (packed == nullptr || x == nullptr || eps == nullptr || y == nullptr))
+    return set_error("naz_cnf_integrate: null pointer");
+  if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr) return set_error("naz_cnf_integrate: context required");
+  return cnf_integrate(d, packed, x, ldx, ctx, ldc, eps, lde, t0, t1, steps, y, ldy, ld, ld_mode, B,
+                       as_stream(stream));
+}
+
 int naz_coupling_supported(const naz_coupling_desc* d) { return coupling_supported(d); }
 int64_t naz_coupling_param_count(const naz_coupling_desc* d) { return coupling_param_count(d); }
 int64_t naz_coupling_packed_bytes(const naz_coupling_desc* d) { return coupling_packed_bytes(d); }

@@ -1,0 +1,460 @@
+// Fused FFJORD solve: one launch integrates a whole continuous-flow block (SURVEY.md §8a row
+// a11, config 5).
+//
+// Reference semantics: naz FFJORDTransform (naz/flows/continuous_transforms.py:70-106) =
+// torchdyn CNF(net, trace_estimator=hutch_trace) on the augmented state [a, x]:
+//     dx/dt = f(x, ctx),   da/dt = -eps^T (df/dx) eps      (eps ~ N(0, I) fixed per solve)
+// f = ConditionalFCNN (continuous_transforms.py:38-60): Linear/act chain, input cat([x, ctx]).
+// Solver pinned by SURVEY.md §8d: fixed-step classical RK4 in the form of naz's in-tree
+// odeint.py:12-19,46-52 (k_i = dt f(.), x += (k1 + 2k2 + 2k3 + k4) / 6).
+//
+// MI355X mapping:
+//   * the reference takes eps^T J with a reverse-mode VJP per RHS evaluation (autograd graph,
+//     ~3x the MLP forward); here it is a FORWARD-mode JVP carried alongside the values:
+//     every layer computes pre = W h + b and dpre = W dh with the SAME weight operand, so
+//     J eps costs one extra MFMA per weight read and eps^T (J eps) is a per-row dot product;
+//   * one workgroup per CU (8 waves) keeps the whole vector-field MLP in LDS (config 5:
+//     37k fp32 = 146 KB of 160 KB) for the kernel's lifetime and walks row tiles
+//     persistently — weights are read from HBM once per CU, not once per RHS evaluation;
+//   * a wave owns 16 rows; activations live TRANSPOSED in v_mfma_f32_16x16x4_f32
+//     accumulators (lane l: feature 4(l>>4)+i of a 16-block, row l&15).  Accumulator
+//     register i of block b IS the B operand of k-step (b, i) of the next layer (B[k=l>>4]
+//     [j=l&15]), so the layers chain with no LDS or shuffles; the packer permutes W
+//     columns to match, and the last layer's rows so its output lands in the lane layout of
+//     the ODE state (lane l: state feature (l>>4) + 4s in register s);
+//   * all RK4 stages, the state, eps and the trace accumulator stay in registers: HBM sees
+//     x, ctx, eps in and y, ld out once per solve.
+// Exact fp32 MFMA (bitwise an fmaf chain) and accurate libm activations.
+#include "naz_device.h"
+#include "naz_internal.h"
+
+namespace naz {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+NAZ_DEV floatx4 mfma16(float a, float b, floatx4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+constexpr int cnf_up(int v, int m) { return (v + m - 1) / m * m; }
+constexpr int cnf_max(int a, int b) { return a > b ? a : b; }
+
+// LDS image layout (floats): [W0][b0][W1][b1]...[W_last][b_last]; layer-0 weights are
+// [NB0][KS0/4][64][4], later layers [NBout][NBin][64][4] (one ds_read_b128 = 4 k-steps).
+constexpr int cnf_hid(int j, int h0, int h1, int h2, int h3) { return j == 0 ? h0 : j == 1 ? h1 : j == 2 ? h2 : h3; }
+constexpr int cnf_wsize(int j, int ks0, int h0, int h1, int h2, int h3) {
+  return j == 0 ? cnf_hid(0, h0, h1, h2, h3) / 16 * ks0 * 64
+                : cnf_hid(j, h0, h1, h2, h3) / 16 * (cnf_hid(j - 1, h0, h1, h2, h3) / 16) * 256;
+}
+constexpr int cnf_offw(int j, int ks0, int h0, int h1, int h2, int h3) {
+  return j == 0 ? 0
+                : cnf_offw(j - 1, ks0, h0, h1, h2, h3) + cnf_wsize(j - 1, ks0, h0, h1, h2, h3) +
+                      cnf_hid(j - 1, h0, h1, h2, h3);
+}
+
+template <int D_, int C_, int H0_, int H1_, int H2_, int H3_, int ACT_>
+struct CnfCfg {
+  static constexpr int D = D_, C = C_, ACT = ACT_;
+  static constexpr int NH = (H0_ > 0) + (H1_ > 0) + (H2_ > 0) + (H3_ > 0);
+  static constexpr int XS = cnf_up(D, 4) / 4;     // state / eps registers per lane
+  static constexpr int CS = cnf_up(C, 4) / 4;     // context registers per lane
+  static constexpr int KS0 = cnf_up(XS + CS, 4);  // layer-0 k-steps (padded to a multiple of 4)
+  static constexpr int NBL = cnf_up(D, 16) / 16;  // 16-blocks of the output layer
+  static constexpr int NBMAX = cnf_max(cnf_max(H0_, H1_), cnf_max(H2_, H3_)) / 16;
+  static constexpr int HL = cnf_hid(NH - 1, H0_, H1_, H2_, H3_);
+  static constexpr int OFF_WL = cnf_offw(NH, KS0, H0_, H1_, H2_, H3_);
+  static constexpr int WL_SIZE = NBL * (HL / 16) * 256;
+  static constexpr int OFF_BL = OFF_WL + WL_SIZE;
+  static constexpr int TOTAL = OFF_BL + NBL * 16;
+  static constexpr int in0 = D + C;
+  static_assert(NH >= 1 && H0_ % 16 == 0 && H1_ % 16 == 0 && H2_ % 16 == 0 && H3_ % 16 == 0, "hidden widths");
+  static_assert(NBMAX <= 8, "hidden width <= 128 (register budget)");
+  static_assert(TOTAL * 4 <= 160 * 1024, "vector-field MLP must fit one CU's LDS");
+  static constexpr int hid(int j) { return cnf_hid(j, H0_, H1_, H2_, H3_); }
+  static constexpr int NB(int j) { return hid(j) / 16; }
+  static constexpr int off_w(int j) { return cnf_offw(j, KS0, H0_, H1_, H2_, H3_); }
+  static constexpr int off_b(int j) { return off_w(j) + cnf_wsize(j, KS0, H0_, H1_, H2_, H3_); }
+  // offset of W_j in the natural flat parameter vector (W_j [out, in] then b_j, layer by layer;
+  // j == NH is the output layer)
+  static constexpr int64_t flat_off_w(int j) {
+    int64_t n = 0;
+    int in = in0;
+    for (int i = 0; i < j; ++i) {
+      n += (int64_t)hid(i) * in + hid(i);
+      in = hid(i);
+    }
+    return n;
+  }
+};
+
+constexpr int kCnfWaves = 8, kCnfRows = 16 * kCnfWaves;
+
+template <int I, int N, class F>
+NAZ_DEV void cnf_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    cnf_static_for<I + 1, N>(f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Packing: natural flat parameters -> the LDS image (one thread per image float)
+// ---------------------------------------------------------------------------
+template <class CF>
+__global__ void cnf_pack_kernel(const float* __restrict__ flat, float* __restrict__ img) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= CF::TOTAL) return;
+  float v = 0.f;
+  // layer 0 weights: [ob][s4][lane][i], k-step s = 4 s4 + i carries x feature q + 4s (s < XS)
+  // or context feature q + 4(s - XS) (XS <= s < XS + CS), q = lane >> 4
+  if (e < CF::off_b(0)) {
+    const int i = e & 3, lane = (e >> 2) & 63, rest = e >> 8;
+    const int s4 = rest % (CF::KS0 / 4), ob = rest / (CF::KS0 / 4);
+    const int s = 4 * s4 + i, o = 16 * ob + (lane & 15), q = lane >> 4;
+    int col = -1;
+    if (s < CF::XS) {
+      const int f = q + 4 * s;
+      col = f < CF::D ? f : -1;
+    } else if (s < CF::XS + CF::CS) {
+      const int f = q + 4 * (s - CF::XS);
+      col = f < CF::C ? CF::D + f : -1;
+    }
+    if (col >= 0) v = flat[(int64_t)o * CF::in0 + col];
+    img[e] = v;
+    return;
+  }
+  bool done = false;
+  cnf_static_for<0, CF::NH>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    if (done) return;
+    constexpr int ob_ = CF::off_b(j);
+    if (j > 0 && e >= CF::off_w(j) && e < ob_) {
+      const int r = e - CF::off_w(j);
+      const int i = r & 3, lane = (r >> 2) & 63, rest = r >> 8;
+      const int nbi = CF::NB(j > 0 ? j - 1 : 0);
+      const int b = rest % nbi, ob = rest / nbi;
+      const int o = 16 * ob + (lane & 15), k = 16 * b + 4 * (lane >> 4) + i;
+      v = flat[CF::flat_off_w(j) + (int64_t)o * CF::hid(j > 0 ? j - 1 : 0) + k];
+      done = true;
+    } else if (e >= ob_ && e < ob_ + CF::hid(j)) {
+      v = flat[CF::flat_off_w(j) + (int64_t)CF::hid(j) * (j == 0 ? CF::in0 : CF::hid(j > 0 ? j - 1 : 0)) +
+               (e - ob_)];
+      done = true;
+    }
+  });
+  if (!done) {
+    constexpr int HL = CF::HL;
+    constexpr int64_t fw = CF::flat_off_w(CF::NH);
+    if (e < CF::OFF_BL) {  // output layer: packed row r_local = lane & 15 <-> state feature q_r + 4(4 ob + i_r)
+      const int r = e - CF::OFF_WL;
+      const int i = r & 3, lane = (r >> 2) & 63, rest = r >> 8;
+      const int b = rest % CF::NB(CF::NH - 1), ob = rest / CF::NB(CF::NH - 1);
+      const int rl = lane & 15, nf = (rl >> 2) + 4 * (4 * ob + (rl & 3));
+      const int k = 16 * b + 4 * (lane >> 4) + i;
+      if (nf < CF::D) v = flat[fw + (int64_t)nf * HL + k];
+    } else {
+      const int p = e - CF::OFF_BL, ob = p >> 4, rl = p & 15;
+      const int nf = (rl >> 2) + 4 * (4 * ob + (rl & 3));
+      if (nf < CF::D) v = flat[fw + (int64_t)CF::D * HL + nf];
+    }
+  }
+  img[e] = v;
+}
+
+// value and tangent through the activation: v = act(pre), t <- t * act'(pre)
+// (torch softplus: pre > 20 -> identity; backward grad * z / (z + 1), z = exp(pre))
+template <int ACT>
+NAZ_DEV void act_jvp(float& v, float& t) {
+  const float pre = v;
+  if constexpr (ACT == ACT_SOFTPLUS) {
+    if (pre > 20.f) return;
+    const float z = expf(pre);
+    v = log1pf(z);
+    t = (t * z) / (z + 1.f);
+  } else if constexpr (ACT == ACT_TANH) {
+    v = tanh_f(pre);
+    t = t * (1.f - v * v);
+  } else if constexpr (ACT == ACT_RELU) {
+    v = fmaxf(pre, 0.f);
+    t = pre > 0.f ? t : 0.f;
+  } else if constexpr (ACT == ACT_SIGMOID) {
+    v = 1.f / (1.f + expf(-pre));
+    t = t * (v * (1.f - v));
+  }
+}
+
+template <int NB>
+NAZ_DEV void init_bias4(floatx4 (&ov)[8], floatx4 (&ot)[8], const float* bias, int q) {
+#pragma unroll
+  for (int ob = 0; ob < NB; ++ob) {
+    ov[ob] = *reinterpret_cast<const floatx4*>(bias + 16 * ob + 4 * q);
+    ot[ob] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+template <int ACT, int NB>
+NAZ_DEV void act_all(floatx4 (&ov)[8], floatx4 (&ot)[8]) {
+#pragma unroll
+  for (int ob = 0; ob < NB; ++ob)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = ov[ob][i], t = ot[ob][i];
+      act_jvp<ACT>(v, t);
+      ov[ob][i] = v;
+      ot[ob][i] = t;
+    }
+}
+
+// one Linear between 16-blocked activations: (ov, ot) = W (iv, it) (+ b for the value)
+template <int NBI, int NBO>
+NAZ_DEV void cnf_linear(const float* __restrict__ W, const floatx4 (&iv)[8], const floatx4 (&it)[8],
+                        floatx4 (&ov)[8], floatx4 (&ot)[8], int lane) {
+#pragma unroll
+  for (int b = 0; b < NBI; ++b) {
+    // one input block at a time: its NBO weight reads, then 8·NBO MFMAs.  The barrier keeps
+    // the scheduler from hoisting every block's ds_reads (64 x 4 VGPRs at H = 128) up front.
+    floatx4 a4[NBO];
+#pragma unroll
+    for (int ob = 0; ob < NBO; ++ob) a4[ob] = *reinterpret_cast<const floatx4*>(W + ((ob * NBI + b) * 64 + lane) * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ob = 0; ob < NBO; ++ob) {
+        ov[ob] = mfma16(a4[ob][i], iv[b][i], ov[ob]);
+        ot[ob] = mfma16(a4[ob][i], it[b][i], ot[ob]);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// f(x) in the state layout and g = -eps^T (df/dx) eps (row total on every lane of the row)
+template <class CF>
+NAZ_DEV void cnf_rhs(const float* __restrict__ lds, const float (&xin)[CF::XS], const float (&e)[CF::XS],
+                     const float (&c)[CF::CS > 0 ? CF::CS : 1], float (&f)[CF::XS], float& g, int lane) {
+  const int q = lane >> 4;
+  floatx4 av[8], at[8], bv[8], bt[8];
+  // layer 0: k-steps over [x | ctx | pad]
+  {
+    constexpr int NB0 = CF::NB(0);
+    const float* W = lds + CF::off_w(0);
+    init_bias4<NB0>(av, at, lds + CF::off_b(0), q);
+#pragma unroll
+    for (int s4 = 0; s4 < CF::KS0 / 4; ++s4)
+#pragma unroll
+      for (int ob = 0; ob < NB0; ++ob) {
+        const floatx4 a4 = *reinterpret_cast<const floatx4*>(W + ((ob * (CF::KS0 / 4) + s4) * 64 + lane) * 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int s = 4 * s4 + i;
+          if (s < CF::XS) {
+            av[ob] = mfma16(a4[i], xin[s], av[ob]);
+            at[ob] = mfma16(a4[i], e[s], at[ob]);
+          } else if (s < CF::XS + CF::CS) {
+            av[ob] = mfma16(a4[i], c[s - CF::XS], av[ob]);
+          }
+        }
+      }
+    act_all<CF::ACT, NB0>(av, at);
+  }
+  // hidden layers 1..NH-1, ping-pong between (av, at) and (bv, bt)
+  cnf_static_for<1, CF::NH>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int NBI = CF::NB(j - 1), NBO = CF::NB(j);
+    if constexpr (j % 2 == 1) {
+      init_bias4<NBO>(bv, bt, lds + CF::off_b(j), q);
+      cnf_linear<NBI, NBO>(lds + CF::off_w(j), av, at, bv, bt, lane);
+      act_all<CF::ACT, NBO>(bv, bt);
+    } else {
+      init_bias4<NBO>(av, at, lds + CF::off_b(j), q);
+      cnf_linear<NBI, NBO>(lds + CF::off_w(j), bv, bt, av, at, lane);
+      act_all<CF::ACT, NBO>(av, at);
+    }
+  });
+  // output layer (no activation); rows permuted so register i of block ob = state slot 4 ob + i
+  constexpr int NBI = CF::NB(CF::NH - 1);
+  floatx4 ov[8], ot[8];
+  init_bias4<CF::NBL>(ov, ot, lds + CF::OFF_BL, q);
+  if constexpr ((CF::NH - 1) % 2 == 0)
+    cnf_linear<NBI, CF::NBL>(lds + CF::OFF_WL, av, at, ov, ot, lane);
+  else
+    cnf_linear<NBI, CF::NBL>(lds + CF::OFF_WL, bv, bt, ov, ot, lane);
+  float tr = 0.f;
+#pragma unroll
+  for (int s = 0; s < CF::XS; ++s) {
+    f[s] = ov[s >> 2][s & 3];
+    tr += e[s] * ot[s >> 2][s & 3];
+  }
+  tr += __shfl_xor(tr, 16);
+  tr += __shfl_xor(tr, 32);
+  g = -tr;
+}
+
+template <class CF>
+__global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_kernel(
+    const float* __restrict__ packed, const float* __restrict__ x, int64_t ldx, const float* __restrict__ ctx,
+    int64_t ldc, const float* __restrict__ eps, int64_t lde, float dt, int steps, float* __restrict__ y,
+    int64_t ldy, float* __restrict__ ld, int ld_mode, int64_t B) {
+  __shared__ __attribute__((aligned(16))) float lds[CF::TOTAL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4;
+  for (int i = tid * 4; i < CF::TOTAL; i += blockDim.x * 4)
+    *reinterpret_cast<floatx4*>(lds + i) = *reinterpret_cast<const floatx4*>(packed + i);
+  __syncthreads();
+  constexpr int CSR = CF::CS > 0 ? CF::CS : 1;
+  for (int64_t tile = blockIdx.x; tile * kCnfRows < B; tile += gridDim.x) {
+    const int64_t row = tile * kCnfRows + wave * 16 + (lane & 15);
+    const bool valid = row < B;
+    float xs[CF::XS], es[CF::XS], cs[CSR];
+#pragma unroll
+    for (int s = 0; s < CF::XS; ++s) {
+      const int fi = q + 4 * s;
+      const bool ok = valid && fi < CF::D;
+      xs[s] = ok ? x[row * ldx + fi] : 0.f;
+      es[s] = ok ? eps[row * lde + fi] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < CSR; ++s) {
+      const int fi = q + 4 * s;
+      cs[s] = (CF::CS > 0 && valid && fi < CF::C) ? ctx[(ldc ? row * ldc : 0) + fi] : 0.f;
+    }
+    float a = 0.f;
+    // classical RK4 (odeint.py:46-52), one RHS body for the four stages:
+    //   k_i = dt f(x_i);  x_2 = x + k1/2, x_3 = x + k2/2, x_4 = x + k3;  x += (k1 + 2k2 + 2k3 + k4)/6
+    float xst[CF::XS], sx[CF::XS], f[CF::XS];
+    float sa = 0.f;
+#pragma unroll
+    for (int s = 0; s < CF::XS; ++s) xst[s] = xs[s];
+    for (int it = 0; it < 4 * steps; ++it) {
+      const int stage = it & 3;
+      float g;
+      cnf_rhs<CF>(lds, xst, es, cs, f, g, lane);
+      const float kg = dt * g;
+      if (stage == 3) {
+#pragma unroll
+        for (int s = 0; s < CF::XS; ++s) {
+          xs[s] = xs[s] + (sx[s] + dt * f[s]) / 6.f;
+          xst[s] = xs[s];
+        }
+        a = a + (sa + kg) / 6.f;
+      } else {
+        const float w = stage == 0 ? 1.f : 2.f;     // weight of k_i in the final sum
+        const float h = stage == 2 ? 1.f : 0.5f;    // x_{i+1} = x + h k_i
+#pragma unroll
+        for (int s = 0; s < CF::XS; ++s) {
+          const float k = dt * f[s];
+          sx[s] = stage == 0 ? k : sx[s] + w * k;
+          xst[s] = xs[s] + h * k;
+        }
+        sa = stage == 0 ? kg : sa + w * kg;
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int s = 0; s < CF::XS; ++s) {
+        const int fi = q + 4 * s;
+        if (fi < CF::D) y[row * ldy + fi] = xs[s];
+      }
+      if (q == 0 && ld != nullptr) {
+        if (ld_mode == NAZ_LD_ROWSUM_ADD) ld[row] += a;
+        else if (ld_mode == NAZ_LD_ROWSUM_SUB) ld[row] -= a;
+        else ld[row] = a;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Instantiations and dispatch
+// ---------------------------------------------------------------------------
+template <class CF>
+struct CnfOps {
+  static int64_t packed_bytes() { return (int64_t)CF::TOTAL * 4; }
+  static int pack(const float* flat, void* packed, hipStream_t s) {
+    hipLaunchKernelGGL((cnf_pack_kernel<CF>), dim3((CF::TOTAL + 255) / 256), dim3(256), 0, s, flat,
+                       static_cast<float*>(packed));
+    return check_launch("cnf_pack_kernel");
+  }
+  static int run(const void* packed, const float* x, int64_t ldx, const float* ctx, int64_t ldc, const float* eps,
+                 int64_t lde, float dt, int steps, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
+                 hipStream_t s) {
+    const int64_t tiles = (B + kCnfRows - 1) / kCnfRows;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess)
+      cus = 256;
+    const int per_cu = (160 * 1024) / (CF::TOTAL * 4) >= 2 ? 2 : 1;
+    const int64_t grid = tiles < (int64_t)cus * per_cu ? tiles : (int64_t)cus * per_cu;
+    hipLaunchKernelGGL((cnf_kernel<CF>), dim3((unsigned)grid), dim3(kCnfRows * 4), 0, s,
+                       static_cast<const float*>(packed), x, ldx, ctx, ldc, eps, lde, dt, steps, y, ldy, ld, ld_mode,
+                       B);
+    return check_launch("cnf_kernel");
+  }
+};
+
+// (D, C, H0, H1, H2, H3, act): config 5 (D=16, H=[128]x3, softplus), the
+// reference's conditional CNF examples (train_mle_all_data_cnf.py:96 D=2, C=2, H=[128,64,64]),
+// and small test shapes.
+#ifndef NAZ_CNF_CONFIGS
+#define NAZ_CNF_CONFIGS(X)                          \
+  X(16, 0, 128, 128, 128, 0, ACT_SOFTPLUS)          \
+  X(2, 2, 128, 64, 64, 0, ACT_SOFTPLUS)             \
+  X(4, 2, 32, 32, 0, 0, ACT_SOFTPLUS)               \
+  X(4, 2, 32, 32, 0, 0, ACT_TANH)                   \
+  X(5, 3, 48, 32, 16, 16, ACT_SOFTPLUS)
+#endif
+
+template <class F>
+static int cnf_dispatch(const naz_cnf_desc* d, F&& f) {
+  if (d == nullptr) return set_error("naz_cnf: null descriptor");
+  int H[4] = {0, 0, 0, 0};
+  if (d->n_hidden < 1 || d->n_hidden > 4) return set_error("naz_cnf: n_hidden must be 1..4");
+  for (int j = 0; j < d->n_hidden; ++j) H[j] = d->H[j];
+#define NAZ_CNF_CASE(D_, C_, H0, H1, H2, H3, A_)                                                              \
+  if (d->D == D_ && d->C == C_ && H[0] == H0 && H[1] == H1 && H[2] == H2 && H[3] == H3 && d->act == A_) \
+    return f(CnfOps<CnfCfg<D_, C_, H0, H1, H2, H3, A_>>{});
+  NAZ_CNF_CONFIGS(NAZ_CNF_CASE)
+#undef NAZ_CNF_CASE
+  return set_error("naz_cnf: shape D=%d C=%d H=[%d,%d,%d,%d] act=%d is not instantiated (NAZ_CNF_CONFIGS)", d->D,
+                   d->C, H[0], H[1], H[2], H[3], d->act);
+}
+
+int cnf_supported(const naz_cnf_desc* d) {
+  return cnf_dispatch(d, [](auto) { return 1; }) == 1 ? 1 : 0;
+}
+
+int64_t cnf_param_count(const naz_cnf_desc* d) {
+  if (d == nullptr || d->n_hidden < 1 || d->n_hidden > 4) return -1;
+  int in = d->D + d->C;
+  int64_t n = 0;
+  for (int j = 0; j < d->n_hidden; ++j) {
+    n += (int64_t)d->H[j] * in + d->H[j];
+    in = d->H[j];
+  }
+  return n + (int64_t)d->D * in + d->D;
+}
+
+int64_t cnf_packed_bytes(const naz_cnf_desc* d) {
+  int64_t n = -1;
+  if (cnf_dispatch(d, [&](auto ops) {
+        n = decltype(ops)::packed_bytes();
+        return 0;
+      }) != 0)
+    return -1;
+  return n;
+}
+
+int cnf_pack(const naz_cnf_desc* d, const float* flat, void* packed, hipStream_t s) {
+  return cnf_dispatch(d, [&](auto ops) { return decltype(ops)::pack(flat, packed, s); });
+}
+
+int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                  int64_t ldc, const float* eps, int64_t lde, float t0, float t1, int steps, float* y, int64_t ldy,
+                  float* ld, int ld_mode, int64_t B, hipStream_t s) {
+  if (B == 0) return 0;
+  if (steps < 1) return set_error("naz_cnf_integrate: steps must be >= 1");
+  // odeint.py:15-16: dt = t1 - t0 of consecutive grid points (a single value for a uniform grid)
+  const float dt = (float)(((double)t1 - (double)t0) / (double)steps);
+  return cnf_dispatch(d, [&](auto ops) {
+    return decltype(ops)::run(packed, x, ldx, ctx, ldc, eps, lde, dt, steps, y, ldy, ld, ld_mode, B, s);
+  });
+}
+
+}  // namespace naz

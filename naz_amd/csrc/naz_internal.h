@@ -51,4 +51,12 @@ int coupling_sample(const naz_coupling_desc* d, const void* packed, const float*
                     int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B,
                     hipStream_t s);
 
+int cnf_supported(const naz_cnf_desc* d);
+int64_t cnf_param_count(const naz_cnf_desc* d);
+int64_t cnf_packed_bytes(const naz_cnf_desc* d);
+int cnf_pack(const naz_cnf_desc* d, const float* flat, void* packed, hipStream_t s);
+int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                  int64_t ldc, const float* eps, int64_t lde, float t0, float t1, int steps, float* y, int64_t ldy,
+                  float* ld, int ld_mode, int64_t B, hipStream_t s);
+
 }  // namespace naz

@@ -1,0 +1,221 @@
+"""naz's continuous normalizing flow (naz/flows/continuous_transforms.py), MI355X-native.
+
+``continuous_free_form(input_dim, condition_dim, hidden_dims, num_blocks, activation=nn.Softplus(),
+...)`` keeps naz's signature and returns ``(flow, transforms, nets)``.  Each block is an FFJORD
+transform over a ``ConditionalFCNN`` vector field (naz :38-60 — same ``.nn`` Sequential, so
+parameter names ``nn.{i}.weight|bias`` match), integrated by ONE ``naz_cnf_integrate``
+launch: the whole fixed-step RK4 solve, the Hutchinson trace and the log-det accumulation in
+registers, the MLP resident in LDS (csrc/cnf.hip).
+
+Solver: naz constructs torchdyn ``NeuralODE(solver='dopri5', atol=rtol=1e-4, sensitivity=
+'adjoint')`` (:73-81).  SURVEY.md §8d pins config 5 to fixed-step classical RK4 with 8 steps
+(NFE 32) — the default here (``solver='rk4', steps=8``); adaptive dopri5 and the adjoint
+backward are §8f rank 3 and raise NotImplementedError.  The Hutchinson probe eps ~ N(0, I)
+is drawn per solve on the device, as torchdyn does; assign ``transform.noise`` to fix it.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+from torch.distributions import Transform, constraints
+
+from .. import ops
+from ..nn import activation_name
+from .transforms import ComposeTransformModule, ConditionalComposeTransformModule, ConditionalTransformModule, \
+    TransformModule
+
+__all__ = ["ConditionalFCNN", "FCNN", "FFJORDTransform", "ConditionalFFJORDTransform", "continuous_free_form"]
+
+
+class ConditionalFCNN(nn.Module):
+    """naz/flows/continuous_transforms.py:38-60: Linear/act (/Dropout) chain, input cat([x, ctx])."""
+
+    def __init__(self, input_dim, context_dim, hidden_dims, act=nn.Softplus(), dropout_p=0.0):
+        super().__init__()
+        hidden_dims = list(hidden_dims)
+        if dropout_p:
+            raise NotImplementedError("naz_amd CNF: dropout in the vector field is SURVEY.md §8f rank 2")
+        layers = [nn.Linear(input_dim + context_dim, hidden_dims[0]), act]
+        if dropout_p is not None:
+            layers.append(nn.Dropout(p=dropout_p))
+        for i, hidden_dim in enumerate(hidden_dims[1:]):
+            layers.append(nn.Linear(hidden_dims[i], hidden_dim))
+            layers.append(act)
+            if dropout_p is not None:
+                layers.append(nn.Dropout(p=dropout_p))
+        layers.append(nn.Linear(hidden_dims[-1], input_dim))
+        self.nn = nn.Sequential(*layers)
+        self.input_dim, self.context_dim, self.hidden_dims = input_dim, context_dim, hidden_dims
+        self.act = activation_name(act)
+
+    def linears(self):
+        return [m for m in self.nn if isinstance(m, nn.Linear)]
+
+    def forward(self, x):
+        raise NotImplementedError("naz_amd: the vector field runs inside naz_cnf_integrate")
+
+
+class FCNN(ConditionalFCNN):
+    """naz :62-67 (whose ``super().__init__(self, ...)`` call is broken in the reference; this is
+    the evident intent: an unconditional ConditionalFCNN)."""
+
+    def __init__(self, input_dim, hidden_dims, act=nn.Softplus(), dropout_p=0.0):
+        super().__init__(input_dim, 0, hidden_dims, act=act, dropout_p=dropout_p)
+
+
+class _CnfPlan:
+    """The block's packed LDS image, re-packed when a parameter changes (version counters)."""
+
+    def __init__(self, net: ConditionalFCNN):
+        self.net = net
+        self.desc = ops.cnf_desc(net.input_dim, net.context_dim, net.hidden_dims, net.act)
+        if not ops.cnf_supported(self.desc):
+            from .._lib import lib
+            raise NotImplementedError(f"naz_amd CNF: {lib().naz_last_error().decode()}")
+        self._sig, self._packed = None, None
+
+    def packed(self):
+        ps = [t for lin in self.net.linears() for t in (lin.weight, lin.bias)]
+        sig = tuple((p.data_ptr(), p._version) for p in ps)
+        if sig != self._sig or self._packed is None:
+            flat = torch.cat([p.detach().reshape(-1) for p in ps])
+            self._packed = ops.cnf_pack(self.desc, flat, self._packed)
+            self._sig = sig
+        return self._packed
+
+
+class _FFJORDCore:
+    """Shared solve logic of the conditional and unconditional transforms."""
+
+    def _solve(self, v, t0, t1, ld_buf, ld_mode):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self._net.parameters()):
+            raise NotImplementedError("naz_amd CNF: differentiating through the ODE solve (adjoint) is SURVEY.md "
+                                      "§8f rank 3; evaluate under torch.no_grad()")
+        noise = self.noise if self.noise is not None else torch.randn(v.shape, device=v.device, dtype=torch.float32)
+        y, ld = ops.cnf_integrate(self._plan.desc, self._plan.packed(), v, noise, t0, t1, self.steps,
+                                  context=self._context, ld_out=ld_buf, ld_mode=ld_mode)
+        return y, ld
+
+    def _inverse(self, x):  # naz :91-95: integrate t 0 -> 1, cache int -tr J
+        y, ld = self._solve(x, 0.0, 1.0, None, ops.LD_ROWSUM)
+        self._cached_logdet = ld
+        return y
+
+    def _call(self, z):  # naz :97-102: integrate t 1 -> 0
+        y, ld = self._solve(z, 1.0, 0.0, None, ops.LD_ROWSUM)
+        self._cached_logdet = ld
+        return y
+
+    def log_abs_det_jacobian(self, x, y):
+        return self._cached_logdet
+
+    def _inverse_acc(self, y, lp):
+        x, _ = self._solve(y, 0.0, 1.0, lp, ops.LD_ROWSUM_SUB)
+        return x
+
+    def _call_acc(self, x, ld):
+        y, _ = self._solve(x, 1.0, 0.0, ld, ops.LD_ROWSUM_ADD)
+        return y
+
+    def _inv_ld(self, y):
+        raise NotImplementedError("naz_amd CNF: differentiating through the ODE solve (adjoint) is SURVEY.md §8f "
+                                  "rank 3; evaluate under torch.no_grad()")
+
+
+def _check_solver(solver, steps):
+    if solver != "rk4":
+        raise NotImplementedError(f"naz_amd CNF: solver {solver!r}: fixed-step 'rk4' is built (SURVEY.md §8d "
+                                  "config 5); adaptive dopri5 is §8f rank 3")
+    if int(steps) < 1:
+        raise ValueError("steps must be >= 1")
+
+
+class FFJORDTransform(_FFJORDCore, TransformModule):
+    """naz :70-106 FFJORDTransform(net, input_dim, solver, sensitivity, atol, rtol)."""
+
+    domain = constraints.real_vector
+    codomain = constraints.real_vector
+    bijective = True
+
+    def __init__(self, net, input_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4, steps=8):
+        super().__init__()
+        _check_solver(solver, steps)
+        self.net, self.input_dim, self.steps = net, input_dim, int(steps)
+        self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
+        self._plan = _CnfPlan(net)
+        self._cached_logdet = None
+        self._context = None
+        self.noise: Optional[torch.Tensor] = None
+
+    @property
+    def _net(self):
+        return self.net
+
+    def __hash__(self):
+        return nn.Module.__hash__(self)
+
+
+class _ConditionedFFJORD(_FFJORDCore, Transform):
+    domain = constraints.real_vector
+    codomain = constraints.real_vector
+    bijective = True
+
+    def __init__(self, module: "ConditionalFFJORDTransform", context):
+        super().__init__(cache_size=0)
+        self.module, self._context = module, context
+        self._cached_logdet = None
+
+    @property
+    def _net(self):
+        return self.module.net
+
+    @property
+    def _plan(self):
+        return self.module._plan
+
+    @property
+    def steps(self):
+        return self.module.steps
+
+    @property
+    def noise(self):
+        return self.module.noise
+
+
+class ConditionalFFJORDTransform(ConditionalTransformModule):
+    """naz :109-121.  ``condition(ctx)`` returns a conditioned transform instead of naz's
+    monkey-patch of the vector field's ``forward``."""
+
+    def __init__(self, net, input_dim, context_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4,
+                 steps=8):
+        super().__init__()
+        _check_solver(solver, steps)
+        self.net, self.input_dim, self.context_dim, self.steps = net, input_dim, context_dim, int(steps)
+        self._plan = _CnfPlan(net)
+        self.noise: Optional[torch.Tensor] = None
+
+    def condition(self, context):
+        return _ConditionedFFJORD(self, context)
+
+
+def continuous_free_form(input_dim, condition_dim, hidden_dims, num_blocks, activation=nn.Softplus(),
+                         use_batchnorm=False, dropout_p=None, **kwargs):
+    """naz/flows/continuous_transforms.py:124-139."""
+    if use_batchnorm:
+        raise NotImplementedError("naz_amd: use_batchnorm is outside the log_prob hot path (SURVEY.md §8)")
+    hidden_dims = list(hidden_dims) if isinstance(hidden_dims, (list, tuple)) else [hidden_dims]
+    nets, transforms = [], []
+    for _ in range(num_blocks):
+        if condition_dim == 0:
+            net = FCNN(input_dim, hidden_dims, act=activation, dropout_p=dropout_p)
+            transform = FFJORDTransform(net, input_dim, **kwargs)
+        else:
+            net = ConditionalFCNN(input_dim, condition_dim, hidden_dims, act=activation, dropout_p=dropout_p)
+            transform = ConditionalFFJORDTransform(net, input_dim, condition_dim, **kwargs)
+        nets.append(net)
+        transforms.append(transform)
+    flow = (ComposeTransformModule(transforms) if condition_dim <= 0 else
+            ConditionalComposeTransformModule(transforms))
+    return flow, transforms, nets

@@ -20,15 +20,10 @@ from torch.distributions import Normal
 from .. import ops
 from ..nn import activation_name
 from ..utils import device
+from .continuous_transforms import continuous_free_form
 from .distributions import ConditionalTransformedDistribution, TransformedDistribution
 from .transforms import (ConditionalSplineCoupling, Permute, SplineCoupling, masked_affine_autoregressive,
                          neural_spline_autoregressive, neural_spline_coupling)
-
-
-def continuous_free_form(*args, **kwargs):
-    """naz "cnf" (naz/flows/continuous_transforms.py:124-139) — SURVEY.md §8a row a11,
-    config 5: not built in this round."""
-    raise NotImplementedError("naz_amd: the FFJORD CNF (flow_type 'cnf') is not implemented yet")
 
 
 flow_makers = {"maf": masked_affine_autoregressive, "nsa": neural_spline_autoregressive,

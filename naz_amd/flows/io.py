@@ -22,6 +22,15 @@ def _layers(flow):
     return [t for t in flow.transforms if not isinstance(t, Permute)]
 
 
+def _linears(t):
+    """The conditioner's Linear layers: pyro-style ``.nn.layers`` or the CNF vector field's
+    ``ConditionalFCNN.nn`` Sequential (naz continuous_transforms.py:41-50)."""
+    net = getattr(t, "net", None)
+    if net is not None and hasattr(net, "linears"):
+        return net.linears()
+    return list(t.nn.layers)
+
+
 def _lower(t):
     inner = getattr(t, "module", None)
     if inner is not None and hasattr(inner, "lower_spline"):
@@ -35,7 +44,7 @@ def named_state_params(flow) -> Dict[str, torch.nn.Parameter]:
     out = {}
     for l, t in enumerate(_layers(flow)):
         p = f"layers.{l}."
-        for i, lin in enumerate(t.nn.layers):
+        for i, lin in enumerate(_linears(t)):
             out[p + f"nn.layers.{i}.weight"] = lin.weight
             out[p + f"nn.layers.{i}.bias"] = lin.bias
         low = _lower(t)
@@ -49,10 +58,10 @@ def export_state(flow) -> Dict[str, np.ndarray]:
     out = {}
     for l, t in enumerate(_layers(flow)):
         p = f"layers.{l}."
-        for i, lin in enumerate(t.nn.layers):
+        for i, lin in enumerate(_linears(t)):
             out[p + f"nn.layers.{i}.weight"] = lin.weight.detach().float().cpu().numpy()
             out[p + f"nn.layers.{i}.bias"] = lin.bias.detach().float().cpu().numpy()
-        if hasattr(t.nn, "permutation"):
+        if hasattr(t, "nn") and hasattr(t.nn, "permutation"):
             out[p + "nn.permutation"] = t.nn.permutation.detach().cpu().numpy().astype(np.int64)
         low = _lower(t)
         if low is not None:
@@ -65,9 +74,9 @@ def export_state(flow) -> Dict[str, np.ndarray]:
 def load_state(flow, state: Dict[str, np.ndarray]) -> None:
     for l, t in enumerate(_layers(flow)):
         p = f"layers.{l}."
-        if hasattr(t.nn, "set_permutation") and (p + "nn.permutation") in state:
+        if hasattr(t, "nn") and hasattr(t.nn, "set_permutation") and (p + "nn.permutation") in state:
             t.nn.set_permutation(torch.as_tensor(np.asarray(state[p + "nn.permutation"])))
-        for i, lin in enumerate(t.nn.layers):
+        for i, lin in enumerate(_linears(t)):
             lin.weight.copy_(torch.as_tensor(np.asarray(state[p + f"nn.layers.{i}.weight"])))
             lin.bias.copy_(torch.as_tensor(np.asarray(state[p + f"nn.layers.{i}.bias"])))
         low = _lower(t)

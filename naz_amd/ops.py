@@ -11,15 +11,16 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB, CouplingDesc,
-                   check, lib)
+from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB, CnfDesc,
+                   CouplingDesc, check, lib)
 
 Tensor = torch.Tensor
 
 __all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
-           "coupling_sample", "LAYOUT_ARN", "LAYOUT_DENSE", "LD_PERDIM", "LD_ROWSUM", "LD_ROWSUM_ADD",
+           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate",
+           "LAYOUT_ARN", "LAYOUT_DENSE", "LD_PERDIM", "LD_ROWSUM", "LD_ROWSUM_ADD",
            "LD_ROWSUM_SUB"]
 
 
@@ -377,3 +378,61 @@ def coupling_sample(d: CouplingDesc, packed: Tensor, z: Tensor, context: Optiona
     check(lib().naz_coupling_sample(d, _p(packed), _p(z), ldz, _p(context), ldc, _p(low), _p(high), _p(y),
                                     y.stride(0), _p(ld), B, _stream(dev)), "coupling_sample")
     return y, ld
+
+
+# ----------------------------------------------------------------------------- a11 CNF
+def cnf_desc(D: int, C: int, hidden, act: str = "softplus") -> CnfDesc:
+    hidden = list(hidden)
+    if not 1 <= len(hidden) <= 4:
+        raise ValueError("naz_amd CNF: 1 to 4 hidden layers")
+    d = CnfDesc()
+    d.D, d.C, d.n_hidden = D, C, len(hidden)
+    for j, h in enumerate(hidden):
+        d.H[j] = int(h)
+    d.act = ACT.get(act, -1)
+    return d
+
+
+def cnf_supported(d: CnfDesc) -> bool:
+    return bool(lib().naz_cnf_supported(d))
+
+
+def cnf_param_count(d: CnfDesc) -> int:
+    return int(lib().naz_cnf_param_count(d))
+
+
+def cnf_pack(d: CnfDesc, flat: Tensor, packed: Optional[Tensor] = None) -> Tensor:
+    dev = _dev(flat)
+    n = cnf_param_count(d)
+    if flat.numel() != n or not flat.is_contiguous():
+        raise ValueError(f"flat CNF params must be a contiguous [{n}] fp32 tensor")
+    nbytes = int(lib().naz_cnf_packed_bytes(d))
+    if nbytes <= 0:
+        raise RuntimeError(f"naz_amd cnf_pack: {lib().naz_last_error().decode()}")
+    if packed is None or packed.numel() * 4 != nbytes:
+        packed = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
+    check(lib().naz_cnf_pack(d, _p(flat), _p(packed), _stream(dev)), "cnf_pack")
+    return packed
+
+
+def cnf_integrate(d: CnfDesc, packed: Tensor, x: Tensor, eps: Tensor, t0: float, t1: float, steps: int,
+                  context: Optional[Tensor] = None, ld_out: Optional[Tensor] = None, ld_mode: int = LD_ROWSUM,
+                  out: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """One FFJORD block solve (naz_cnf_integrate): (y, ld) with ld = int_{t0}^{t1} -eps^T J eps dt."""
+    dev = _dev(packed, x, eps, context, ld_out, out)
+    x, ldx = _rows(x)
+    eps, lde = _rows(eps)
+    B = x.shape[0]
+    if eps.shape != x.shape:
+        raise ValueError("eps must match x")
+    context, ldc = _ctx_arg(context, B)
+    if out is None:
+        out = torch.empty_like(x)
+    if ld_out is None:
+        ld_out = torch.empty((B,), device=dev, dtype=torch.float32)
+        if ld_mode in (LD_ROWSUM_ADD, LD_ROWSUM_SUB):
+            ld_out.zero_()
+    check(lib().naz_cnf_integrate(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(eps), lde, float(t0), float(t1),
+                                  int(steps), _p(out), out.stride(0), _p(ld_out), ld_mode, B, _stream(dev)),
+          "cnf_integrate")
+    return out, ld_out

@@ -63,8 +63,51 @@ def _flow_fixture(name, spec, n, seed_w=1234, seed_x=0, seed_c=1):
     return f64, state32, x, c
 
 
+def _cnf_fixture(name, spec, n, seed_w=1234, seed_x=0, seed_c=1, seed_e=5):
+    """a11: FFJORD blocks with the Hutchinson probes fixed and stored (eps_l/{l}: log_prob
+    direction, eps_s/{l}: sampling direction)."""
+    state = O.random_state(spec, seed=seed_w, last_layer_scale=1.0)
+    state32 = {k: v.float() for k, v in state.items()}
+    D, C, L = spec["D"], spec["C"], spec["L"]
+    x = torch.as_tensor(O.gaussian_mixture(n, D, seed=seed_x)) * 0.5
+    c = torch.as_tensor(O.context_normal(n, C, seed=seed_c)) if C > 0 else None
+    g = torch.Generator().manual_seed(seed_e)
+    eps_l = [torch.randn(n, D, generator=g).float() for _ in range(L)]
+    eps_s = [torch.randn(n, D, generator=g).float() for _ in range(L)]
+    z = torch.randn(n, D, generator=g).float()
+    out = {}
+    for dt, key in ((torch.float64, "64"), (torch.float32, "32")):
+        f = O.build_flow(spec, state32, dt)
+        for layer, e in zip(f.layers, eps_l):
+            layer.eps = e
+        out["lp" + key] = f.log_prob(x.to(dt), None if c is None else c.to(dt)).numpy()
+        for layer, e in zip(f.layers, eps_s):
+            layer.eps = e
+        ys, lds = f.forward_with_logdet(z.to(dt), None if c is None else c.to(dt))
+        out["y_sample" + key], out["ld_sample" + key] = ys.numpy(), lds.numpy()
+    arrays = {"x": x.numpy(), "z": z.numpy(), **out}
+    for l in range(L):
+        arrays[f"eps_l/{l}"], arrays[f"eps_s/{l}"] = eps_l[l].numpy(), eps_s[l].numpy()
+    if c is not None:
+        arrays["ctx"] = c.numpy()
+    for k, v in state32.items():
+        arrays["state/" + k] = v.numpy()
+    for k, v in spec.items():
+        arrays["spec/" + k] = np.asarray(v)
+    np.savez(OUT / name, **arrays)
+
+
+def cnf_fixtures():
+    _cnf_fixture("cnf_d4c2.npz", dict(flow_type="cnf", D=4, C=2, hidden=[32, 32], L=2, activation="softplus",
+                                      steps=8), 256)
+    # config 5's block shape (D=16, H=[128]*3, unconditional), one block
+    _cnf_fixture("cnf_d16c0.npz", dict(flow_type="cnf", D=16, C=0, hidden=[128, 128, 128], L=1,
+                                       activation="softplus", steps=8), 256)
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
+    cnf_fixtures()
     _spline_fixture("rqs_dense_k8.npz", 512, 4, 8, O.LAYOUT_DENSE, seed=11)
     _spline_fixture("rqs_arn_k5.npz", 384, 3, 5, O.LAYOUT_ARN, seed=12)
     _spline_fixture("rqs_dense_k16.npz", 256, 6, 16, O.LAYOUT_DENSE, seed=13)
@@ -101,4 +144,9 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    if sys.argv[1:] == ["cnf"]:
+        OUT.mkdir(parents=True, exist_ok=True)
+        cnf_fixtures()
+    else:
+        main()

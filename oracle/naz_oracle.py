@@ -354,6 +354,84 @@ class Permute:
 
 
 # ---------------------------------------------------------------------------
+# a11: continuous normalizing flow (FFJORD with Hutchinson's trace), pinned RK4 solver
+# ---------------------------------------------------------------------------
+class FCNN:
+    """naz: flows/continuous_transforms.py:38-60 ``ConditionalFCNN``: Linear/act chain (Softplus
+    default, no dropout when dropout_p is None), input ``cat([x, context])`` — x FIRST
+    (``_conditioned_forward``, :54-56), output D."""
+
+    def __init__(self, weights: List[Tensor], biases: List[Tensor], activation: str = "softplus"):
+        self.weights, self.biases = weights, biases
+        self.f = ACTIVATIONS[activation]
+
+    def __call__(self, x: Tensor, context: Optional[Tensor] = None) -> Tensor:
+        h = x if context is None else torch.cat([x, context.expand(x.shape[:-1] + (context.shape[-1],))], -1)
+        n = len(self.weights)
+        for i in range(n):
+            h = F.linear(h, self.weights[i], self.biases[i])
+            if i < n - 1:
+                h = self.f(h)
+        return h
+
+
+def hutchinson_rhs(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor) -> Tuple[Tensor, Tensor]:
+    """torchdyn ``CNF.forward`` with naz's ``hutch_trace`` (continuous_transforms.py:78,85-89):
+    d[a, x]/dt = [-eps^T (df/dx) eps, f(x)], the VJP eps^T J taken by reverse-mode autograd
+    exactly as the reference does; eps is fixed for one solve."""
+    with torch.enable_grad():
+        x_in = x.detach().requires_grad_(True)
+        f = net(x_in, ctx)
+        vjp = torch.autograd.grad(f, x_in, eps)[0]
+    tr = torch.einsum("bi,bi->b", vjp, eps)
+    return f.detach(), -tr.detach()
+
+
+def rk4_augmented(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor, t0: float, t1: float,
+                  steps: int) -> Tuple[Tensor, Tensor]:
+    """Fixed-step classical RK4 on the augmented state [a, x], a(t0) = 0, in the form of naz's
+    in-tree solver (neural_nets/__deprecated__/neural_odes/odeint.py:12-19 integrate,
+    :46-52 RK4._step_fn): k_i = dt f(.), x += (k1 + 2 k2 + 2 k3 + k4) / 6.  SURVEY.md §8d pins
+    config 5 to this solver with 8 steps (NFE 32); torchdyn's adaptive dopri5 is §8f rank 3."""
+    times = torch.linspace(t0, t1, steps + 1, dtype=torch.float64)
+    a = torch.zeros(x.shape[:-1], dtype=x.dtype)
+    for i in range(steps):
+        dt = float(times[i + 1] - times[i])
+        f1, g1 = hutchinson_rhs(net, x, ctx, eps)
+        k1x, k1a = dt * f1, dt * g1
+        f2, g2 = hutchinson_rhs(net, x + 0.5 * k1x, ctx, eps)
+        k2x, k2a = dt * f2, dt * g2
+        f3, g3 = hutchinson_rhs(net, x + 0.5 * k2x, ctx, eps)
+        k3x, k3a = dt * f3, dt * g3
+        f4, g4 = hutchinson_rhs(net, x + k3x, ctx, eps)
+        k4x, k4a = dt * f4, dt * g4
+        x = x + (k1x + 2.0 * k2x + 2.0 * k3x + k4x) / 6.0
+        a = a + (k1a + 2.0 * k2a + 2.0 * k3a + k4a) / 6.0
+    return x, a
+
+
+class FFJORD:
+    """a11: naz ``FFJORDTransform`` (continuous_transforms.py:70-106).  ``inverse`` = its
+    ``_inverse`` (integrate t 0 -> 1, the log_prob direction), ``forward`` = ``_call``
+    (t 1 -> 0, sampling).  Both return the cached log-det a(t_end) = int -eps^T J eps dt as a
+    [B, 1] 'per-dim' ld so Flow.log_prob's ``lp -= ld.sum(-1)`` applies it as torch's
+    TransformedDistribution does with ``log_abs_det_jacobian``.  ``eps`` [B, D] must be set
+    before each call (torchdyn draws it per solve)."""
+
+    def __init__(self, D: int, net: FCNN, steps: int = 8):
+        self.D, self.nn, self.steps = D, net, steps
+        self.eps: Optional[Tensor] = None
+
+    def inverse(self, y, ctx=None):
+        x, a = rk4_augmented(self.nn, y, ctx, self.eps.to(y.dtype), 0.0, 1.0, self.steps)
+        return x, a[..., None]
+
+    def forward(self, z, ctx=None):
+        x, a = rk4_augmented(self.nn, z, ctx, self.eps.to(z.dtype), 1.0, 0.0, self.steps)
+        return x, a[..., None]
+
+
+# ---------------------------------------------------------------------------
 # a8/a9: flow composition, bounding, density and sampling
 # ---------------------------------------------------------------------------
 def bounding_transform(x: Tensor, low: Tensor, high: Tensor) -> Tuple[Tensor, Tensor]:
@@ -443,6 +521,8 @@ def build_flow(spec: dict, state: Dict[str, Tensor], dtype=torch.float64) -> Flo
                 lower = tuple(t[p + "lower_spline.unnormalized_" + n].to(dtype)
                               for n in ("widths", "heights", "derivatives"))
             layers.append(SplineCoupling(D, s, K, MLP(Ws, bs, act), lower, bound))
+        elif ft == "cnf":
+            layers.append(FFJORD(D, FCNN(Ws, bs, spec.get("activation", "softplus")), spec.get("steps", 8)))
         elif ft in ("nsa", "maf"):
             perm = t[p + "nn.permutation"].long()
             mult = (3 * K - 1) if ft == "nsa" else 2
@@ -479,6 +559,8 @@ def random_state(spec: dict, seed: int = 1234, last_layer_scale: float = 3.0) ->
             dims = [s + C] + hidden + [(D - s) * (3 * K - 1)]
         elif ft == "nsa":
             dims = [D + C] + hidden + [D * (3 * K - 1)]
+        elif ft == "cnf":
+            dims = [D + C] + hidden + [D]  # ConditionalFCNN, continuous_transforms.py:41-50
         else:
             dims = [D + C] + hidden + [2 * D]
         n_lin = len(dims) - 1

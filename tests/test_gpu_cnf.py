@@ -1,0 +1,186 @@
+"""GPU: the fused FFJORD solve against the oracle
+(oracle/naz_oracle.py FFJORD: torch autograd VJP Hutchinson trace + odeint.py RK4) on the same
+fp32 weights, inputs and Hutchinson probes.  Criterion: tests/parity.py."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import naz_oracle as O
+from tests.conftest import load_golden
+from tests.parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _cuda(a):
+    return torch.as_tensor(np.asarray(a), dtype=torch.float32, device=DEV)
+
+
+def _np(t):
+    return t.detach().double().cpu().numpy()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from naz_amd import _lib
+    _lib.lib()
+
+
+@pytest.fixture(autouse=True)
+def _inference():
+    with torch.no_grad():
+        yield
+
+
+def _spec_state(fx):
+    spec = {k[5:]: fx[k].tolist() for k in fx if k.startswith("spec/")}
+    state = {k[6:]: fx[k] for k in fx if k.startswith("state/")}
+    return spec, state
+
+
+def _product_cnf(spec, state):
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    f = NormalizingFlow("cnf", None, spec["D"], spec["C"], spec["hidden"], spec["L"], steps=spec.get("steps", 8))
+    fio.load_state(f, state)
+    return f
+
+
+@pytest.mark.parametrize("name", ["cnf_d4c2.npz", "cnf_d16c0.npz"])
+def test_cnf_log_prob_vs_golden(name):
+    fx = load_golden(name)
+    spec, state = _spec_state(fx)
+    f = _product_cnf(spec, state)
+    for l, t in enumerate(f.transforms):
+        t.noise = _cuda(fx[f"eps_l/{l}"])
+    c = _cuda(fx["ctx"]) if "ctx" in fx else None
+    lp = f.log_prob(_cuda(fx["x"]), condition=c)
+    assert_parity(_np(lp), fx["lp64"], fx["lp32"], what=f"{name} log_prob")
+
+
+@pytest.mark.parametrize("name", ["cnf_d4c2.npz", "cnf_d16c0.npz"])
+def test_cnf_sample_direction_vs_golden(name):
+    """naz _call (t 1 -> 0) per block, accumulated log-det (sampling direction)."""
+    fx = load_golden(name)
+    spec, state = _spec_state(fx)
+    f = _product_cnf(spec, state)
+    c = _cuda(fx["ctx"]) if "ctx" in fx else None
+    y = _cuda(fx["z"])
+    ld = torch.zeros(y.shape[0], device=DEV)
+    for l, t in enumerate(f.transforms):
+        t.noise = _cuda(fx[f"eps_s/{l}"])
+        tt = t.condition(c) if c is not None else t
+        y = tt._call_acc(y, ld)
+    assert_parity(_np(y), fx["y_sample64"], fx["y_sample32"], what=f"{name} sample y")
+    assert_parity(_np(ld), fx["ld_sample64"], fx["ld_sample32"], what=f"{name} sample ld")
+
+
+def _oracle_block(D, C, hidden, act, x, c, eps, t0, t1, steps, dt, seed=3):
+    spec = dict(flow_type="cnf", D=D, C=C, hidden=hidden, L=1, activation=act)
+    st = {k: v.float() for k, v in O.random_state(spec, seed=seed, last_layer_scale=1.0).items()}
+    net = O.build_flow(spec, st, dt).layers[0].nn
+    y, a = O.rk4_augmented(net, torch.as_tensor(x).to(dt), None if c is None else torch.as_tensor(c).to(dt),
+                           torch.as_tensor(eps).to(dt), t0, t1, steps)
+    flat = torch.cat([st[f"layers.0.nn.layers.{i}.{n}"].reshape(-1) for i in range(len(hidden) + 1)
+                      for n in ("weight", "bias")])
+    return y.numpy(), a.numpy(), flat
+
+
+@pytest.mark.parametrize("D,C,hidden,act", [(4, 2, [32, 32], "softplus"), (4, 2, [32, 32], "tanh"),
+                                            (5, 3, [48, 32, 16, 16], "softplus"), (2, 2, [128, 64, 64], "softplus"),
+                                            (16, 0, [128, 128, 128], "softplus")])
+@pytest.mark.parametrize("direction", [(0.0, 1.0), (1.0, 0.0)])
+def test_cnf_kernel_vs_oracle(D, C, hidden, act, direction):
+    from naz_amd import ops
+    B = 300
+    rng = np.random.default_rng(D * 10 + C)
+    x = (rng.standard_normal((B, D)) * 0.8).astype(np.float32)
+    c = rng.standard_normal((B, C)).astype(np.float32) if C else None
+    eps = rng.standard_normal((B, D)).astype(np.float32)
+    t0, t1 = direction
+    y64, a64, flat = _oracle_block(D, C, hidden, act, x, c, eps, t0, t1, 8, torch.float64)
+    y32, a32, _ = _oracle_block(D, C, hidden, act, x, c, eps, t0, t1, 8, torch.float32)
+    d = ops.cnf_desc(D, C, hidden, act)
+    assert ops.cnf_supported(d)
+    packed = ops.cnf_pack(d, _cuda(flat))
+    y, a = ops.cnf_integrate(d, packed, _cuda(x), _cuda(eps), t0, t1, 8, context=None if c is None else _cuda(c))
+    assert_parity(_np(y), y64, y32, what=f"cnf D{D} C{C} {hidden} {act} y")
+    assert_parity(_np(a), a64, a32, what=f"cnf D{D} C{C} {hidden} {act} ld")
+
+
+def test_cnf_ld_modes_broadcast_context_and_ragged_batches():
+    from naz_amd import ops
+    D, C, hidden = 4, 2, [32, 32]
+    rng = np.random.default_rng(9)
+    for B in (1, 15, 127, 129, 1000):
+        x = rng.standard_normal((B, D)).astype(np.float32)
+        c1 = rng.standard_normal((1, C)).astype(np.float32)
+        eps = rng.standard_normal((B, D)).astype(np.float32)
+        y64, a64, flat = _oracle_block(D, C, hidden, "softplus", x, np.repeat(c1, B, 0), eps, 0.0, 1.0, 8,
+                                       torch.float64)
+        y32, a32, _ = _oracle_block(D, C, hidden, "softplus", x, np.repeat(c1, B, 0), eps, 0.0, 1.0, 8,
+                                    torch.float32)
+        d = ops.cnf_desc(D, C, hidden)
+        packed = ops.cnf_pack(d, _cuda(flat))
+        base = torch.full((B,), 2.5, device=DEV)
+        y, ld = ops.cnf_integrate(d, packed, _cuda(x), _cuda(eps), 0.0, 1.0, 8, context=_cuda(c1[0]),
+                                  ld_out=base.clone(), ld_mode=ops.LD_ROWSUM_SUB)
+        assert_parity(_np(y), y64, y32, what=f"B={B} y")
+        assert_parity(_np(ld) - 2.5, -a64, -a32, what=f"B={B} ld SUB")
+        _, ld_add = ops.cnf_integrate(d, packed, _cuda(x), _cuda(eps), 0.0, 1.0, 8, context=_cuda(c1[0]),
+                                      ld_out=base.clone(), ld_mode=ops.LD_ROWSUM_ADD)
+        assert torch.equal(ld_add - 2.5, -(ld - 2.5)) or np.allclose(_np(ld_add) - 2.5, a64, rtol=1e-4, atol=1e-5)
+
+
+def test_cnf_full_size_exact_properties():
+    """Config 5 at BASELINE's batch (2^18 rows): rows are independent, so the solve is bitwise
+    deterministic, permutation-equivariant and chunk-invariant."""
+    from naz_amd import ops
+    D, hidden, B = 16, [128, 128, 128], 1 << 18
+    g = torch.Generator().manual_seed(0)
+    _, _, flat = _oracle_block(D, 0, hidden, "softplus", np.zeros((1, D), np.float32), None,
+                               np.zeros((1, D), np.float32), 0.0, 1.0, 1, torch.float32)
+    d = ops.cnf_desc(D, 0, hidden)
+    packed = ops.cnf_pack(d, _cuda(flat))
+    x = torch.randn(B, D, generator=g).to(DEV)
+    eps = torch.randn(B, D, generator=g).to(DEV)
+    y, a = ops.cnf_integrate(d, packed, x, eps, 0.0, 1.0, 8)
+    y2, a2 = ops.cnf_integrate(d, packed, x, eps, 0.0, 1.0, 8)
+    assert torch.equal(y, y2) and torch.equal(a, a2)
+    perm = torch.randperm(B, generator=g).to(DEV)
+    yp, ap = ops.cnf_integrate(d, packed, x[perm], eps[perm], 0.0, 1.0, 8)
+    assert torch.equal(yp, y[perm]) and torch.equal(ap, a[perm])
+    ys, as_ = [], []
+    for i in range(0, B, 70001):
+        yc, ac = ops.cnf_integrate(d, packed, x[i:i + 70001], eps[i:i + 70001], 0.0, 1.0, 8)
+        ys.append(yc)
+        as_.append(ac)
+    assert torch.equal(torch.cat(ys), y) and torch.equal(torch.cat(as_), a)
+    # spot-check a slice against the oracle
+    idx = torch.arange(0, B, B // 256)
+    y64, a64, _ = _oracle_block(D, 0, hidden, "softplus", x[idx].cpu().numpy(), None, eps[idx].cpu().numpy(), 0.0,
+                                1.0, 8, torch.float64)
+    y32, a32, _ = _oracle_block(D, 0, hidden, "softplus", x[idx].cpu().numpy(), None, eps[idx].cpu().numpy(), 0.0,
+                                1.0, 8, torch.float32)
+    assert_parity(_np(a[idx.to(DEV)]), a64, a32, what="full-size spot ld")
+
+
+def test_cnf_flow_api():
+    """naz surface: NormalizingFlow('cnf', ...) log_prob / sample, fresh probes per call."""
+    from naz_amd.flows import NormalizingFlow
+    f = NormalizingFlow("cnf", None, 4, 2, [32, 32], 2)
+    x = torch.randn(500, 4, device=DEV)
+    c = torch.randn(500, 2, device=DEV)
+    lp1 = f.log_prob(x, condition=c)
+    lp2 = f.log_prob(x, condition=c)
+    assert lp1.shape == (500,) and bool(torch.isfinite(lp1).all())
+    assert not torch.equal(lp1, lp2)  # Hutchinson probes are redrawn per solve, as torchdyn does
+    s = f.sample([64], condition=c[0])
+    assert s.shape == (64, 4) and bool(torch.isfinite(s).all())
+    with torch.enable_grad():
+        with pytest.raises(NotImplementedError):
+            f.log_prob(x, condition=c)

@@ -179,3 +179,59 @@ def test_synthetic_inputs_match_baseline_spec():
     assert x.dtype == np.float32 and x.shape == (20000, 16)
     out = np.mean(np.abs(x) > 3.0)
     assert 0.05 < out < 0.4  # a meaningful share of coordinates hits the identity tails
+
+
+# ------------------------------------------------------------------ a11: CNF restatement
+def _cnf_flow(spec, seed=1234, dtype=torch.float64):
+    st = O.random_state(spec, seed=seed, last_layer_scale=1.0)
+    return O.build_flow(spec, st, dtype)
+
+
+def test_cnf_hutchinson_is_unbiased_for_the_trace():
+    """naz hutch_trace (continuous_transforms.py:85-89): E_eps[eps^T J eps] = tr J."""
+    spec = dict(flow_type="cnf", D=4, C=2, hidden=[32, 32], L=1)
+    net = _cnf_flow(spec).layers[0].nn
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(3, 4, generator=g, dtype=torch.float64)
+    c = torch.randn(3, 2, generator=g, dtype=torch.float64)
+    n = 40000
+    xr, cr = x.repeat_interleave(n, 0), c.repeat_interleave(n, 0)
+    eps = torch.randn(3 * n, 4, generator=g, dtype=torch.float64)
+    _, neg_tr = O.hutchinson_rhs(net, xr, cr, eps)
+    est = (-neg_tr).reshape(3, n)
+    for r in range(3):
+        J = torch.autograd.functional.jacobian(lambda v: net(v[None], c[r:r + 1])[0], x[r])
+        exact = torch.trace(J)
+        sem = est[r].std() / math.sqrt(n)
+        assert abs(est[r].mean() - exact) < 5 * sem
+
+
+def test_cnf_rk4_converges_and_inverts():
+    """Pinned 8-step RK4 (odeint.py:46-52) is within RK4 error of a 128-step solve, and the
+    sampling solve (t 1 -> 0) inverts the density solve (t 0 -> 1) for the same probe."""
+    spec = dict(flow_type="cnf", D=4, C=2, hidden=[32, 32], L=1)
+    blk = _cnf_flow(spec).layers[0]
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(64, 4, generator=g, dtype=torch.float64)
+    c = torch.randn(64, 2, generator=g, dtype=torch.float64)
+    eps = torch.randn(64, 4, generator=g, dtype=torch.float64)
+    z8, a8 = O.rk4_augmented(blk.nn, x, c, eps, 0.0, 1.0, 8)
+    z128, a128 = O.rk4_augmented(blk.nn, x, c, eps, 0.0, 1.0, 128)
+    assert (z8 - z128).abs().max() < 1e-5 and (a8 - a128).abs().max() < 1e-5
+    xb, ab = O.rk4_augmented(blk.nn, z128, c, eps, 1.0, 0.0, 128)
+    assert (xb - x).abs().max() < 1e-10 and (ab + a128).abs().max() < 1e-10
+
+
+@pytest.mark.parametrize("name", ["cnf_d4c2.npz", "cnf_d16c0.npz"])
+def test_golden_cnf_fixture(name):
+    fx = load_golden(name)
+    spec = {k[5:]: fx[k].tolist() for k in fx if k.startswith("spec/")}
+    state = {k[6:]: fx[k] for k in fx if k.startswith("state/")}
+    f = O.build_flow(spec, state, torch.float64)
+    c = torch.as_tensor(fx["ctx"]).double() if "ctx" in fx else None
+    for l, layer in enumerate(f.layers):
+        layer.eps = torch.as_tensor(fx[f"eps_l/{l}"])
+    lp = f.log_prob(torch.as_tensor(fx["x"]).double(), c)
+    np.testing.assert_allclose(lp.numpy(), fx["lp64"], rtol=1e-12, atol=1e-10)
+    r = rel_err(fx["lp32"], fx["lp64"])
+    assert np.median(r) < 1e-6 and r.max() < 1e-4

@@ -44,10 +44,12 @@ constexpr int cnf_wsize(int j, int ks0, int h0, int h1, int h2, int h3) {
   return j == 0 ? cnf_hid(0, h0, h1, h2, h3) / 16 * ks0 * 64
                 : cnf_hid(j, h0, h1, h2, h3) / 16 * (cnf_hid(j - 1, h0, h1, h2, h3) / 16) * 256;
 }
+// non-recursive on purpose: every use must fold to a constant (a recursive constexpr helper
+// called outside a constant expression becomes a real device call with an unbounded stack)
 constexpr int cnf_offw(int j, int ks0, int h0, int h1, int h2, int h3) {
-  return j == 0 ? 0
-                : cnf_offw(j - 1, ks0, h0, h1, h2, h3) + cnf_wsize(j - 1, ks0, h0, h1, h2, h3) +
-                      cnf_hid(j - 1, h0, h1, h2, h3);
+  int off = 0;
+  for (int i = 0; i < j; ++i) off += cnf_wsize(i, ks0, h0, h1, h2, h3) + cnf_hid(i, h0, h1, h2, h3);
+  return off;
 }
 
 template <int D_, int C_, int H0_, int H1_, int H2_, int H3_, int ACT_>
@@ -105,7 +107,8 @@ __global__ void cnf_pack_kernel(const float* __restrict__ flat, float* __restric
   float v = 0.f;
   // layer 0 weights: [ob][s4][lane][i], k-step s = 4 s4 + i carries x feature q + 4s (s < XS)
   // or context feature q + 4(s - XS) (XS <= s < XS + CS), q = lane >> 4
-  if (e < CF::off_b(0)) {
+  constexpr int OB0 = CF::off_b(0);
+  if (e < OB0) {
     const int i = e & 3, lane = (e >> 2) & 63, rest = e >> 8;
     const int s4 = rest % (CF::KS0 / 4), ob = rest / (CF::KS0 / 4);
     const int s = 4 * s4 + i, o = 16 * ob + (lane & 15), q = lane >> 4;
@@ -125,18 +128,19 @@ __global__ void cnf_pack_kernel(const float* __restrict__ flat, float* __restric
   cnf_static_for<0, CF::NH>([&](auto J) {
     constexpr int j = decltype(J)::value;
     if (done) return;
-    constexpr int ob_ = CF::off_b(j);
-    if (j > 0 && e >= CF::off_w(j) && e < ob_) {
-      const int r = e - CF::off_w(j);
+    constexpr int ob_ = CF::off_b(j), ow_ = CF::off_w(j);
+    constexpr int nbi = CF::NB(j > 0 ? j - 1 : 0), hin = j == 0 ? CF::in0 : CF::hid(j > 0 ? j - 1 : 0);
+    constexpr int hj = CF::hid(j);
+    constexpr int64_t fo = CF::flat_off_w(j);
+    if (j > 0 && e >= ow_ && e < ob_) {
+      const int r = e - ow_;
       const int i = r & 3, lane = (r >> 2) & 63, rest = r >> 8;
-      const int nbi = CF::NB(j > 0 ? j - 1 : 0);
       const int b = rest % nbi, ob = rest / nbi;
       const int o = 16 * ob + (lane & 15), k = 16 * b + 4 * (lane >> 4) + i;
-      v = flat[CF::flat_off_w(j) + (int64_t)o * CF::hid(j > 0 ? j - 1 : 0) + k];
+      v = flat[fo + (int64_t)o * hin + k];
       done = true;
-    } else if (e >= ob_ && e < ob_ + CF::hid(j)) {
-      v = flat[CF::flat_off_w(j) + (int64_t)CF::hid(j) * (j == 0 ? CF::in0 : CF::hid(j > 0 ? j - 1 : 0)) +
-               (e - ob_)];
+    } else if (e >= ob_ && e < ob_ + hj) {
+      v = flat[fo + (int64_t)hj * hin + (e - ob_)];
       done = true;
     }
   });
@@ -146,7 +150,8 @@ __global__ void cnf_pack_kernel(const float* __restrict__ flat, float* __restric
     if (e < CF::OFF_BL) {  // output layer: packed row r_local = lane & 15 <-> state feature q_r + 4(4 ob + i_r)
       const int r = e - CF::OFF_WL;
       const int i = r & 3, lane = (r >> 2) & 63, rest = r >> 8;
-      const int b = rest % CF::NB(CF::NH - 1), ob = rest / CF::NB(CF::NH - 1);
+      constexpr int nbl_in = CF::HL / 16;
+      const int b = rest % nbl_in, ob = rest / nbl_in;
       const int rl = lane & 15, nf = (rl >> 2) + 4 * (4 * ob + (rl & 3));
       const int k = 16 * b + 4 * (lane >> 4) + i;
       if (nf < CF::D) v = flat[fw + (int64_t)nf * HL + k];
@@ -233,9 +238,9 @@ NAZ_DEV void cnf_rhs(const float* __restrict__ lds, const float (&xin)[CF::XS], 
   floatx4 av[8], at[8], bv[8], bt[8];
   // layer 0: k-steps over [x | ctx | pad]
   {
-    constexpr int NB0 = CF::NB(0);
-    const float* W = lds + CF::off_w(0);
-    init_bias4<NB0>(av, at, lds + CF::off_b(0), q);
+    constexpr int NB0 = CF::NB(0), OW0 = CF::off_w(0), OB0 = CF::off_b(0);
+    const float* W = lds + OW0;
+    init_bias4<NB0>(av, at, lds + OB0, q);
 #pragma unroll
     for (int s4 = 0; s4 < CF::KS0 / 4; ++s4)
 #pragma unroll
@@ -257,19 +262,19 @@ NAZ_DEV void cnf_rhs(const float* __restrict__ lds, const float (&xin)[CF::XS], 
   // hidden layers 1..NH-1, ping-pong between (av, at) and (bv, bt)
   cnf_static_for<1, CF::NH>([&](auto J) {
     constexpr int j = decltype(J)::value;
-    constexpr int NBI = CF::NB(j - 1), NBO = CF::NB(j);
+    constexpr int NBI = CF::NB(j - 1), NBO = CF::NB(j), OW = CF::off_w(j), OB = CF::off_b(j);
     if constexpr (j % 2 == 1) {
-      init_bias4<NBO>(bv, bt, lds + CF::off_b(j), q);
-      cnf_linear<NBI, NBO>(lds + CF::off_w(j), av, at, bv, bt, lane);
+      init_bias4<NBO>(bv, bt, lds + OB, q);
+      cnf_linear<NBI, NBO>(lds + OW, av, at, bv, bt, lane);
       act_all<CF::ACT, NBO>(bv, bt);
     } else {
-      init_bias4<NBO>(av, at, lds + CF::off_b(j), q);
-      cnf_linear<NBI, NBO>(lds + CF::off_w(j), bv, bt, av, at, lane);
+      init_bias4<NBO>(av, at, lds + OB, q);
+      cnf_linear<NBI, NBO>(lds + OW, bv, bt, av, at, lane);
       act_all<CF::ACT, NBO>(av, at);
     }
   });
   // output layer (no activation); rows permuted so register i of block ob = state slot 4 ob + i
-  constexpr int NBI = CF::NB(CF::NH - 1);
+  constexpr int NBI = CF::HL / 16;
   floatx4 ov[8], ot[8];
   init_bias4<CF::NBL>(ov, ot, lds + CF::OFF_BL, q);
   if constexpr ((CF::NH - 1) % 2 == 0)

@@ -114,10 +114,12 @@ int naz_rqs_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int6
 /* C[m,n] (+)= sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn]; exact fp32 MFMA.  With a mask:
  * mask_b = 0 multiplies the OUTPUT by mask[m*smm + n*smn] (dW of a MADE layer), mask_b = 1
  * multiplies the B OPERAND by mask[k*smm + n*smn] (dX through W*mask).
- * split_k > 1 accumulates atomically (zero C first for an overwrite).                     */
+ * split_k > 1 accumulates atomically (zero C first for an overwrite).
+ * rowsum (may be NULL): also (+)= sum_k A(m,k) into rowsum[m] — with A = dPre^T this is the
+ * bias gradient, computed as an extra all-ones column of B in the same MFMA reduction.      */
 int naz_gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
              int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
-             int mask_b, int accumulate, int split_k, void* stream);
+             int mask_b, int accumulate, int split_k, float* rowsum, void* stream);
 /* VJP of naz_affine_ar (the kernel reports the FORWARD log-det sum(clamp(ls)) in both
  * directions).  x = the map's input, y = its output, g_ld [B] = dL/d(row ld) (may be NULL).
  * pyro clamps log_scale with clamp_preserve_gradients: the clamp passes gradients through.

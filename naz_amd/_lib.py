@@ -46,7 +46,7 @@ SIGNATURES = {
     "naz_rqs_bwd": (C.c_int, [_i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _vp, _i64, _vp, _i64, _i64, _i, _i, _i,
                               C.c_float, _vp]),
     "naz_gemm": (C.c_int, [_i, _i, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i, _i,
-                           _i, _vp]),
+                           _i, _vp, _vp]),
     "naz_affine_ar_bwd": (C.c_int, [_i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64,
                                     _i, _vp]),
     "naz_colsum": (C.c_int, [_vp, _i64, _i64, _i, _vp, _vp]),

@@ -5,8 +5,8 @@ naz's ``train`` (naz/trainers/train_flows.py:194-213) differentiates
 Here every node of that graph is a ``torch.autograd.Function`` whose forward AND backward
 are HIP kernels:
 
-  LinearActFn   act(cat[ctx, x] @ (W*mask)^T + b)   bwd: naz_act_bwd, naz_gemm (dX, dW with the
-                                                     MADE mask fused), naz_colsum (db)
+  LinearActFn   act(cat[ctx, x] @ (W*mask)^T + b)   bwd: naz_act_bwd, naz_gemm (dX; dW with the
+                                                     MADE mask fused and db as an extra ones column)
   RqsFn         RQ spline, either direction          bwd: naz_rqs_bwd (implicit-function rule
                                                      for the inverse)
   AffineARFn    pyro AffineAutoregressive step       bwd: naz_affine_ar_bwd
@@ -50,16 +50,21 @@ class LinearActFn(Function):
         M = y.shape[0]
         Cd = 0 if c is None else c.shape[-1]
         g_x = g_c = g_W = g_b = None
+        want_b = ctx.has_bias and _needs(ctx, 3)
+        if want_b:
+            g_b = torch.empty(W.shape[0], device=W.device, dtype=torch.float32)
+        gT = gpre.t()  # [N, M] view
         if _needs(ctx, 2):
             g_W = torch.empty_like(W)
-            gT = gpre.t()  # [N, M] view
-            if Cd:
+            if Cd:  # db rides on the first dW GEMM as an all-ones column
                 cc = c.reshape(1, -1).expand(M, Cd) if (c.dim() == 1 or c.shape[0] == 1) and M != 1 else c
-                ops.gemm(gT, cc, out=g_W[:, :Cd], mask=None if mask is None else mask[:, :Cd])
+                ops.gemm(gT, cc, out=g_W[:, :Cd], mask=None if mask is None else mask[:, :Cd],
+                         rowsum=g_b)
             if x is not None:
-                ops.gemm(gT, x, out=g_W[:, Cd:], mask=None if mask is None else mask[:, Cd:])
-        if ctx.has_bias and _needs(ctx, 3):
-            g_b = ops.colsum(gpre)
+                ops.gemm(gT, x, out=g_W[:, Cd:], mask=None if mask is None else mask[:, Cd:],
+                         rowsum=None if Cd else g_b)
+        elif want_b:
+            ops.gemm(gT, gT[:0].t(), out=torch.empty(W.shape[0], 0, device=W.device), rowsum=g_b)
         if x is not None and _needs(ctx, 0):
             g_x = ops.gemm(gpre, W[:, Cd:], mask=None if mask is None else mask[:, Cd:], mask_b=True)
         if Cd and _needs(ctx, 1):

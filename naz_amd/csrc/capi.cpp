@@ -101,9 +101,9 @@ int naz_rqs_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int6
 
 int naz_gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
              int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
-             int mask_b, int accumulate, int split_k, void* stream) {
+             int mask_b, int accumulate, int split_k, float* rowsum, void* stream) {
   if (M < 0 || N < 0 || K < 0) return set_error("naz_gemm: negative shape");
-  return gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, mask, smm, smn, mask_b, accumulate, split_k,
+  return gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, mask, smm, smn, mask_b, accumulate, split_k, rowsum,
               as_stream(stream));
 }
 

@@ -22,7 +22,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(int M, int N, int64_t K, cons
                                                    int64_t sak, const float* __restrict__ Bm, int64_t sbk, int64_t sbn,
                                                    float* __restrict__ Cm, int64_t scm, int64_t scn,
                                                    const float* __restrict__ mask, int64_t smm, int64_t smn,
-                                                   int mask_b, int accumulate, int atomic, int64_t k_per_split) {
+                                                   int mask_b, int accumulate, int atomic, int64_t k_per_split,
+                                                   float* __restrict__ rowsum) {
   __shared__ float As[GBK][GBM + GPAD];
   __shared__ float Bs[GBK][GBN + GPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -31,6 +32,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(int M, int N, int64_t K, cons
   const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
   const int64_t kend = (kbeg + k_per_split) < K ? (kbeg + k_per_split) : K;
   const bool a_kfast = sak == 1, b_nfast = sbn == 1;
+  // rowsum != null: logical column N is an all-ones B column, its C column goes to rowsum[m]
+  const int NE = rowsum != nullptr ? N + 1 : N;
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -47,7 +50,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(int M, int N, int64_t K, cons
       if (b_nfast) { kb = e >> 6; nn = e & 63; } else { nn = e >> 4; kb = e & 15; }
       const int n = n0 + nn;
       const int64_t kq = k0 + kb;
-      float bv = (n < N && kq < kend) ? Bm[kq * sbk + (int64_t)n * sbn] : 0.f;
+      float bv = (n < N && kq < kend) ? Bm[kq * sbk + (int64_t)n * sbn] : ((n == N && n < NE && kq < kend) ? 1.f : 0.f);
       if (mask_b && n < N && kq < kend) bv *= mask[kq * smm + (int64_t)n * smn];
       Bs[kb][nn] = bv;
     }
@@ -61,14 +64,14 @@ __global__ void __launch_bounds__(256) gemm_kernel(int M, int N, int64_t K, cons
     __syncthreads();
   }
   const int n = n0 + wn * 32 + (lane & 31);
-  if (n >= N) return;
+  if (n >= NE) return;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (m >= M) continue;
     float v = acc[r];
-    if (mask != nullptr && !mask_b) v *= mask[(int64_t)m * smm + (int64_t)n * smn];
-    float* dst = Cm + (int64_t)m * scm + (int64_t)n * scn;
+    if (mask != nullptr && !mask_b && n < N) v *= mask[(int64_t)m * smm + (int64_t)n * smn];
+    float* dst = n < N ? Cm + (int64_t)m * scm + (int64_t)n * scn : rowsum + m;
     if (atomic) atomicAdd(dst, v);
     else *dst = accumulate ? *dst + v : v;
   }
@@ -98,8 +101,8 @@ __global__ void act_bwd_kernel(const float* __restrict__ gy, int64_t ldg, const 
 
 int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
          float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn, int mask_b, int accumulate,
-         int split_k, hipStream_t s) {
-  if (M <= 0 || N <= 0) return 0;
+         int split_k, float* rowsum, hipStream_t s) {
+  if (M <= 0 || (N <= 0 && rowsum == nullptr)) return 0;
   if (K <= 0) {
     if (!accumulate && split_k <= 1) return set_error("naz_gemm: K = 0 with overwrite is not supported");
     return 0;
@@ -108,11 +111,12 @@ int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, cons
   int64_t kps = (K + split_k - 1) / split_k;
   kps = (kps + GBK - 1) / GBK * GBK;
   const int64_t splits = (K + kps - 1) / kps;
-  dim3 grid((unsigned)((M + GBM - 1) / GBM), (unsigned)((N + GBN - 1) / GBN), (unsigned)splits);
+  const int NE = rowsum != nullptr ? N + 1 : N;
+  dim3 grid((unsigned)((M + GBM - 1) / GBM), (unsigned)((NE + GBN - 1) / GBN), (unsigned)splits);
   // split-K always accumulates atomically into C (the caller zeroes C for an overwrite)
   const int atomic = splits > 1 ? 1 : 0;
   hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, mask, smm,
-                     smn, mask_b && mask != nullptr, accumulate, atomic, kps);
+                     smn, mask_b && mask != nullptr, accumulate, atomic, kps, rowsum);
   return check_launch("gemm_kernel");
 }
 

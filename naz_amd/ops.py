@@ -258,11 +258,13 @@ def _split_k(M: int, N: int, K: int) -> int:
 
 
 def gemm(a: Tensor, b: Tensor, out: Optional[Tensor] = None, mask: Optional[Tensor] = None, mask_b: bool = False,
-         accumulate: bool = False, split_k: Optional[int] = None) -> Tensor:
+         accumulate: bool = False, split_k: Optional[int] = None, rowsum: Optional[Tensor] = None) -> Tensor:
     """out (+)= a @ b for arbitrary-strided 2-D views (transposes / stride-0 broadcasts are
     free); ``mask`` multiplies the output (mask_b False) or ``b`` (mask_b True).  Exact fp32
-    MFMA (naz_gemm); long reductions are split over the grid with atomic accumulation."""
-    dev = _dev(a, b, out, mask)
+    MFMA (naz_gemm); long reductions are split over the grid with atomic accumulation.
+    ``rowsum`` [M] (contiguous) also receives a.sum(1) through the same MFMA reduction
+    (accumulated like ``out``)."""
+    dev = _dev(a, b, out, mask, rowsum)
     M, K = a.shape
     K2, N = b.shape
     if K2 != K:
@@ -274,13 +276,17 @@ def gemm(a: Tensor, b: Tensor, out: Optional[Tensor] = None, mask: Optional[Tens
         raise ValueError(f"gemm: out must be {(M, N)}")
     if mask is not None and mask.shape != ((K, N) if mask_b else (M, N)):
         raise ValueError("gemm: mask shape mismatch")
-    sk = _split_k(M, N, K) if split_k is None else int(split_k)
+    if rowsum is not None and (rowsum.shape != (M,) or not rowsum.is_contiguous()):
+        raise ValueError("gemm: rowsum must be a contiguous [M] tensor")
+    sk = _split_k(M, N + (rowsum is not None), K) if split_k is None else int(split_k)
     if sk > 1 and not accumulate:
         out.zero_()
+        if rowsum is not None:
+            rowsum.zero_()
     smm, smn = (0, 0) if mask is None else mask.stride()
     check(lib().naz_gemm(M, N, K, _p(a), a.stride(0), a.stride(1), _p(b), b.stride(0), b.stride(1), _p(out),
                          out.stride(0), out.stride(1), _p(mask), smm, smn, int(mask_b), int(accumulate), sk,
-                         _stream(dev)), "gemm")
+                         _p(rowsum), _stream(dev)), "gemm")
     return out
 
 

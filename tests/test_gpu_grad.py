@@ -148,10 +148,12 @@ def test_gemm_strided_split_k(M, N, K, split):
     a = torch.randn(K, M, generator=g)  # used transposed
     b = torch.randn(K, N, generator=g)
     mask = (torch.rand(M, N, generator=g) > 0.5).float()
-    out = ops.gemm(_cuda(a).t(), _cuda(b), mask=_cuda(mask), split_k=split)
+    rs = torch.empty(M, device=DEV)
+    out = ops.gemm(_cuda(a).t(), _cuda(b), mask=_cuda(mask), split_k=split, rowsum=rs)
     ref64 = (a.double().t() @ b.double()) * mask.double()
     ref32 = (a.t() @ b) * mask
     _check(out, ref64, ref32, f"gemm {M}x{N}x{K}")
+    _check(rs, a.double().sum(0), a.sum(0), f"gemm {M}x{N}x{K} fused row sums (bias gradient)")
 
 
 # ------------------------------------------------------------------ a5 affine step VJP

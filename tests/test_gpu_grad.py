@@ -2,8 +2,8 @@
 float64 torch autograd (the gradient pyro's eager transforms produce, restated in
 oracle/naz_oracle.py), with the oracle's float32 autograd as the reference-precision yardstick.
 
-Criterion: tests/parity.py statistics with the gradient floor max(|g64|, rms(g64)) and the
-4x exceedance-count factor (see tests/parity.py).
+Criterion: tests/parity.py median / q99 / max bounds with the gradient floor
+max(|g64|, rms(g64)) and no exceedance-count bound (see tests/parity.py).
 """
 import numpy as np
 import pytest
@@ -29,7 +29,7 @@ def _np(t):
 def _check(v, g64, g32, what):
     g64 = _np(g64) if torch.is_tensor(g64) else g64
     g32 = _np(g32) if torch.is_tensor(g32) else g32
-    return assert_parity(_np(v), g64, g32, what=what, floor=grad_floor(g64), count_factor=4.0)
+    return assert_parity(_np(v), g64, g32, what=what, floor=grad_floor(g64), count_factor=None)
 
 
 @pytest.fixture(scope="module", autouse=True)

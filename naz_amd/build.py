@@ -18,6 +18,10 @@ OBJ = PKG / "build"
 LIB = PKG / "lib" / "libnazhip.so"
 INCLUDE = PKG.parent / "include"
 ARCH = os.environ.get("NAZ_OFFLOAD_ARCH", "gfx950")
+# Per-source flags.  The MFMA kernels are built without the SLP vectorizer: the packed f32 VALU
+# ops it forms (v_pk_add/mul/fma_f32) issue slower than scalar ones beside MFMAs, and the
+# packing moves add register pressure (spills in coupling_x6_kernel with it on).
+SOURCE_FLAGS = {"coupling.hip": ["-fno-slp-vectorize"], "cnf.hip": ["-fno-slp-vectorize"]}
 SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "elementwise.hip", "coupling.hip", "cnf.hip", "capi.cpp"]
 
 
@@ -35,7 +39,7 @@ def _headers_mtime() -> float:
 
 def _compile(src: Path, obj: Path, extra: list) -> str:
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
-           f"-I{INCLUDE}", "-c", str(src), "-o", str(obj)] + extra
+           f"-I{INCLUDE}", "-c", str(src), "-o", str(obj)] + SOURCE_FLAGS.get(src.name, []) + extra
     if src.suffix == ".cpp":
         cmd[1:2] = []  # host-only TU
         cmd += ["-x", "c++"] if False else []
@@ -45,16 +49,20 @@ def _compile(src: Path, obj: Path, extra: list) -> str:
     return r.stderr
 
 
-def build(verbose: bool = False, jobs: int = 4, extra: list | None = None) -> Path:
+def build(verbose: bool = False, jobs: int = 4, extra: list | None = None, variant: str | None = None) -> Path:
+    """Build the library.  `variant` (with `extra` flags, e.g. ablation -D's) builds
+    naz_amd/lib/libnazhip_<variant>.so from objects in naz_amd/build/<variant>/ instead."""
     extra = list(extra or [])
-    OBJ.mkdir(exist_ok=True)
-    LIB.parent.mkdir(exist_ok=True)
+    obj_dir = OBJ / variant if variant else OBJ
+    lib_path = LIB.with_name(f"libnazhip_{variant}.so") if variant else LIB
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    lib_path.parent.mkdir(exist_ok=True)
     hm = _headers_mtime()
     todo = []
     objs = []
     for s in SOURCES:
         src = CSRC / s
-        obj = OBJ / (src.stem + ".o")
+        obj = obj_dir / (src.stem + ".o")
         objs.append(obj)
         if not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hm):
             todo.append((src, obj))
@@ -64,13 +72,17 @@ def build(verbose: bool = False, jobs: int = 4, extra: list | None = None) -> Pa
                 print(f"[naz_amd.build] {src.name} -> {obj.name}", file=sys.stderr)
                 if warn.strip():
                     print(warn, file=sys.stderr)
-    if todo or not LIB.exists() or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB)] + [str(o) for o in objs]
+    if todo or not lib_path.exists() or lib_path.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib_path)] + [str(o) for o in objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    return LIB
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build(verbose=True))
+    # python -m naz_amd.build [variant -DFLAG ...]
+    if len(sys.argv) > 1:
+        print(build(verbose=True, variant=sys.argv[1], extra=sys.argv[2:]))
+    else:
+        print(build(verbose=True))

@@ -556,15 +556,26 @@ struct Frag2 {
   half8 h, l;
 };
 
+// v - f32(f16 half of hp) in ONE v_fma_mix_f32 (the compiler emits cvt + sub); exact, since
+// v - hi is representable.  HI selects the upper f16 of the packed pair.
+template <bool HI>
+NAZ_DEV float sub_f16_piece(float v, unsigned hp) {
+  float r;
+  if constexpr (HI)
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(v));
+  else
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(v));
+  return r;
+}
+
 NAZ_DEV Frag2 split8_f16(const float (&v)[8]) {
   u32x4 H, Lo;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const auto hp = __builtin_amdgcn_cvt_pkrtz(v[2 * q], v[2 * q + 1]);
-    const float r0 = v[2 * q] - (float)hp[0], r1 = v[2 * q + 1] - (float)hp[1];
-    const auto lp = __builtin_amdgcn_cvt_pkrtz(r0, r1);
-    H[q] = __builtin_bit_cast(unsigned, hp);
-    Lo[q] = __builtin_bit_cast(unsigned, lp);
+    const unsigned hp = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v[2 * q], v[2 * q + 1]));
+    const float r0 = sub_f16_piece<false>(v[2 * q], hp), r1 = sub_f16_piece<true>(v[2 * q + 1], hp);
+    H[q] = hp;
+    Lo[q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(r0, r1));
   }
   return Frag2{__builtin_bit_cast(half8, H), __builtin_bit_cast(half8, Lo)};
 }
@@ -596,8 +607,14 @@ NAZ_DEV unsigned f16_piece_bits(float v, int piece) {
 
 // LDS ring: two slots of 40 KB per 128-row workgroup (two workgroups per CU use all 160 KB).
 // Stage s+1's LDS-DMA copy lands in one slot while stage s computes from the other.
-constexpr int kX6Slot = 10240;     // 40 KB: two 256-thread workgroups per CU (2 x 2 slots = 160 KB)
-constexpr int kX6Waves = 4;        // 128 rows per workgroup (8-wave / 256-row workgroups measured no faster)
+#ifndef NAZ_X6_SLOT
+#define NAZ_X6_SLOT 10240
+#endif
+#ifndef NAZ_X6_WAVES
+#define NAZ_X6_WAVES 4
+#endif
+constexpr int kX6Slot = NAZ_X6_SLOT;   // 40 KB: two workgroups per CU (2 x 2 slots = 160 KB)
+constexpr int kX6Waves = NAZ_X6_WAVES; // 128 rows per workgroup
 constexpr int kX6Rows = 32 * kX6Waves;
 constexpr int kChunk = 256;            // one (block, k-step, piece) A fragment set: 64 lanes x 16 B
 
@@ -882,7 +899,7 @@ NAZ_DEV void frags_from_acc(const floatx16 (&x)[NB], Frag3 (&bf)[KB]) {
 }
 
 template <class CF, bool DIR_INV>
-__global__ void __launch_bounds__(kX6Rows * 2, 2) coupling_x6_kernel(
+__global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound) {
@@ -953,10 +970,8 @@ __global__ void __launch_bounds__(kX6Rows * 2, 2) coupling_x6_kernel(
 #else
           if constexpr (DIR_INV && CF::LOWER) {
 #endif
-            SplineTables<CF::K> t;
-            load_tables<CF>(cur + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
             float ld;
-            zl[q] = rqs_apply<CF::K, true, true>(t, zl[q], bound, ld);
+            zl[q] = rqs_table<CF::K, true>(cur + CF::A_TBL + (h * CF::SH + q) * CF::TBL, zl[q], bound, ld);
             ldsum -= ld;
           }
           x1[q] = zl[q];
@@ -982,10 +997,8 @@ __global__ void __launch_bounds__(kX6Rows * 2, 2) coupling_x6_kernel(
         if constexpr (!DIR_INV && CF::LOWER) {
 #pragma unroll
           for (int q = 0; q < CF::SH; ++q) {
-            SplineTables<CF::K> t;
-            load_tables<CF>(cur + CF::A_TBL + (h * CF::SH + q) * CF::TBL, t);
             float ld;
-            zl[q] = rqs_apply<CF::K, false, true>(t, zl[q], bound, ld);
+            zl[q] = rqs_table<CF::K, false>(cur + CF::A_TBL + (h * CF::SH + q) * CF::TBL, zl[q], bound, ld);
             ldsum += ld;
           }
         }
@@ -1037,10 +1050,8 @@ __global__ void __launch_bounds__(kX6Rows * 2, 2) coupling_x6_kernel(
         const int sd = q * CF::P + 2 * CF::K + k;
         ud[k] = acc3[sd >> 4][sd & 15];
       }
-      SplineTables<CF::K> t;
-      build_tables<CF::K, true>(uw, uh, ud, bound, t);
       float ld;
-      zu[q] = rqs_apply<CF::K, DIR_INV, true>(t, zu[q], bound, ld);
+      zu[q] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[q], bound, ld);
       ldsum += DIR_INV ? -ld : ld;
     }
   }

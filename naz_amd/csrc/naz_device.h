@@ -234,4 +234,124 @@ NAZ_DEV float rqs_apply(const SplineTables<K>& t, float x, float bound, float& l
   return out;
 }
 
+// Rational-quadratic map on one selected bin (cw0, w, ch0, h, d0, d1): forward or inverse,
+// with the ld of the map applied.  Shared by the select-first evaluators below.
+template <bool INV>
+NAZ_DEV float rqs_bin(float x, float cw0, float w, float ch0, float h, float d0, float d1, float& ld) {
+  using M = Math<true>;
+  const float delta = h * M::rcp(w);
+  const float t1 = (d0 + d1) - 2.f * delta;
+  if constexpr (INV) {
+    const float dy = x - ch0;
+    const float a = dy * t1 + h * (delta - d0);
+    const float b = h * d0 - dy * t1;
+    const float c = -delta * dy;
+    const float disc = fmaxf(b * b - 4.f * a * c, 0.f);
+    const float root = M::div(2.f * c, -b - M::sqrt(disc));
+    const float tomt = root * (1.f - root);
+    const float den = delta + t1 * tomt;
+    const float omr = 1.f - root;
+    const float dnum = delta * delta * (d1 * root * root + 2.f * delta * tomt + d0 * omr * omr);
+    ld = -(M::log(dnum) - 2.f * M::log(den));
+    return root * w + cw0;
+  } else {
+    const float th = M::div(x - cw0, w);
+    const float tomt = th * (1.f - th);
+    const float num = h * (delta * th * th + d0 * tomt);
+    const float den = delta + t1 * tomt;
+    const float omt = 1.f - th;
+    const float dnum = delta * delta * (d1 * th * th + 2.f * delta * tomt + d0 * omt * omt);
+    ld = M::log(dnum) - 2.f * M::log(den);
+    return ch0 + M::div(num, den);
+  }
+}
+
+// Select-first spline for the fused MFMA kernels: the same map as build_tables<K, true> +
+// rqs_apply<K, INV, true> (pyro _monotonic_rational_spline, quadratic), restated so that only
+// the selected bin's quantities are formed:
+//   * knot k of either table is  2B·(k·m + (1 − K·m)·E_k / E_K) − B  with E_k the prefix sum of
+//     the softmax numerators exp(u − max u): ONE fma per knot, no normalised fractions;
+//   * only the searched table (y knots for INV, x knots for the forward map) is formed at all
+//     K−1 interior knots; bin k = #{interior knots with x ≥ knot + eps} (pyro's
+//     clamp(searchsorted − 1, 0, K−1) over the padded knots);
+//   * the other table's two knots and the two knot slopes (softplus) are formed only for that bin.
+// Knot positions agree with the cumsum form to a few ulp (fp32 prefix sums, fused multiply-add);
+// the map is C¹ across knots, so a bin flip at a knot changes y and ld only at rounding level.
+// Out-of-box inputs (|x| > B, NaN) pass through with ld = 0, branch-free.
+template <int K, bool INV>
+NAZ_DEV float rqs_select(const float* uw, const float* uh, const float* ud, float x, float bound, float& ld) {
+  constexpr float kL2E = 1.44269504088896341f;
+  float Ew[K + 1], Eh[K + 1];
+  {
+    float mw = uw[0], mh = uh[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+      mw = fmaxf(mw, uw[k]);
+      mh = fmaxf(mh, uh[k]);
+    }
+    const float mwl = mw * kL2E, mhl = mh * kL2E;
+    Ew[0] = 0.f;
+    Eh[0] = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      Ew[k + 1] = Ew[k] + __builtin_amdgcn_exp2f(__builtin_fmaf(uw[k], kL2E, -mwl));
+      Eh[k + 1] = Eh[k] + __builtin_amdgcn_exp2f(__builtin_fmaf(uh[k], kL2E, -mhl));
+    }
+  }
+  const float two_b = 2.f * bound;
+  const float Aw = two_b * (1.f - kMinBinWidth * (float)K) * Math<true>::rcp(Ew[K]);
+  const float Ah = two_b * (1.f - kMinBinHeight * (float)K) * Math<true>::rcp(Eh[K]);
+  const float* Es = INV ? Eh : Ew;  // searched table
+  const float* Eo = INV ? Ew : Eh;
+  const float As = INV ? Ah : Aw, Ao = INV ? Aw : Ah;
+  const float ms = two_b * (INV ? kMinBinHeight : kMinBinWidth), mo = two_b * (INV ? kMinBinWidth : kMinBinHeight);
+  float s0 = 0.f, s1 = Es[1], o0 = 0.f, o1 = Eo[1], udl = ud[0], udh = ud[0];
+  int idx = 0;
+#pragma unroll
+  for (int k = 1; k < K; ++k) {
+    const float key = __builtin_fmaf(As, Es[k], __builtin_fmaf(ms, (float)k, -bound) + kSearchEps);
+    const bool s = x >= key;
+    s0 = s ? Es[k] : s0;
+    s1 = s ? Es[k + 1] : s1;
+    o0 = s ? Eo[k] : o0;
+    o1 = s ? Eo[k + 1] : o1;
+    udl = s ? ud[k - 1] : udl;
+    if (k < K - 1) udh = s ? ud[k] : udh;
+    idx += s ? 1 : 0;
+  }
+  const bool first = idx == 0, last = idx == K - 1;
+  const float fi = (float)idx;
+  const float cs0 = __builtin_fmaf(As, s0, __builtin_fmaf(ms, fi, -bound));
+  const float cs1 = last ? bound : __builtin_fmaf(As, s1, __builtin_fmaf(ms, fi + 1.f, -bound));
+  const float co0 = __builtin_fmaf(Ao, o0, __builtin_fmaf(mo, fi, -bound));
+  const float co1 = last ? bound : __builtin_fmaf(Ao, o1, __builtin_fmaf(mo, fi + 1.f, -bound));
+  const float d0 = first ? 1.f - kMinDerivative : kMinDerivative + softplus<true>(udl);
+  const float d1 = last ? 1.f - kMinDerivative : kMinDerivative + softplus<true>(udh);
+  float lb;
+  const float y = INV ? rqs_bin<true>(x, co0, co1 - co0, cs0, cs1 - cs0, d0, d1, lb)
+                      : rqs_bin<false>(x, cs0, cs1 - cs0, co0, co1 - co0, d0, d1, lb);
+  const bool inside = x >= -bound && x <= bound;
+  ld = inside ? lb : 0.f;
+  return inside ? y : x;
+}
+
+// Select-first evaluation from a precomputed table [cw(K+1) | ch(K+1) | dv(K+1)] in LDS (the
+// fused kernels' lower spline): K−1 compares against the searched knots, then the bin's six
+// values are fetched by a per-lane LDS index instead of being selected in registers.
+template <int K, bool INV>
+NAZ_DEV float rqs_table(const float* tb, float x, float bound, float& ld) {
+  const float* srch = tb + (INV ? (K + 1) : 0);
+  int idx = 0;
+#pragma unroll
+  for (int k = 1; k < K; ++k) idx += (x >= srch[k] + kSearchEps) ? 1 : 0;
+  const float cw0 = tb[idx], cw1 = tb[idx + 1];
+  const float ch0 = tb[K + 1 + idx], ch1 = tb[K + 2 + idx];
+  const float d0 = tb[2 * (K + 1) + idx], d1 = tb[2 * (K + 1) + idx + 1];
+  float lb;
+  const float y = rqs_bin<INV>(x, cw0, cw1 - cw0, ch0, ch1 - ch0, d0, d1, lb);
+  const bool inside = x >= -bound && x <= bound;
+  ld = inside ? lb : 0.f;
+  return inside ? y : x;
+}
+
 }  // namespace naz

@@ -599,10 +599,12 @@ NAZ_DEV unsigned f16_piece_bits(float v, int piece) {
   return (unsigned)__builtin_bit_cast(unsigned short, lo);
 }
 
+// activation of the x6 kernels: δ = σ − ½ of the pre-scaled accumulator (see kSigScale)
+NAZ_DEV float sig_fold(float a) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a)) - 0.5f; }
 #ifdef NAZ_ABL_NOTANH
 #define NAZ_TANH(v) (v)
 #else
-#define NAZ_TANH(v) tanh_f<true>(v)
+#define NAZ_TANH(v) sig_fold(v)
 #endif
 
 // LDS ring: two slots of 40 KB per 128-row workgroup (two workgroups per CU use all 160 KB).
@@ -692,6 +694,16 @@ __host__ __device__ constexpr int x6_out_row(int o, int r, int h) {
   return 2 * CF::Dt * CF::K + dim * (CF::K - 1) + (p - 2 * CF::K);
 }
 
+// Sigmoid fold.  tanh(a) = −2δ with δ = σ(−2a) − ½ = 1 / (1 + 2^(a·2·log2 e)) − ½, so the fused
+// kernel's activation is rcp(1 + exp2(acc)) − ½ (4 VALU instead of 5) when the packer
+//   * scales GEMM1 and GEMM2 rows (weights and bias) by kSigScale = 2·log2 e, so their
+//     accumulators hold a·2·log2 e, and
+//   * scales the weights of each activation's consumer (GEMM2, GEMM3) by −2 (exact).
+// δ keeps tanh's relative precision near 0 (σ itself would not: its f16 hi/lo split loses
+// ~2^-23 absolute at σ ≈ ½).  The pre-activations equal the tanh form's up to one rounding of
+// the kSigScale-scaled weights (2^-24 relative), below the fp32 GEMM's own rounding.
+constexpr float kSigScale = 2.88539008177792681f;
+
 template <class CF>
 __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* __restrict__ packed, int L,
                                         float bound) {
@@ -735,6 +747,7 @@ __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* _
         } else if (col >= 0) {
           v = W[row * ldw + col];
         }
+        v *= W == W0 ? kSigScale : (W == W1 ? -2.f * kSigScale : -2.f);  // sigmoid fold (see kSigScale)
         out |= (f16 ? f16_piece_bits(v, piece) : bf16_hi_bits(v, piece)) << (16 * e2);
       }
       return out;
@@ -748,7 +761,7 @@ __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* _
         is_word = true;
       } else if (off < CF::A_TBL) {
         const int q = off - CF::A_BIAS, o = q / 32, h = (q >> 4) & 1, r = q & 15;
-        fv = b0[32 * o + acc_row(r, h)];
+        fv = kSigScale * b0[32 * o + acc_row(r, h)];
       } else if (CF::LOWER && off < CF::A_TBL + CF::S * CF::TBL) {
         const int q = off - CF::A_TBL, g = q / CF::TBL, w = q - g * CF::TBL;
         float uw[CF::K], uh[CF::K], ud[CF::K - 1];
@@ -769,7 +782,8 @@ __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* _
         is_word = true;
       } else if (q < CF::B_BIAS + CF::HB * 32) {
         const int qq = q - CF::B_BIAS, o = qq / 32, h = (qq >> 4) & 1, r = qq & 15;
-        fv = b1[32 * o + acc_row(r, h)];
+        const int orow = 32 * o + acc_row(r, h);
+        fv = kSigScale * b1[orow];
       }
     } else {
       const int sq = (off - CF::C_OFF) / CF::C_SIZE, q = off - CF::C_OFF - sq * CF::C_SIZE;

@@ -37,8 +37,10 @@ class _FusedCoupling:
     kernel's MFMA panel order by ``naz_coupling_pack`` — only when a parameter changed
     (tracked by tensor version counters), so inference pays it once."""
 
-    # fp16 pieces of GEMM2/3 weights must stay finite with margin: |W| < 2^15
+    # fp16 pieces of the PACKED GEMM2/3 weights must stay finite with margin: |W'| < 2^15.  The
+    # packer's sigmoid fold scales W1 by -2*(2 log2 e) and W2 by -2 (coupling.hip, kSigScale).
     F16_WEIGHT_LIMIT = 32768.0
+    F16_PACK_SCALE = {1: 2.0 * 2.88539008177792681, 2: 2.0}
 
     def __init__(self, layers: List[nn.Module], D: int, C: int, S: int, K: int, H: int, act: str, lower: bool,
                  bound: float, mfma: str = "auto"):
@@ -59,7 +61,8 @@ class _FusedCoupling:
     def _resolve_mode(self) -> str:
         if self.mfma != "auto":
             return self.mfma
-        big = max(float(t.nn.layers[i].weight.detach().abs().max()) for t in self.layers for i in (1, 2))
+        big = max(float(t.nn.layers[i].weight.detach().abs().max()) * self.F16_PACK_SCALE[i]
+                  for t in self.layers for i in (1, 2))
         return "f16x3" if big < self.F16_WEIGHT_LIMIT else "bf16x6"
 
     def params(self) -> List[torch.Tensor]:

@@ -657,7 +657,14 @@ struct CfgX6 {
   static constexpr int C_OFF = B_OFF + NB2 * B_SIZE;
   static constexpr int C_BIAS = NO * KB3 * OT23;
   static constexpr int C_SIZE = pad(C_BIAS + NO * 32);
-  static constexpr int LAYER = C_OFF + NB3 * C_SIZE;
+  // f16x3 configs also carry stage A with GEMM1 in fp16 pieces (same bias/table offsets), used
+  // by workgroups whose context and data values all fit fp16's range (kG1F16Limit)
+  static constexpr int A16_OFF = C_OFF + NB3 * C_SIZE;
+#ifdef NAZ_NO_A16
+  static constexpr int LAYER = A16_OFF;
+#else
+  static constexpr int LAYER = F16 ? A16_OFF + A_SIZE : A16_OFF;
+#endif
   static constexpr int NSTG = 1 + NB2 + NB3;       // stages per layer
   static constexpr int MAXSTAGE = 2 * kX6Slot;      // LDS floats per workgroup (the ring)
   static constexpr __host__ __device__ int stage_off(int j) {
@@ -670,7 +677,12 @@ struct CfgX6 {
   static constexpr int FLAT = N_W0 + N_B0 + N_W1 + N_B1 + N_W2 + N_B2 + N_LOW;
   static_assert(Dt % 2 == 0 && S % 2 == 0 && H % 32 == 0 && S > 0 && Dt > 0, "unsupported coupling shape");
   static_assert(A_SIZE <= kX6Slot && B_SIZE <= kX6Slot && C_SIZE <= kX6Slot, "stage exceeds one LDS ring slot");
+  static_assert(HB * KS0 * 2 * kChunk <= A_BIAS, "fp16 GEMM1 panels must fit stage A's panel region");
 };
+
+// |value| bound under which GEMM1's B operand (context, x1) is split into fp16 hi + lo: hi
+// (round-toward-zero) stays finite and lo = v - hi is exact with 11 significant bits.
+constexpr float kG1F16Limit = 32768.f;
 
 // GEMM1 input column (in cat([ctx, x1]) order) for k-step t, element j, lane-half h; -1 = zero pad
 template <class CF>
@@ -720,9 +732,9 @@ __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* _
     const float* b2 = W2 + CF::N_W2;
     const float* low = b2 + CF::N_B2;
     // operand chunk entry: (o, t, piece, lane, pair) -> two bf16 of W[row][col(j)], W[row][col(j+1)]
-    auto chunk_word = [&](int q, int nt, int t0, const float* W, int ldw, bool gemm1) -> unsigned {
-      const int ot = gemm1 ? CF::OT : CF::OT23;
-      const bool f16 = !gemm1 && CF::F16;
+    auto chunk_word = [&](int q, int nt, int t0, const float* W, int ldw, bool gemm1, bool f16g1 = false) -> unsigned {
+      const int ot = f16g1 ? 2 * kChunk : (gemm1 ? CF::OT : CF::OT23);
+      const bool f16 = f16g1 || (!gemm1 && CF::F16);
       const int o = q / (nt * ot), r1 = q - o * nt * ot;
       const int tl = r1 / ot, r2 = r1 - tl * ot;
       const int piece = r2 / kChunk, u = r2 - piece * kChunk;
@@ -755,10 +767,15 @@ __global__ void coupling_pack_x6_kernel(const float* __restrict__ flat, float* _
     unsigned word = 0;
     float fv = 0.f;
     bool is_word = false;
-    if (off < CF::A_SIZE) {
+    const bool a16 = CF::F16 && off >= CF::A16_OFF;
+    const int offa = a16 ? off - CF::A16_OFF : off;
+    if (offa < CF::A_SIZE && (a16 || off < CF::A16_OFF)) {
+      const int off = offa;
       if (off < CF::A_BIAS) {
-        word = chunk_word(off, CF::KS0, 0, W0, CF::C + CF::S, true);
-        is_word = true;
+        if (!a16 || off < CF::HB * CF::KS0 * 2 * kChunk) {
+          word = chunk_word(off, CF::KS0, 0, W0, CF::C + CF::S, true, a16);
+          is_word = true;
+        }
       } else if (off < CF::A_TBL) {
         const int q = off - CF::A_BIAS, o = q / 32, h = (q >> 4) & 1, r = q & 15;
         fv = kSigScale * b0[32 * o + acc_row(r, h)];
@@ -927,8 +944,6 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
   const bool valid = row < B;
   const int64_t crow = valid ? row : 0;
 
-  stage_issue<CF::A_SIZE, kX6Waves>(slot0, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER);
-
   float zl[CF::SH], zu[CF::DH];
   float ldsum = 0.f, logjac = 0.f;
 #pragma unroll
@@ -953,6 +968,51 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
     }
   }
 
+  // GEMM1 precision path for this workgroup: fp16 pieces when every context and data value of
+  // its rows is inside kG1F16Limit (x1 stays inside max(|x|, bound) through the lower
+  // splines), else the exact-split bf16x6 path.  Uniform per workgroup: it picks stage A.
+  int a_off = 0;
+#ifdef NAZ_NO_G1CHECK
+  if constexpr (false) {
+#else
+  if constexpr (CF::F16) {
+#endif
+    bool ok = bound < kG1F16Limit;
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) ok = ok && fabsf(zl[q]) < kG1F16Limit;
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) ok = ok && fabsf(zu[q]) < kG1F16Limit;
+#pragma unroll
+    for (int t = 0; t < CF::CT; ++t)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int c = 16 * t + 8 * h + jj;
+        // nontemporal: a separate read the compiler cannot merge with GEMM1's per-layer context
+        // loads (merging keeps 16 context values live across the layer loop: +20% time)
+        if (c < CF::C) ok = ok && fabsf(__builtin_nontemporal_load(&ctx[crow * ldc + c])) < kG1F16Limit;
+      }
+    // workgroup AND through ring slot 1 (unused until the first in-loop barrier; static LDS
+    // for __syncthreads_and would push the workgroup past 80 KB = one workgroup per CU)
+    int* flags = reinterpret_cast<int*>(slot1);
+    if (lane == 0) flags[wave] = __all(ok) ? 1 : 0;
+    __syncthreads();
+    bool all_ok = true;
+#pragma unroll
+    for (int w = 0; w < kX6Waves; ++w) all_ok = all_ok && flags[w] != 0;
+    a_off = all_ok ? CF::A16_OFF : 0;
+  }
+#if defined(NAZ_G1_FORCE) && NAZ_G1_FORCE == 1
+  const bool g1f16 = true;
+  a_off = CF::F16 ? CF::A16_OFF : 0;
+#elif defined(NAZ_G1_FORCE) && NAZ_G1_FORCE == 2
+  const bool g1f16 = false;
+  a_off = 0;
+#else
+  const bool g1f16 = a_off != 0;
+#endif
+
+  stage_issue<CF::A_SIZE, kX6Waves>(slot0, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER + a_off);
+
   int g = 0;  // global stage counter: stage g lives in slot (g & 1)
   for (int li = 0; li < L; ++li) {
     const int l = DIR_INV ? (L - 1 - li) : li;
@@ -970,7 +1030,7 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
       if constexpr (j + 1 < CF::NSTG) {
         stage_issue<CF::stage_size(j + 1), kX6Waves>(nxt, lp + CF::stage_off(j + 1));
       } else {
-        if (li + 1 < L) stage_issue<CF::A_SIZE, kX6Waves>(nxt, lnext);
+        if (li + 1 < L) stage_issue<CF::A_SIZE, kX6Waves>(nxt, lnext + a_off);
       }
       ++g;
 
@@ -990,10 +1050,7 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
           }
           x1[q] = zl[q];
         }
-        Frag3 bf[CF::KS0];
-#pragma unroll
-        for (int t = 0; t < CF::KS0; ++t) {
-          float v[8];
+        auto g1_in = [&](int t, float (&v)[8]) {
 #pragma unroll
           for (int jj = 0; jj < 8; ++jj) {
             if (t < CF::CT) {
@@ -1004,10 +1061,27 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
               v[jj] = q < CF::SH ? x1[q < CF::SH ? q : 0] : 0.f;
             }
           }
-          bf[t] = split8(v);
-        }
+        };
         init_bias<CF::HB>(acc1, cur + CF::A_BIAS, h);
-        gemm_x6_stage<CF::HB, CF::KS0>(acc1, cur, lane, bf);
+        if (CF::F16 && g1f16) {
+          Frag2 bf[CF::KS0];
+#pragma unroll
+          for (int t = 0; t < CF::KS0; ++t) {
+            float v[8];
+            g1_in(t, v);
+            bf[t] = split8_f16(v);
+          }
+          gemm_f16_stage<CF::HB, CF::KS0>(acc1, cur, lane, bf);
+        } else {
+          Frag3 bf[CF::KS0];
+#pragma unroll
+          for (int t = 0; t < CF::KS0; ++t) {
+            float v[8];
+            g1_in(t, v);
+            bf[t] = split8(v);
+          }
+          gemm_x6_stage<CF::HB, CF::KS0>(acc1, cur, lane, bf);
+        }
         if constexpr (!DIR_INV && CF::LOWER) {
 #pragma unroll
           for (int q = 0; q < CF::SH; ++q) {

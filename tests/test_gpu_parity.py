@@ -320,3 +320,21 @@ def test_native_library_is_the_path():
     from naz_amd import _lib
     maps = open(f"/proc/{os.getpid()}/maps").read()
     assert str(_lib.LIB_PATH) in maps
+
+
+@pytest.mark.parametrize("scale", [1.0, 5e4])
+def test_config3_gemm1_precision_paths(scale):
+    """f16x3 picks GEMM1's fp16 path per 128-row workgroup only when every context / data value
+    of its rows is below 2^15; rows 128..255 get context values x`scale` so that workgroup (and
+    only it) takes the bf16x6 path at 5e4.  Both must match the oracle."""
+    f, spec, state = _config3_flow()
+    f._plan.set_mfma("f16x3")
+    n = 1024
+    x = torch.as_tensor(O.gaussian_mixture(n, 16, seed=3))
+    c = torch.as_tensor(O.context_normal(n, 32, seed=4))
+    c[128:256] *= scale
+    lp = f.log_prob(x.to(DEV), condition=c.to(DEV))
+    lp64 = O.build_flow(spec, state, torch.float64).log_prob(x.double(), c.double()).numpy()
+    lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, c).numpy()
+    st = assert_parity(_np(lp), lp64, lp32, what=f"config3 gemm1 paths scale={scale}")
+    print("gemm1 paths", scale, st)

@@ -22,7 +22,7 @@ ARCH = os.environ.get("NAZ_OFFLOAD_ARCH", "gfx950")
 # ops it forms (v_pk_add/mul/fma_f32) issue slower than scalar ones beside MFMAs, and the
 # packing moves add register pressure (spills in coupling_x6_kernel with it on).
 SOURCE_FLAGS = {"coupling.hip": ["-fno-slp-vectorize"], "cnf.hip": ["-fno-slp-vectorize"]}
-SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "elementwise.hip", "coupling.hip", "cnf.hip", "capi.cpp"]
+SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "gemm_rows.hip", "elementwise.hip", "coupling.hip", "cnf.hip", "capi.cpp"]
 
 
 def hipcc() -> str:

@@ -76,6 +76,10 @@ int linear_act(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx
   if (C > 0 && ctx == nullptr) return set_error("naz_linear_act: C=%d but ctx is NULL", C);
   if (Kx > 0 && x == nullptr) return set_error("naz_linear_act: Kx=%d but x is NULL", Kx);
   if (act < 0 || act > NAZ_ACT_SIGMOID) return set_error("naz_linear_act: unknown activation %d", act);
+  if (M >= 1024) {  // batch-row kernel (gemm_rows.hip); 1 = shape not taken
+    const int rc = rowgemm_linear(ctx, ldc, C, x, ldx, Kx, W, mask, b, y, ldy, M, N, act, s);
+    if (rc != 1) return rc;
+  }
   dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((N + BN - 1) / BN));
   hipLaunchKernelGGL(linear_act_kernel, grid, dim3(256), 0, s, ctx, ldc, C, x, ldx, Kx, W, mask, b, y, ldy, M, N,
                      act);

@@ -107,6 +107,12 @@ int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, cons
     if (!accumulate && split_k <= 1) return set_error("naz_gemm: K = 0 with overwrite is not supported");
     return 0;
   }
+  {  // batch-row fast paths (gemm_rows.hip)
+    int rc = 0;
+    if (gemm_rows_try(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, mask, smm, smn, mask_b, accumulate, rowsum, s,
+                      &rc) == 0)
+      return rc;
+  }
   if (split_k < 1) split_k = 1;
   int64_t kps = (K + split_k - 1) / split_k;
   kps = (kps + GBK - 1) / GBK * GBK;

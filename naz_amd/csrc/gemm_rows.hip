@@ -1,0 +1,442 @@
+// Batch-row GEMMs for the NLL training step: every conditioner GEMM
+// of a flow has one huge dimension — the batch (2^20 rows per GPU at config 4) — and small
+// feature dimensions (<= a few hundred).  Two shapes cover all of them:
+//
+//   rowgemm  C[m, n] = act(Σ_k A(m, k) · B(k, n) + bias[n])   m over the batch, n, k small
+//            forward F.linear / MaskedLinear (A = cat[ctx, x], B = (W ⊙ mask)ᵀ) and the input
+//            gradients dX = dPre · (W ⊙ mask) of the backward pass;
+//   wgrad    C[n1, n2] (+)= Σ_m G(m, n1) · X(m, n2) [· mask(n1, n2)]   reduction over the batch
+//            the weight gradients dW = mask ⊙ (dPreᵀ · X), with db = Σ_m dPre riding along as an
+//            all-ones X column.
+//
+// Both are exact fp32 (v_mfma_f32_32x32x2_f32, the gfx950 FP32 matrix rate) and tile the batch
+// into 128-row workgroup panels so that every HBM byte of the big operand is read once:
+//   * rowgemm: a workgroup owns 128 rows × up to 256 output columns (NB 32-column blocks per
+//     wave, the wave's 32 rows); k runs in 16-deep chunks through a double-buffered LDS pair
+//     [k][m] / [k][n] with the next chunk's global loads in flight during the current chunk's
+//     MFMAs; the epilogue fuses bias + activation (+ accumulate);
+//   * wgrad: a workgroup reduces a contiguous slice of rows into the full (small) output in
+//     registers — each wave owns a set of 32×32 output blocks — and adds it to C with one fp32
+//     atomic per element at the end (split-K over workgroups, no partial buffers).
+#include "naz_device.h"
+#include "naz_internal.h"
+
+namespace naz {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int RG_BM = 128;  // batch rows per workgroup (4 waves x 32)
+#ifndef NAZ_RG_BK
+#define NAZ_RG_BK 16
+#endif
+constexpr int RG_BK = NAZ_RG_BK;  // k per LDS chunk
+constexpr int RG_PAD = 4;
+constexpr int RG_APAD = 1;  // As rows 129 floats: the two k-halves a thread pair stores differ by 8 banks
+
+NAZ_DEV floatx16 mfma_f32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+struct RowGemmArgs {
+  const float* a0;  // first A segment: [M, ka0] rows at stride lda0 (lda0 = 0: one broadcast row)
+  int64_t lda0;
+  int ka0;
+  const float* a1;  // second A segment: [M, ka1] rows at stride lda1
+  int64_t lda1;
+  int ka1;
+  const float* b;  // B(k, n) = b[k * sbk + n * sbn] (* mask[k * smk + n * smn])
+  int64_t sbk, sbn;
+  const float* mask;
+  int64_t smk, smn;
+  const float* bias;  // [N] or null
+  float* c;           // C[m * ldc + n]
+  int64_t ldc;
+  int64_t M;
+  int N;
+  int act;
+  int accumulate;
+  int vec;  // A segments allow 16-byte loads of 8-k groups (set by rowgemm())
+};
+
+// A(m, k) of the concatenated row [a0 | a1]
+NAZ_DEV float rg_a(const RowGemmArgs& p, int64_t m, int k) {
+  if (k < p.ka0) return p.a0[m * p.lda0 + k];
+  return p.a1[m * p.lda1 + (k - p.ka0)];
+}
+
+#ifndef NAZ_RG_OCC
+#define NAZ_RG_OCC 4
+#endif
+// waves per SIMD: up to 4 blocks of accumulators fit 128 VGPRs (4 waves/SIMD); wider tiles 2
+template <int NB>
+__global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(RowGemmArgs p) {
+  constexpr int BN = 32 * NB;
+  __shared__ float As[2][RG_BK][RG_BM + RG_APAD];
+  __shared__ float Bs[2][RG_BK][BN + RG_PAD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * RG_BM;
+  const int n0 = blockIdx.y * BN;
+  const int K = p.ka0 + p.ka1;
+  const int nk = (K + RG_BK - 1) / RG_BK;
+
+  // A chunk: 128 rows x RG_BK k, APT per thread in 8-k groups: thread -> (row = tid >> 1, k-half)
+  constexpr int APT = RG_BK / 2;
+  const int ar = tid >> 1, ak = (tid & 1) * APT;
+  const int64_t am = m0 + ar;
+  const bool arow = am < p.M;
+  // B chunk: RG_BK k x BN n: thread -> (k = tid % RG_BK, n = tid / RG_BK + (256 / RG_BK) j)
+  constexpr int BKS = 256 / RG_BK;
+  const int bk = tid % RG_BK, bn0 = tid / RG_BK;
+  constexpr int BPT = BN / BKS;
+
+  const auto bsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), (short)0, 0x7fffffff, 0x00020000);
+  const auto msrd =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.mask ? p.mask : p.b), (short)0, 0x7fffffff, 0x00020000);
+  const int sbk = (int)p.sbk, sbn = (int)p.sbn, smk = (int)p.smk, smn = (int)p.smn;
+  float ra[APT], rb[BPT];
+  auto load = [&](int kc) {
+    const int kc0 = kc * RG_BK;
+#pragma unroll
+    for (int g8 = 0; g8 < APT; g8 += 8) {
+      const int kb = kc0 + ak + g8;
+      if (p.vec && arow && kb + 8 <= K && (kb >= p.ka0 || kb + 8 <= p.ka0)) {
+        // 8 consecutive k inside one segment, 16-byte aligned rows (checked on the host)
+        const float* src = kb < p.ka0 ? p.a0 + am * p.lda0 + kb : p.a1 + am * p.lda1 + (kb - p.ka0);
+        const float4 v0 = *reinterpret_cast<const float4*>(src);
+        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+        ra[g8 + 0] = v0.x; ra[g8 + 1] = v0.y; ra[g8 + 2] = v0.z; ra[g8 + 3] = v0.w;
+        ra[g8 + 4] = v1.x; ra[g8 + 5] = v1.y; ra[g8 + 6] = v1.z; ra[g8 + 7] = v1.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k = kb + i;
+          ra[g8 + i] = (arow && k < K) ? rg_a(p, am, k) : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      // weights / masks are small: 32-bit buffer offsets (no 64-bit address registers)
+      const int k = kc0 + bk, n = n0 + bn0 + BKS * j;
+      float v = 0.f;
+      if (k < K && n < p.N) {
+        v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bsrd, 4 * (k * sbk + n * sbn), 0, 0));
+        if (p.mask != nullptr)
+          v *= __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(msrd, 4 * (k * smk + n * smn), 0, 0));
+      }
+      rb[j] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < APT; ++i) As[buf][ak + i][ar] = ra[i];
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) Bs[buf][bk][bn0 + BKS * j] = rb[j];
+  };
+
+  floatx16 acc[NB];
+#pragma unroll
+  for (int o = 0; o < NB; ++o)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[o][r] = 0.f;
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nk) load(kc + 1);  // in flight during this chunk's MFMAs
+#pragma unroll
+    for (int kk = 0; kk < RG_BK; kk += 2) {
+      const float a = As[buf][kk + (lane >> 5)][wave * 32 + (lane & 31)];
+#pragma unroll
+      for (int o = 0; o < NB; ++o) acc[o] = mfma_f32(a, Bs[buf][kk + (lane >> 5)][32 * o + (lane & 31)], acc[o]);
+    }
+    if (kc + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: accumulator (block o, reg r) = C[row, col]
+#pragma unroll
+  for (int o = 0; o < NB; ++o) {
+    const int n = n0 + 32 * o + (lane & 31);
+    if (n >= p.N) continue;
+    const float bn = p.bias != nullptr ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m >= p.M) continue;
+      float* dst = p.c + m * p.ldc + n;
+      const float v = activate_rt(p.act, acc[o][r] + bn);
+      *dst = p.accumulate ? *dst + v : v;
+    }
+  }
+}
+
+template <int NB>
+void rowgemm_launch(const RowGemmArgs& p, hipStream_t s) {
+  dim3 grid((unsigned)((p.M + RG_BM - 1) / RG_BM), (unsigned)((p.N + 32 * NB - 1) / (32 * NB)));
+  hipLaunchKernelGGL(rowgemm_kernel<NB>, grid, dim3(256), 0, s, p);
+}
+
+static bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+int rowgemm(RowGemmArgs p, hipStream_t s) {
+  if (p.M <= 0 || p.N <= 0) return 0;
+  const int64_t K = p.ka0 + p.ka1;
+  const int64_t bspan = (K - 1) * (p.sbk < 0 ? -p.sbk : p.sbk) + (int64_t)(p.N - 1) * (p.sbn < 0 ? -p.sbn : p.sbn);
+  const int64_t mspan = (K - 1) * (p.smk < 0 ? -p.smk : p.smk) + (int64_t)(p.N - 1) * (p.smn < 0 ? -p.smn : p.smn);
+  if (p.sbk < 0 || p.sbn < 0 || p.smk < 0 || p.smn < 0 || 4 * bspan >= (1ll << 31) || 4 * mspan >= (1ll << 31))
+    return 1;  // weights too large for the 32-bit buffer offsets: caller falls back
+  p.vec = (p.ka0 % 8 == 0) && (p.ka0 == 0 || (al16(p.a0) && p.lda0 % 4 == 0)) &&
+          (p.ka1 == 0 || (al16(p.a1) && p.lda1 % 4 == 0));
+  const int nb = (p.N + 31) / 32;
+  switch (nb > 8 ? 8 : nb) {
+    case 1: rowgemm_launch<1>(p, s); break;
+    case 2: rowgemm_launch<2>(p, s); break;
+    case 3: rowgemm_launch<3>(p, s); break;
+    case 4: rowgemm_launch<4>(p, s); break;
+    case 5: rowgemm_launch<5>(p, s); break;
+    case 6: rowgemm_launch<6>(p, s); break;
+    case 7: rowgemm_launch<7>(p, s); break;
+    default: rowgemm_launch<8>(p, s); break;
+  }
+  return check_launch("rowgemm_kernel");
+}
+
+// ------------------------------------------------------------------------------------------
+// wgrad: C[n1, n2] += Σ_{m in slice} G[m * sgm + n1] · X[m * sxm + n2]
+// ------------------------------------------------------------------------------------------
+constexpr int WG_BK = 16;     // rows per LDS chunk
+constexpr int WG_MAXB = 8;    // 32x32 output blocks per wave (<= 128 accumulator regs)
+
+struct WGradArgs {
+  const float* g;  // [M, N1] at row stride sgm, unit column stride
+  int64_t sgm;
+  const float* x;  // [M, N2] at row stride sxm (0: one broadcast row), unit column stride
+  int64_t sxm;
+  int64_t M;
+  int N1, N2;
+  int ones;        // 1: logical X column N2 is all ones, its C column goes to rowsum[n1]
+  float* c;        // C[n1 * scm + n2 * scn]
+  int64_t scm, scn;
+  const float* mask;  // mask[n1 * smm + n2 * smn] or null
+  int64_t smm, smn;
+  float* rowsum;
+  int64_t rows_per_wg;
+  int blk0;        // first output block (of NB1 x NB2, n2-fastest) this launch owns
+};
+
+// one workgroup: rows [mb, me) of G and X -> its share of every output block, added atomically
+__global__ void __launch_bounds__(256, 2) wgrad_kernel(WGradArgs p) {
+  constexpr int BN = 256;  // max n1 / n2 (8 blocks of 32)
+  __shared__ float Gs[2][WG_BK][BN + RG_PAD];
+  __shared__ float Xs[2][WG_BK][BN + RG_PAD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N2e = p.N2 + p.ones;
+  const int NB1 = (p.N1 + 31) / 32, NB2 = (N2e + 31) / 32;
+  const int64_t mb = (int64_t)blockIdx.x * p.rows_per_wg;
+  const int64_t me = (mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M;
+  int bi[WG_MAXB], bj[WG_MAXB];
+  bool bv[WG_MAXB];
+#pragma unroll
+  for (int j = 0; j < WG_MAXB; ++j) {
+    const int q = p.blk0 + wave + 4 * j;
+    bv[j] = q < NB1 * NB2;
+    bi[j] = bv[j] ? q / NB2 : 0;
+    bj[j] = bv[j] ? q - (q / NB2) * NB2 : 0;
+  }
+  floatx16 acc[WG_MAXB];
+#pragma unroll
+  for (int j = 0; j < WG_MAXB; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  const int ncol1 = NB1 * 32, ncol2 = NB2 * 32;
+  const int rr = tid >> 4, cc = tid & 15;  // chunk load: row rr, columns cc + 16 i
+  float rg[16], rx[16];
+  auto load = [&](int64_t m0) {
+    const int64_t m = m0 + rr;
+    const bool mrow = m < me;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = cc + 16 * i;
+      rg[i] = (mrow && n < p.N1) ? p.g[m * p.sgm + n] : 0.f;
+      rx[i] = mrow ? (n < p.N2 ? p.x[m * p.sxm + n] : (n == p.N2 && p.ones ? 1.f : 0.f)) : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = cc + 16 * i;
+      if (n < ncol1) Gs[buf][rr][n] = rg[i];
+      if (n < ncol2) Xs[buf][rr][n] = rx[i];
+    }
+  };
+  if (mb < me) {
+    load(mb);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int64_t m0 = mb; m0 < me; m0 += WG_BK, buf ^= 1) {
+    const bool more = m0 + WG_BK < me;
+    if (more) load(m0 + WG_BK);
+#pragma unroll
+    for (int kk = 0; kk < WG_BK; kk += 2) {
+      const int k = kk + (lane >> 5);
+#pragma unroll
+      for (int j = 0; j < WG_MAXB; ++j) {
+        if (!bv[j]) continue;
+        const float a = Gs[buf][k][32 * bi[j] + (lane & 31)];
+        const float b = Xs[buf][k][32 * bj[j] + (lane & 31)];
+        acc[j] = mfma_f32(a, b, acc[j]);
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < WG_MAXB; ++j) {
+    if (!bv[j]) continue;
+    const int n2 = 32 * bj[j] + (lane & 31);
+    if (n2 >= N2e) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n1 = 32 * bi[j] + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (n1 >= p.N1) continue;
+      float v = acc[j][r];
+      if (n2 < p.N2) {
+        if (p.mask != nullptr) v *= p.mask[(int64_t)n1 * p.smm + (int64_t)n2 * p.smn];
+        atomicAdd(p.c + (int64_t)n1 * p.scm + (int64_t)n2 * p.scn, v);
+      } else {
+        atomicAdd(p.rowsum + n1, v);
+      }
+    }
+  }
+}
+
+__global__ void zero2d_kernel(float* c, int64_t scm, int64_t scn, int M, int N) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)M * N) return;
+  const int m = (int)(e / N), n = (int)(e - (int64_t)m * N);
+  c[m * scm + n * scn] = 0.f;
+}
+
+int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
+  if (p.N1 <= 0 || (p.N2 <= 0 && !p.ones)) return 0;
+  if (!accumulate) {
+    if (p.N2 > 0) {
+      const int64_t n = (int64_t)p.N1 * p.N2;
+      hipLaunchKernelGGL(zero2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p.c, p.scm, p.scn, p.N1,
+                         p.N2);
+    }
+    if (p.ones) (void)hipMemsetAsync(p.rowsum, 0, sizeof(float) * p.N1, s);
+  }
+  if (p.M <= 0) return check_launch("zero2d_kernel");
+  // enough workgroups to fill the chip twice over, each reducing a multiple of 16 rows
+  int64_t rpw = (p.M + 1023) / 1024;
+  rpw = (rpw + WG_BK - 1) / WG_BK * WG_BK;
+  if (rpw < 256) rpw = 256;
+  p.rows_per_wg = rpw;
+  const int NB1 = (p.N1 + 31) / 32, NB2 = (p.N2 + p.ones + 31) / 32;
+  const int nblk = NB1 * NB2, per = 4 * WG_MAXB;
+  const unsigned gx = (unsigned)((p.M + rpw - 1) / rpw);
+  for (int b0 = 0; b0 < nblk; b0 += per) {  // output-block slices of 16 (one grid each)
+    p.blk0 = b0;
+    hipLaunchKernelGGL(wgrad_kernel, dim3(gx), dim3(256), 0, s, p);
+  }
+  return check_launch("wgrad_kernel");
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Entry points used by dense.hip / gemm.hip
+// ------------------------------------------------------------------------------------------
+int rowgemm_linear(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx, int Kx, const float* W,
+                   const float* mask, const float* b, float* y, int64_t ldy, int64_t M, int N, int act,
+                   hipStream_t s) {
+  RowGemmArgs p{};
+  p.a0 = ctx;
+  p.lda0 = ldc;
+  p.ka0 = C;
+  p.a1 = x;
+  p.lda1 = ldx;
+  p.ka1 = Kx;
+  p.b = W;  // B(k, n) = W[n, k]
+  p.sbk = 1;
+  p.sbn = C + Kx;
+  p.mask = mask;
+  p.smk = 1;
+  p.smn = C + Kx;
+  p.bias = b;
+  p.c = y;
+  p.ldc = ldy;
+  p.M = M;
+  p.N = N;
+  p.act = act;
+  p.accumulate = 0;
+  return rowgemm(p, s);
+}
+
+// gemm() fast paths; return 1 when the shape was not taken (caller falls back)
+int gemm_rows_try(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                  int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
+                  int mask_b, int accumulate, float* rowsum, hipStream_t s, int* rc) {
+  // dX-type: A row-major over a long M, small K and N, plain output rows
+  if (sak == 1 && scn == 1 && rowsum == nullptr && (mask == nullptr || mask_b) && M >= 1024 && K <= 4096 &&
+      N <= 4096) {
+    RowGemmArgs p{};
+    p.a0 = nullptr;
+    p.lda0 = 0;
+    p.ka0 = 0;
+    p.a1 = A;
+    p.lda1 = sam;
+    p.ka1 = (int)K;
+    p.b = B;
+    p.sbk = sbk;
+    p.sbn = sbn;
+    p.mask = mask;
+    p.smk = smm;
+    p.smn = smn;
+    p.c = C;
+    p.ldc = scm;
+    p.M = M;
+    p.N = N;
+    p.act = NAZ_ACT_IDENTITY;
+    p.accumulate = accumulate;
+    const int r = rowgemm(p, s);
+    if (r == 1) return 1;  // not taken
+    *rc = r;
+    return 0;
+  }
+  // dW-type: C[M, N] = Σ_k A(m, k) B(k, n) with A = Gᵀ (unit m stride) and B = X (unit n stride)
+  // over a long K: the reduction runs over the batch
+  if (sam == 1 && sbn == 1 && (mask == nullptr || !mask_b) && M <= 256 && N + (rowsum != nullptr) <= 256 &&
+      K >= 1024) {
+    WGradArgs p{};
+    p.g = A;
+    p.sgm = sak;
+    p.x = B;
+    p.sxm = sbk;
+    p.M = K;
+    p.N1 = M;
+    p.N2 = N;
+    p.ones = rowsum != nullptr;
+    p.c = C;
+    p.scm = scm;
+    p.scn = scn;
+    p.mask = mask;
+    p.smm = smm;
+    p.smn = smn;
+    p.rowsum = rowsum;
+    *rc = wgrad(p, accumulate, s);
+    return 0;
+  }
+  return 1;
+}
+
+}  // namespace naz

@@ -32,6 +32,12 @@ int bounding_inv(const float* y, int64_t ldy, const float* low, const float* hig
 int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
          float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn, int mask_b, int accumulate,
          int split_k, float* rowsum, hipStream_t s);
+// gemm_rows.hip: batch-row GEMMs (forward linear layers, dX, dW)
+int rowgemm_linear(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx, int Kx, const float* W,
+                   const float* mask, const float* b, float* y, int64_t ldy, int64_t M, int N, int act, hipStream_t s);
+int gemm_rows_try(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                  int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
+                  int mask_b, int accumulate, float* rowsum, hipStream_t s, int* rc);
 int affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y, int64_t ldy,
                   const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx, float* g_raw,
                   int64_t ldgr, int64_t B, int D, hipStream_t s);

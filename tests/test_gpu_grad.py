@@ -99,10 +99,13 @@ def test_rqs_bwd_broadcast_params(inverse):
 @pytest.mark.parametrize("act", ["identity", "tanh", "relu", "softplus", "sigmoid"])
 @pytest.mark.parametrize("ctx_kind", ["none", "rows", "one_row"])
 @pytest.mark.parametrize("masked", [False, True])
-def test_linear_act_grad(act, ctx_kind, masked):
+@pytest.mark.parametrize("M", [1000, 3000])
+def test_linear_act_grad(act, ctx_kind, masked, M):
+    """M = 1000 runs the generic 64x64-tile kernels, M = 3000 the batch-row kernels
+    (gemm_rows.hip: rowgemm forward / dX, wgrad dW + db)."""
     from naz_amd import autograd as ag
     rng = np.random.default_rng(11)
-    M, Kx, C, N = 1000, 24, (0 if ctx_kind == "none" else 13), 70
+    Kx, C, N = 24, (0 if ctx_kind == "none" else 13), 70
     x = rng.standard_normal((M, Kx)).astype(np.float32)
     W = (rng.standard_normal((N, C + Kx)) / np.sqrt(C + Kx)).astype(np.float32)
     b = rng.standard_normal(N).astype(np.float32) * 0.1
@@ -137,6 +140,31 @@ def test_linear_act_grad(act, ctx_kind, masked):
     r32 = run("cpu", torch.float32, False)
     for k in got:
         _check(got[k], r64[k], r32[k], f"linear_act[{act},{ctx_kind},mask={masked}] d/d{k}")
+
+
+def test_rowgemm_config3_shapes():
+    """The batch-row forward kernel at config-3 conditioner shapes (ctx 32 | x1 8 -> 128 -> 128
+    -> 184), odd row count, 16-byte and unaligned row strides, and the dX GEMM with a mask."""
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(5)
+    M = 5003
+    for C, Kx, N, ldx_pad in [(32, 8, 128, 8), (0, 128, 128, 0), (0, 128, 184, 3), (13, 5, 300, 1)]:
+        ctx = torch.randn(M, C, generator=g)
+        xfull = torch.randn(M, Kx + ldx_pad, generator=g)
+        x = xfull[:, :Kx]
+        W = torch.randn(N, C + Kx, generator=g) / (C + Kx) ** 0.5
+        b = torch.randn(N, generator=g) * 0.1
+        y = ops.linear_act(_cuda(x) if ldx_pad == 0 else _cuda(xfull)[:, :Kx], _cuda(W), _cuda(b), "tanh",
+                           context=_cuda(ctx) if C else None)
+        inp = torch.cat([ctx, x], 1) if C else x
+        ref64 = torch.tanh(inp.double() @ W.double().t() + b.double())
+        ref32 = torch.tanh(inp @ W.t() + b)
+        _check(y, ref64, ref32, f"rowgemm fwd C={C} Kx={Kx} N={N}")
+    G = torch.randn(M, 184, generator=g)
+    W = torch.randn(184, 128, generator=g) / 13.0
+    mask = (torch.rand(184, 128, generator=g) > 0.3).float()
+    dx = ops.gemm(_cuda(G), _cuda(W), mask=_cuda(mask), mask_b=True)
+    _check(dx, G.double() @ (W.double() * mask.double()), G @ (W * mask), "rowgemm dX masked")
 
 
 @pytest.mark.parametrize("M,N,K,split", [(128, 40, 50000, None), (184, 128, 4097, 7), (3, 5, 1, None),

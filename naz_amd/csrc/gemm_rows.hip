@@ -58,6 +58,7 @@ struct RowGemmArgs {
   int act;
   int accumulate;
   int vec;  // A segments allow 16-byte loads of 8-k groups (set by rowgemm())
+  int vst;  // C rows allow 16-byte stores (N % 4 == 0, aligned; set by rowgemm())
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -73,8 +74,10 @@ NAZ_DEV float rg_a(const RowGemmArgs& p, int64_t m, int k) {
 template <int NB>
 __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(RowGemmArgs p) {
   constexpr int BN = 32 * NB;
-  __shared__ float As[2][RG_BK][RG_BM + RG_APAD];
-  __shared__ float Bs[2][RG_BK][BN + RG_PAD];
+  constexpr int AS_F = 2 * RG_BK * (RG_BM + RG_APAD), BS_F = 2 * RG_BK * (BN + RG_PAD);
+  __shared__ float smem[AS_F + BS_F];
+  auto As = reinterpret_cast<float(*)[RG_BK][RG_BM + RG_APAD]>(smem);
+  auto Bs = reinterpret_cast<float(*)[RG_BK][BN + RG_PAD]>(smem + AS_F);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t m0 = (int64_t)blockIdx.x * RG_BM;
   const int n0 = blockIdx.y * BN;
@@ -159,6 +162,46 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
   }
 
   // epilogue: accumulator (block o, reg r) = C[row, col]
+  if (p.vst) {
+    // staged through this wave's share of the (now free) LDS: EG blocks at a time are written
+    // [32 rows][32 EG cols] and stored back as whole 16-byte row pieces
+    constexpr int SHARE = (AS_F + BS_F) / 4;
+    constexpr int EG = SHARE >= 32 * (64 + 4) ? 2 : 1;
+    constexpr int EP = 32 * EG + 4;  // pitch
+    float* E = smem + wave * SHARE;
+#pragma unroll
+    for (int o0 = 0; o0 < NB; o0 += EG) {
+#pragma unroll
+      for (int oo = 0; oo < EG; ++oo) {
+        if (o0 + oo >= NB) continue;
+        const int n = n0 + 32 * (o0 + oo) + (lane & 31);
+        const float bn = (p.bias != nullptr && n < p.N) ? p.bias[n] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          E[row * EP + 32 * oo + (lane & 31)] = activate_rt(p.act, acc[o0 + oo][r] + bn);
+        }
+      }
+      // 8 EG float4 per row; 64 / (8 EG) rows per wave-instruction
+      constexpr int F4R = 8 * EG, RPI = 64 / F4R;
+      const int rr = lane / F4R, c4 = lane % F4R;
+      const int col = n0 + 32 * o0 + 4 * c4;
+#pragma unroll
+      for (int it = 0; it < 32 / RPI; ++it) {
+        const int row = it * RPI + rr;
+        const int64_t m = m0 + wave * 32 + row;
+        if (m >= p.M || col >= p.N) continue;
+        float4 v = *reinterpret_cast<const float4*>(E + row * EP + 4 * c4);
+        float4* dst = reinterpret_cast<float4*>(p.c + m * p.ldc + col);
+        if (p.accumulate) {
+          const float4 o = *dst;
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *dst = v;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int o = 0; o < NB; ++o) {
     const int n = n0 + 32 * o + (lane & 31);
@@ -192,6 +235,7 @@ int rowgemm(RowGemmArgs p, hipStream_t s) {
     return 1;  // weights too large for the 32-bit buffer offsets: caller falls back
   p.vec = (p.ka0 % 8 == 0) && (p.ka0 == 0 || (al16(p.a0) && p.lda0 % 4 == 0)) &&
           (p.ka1 == 0 || (al16(p.a1) && p.lda1 % 4 == 0));
+  p.vst = p.N % 4 == 0 && p.ldc % 4 == 0 && al16(p.c);
   const int nb = (p.N + 31) / 32;
   switch (nb > 8 ? 8 : nb) {
     case 1: rowgemm_launch<1>(p, s); break;
@@ -318,6 +362,106 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WGradArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// wgrad_flat: the same reduction for dense operands (G and X contiguous [M, N] rows, 16-byte
+// aligned, N % 4 == 0), which is what the training walk passes.  A chunk of R rows of either
+// operand is then ONE contiguous span: it is fetched with flat 16-byte loads spread over all
+// 256 threads, R sized so every chunk moves ~32 KB (narrow X -> more rows), and copied to LDS
+// unpadded ([row][N]; MFMA operand reads past column N only feed discarded outputs).  db is a
+// VALU column sum of the G chunk, so it costs no MFMA block.  Loads of chunk i+1 are in flight
+// (registers) while chunk i's MFMAs run.
+// ------------------------------------------------------------------------------------------
+constexpr int WF_Q = 8;          // float4 prefetch slots per thread (32 KB per 256-thread chunk)
+
+template <int MAXB>
+__global__ void __launch_bounds__(256, MAXB <= 2 ? 4 : (MAXB == 4 ? 3 : 2)) wgrad_flat_kernel(WGradArgs p, int R) {
+  extern __shared__ float wlds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N1 = p.N1, N2 = p.N2;
+  float* const Gs = wlds;             // [R][N1]
+  float* const Xs = wlds + R * N1;    // [R][N2] (+ slack for reads past the last row)
+  const int NB1 = (N1 + 31) / 32, NB2 = (N2 + 31) / 32;
+  const int64_t mb = (int64_t)blockIdx.x * p.rows_per_wg;
+  const int64_t me = (mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M;
+  int bi[MAXB], bj[MAXB];
+  bool bv[MAXB];
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    const int q = p.blk0 + wave + 4 * j;
+    bv[j] = q < NB1 * NB2;
+    bi[j] = bv[j] ? q / NB2 : 0;
+    bj[j] = bv[j] ? q - (q / NB2) * NB2 : 0;
+  }
+  floatx16 acc[MAXB];
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  float dbs = 0.f;  // column sum of G for column tid (db)
+
+  const int fg = R * N1 / 4, fx = R * N2 / 4;  // float4 per chunk
+  float4 rq[WF_Q];
+  auto load = [&](int64_t m0) {
+    const int64_t rows = (me - m0) < R ? (me - m0) : R;
+    const int lg = (int)(rows * N1 / 4), lx = (int)(rows * N2 / 4);  // valid float4 (zero past them)
+    const float4* g4 = reinterpret_cast<const float4*>(p.g + m0 * N1);
+    const float4* x4 = reinterpret_cast<const float4*>(p.x + m0 * N2);
+#pragma unroll
+    for (int i = 0; i < WF_Q; ++i) {
+      const int q = tid + 256 * i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < fg) {
+        if (q < lg) v = g4[q];
+      } else if (q - fg < fx) {
+        if (q - fg < lx) v = x4[q - fg];
+      }
+      rq[i] = v;
+    }
+  };
+  auto store = [&]() {
+    float4* l4 = reinterpret_cast<float4*>(wlds);
+#pragma unroll
+    for (int i = 0; i < WF_Q; ++i) {
+      const int q = tid + 256 * i;
+      if (q < fg + fx) l4[q] = rq[i];
+    }
+  };
+  if (mb < me) load(mb);
+  for (int64_t m0 = mb; m0 < me; m0 += R) {
+    __syncthreads();  // the previous chunk's readers are done
+    store();
+    __syncthreads();
+    if (m0 + R < me) load(m0 + R);  // in flight during this chunk's MFMAs
+    for (int kk = 0; kk < R; kk += 2) {
+      const int k = kk + (lane >> 5);
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j) {
+        if (!bv[j]) continue;
+        const float a = Gs[k * N1 + 32 * bi[j] + (lane & 31)];
+        const float b = Xs[k * N2 + 32 * bj[j] + (lane & 31)];
+        acc[j] = mfma_f32(a, b, acc[j]);
+      }
+    }
+    if (p.ones && tid < N1)
+      for (int r = 0; r < R; ++r) dbs += Gs[r * N1 + tid];
+  }
+#pragma unroll
+  for (int j = 0; j < MAXB; ++j) {
+    if (!bv[j]) continue;
+    const int n2 = 32 * bj[j] + (lane & 31);
+    if (n2 >= N2) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n1 = 32 * bi[j] + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (n1 >= N1) continue;
+      float v = acc[j][r];
+      if (p.mask != nullptr) v *= p.mask[(int64_t)n1 * p.smm + (int64_t)n2 * p.smn];
+      atomicAdd(p.c + (int64_t)n1 * p.scm + (int64_t)n2 * p.scn, v);
+    }
+  }
+  if (p.ones && tid < N1) atomicAdd(p.rowsum + tid, dbs);
+}
+
 __global__ void zero2d_kernel(float* c, int64_t scm, int64_t scn, int M, int N) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)M * N) return;
@@ -336,6 +480,36 @@ int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
     if (p.ones) (void)hipMemsetAsync(p.rowsum, 0, sizeof(float) * p.N1, s);
   }
   if (p.M <= 0) return check_launch("zero2d_kernel");
+  const bool flat = p.sgm == p.N1 && p.sxm == p.N2 && p.N1 % 4 == 0 && p.N2 % 4 == 0 && p.N2 > 0 &&
+                    (reinterpret_cast<uintptr_t>(p.g) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.x) & 15) == 0 &&
+                    p.N1 <= 256 && p.N2 <= 256;
+  if (flat) {
+    // rows per chunk: ~8192 floats of G + X (a multiple of 16, <= 128); ~1024 workgroups
+    int R = 8192 / (p.N1 + p.N2);
+    R = R > 128 ? 128 : (R / 16) * 16;
+    if (R < 16) R = 16;
+    while (R * (p.N1 + p.N2) / 4 > 256 * WF_Q) R -= 16;
+    int64_t rpw = (p.M + 1023) / 1024;
+    rpw = (rpw + R - 1) / R * R;
+    if (rpw < 4 * R) rpw = 4 * R;
+    p.rows_per_wg = rpw;
+    const int nblk = ((p.N1 + 31) / 32) * ((p.N2 + 31) / 32);
+    const int maxb = nblk <= 4 ? 1 : (nblk <= 8 ? 2 : (nblk <= 16 ? 4 : 8));
+    const size_t lds = sizeof(float) * (R * (p.N1 + p.N2) + 64);
+    const unsigned gx = (unsigned)((p.M + rpw - 1) / rpw);
+    for (int b0 = 0; b0 < nblk; b0 += 4 * maxb) {
+      p.blk0 = b0;
+      WGradArgs q = p;
+      if (b0 > 0) q.ones = 0;  // db once
+      switch (maxb) {
+        case 1: hipLaunchKernelGGL(wgrad_flat_kernel<1>, dim3(gx), dim3(256), lds, s, q, R); break;
+        case 2: hipLaunchKernelGGL(wgrad_flat_kernel<2>, dim3(gx), dim3(256), lds, s, q, R); break;
+        case 4: hipLaunchKernelGGL(wgrad_flat_kernel<4>, dim3(gx), dim3(256), lds, s, q, R); break;
+        default: hipLaunchKernelGGL(wgrad_flat_kernel<8>, dim3(gx), dim3(256), lds, s, q, R); break;
+      }
+    }
+    return check_launch("wgrad_flat_kernel");
+  }
   // enough workgroups to fill the chip twice over, each reducing a multiple of 16 rows
   int64_t rpw = (p.M + 1023) / 1024;
   rpw = (rpw + WG_BK - 1) / WG_BK * WG_BK;

@@ -68,7 +68,7 @@ def build_flow():
     return f
 
 
-def cpu_baseline(flow, x_host: np.ndarray, c_host: np.ndarray, budget_rows: int = 1 << 18):
+def cpu_baseline(flow, x_host: np.ndarray, c_host: np.ndarray, budget_rows: int = 1 << 19):
     """The reference's CPU path (the oracle: pure-torch restatement of pyro's eager per-layer
     semantics, fp32) timed on this host's cores over a bounded sample of the same workload."""
     from naz_amd.flows import io as fio
@@ -274,7 +274,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1 << 20, help="rows per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train", action="store_true",

@@ -683,6 +683,9 @@ struct CfgX6 {
 // |value| bound under which GEMM1's B operand (context, x1) is split into fp16 hi + lo: hi
 // (round-toward-zero) stays finite and lo = v - hi is exact with 11 significant bits.
 constexpr float kG1F16Limit = 32768.f;
+#ifndef NAZ_CTX_CHECK_LOAD
+#define NAZ_CTX_CHECK_LOAD(p) (*(p))
+#endif
 
 // GEMM1 input column (in cat([ctx, x1]) order) for k-step t, element j, lane-half h; -1 = zero pad
 template <class CF>
@@ -987,9 +990,7 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int c = 16 * t + 8 * h + jj;
-        // nontemporal: a separate read the compiler cannot merge with GEMM1's per-layer context
-        // loads (merging keeps 16 context values live across the layer loop: +20% time)
-        if (c < CF::C) ok = ok && fabsf(__builtin_nontemporal_load(&ctx[crow * ldc + c])) < kG1F16Limit;
+        if (c < CF::C) ok = ok && fabsf(NAZ_CTX_CHECK_LOAD(&ctx[crow * ldc + c])) < kG1F16Limit;
       }
     // workgroup AND through ring slot 1 (unused until the first in-loop barrier; static LDS
     // for __syncthreads_and would push the workgroup past 80 KB = one workgroup per CU)

@@ -283,9 +283,9 @@ def main():
     ap.add_argument("--cnf", action="store_true",
                     help="BASELINE configs[4]: 16-dim FFJORD CNF (H=[128]*3, softplus, Hutchinson trace, RK4 x 8 "
                          "steps) log_prob at 2^18 rows per GPU")
-    ap.add_argument("--mfma", choices=["auto", "f16x3", "bf16x6", "f32"], default="auto",
-                    help="auto (default): f16x3 when the hidden-layer weights fit fp16 (GEMM1 bf16x6, GEMM2/3 as "
-                         "three exact-split fp16 products), else bf16x6; f32: exact FP32 MFMA")
+    ap.add_argument("--mfma", choices=["auto", "f16x3", "f16x3r16", "bf16x6", "f32"], default="auto",
+                    help="auto (default): f16x3r16 (16-row waves) when the packed hidden-layer weights fit fp16 and "
+                         "the shape allows, else f16x3, else bf16x6; f32: exact FP32 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -364,6 +364,8 @@ def main():
             peak = FP32_PEAK_TFLOPS
         elif mode == "bf16x6":
             peak = BF16_PEAK_TFLOPS / X6_PRODUCTS
+        elif mode == "f16x3r16":  # GEMM1's out-of-range fallback is exact FP32 MFMA
+            peak = BF16_PEAK_TFLOPS / 3 if g1_range_ok else 1.0 / (g1 / FP32_PEAK_TFLOPS + (1 - g1) * 3 / BF16_PEAK_TFLOPS)
         else:
             peak = BF16_PEAK_TFLOPS / (g1 * (3 if g1_range_ok else X6_PRODUCTS) + (1 - g1) * 3)
         traffic, traffic_src = load_traffic(mode)
@@ -384,8 +386,8 @@ def main():
                                        "algorithmic fp32 FLOP/s vs the dense bf16/fp16 MFMA peak (2.5 PF) divided by "
                                        "the MFMA products per fp32 product (bf16x6: 6; f16x3: 3, GEMM1 6 only for "
                                        f"workgroups outside fp16 range); the exact-FP32 MFMA peak is {FP32_PEAK_TFLOPS}"),
-                         "kernel": ("coupling_flow_kernel" if mode == "f32" else "coupling_x6_kernel")
-                                   + f"<16,32,8,8,128,lower,inv,{mode}>",
+                         "kernel": {"f32": "coupling_flow_kernel", "f16x3r16": "coupling_r16_kernel"}.get(
+                                   mode, "coupling_x6_kernel") + f"<16,32,8,8,128,lower,inv,{mode}>",
                          "flop_per_row": flops_per_row(), "avg_kernel_ms": avg_kern_s * 1e3,
                          "hbm_alg_GBps": bytes_per_row() * B / avg_kern_s / 1e9},
         }

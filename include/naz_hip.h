@@ -42,7 +42,10 @@ extern "C" {
 #define NAZ_MFMA_BF16X6 0 /* default: FP32 GEMMs as 6 exact-split bf16 MFMA products (fp32-grade error) */
 #define NAZ_MFMA_F32 1    /* exact FP32 MFMA (v_mfma_f32_32x32x2_f32)                                  */
 #define NAZ_MFMA_F16X3 2  /* GEMM1 bf16x6, GEMM2/3 as 3 exact-split fp16 products (fp32-grade error;
-                             requires every |W1|, |W2| < 2^15 — the caller checks at pack time)       */
+                             requires every packed |W1|, |W2| < 2^15 — the caller checks at pack time;
+                             GEMM1 also fp16x3 for workgroups whose data is inside fp16 range)         */
+#define NAZ_MFMA_F16X3_R16 3 /* the f16x3 arithmetic on 16-row waves (16x16x32 MFMA, 4 waves/SIMD);
+                                GEMM1 falls back to exact fp32 MFMA per workgroup; S, D-S multiples of 4 */
 
 /* ---- library ------------------------------------------------------------ */
 const char* naz_last_error(void);

@@ -1181,12 +1181,20 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
   }
 }
 
+}  // namespace naz
+
+#include "coupling_r16.h"
+
+namespace naz {
+
 // ---------------------------------------------------------------------------
 // Host dispatch over the compiled instantiations
 // ---------------------------------------------------------------------------
-template <class CF, class CX, class CH>
+template <class CF, class CX, class CH, class CR, bool R16OK>
 struct CouplingOps {
+  static bool supports(int mode) { return mode != NAZ_MFMA_F16X3_R16 || R16OK; }
   static int64_t layer_floats(int mode) {
+    if (mode == NAZ_MFMA_F16X3_R16) return CR::LAYER;
     return mode == NAZ_MFMA_F32 ? CF::LAYER : (mode == NAZ_MFMA_BF16X6 ? CX::LAYER : CH::LAYER);
   }
   static int64_t packed_bytes(int L, int mode) { return (int64_t)L * layer_floats(mode) * 4; }
@@ -1196,7 +1204,9 @@ struct CouplingOps {
     int64_t grid = (n + 255) / 256;
     if (grid > 8192) grid = 8192;
     float* pk = reinterpret_cast<float*>(packed);
-    if (mode == NAZ_MFMA_F32)
+    if (mode == NAZ_MFMA_F16X3_R16)
+      hipLaunchKernelGGL((coupling_pack_r16_kernel<CR>), dim3((unsigned)grid), dim3(256), 0, s, flat, pk, L, bound);
+    else if (mode == NAZ_MFMA_F32)
       hipLaunchKernelGGL((coupling_pack_kernel<CF>), dim3((unsigned)grid), dim3(256), 0, s, flat, pk, L, bound);
     else if (mode == NAZ_MFMA_BF16X6)
       hipLaunchKernelGGL((coupling_pack_x6_kernel<CX>), dim3((unsigned)grid), dim3(256), 0, s, flat, pk, L, bound);
@@ -1204,12 +1214,16 @@ struct CouplingOps {
       hipLaunchKernelGGL((coupling_pack_x6_kernel<CH>), dim3((unsigned)grid), dim3(256), 0, s, flat, pk, L, bound);
     return check_launch("coupling_pack_kernel");
   }
-  template <class G, bool INV, bool X6>
+  template <class G, bool INV, int X6>
   static void launch(const float* pk, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
                      const float* low, const float* high, float* out_lp, float* y, int64_t ldy, int64_t B, float bound,
                      hipStream_t s) {
     const size_t lds = (size_t)G::MAXSTAGE * 4;
-    if constexpr (X6) {
+    if constexpr (X6 == 2) {
+      const int64_t grid = (B + kR16Rows - 1) / kR16Rows;
+      hipLaunchKernelGGL((coupling_r16_kernel<G, INV>), dim3((unsigned)grid), dim3(kR16Rows * 4), lds, s, pk, L, x,
+                         ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+    } else if constexpr (X6 == 1) {
       const int64_t grid = (B + kX6Rows - 1) / kX6Rows;
       hipLaunchKernelGGL((coupling_x6_kernel<G, INV>), dim3((unsigned)grid), dim3(kX6Rows * 2), lds, s, pk, L, x,
                          ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound);
@@ -1227,9 +1241,12 @@ struct CouplingOps {
 #define NAZ_RUN(G, X6)                                                                                   \
   (inv ? launch<G, true, X6>(pk, L, x, ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound, s)            \
        : launch<G, false, X6>(pk, L, x, ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound, s))
-    if (mode == NAZ_MFMA_F32) NAZ_RUN(CF, false);
-    else if (mode == NAZ_MFMA_BF16X6) NAZ_RUN(CX, true);
-    else NAZ_RUN(CH, true);
+    if (mode == NAZ_MFMA_F32) NAZ_RUN(CF, 0);
+    else if (mode == NAZ_MFMA_BF16X6) NAZ_RUN(CX, 1);
+    else if (mode == NAZ_MFMA_F16X3_R16) {
+      if constexpr (R16OK) NAZ_RUN(CR, 2);
+      else return -2;
+    } else NAZ_RUN(CH, 1);
 #undef NAZ_RUN
     return check_launch("coupling_flow_kernel");
   }
@@ -1253,11 +1270,20 @@ template <class F>
 static int coupling_dispatch(const naz_coupling_desc* d, F&& f) {
   if (d == nullptr) return set_error("naz_coupling: null descriptor");
   if (d->act != NAZ_ACT_TANH) return -2;
-  if (d->mfma_mode != NAZ_MFMA_BF16X6 && d->mfma_mode != NAZ_MFMA_F32 && d->mfma_mode != NAZ_MFMA_F16X3) return -2;
+  if (d->mfma_mode != NAZ_MFMA_BF16X6 && d->mfma_mode != NAZ_MFMA_F32 && d->mfma_mode != NAZ_MFMA_F16X3 &&
+      d->mfma_mode != NAZ_MFMA_F16X3_R16)
+    return -2;
+#define NAZ_R16OK(D_, S_, H_) ((S_) % 4 == 0 && ((D_) - (S_)) % 4 == 0 && (S_) / 4 <= 8 && (H_) % 32 == 0 && (H_) <= 128)
 #define NAZ_TRY(D_, C_, S_, K_, H_, LOW_)                                                                  \
-  if (d->D == D_ && d->C == C_ && d->S == S_ && d->K == K_ && d->H == H_ && (d->has_lower != 0) == LOW_) \
-    return f(CouplingOps<CouplingCfg<D_, C_, S_, K_, H_, LOW_>, CfgX6<D_, C_, S_, K_, H_, LOW_, 3>, \
-                         CfgX6<D_, C_, S_, K_, H_, LOW_, 2>>{});
+  if (d->D == D_ && d->C == C_ && d->S == S_ && d->K == K_ && d->H == H_ && (d->has_lower != 0) == LOW_) {  \
+    using Ops = CouplingOps<CouplingCfg<D_, C_, S_, K_, H_, LOW_>, CfgX6<D_, C_, S_, K_, H_, LOW_, 3>,         \
+                            CfgX6<D_, C_, S_, K_, H_, LOW_, 2>,                                                \
+                            std::conditional_t<NAZ_R16OK(D_, S_, H_), CfgR16<D_, C_, S_, K_, H_, LOW_>,        \
+                                               CfgR16<8, 0, 4, 8, 128, true>>,                                 \
+                            NAZ_R16OK(D_, S_, H_)>;                                                            \
+    if (!Ops::supports(d->mfma_mode)) return -2;                                                               \
+    return f(Ops{});                                                                                           \
+  }
   NAZ_COUPLING_CONFIGS(NAZ_TRY)
 #undef NAZ_TRY
   return -2;

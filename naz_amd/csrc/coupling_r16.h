@@ -1,0 +1,495 @@
+// 16-row-wave variant of the fused coupling flow (NAZ_MFMA_F16X3_R16; included by coupling.hip,
+// which supplies split8_f16, f16_piece_bits, sig_fold, kSigScale, stage_issue, kChunk, ...).
+//
+// Why: the 32-row x6 kernel keeps each activation block in a 32x32 accumulator (16 VGPRs per
+// feature block) and needs ~250 VGPRs, i.e. two waves per SIMD; PMC shows ~28 % of its cycles
+// with neither the matrix nor the vector pipe busy.  Here every wave owns 16 batch rows and
+// every GEMM runs on v_mfma_f32_16x16x32_f16 (same FLOP per cycle as 32x32x16): a 16-feature
+// block costs 4 VGPRs per lane, the whole live set fits 128 VGPRs and FOUR waves share each
+// SIMD (512-thread workgroups of 128 rows, two per CU, the same 2 x 40 KB LDS ring per
+// workgroup).
+//
+// Lane l owns batch row (l & 15) and quarter q = l >> 4 of that row's dims: lower dims
+// [q*SQ, q*SQ + SQ) and upper dims [q*DQ, q*DQ + DQ) (S, D - S multiples of 4).
+//   * accumulator register i of block b on quarter q = feature 16b + 4q + i (16x16 C layout);
+//   * B operand of a 32-k step t on quarter q, element j = k-slot 8q + j; the packer maps that
+//     slot to feature 32t + 16(j >> 2) + 4q + (j & 3), i.e. the lane's OWN accumulator
+//     registers of blocks 2t, 2t + 1 — layers chain with no LDS and no shuffles;
+//   * GEMM3's rows are permuted so quarter q receives, in (block, register) order, the 3K-1
+//     parameters of its own DQ upper dims;
+//   * GEMM1's k-slots put quarter q's x1 dims (which only that lane computes) in its own
+//     slots of the last k-step; the context fills the other slots (loaded from HBM/L2).
+// Precision: fp16 hi/lo pieces, 3 products (Wh·Xh + Wh·Xl + Wl·Xh) as in the x6 kernel's
+// f16x3 GEMM2/3.  GEMM1 takes that path when every context/data value of the workgroup's rows
+// is below 2^15; otherwise the workgroup runs GEMM1 in EXACT fp32 (v_mfma_f32_16x16x4_f32,
+// a second stage-A image of the same size).  Activation fold, select-first spline and LDS-DMA
+// ring as in coupling_x6_kernel.
+#pragma once
+
+namespace naz {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+NAZ_DEV floatx4 mfma16_f16(half8 a, half8 b, floatx4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+NAZ_DEV floatx4 mfma16_f32(float a, float b, floatx4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+NAZ_DEV floatx4 mfma3_16(const Frag2& a, const Frag2& b, floatx4 acc) {
+  acc = mfma16_f16(a.l, b.h, acc);  // small terms first
+  acc = mfma16_f16(a.h, b.l, acc);
+  acc = mfma16_f16(a.h, b.h, acc);
+  return acc;
+}
+
+constexpr int kR16Waves = 8;                 // 8 waves x 16 rows = 128 rows per workgroup
+constexpr int kR16Rows = 16 * kR16Waves;
+
+// feature carried by k-slot 8q + j of 32-k step t (GEMM2/3 inputs)
+__host__ __device__ constexpr int r16_feat(int t, int q, int j) { return 32 * t + 16 * (j >> 2) + 4 * q + (j & 3); }
+
+template <int D_, int C_, int S_, int K_, int H_, bool LOWER_>
+struct CfgR16 {
+  static constexpr int D = D_, C = C_, S = S_, K = K_, H = H_;
+  static constexpr bool LOWER = LOWER_;
+  static constexpr int Dt = D - S, P = 3 * K - 1, DQ = Dt / 4, SQ = S / 4;
+  static constexpr int HB = H / 16;                    // 16-feature blocks
+  static constexpr int KS1 = (C + S + 31) / 32;        // GEMM1 32-k steps
+  static constexpr int KS2 = H / 32;                   // GEMM2/3 32-k steps
+  static constexpr int NO = (DQ * P + 3) / 4;          // GEMM3 output blocks
+  static constexpr int TBL = 3 * (K + 1);
+  static constexpr int OT = 2 * kChunk;                // floats per (block, k-step): hi + lo pieces
+  static constexpr int pad(int n) { return (n + 255) / 256 * 256; }
+  static constexpr int pick_kb(int nb, int bias) {
+    int best = 1;
+    for (int kb = 1; kb <= KS2; ++kb)
+      if (KS2 % kb == 0 && pad(nb * kb * OT + bias) <= kX6Slot) best = kb;
+    return best;
+  }
+  static constexpr int KB2 = pick_kb(HB, H), NB2 = KS2 / KB2;
+  static constexpr int KB3 = pick_kb(NO, 16 * NO), NB3 = KS2 / KB3;
+  // stage A (fp16 image; the fp32 image A32 has the same size and bias/table offsets):
+  //   [HB][KS1][2][256] | bias [H] | tables [S][TBL]
+  static constexpr int A_BIAS = HB * KS1 * OT;
+  static constexpr int A_TBL = A_BIAS + H;
+  static constexpr int A_SIZE = pad(A_TBL + S * TBL);
+  static constexpr int B_OFF = A_SIZE;
+  static constexpr int B_BIAS = HB * KB2 * OT;
+  static constexpr int B_SIZE = pad(B_BIAS + H);
+  static constexpr int C_OFF = B_OFF + NB2 * B_SIZE;
+  static constexpr int C_BIAS = NO * KB3 * OT;
+  static constexpr int C_SIZE = pad(C_BIAS + 16 * NO);
+  static constexpr int A32_OFF = C_OFF + NB3 * C_SIZE;
+  static constexpr int LAYER = A32_OFF + A_SIZE;
+  static constexpr int NSTG = 1 + NB2 + NB3;
+  static constexpr int MAXSTAGE = 2 * kX6Slot;
+  static constexpr __host__ __device__ int stage_off(int j) {
+    return j == 0 ? 0 : (j <= NB2 ? B_OFF + (j - 1) * B_SIZE : C_OFF + (j - 1 - NB2) * C_SIZE);
+  }
+  static constexpr __host__ __device__ int stage_size(int j) { return j == 0 ? A_SIZE : (j <= NB2 ? B_SIZE : C_SIZE); }
+  // natural flat layout (same as every other coupling variant)
+  static constexpr int N_W0 = H * (C + S), N_B0 = H, N_W1 = H * H, N_B1 = H, N_W2 = Dt * P * H, N_B2 = Dt * P;
+  static constexpr int N_LOW = LOWER ? S * (3 * K - 1) : 0;
+  static constexpr int FLAT = N_W0 + N_B0 + N_W1 + N_B1 + N_W2 + N_B2 + N_LOW;
+  static_assert(S % 4 == 0 && Dt % 4 == 0 && H % 32 == 0 && S > 0 && SQ <= 8, "unsupported r16 coupling shape");
+  static_assert(A_SIZE <= kX6Slot && B_SIZE <= kX6Slot && C_SIZE <= kX6Slot, "stage exceeds one LDS ring slot");
+  static_assert(HB <= 8 && NO <= 16, "register budget");
+};
+
+// GEMM1 input column for k-slot j of 32-k step t on quarter q (cat([ctx, x1]) order), -1 = pad.
+// Quarter q's own x1 dims sit in slots j < SQ of the last step; the context fills the rest.
+template <class CF>
+__host__ __device__ constexpr int r16_in_col(int t, int q, int j) {
+  constexpr int TX = CF::KS1 - 1;
+  if (t == TX && j < CF::SQ) return CF::C + q * CF::SQ + j;
+  int idx;
+  if (t < TX) idx = 32 * t + 8 * q + j;
+  else idx = 32 * TX + q * (8 - CF::SQ) + (j - CF::SQ);
+  return idx < CF::C ? idx : -1;
+}
+
+// DenseNN output column of GEMM3 output row r (0..15) of block o; -1 = pad
+template <class CF>
+__host__ __device__ constexpr int r16_out_row(int o, int r) {
+  const int q = r >> 2, slot = 4 * o + (r & 3), dq = slot / CF::P, p = slot - dq * CF::P;
+  if (dq >= CF::DQ) return -1;
+  const int dim = q * CF::DQ + dq;
+  if (p < CF::K) return dim * CF::K + p;
+  if (p < 2 * CF::K) return CF::Dt * CF::K + dim * CF::K + (p - CF::K);
+  return 2 * CF::Dt * CF::K + dim * (CF::K - 1) + (p - 2 * CF::K);
+}
+
+template <class CF>
+__global__ void coupling_pack_r16_kernel(const float* __restrict__ flat, float* __restrict__ packed, int L,
+                                         float bound) {
+  const int64_t n = (int64_t)L * CF::LAYER;
+  unsigned* pu = reinterpret_cast<unsigned*>(packed);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(e / CF::LAYER);
+    const int off = (int)(e - (int64_t)l * CF::LAYER);
+    const float* W0 = flat + (int64_t)l * CF::FLAT;
+    const float* b0 = W0 + CF::N_W0;
+    const float* W1 = b0 + CF::N_B0;
+    const float* b1 = W1 + CF::N_W1;
+    const float* W2 = b1 + CF::N_B1;
+    const float* b2 = W2 + CF::N_W2;
+    const float* low = b2 + CF::N_B2;
+    // f16 chunk word: (o, t, piece, lane, pair) -> two fp16 pieces of the scaled weight
+    auto chunk_word = [&](int q, int nt, int t0, int which) -> unsigned {
+      const int o = q / (nt * CF::OT), r1 = q - o * nt * CF::OT;
+      const int tl = r1 / CF::OT, r2 = r1 - tl * CF::OT;
+      const int piece = r2 / kChunk, u = r2 - piece * kChunk;
+      const int lane = u >> 2, pair = u & 3, i = lane & 15, qq = lane >> 4;
+      const int t = t0 + tl;
+      unsigned out = 0;
+      for (int e2 = 0; e2 < 2; ++e2) {
+        const int j = 2 * pair + e2;
+        float v = 0.f;
+        if (which == 0) {
+          const int col = r16_in_col<CF>(t, qq, j);
+          v = col >= 0 ? kSigScale * W0[(16 * o + i) * (CF::C + CF::S) + col] : 0.f;
+        } else if (which == 1) {
+          v = -2.f * kSigScale * W1[(16 * o + i) * CF::H + r16_feat(t, qq, j)];
+        } else {
+          const int orow = r16_out_row<CF>(o, i);
+          v = orow >= 0 ? -2.f * W2[orow * CF::H + r16_feat(t, qq, j)] : 0.f;
+        }
+        out |= f16_piece_bits(v, piece) << (16 * e2);
+      }
+      return out;
+    };
+    unsigned word = 0;
+    float fv = 0.f;
+    bool is_word = false;
+    const bool a32 = off >= CF::A32_OFF;
+    if (off < CF::A_SIZE || a32) {
+      const int oa = a32 ? off - CF::A32_OFF : off;
+      if (oa < CF::A_BIAS) {
+        if (!a32) {
+          word = chunk_word(oa, CF::KS1, 0, 0);
+          is_word = true;
+        } else {
+          // fp32 image [o][s4][lane][4]: k-step s = 4 s4 + i of v_mfma_f32_16x16x4_f32 on quarter
+          // lane >> 4 carries the fp16 path's slot (t = s / 8, j = s % 8)
+          const int i4 = oa & 3, lane = (oa >> 2) & 63, rest = oa >> 8;
+          const int s4 = rest % (2 * CF::KS1), o = rest / (2 * CF::KS1);
+          const int s = 4 * s4 + i4;
+          const int col = r16_in_col<CF>(s / 8, lane >> 4, s % 8);
+          fv = col >= 0 ? kSigScale * W0[(16 * o + (lane & 15)) * (CF::C + CF::S) + col] : 0.f;
+        }
+      } else if (oa < CF::A_TBL) {
+        fv = kSigScale * b0[oa - CF::A_BIAS];
+      } else if (CF::LOWER && oa < CF::A_TBL + CF::S * CF::TBL) {
+        const int q = oa - CF::A_TBL, g = q / CF::TBL, w = q - g * CF::TBL;
+        float uw[CF::K], uh[CF::K], ud[CF::K - 1];
+        for (int k = 0; k < CF::K; ++k) {
+          uw[k] = low[g * CF::K + k];
+          uh[k] = low[CF::S * CF::K + g * CF::K + k];
+        }
+        for (int k = 0; k < CF::K - 1; ++k) ud[k] = low[2 * CF::S * CF::K + g * (CF::K - 1) + k];
+        SplineTables<CF::K> tb;
+        build_tables<CF::K>(uw, uh, ud, bound, tb);
+        const int which = w / (CF::K + 1), k = w - which * (CF::K + 1);
+        fv = which == 0 ? tb.cw[k] : (which == 1 ? tb.ch[k] : tb.dv[k]);
+      }
+    } else if (off < CF::C_OFF) {
+      const int sq = (off - CF::B_OFF) / CF::B_SIZE, q = off - CF::B_OFF - sq * CF::B_SIZE;
+      if (q < CF::B_BIAS) {
+        word = chunk_word(q, CF::KB2, sq * CF::KB2, 1);
+        is_word = true;
+      } else if (q < CF::B_BIAS + CF::H) {
+        fv = kSigScale * b1[q - CF::B_BIAS];
+      }
+    } else {
+      const int sq = (off - CF::C_OFF) / CF::C_SIZE, q = off - CF::C_OFF - sq * CF::C_SIZE;
+      if (q < CF::C_BIAS) {
+        word = chunk_word(q, CF::KB3, sq * CF::KB3, 2);
+        is_word = true;
+      } else if (q < CF::C_BIAS + 16 * CF::NO) {
+        const int r = q - CF::C_BIAS, orow = r16_out_row<CF>(r >> 4, r & 15);
+        fv = orow >= 0 ? b2[orow] : 0.f;
+      }
+    }
+    if (is_word) pu[e] = word;
+    else packed[e] = fv;
+  }
+}
+
+// acc[o] += A(o, t) · B(t) over k-steps [0, KB) with B fragments given
+template <int NB, int KB>
+NAZ_DEV void gemm_r16_stage(floatx4 (&acc)[NB], const float* __restrict__ stage, int lane, const Frag2 (&bf)[KB]) {
+  const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
+#pragma unroll
+  for (int t = 0; t < KB; ++t)
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const int base = ((o * KB + t) * 2) * 64 + lane;
+      const Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+      acc[o] = mfma3_16(a, bf[t], acc[o]);
+    }
+}
+
+// k-steps [T0, T0 + KB) with each B fragment split from the activated accumulators just
+// before its MFMAs (blocks 2t, 2t + 1 hold the step's 8 values)
+template <int NB, int KB, int T0, int NX>
+NAZ_DEV void gemm_r16_lazy(floatx4 (&acc)[NB], const float* __restrict__ stage, int lane, const floatx4 (&x)[NX]) {
+  const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
+#pragma unroll
+  for (int t = 0; t < KB; ++t) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[2 * (T0 + t) + (j >> 2)][j & 3];
+    const Frag2 b = split8_f16(v);
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const int base = ((o * KB + t) * 2) * 64 + lane;
+      const Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+      acc[o] = mfma3_16(a, b, acc[o]);
+    }
+  }
+}
+
+template <class CF, bool DIR_INV>
+__global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
+    const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
+    const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
+    float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound) {
+  extern __shared__ float4 lds4[];
+  float* const slot0 = reinterpret_cast<float*>(lds4);
+  float* const slot1 = slot0 + kX6Slot;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane >> 4;
+  const int64_t row = (int64_t)blockIdx.x * kR16Rows + wave * 16 + (lane & 15);
+  const bool valid = row < B;
+  const int64_t crow = valid ? row : 0;
+
+  float zl[CF::SQ], zu[CF::DQ];
+  float ldsum = 0.f, logjac = 0.f;
+#pragma unroll
+  for (int u = 0; u < CF::SQ; ++u) zl[u] = valid ? x[crow * ldx + q * CF::SQ + u] : 0.f;
+#pragma unroll
+  for (int u = 0; u < CF::DQ; ++u) zu[u] = valid ? x[crow * ldx + CF::S + q * CF::DQ + u] : 0.f;
+  if (DIR_INV && low != nullptr) {  // naz bounding_transform (transforms.py:20-23)
+    auto bnd = [&](float& v, int dim) {
+      const float lo = low[dim], hi = high[dim];
+      const float u = (v - lo) / (hi - lo);
+      logjac -= logf(u) + log1pf(-u);
+      v = logf(u / (1.f - u));
+    };
+#pragma unroll
+    for (int u = 0; u < CF::SQ; ++u) bnd(zl[u], q * CF::SQ + u);
+#pragma unroll
+    for (int u = 0; u < CF::DQ; ++u) bnd(zu[u], CF::S + q * CF::DQ + u);
+    if (q == 0) {
+      float sl = 0.f;
+      for (int d = 0; d < CF::D; ++d) sl += logf(high[d] - low[d]);
+      logjac -= sl;
+    }
+  }
+
+  // GEMM1 precision path of this workgroup (see the file comment); reduced through ring slot 1
+  bool ok = bound < kG1F16Limit;
+#pragma unroll
+  for (int u = 0; u < CF::SQ; ++u) ok = ok && fabsf(zl[u]) < kG1F16Limit;
+#pragma unroll
+  for (int u = 0; u < CF::DQ; ++u) ok = ok && fabsf(zu[u]) < kG1F16Limit;
+#pragma unroll
+  for (int t = 0; t < CF::KS1; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = r16_in_col<CF>(t, q, j);
+      if (col >= 0 && col < CF::C) ok = ok && fabsf(ctx[crow * ldc + col]) < kG1F16Limit;
+    }
+  {
+    int* flags = reinterpret_cast<int*>(slot1);
+    if (lane == 0) flags[wave] = __all(ok) ? 1 : 0;
+    __syncthreads();
+    bool all_ok = true;
+#pragma unroll
+    for (int w = 0; w < kR16Waves; ++w) all_ok = all_ok && flags[w] != 0;
+    ok = all_ok;
+  }
+  const bool g1f16 = ok;
+  const int a_off = g1f16 ? 0 : CF::A32_OFF;
+
+  stage_issue<CF::A_SIZE, kR16Waves>(slot0, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER + a_off);
+
+  int g = 0;  // global stage counter: stage g lives in slot (g & 1)
+  for (int li = 0; li < L; ++li) {
+    const int l = DIR_INV ? (L - 1 - li) : li;
+    const float* lp = packed + (int64_t)l * CF::LAYER;
+    const float* lnext = packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER;
+    floatx4 acc1[CF::HB], acc2[CF::HB], acc3[CF::NO];
+
+    static_for<0, CF::NSTG>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      __syncthreads();  // stage j has landed in slot (g&1); every wave is done with the other slot
+      const float* cur = (g & 1) ? slot1 : slot0;
+      float* nxt = (g & 1) ? slot0 : slot1;
+      if constexpr (j + 1 < CF::NSTG) {
+        stage_issue<CF::stage_size(j + 1), kR16Waves>(nxt, lp + CF::stage_off(j + 1));
+      } else {
+        if (li + 1 < L) stage_issue<CF::A_SIZE, kR16Waves>(nxt, lnext + a_off);
+      }
+      ++g;
+
+      if constexpr (j == 0) {
+        // ---------------- stage A: lower spline (inverse), GEMM1 over [ctx | x1]
+#pragma unroll
+        for (int u = 0; u < CF::SQ; ++u) {
+          if constexpr (DIR_INV && CF::LOWER) {
+            float ld;
+            zl[u] = rqs_table<CF::K, true>(cur + CF::A_TBL + (q * CF::SQ + u) * CF::TBL, zl[u], bound, ld);
+            ldsum -= ld;
+          }
+        }
+        float in[CF::KS1 * 8];
+#pragma unroll
+        for (int t = 0; t < CF::KS1; ++t)
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            const int col = r16_in_col<CF>(t, q, jj);
+            float v = 0.f;
+            if (col >= CF::C) v = zl[(col - CF::C - q * CF::SQ) < CF::SQ ? (col - CF::C - q * CF::SQ) : 0];
+            else if (col >= 0) v = ctx[crow * ldc + col];
+            in[8 * t + jj] = v;
+          }
+        {
+          const float4* b4 = reinterpret_cast<const float4*>(cur + CF::A_BIAS);
+#pragma unroll
+          for (int o = 0; o < CF::HB; ++o) {
+            const float4 bv = b4[4 * o + q];
+            acc1[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+          }
+        }
+#ifdef NAZ_R16_NO_F32_G1
+        if (true) {
+#else
+        if (g1f16) {
+#endif
+          Frag2 bf[CF::KS1];
+#pragma unroll
+          for (int t = 0; t < CF::KS1; ++t) {
+            float v[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) v[jj] = in[8 * t + jj];
+            bf[t] = split8_f16(v);
+          }
+          gemm_r16_stage<CF::HB, CF::KS1>(acc1, cur, lane, bf);
+        } else {
+          // exact fp32: 8 KS1 k-steps of 4; k-step s on this lane = slot (s / 8, s % 8)
+          const float4* p4 = reinterpret_cast<const float4*>(cur);
+#pragma unroll
+          for (int s4 = 0; s4 < 2 * CF::KS1; ++s4)
+#pragma unroll
+            for (int o = 0; o < CF::HB; ++o) {
+              const float4 a = p4[(o * 2 * CF::KS1 + s4) * 64 + lane];
+              acc1[o] = mfma16_f32(a.x, in[4 * s4 + 0], acc1[o]);
+              acc1[o] = mfma16_f32(a.y, in[4 * s4 + 1], acc1[o]);
+              acc1[o] = mfma16_f32(a.z, in[4 * s4 + 2], acc1[o]);
+              acc1[o] = mfma16_f32(a.w, in[4 * s4 + 3], acc1[o]);
+            }
+        }
+        if constexpr (!DIR_INV && CF::LOWER) {
+#pragma unroll
+          for (int u = 0; u < CF::SQ; ++u) {
+            float ld;
+            zl[u] = rqs_table<CF::K, false>(cur + CF::A_TBL + (q * CF::SQ + u) * CF::TBL, zl[u], bound, ld);
+            ldsum += ld;
+          }
+        }
+      } else if constexpr (j <= CF::NB2) {
+        // ---------------- stage B_s: GEMM2 k-steps [T0, T0 + KB2)
+        constexpr int s = j - 1, T0 = s * CF::KB2;
+#pragma unroll
+        for (int b = 2 * T0; b < 2 * (T0 + CF::KB2); ++b)  // activate the blocks these k-steps read
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc1[b][r] = sig_fold(acc1[b][r]);
+        if constexpr (s == 0) {
+          const float4* b4 = reinterpret_cast<const float4*>(cur + CF::B_BIAS);
+#pragma unroll
+          for (int o = 0; o < CF::HB; ++o) {
+            const float4 bv = b4[4 * o + q];
+            acc2[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+          }
+        }
+        gemm_r16_lazy<CF::HB, CF::KB2, T0>(acc2, cur, lane, acc1);
+      } else {
+        // ---------------- stage C_s: GEMM3 k-steps [T0, T0 + KB3) -> raw spline params
+        constexpr int s = j - 1 - CF::NB2, T0 = s * CF::KB3;
+#pragma unroll
+        for (int b = 2 * T0; b < 2 * (T0 + CF::KB3); ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc2[b][r] = sig_fold(acc2[b][r]);
+        if constexpr (s == 0) {
+          const float4* b4 = reinterpret_cast<const float4*>(cur + CF::C_BIAS);
+#pragma unroll
+          for (int o = 0; o < CF::NO; ++o) {
+            const float4 bv = b4[4 * o + q];
+            acc3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+          }
+        }
+        gemm_r16_lazy<CF::NO, CF::KB3, T0>(acc3, cur, lane, acc2);
+      }
+    });
+
+    // ---------------- upper spline on this quarter's DQ dims (next layer's stage A in flight)
+#pragma unroll
+    for (int u = 0; u < CF::DQ; ++u) {
+      float uw[CF::K], uh[CF::K], ud[CF::K - 1];
+#pragma unroll
+      for (int k = 0; k < CF::K; ++k) {
+        const int sw = u * CF::P + k, sh = u * CF::P + CF::K + k;
+        uw[k] = acc3[sw >> 2][sw & 3];
+        uh[k] = acc3[sh >> 2][sh & 3];
+      }
+#pragma unroll
+      for (int k = 0; k < CF::K - 1; ++k) {
+        const int sd = u * CF::P + 2 * CF::K + k;
+        ud[k] = acc3[sd >> 2][sd & 3];
+      }
+      float ld;
+      zu[u] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[u], bound, ld);
+      ldsum += DIR_INV ? -ld : ld;
+    }
+  }
+
+  if constexpr (DIR_INV) {
+    constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+    float base = 0.f;
+#pragma unroll
+    for (int u = 0; u < CF::SQ; ++u) base += -(zl[u] * zl[u]) / 2.f - kLogSqrt2Pi;
+#pragma unroll
+    for (int u = 0; u < CF::DQ; ++u) base += -(zu[u] * zu[u]) / 2.f - kLogSqrt2Pi;
+    float v = base - ldsum + logjac;
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (q == 0 && valid) out_lp[row] = v;
+  } else {
+    if (low != nullptr) {
+#pragma unroll
+      for (int u = 0; u < CF::SQ; ++u) {
+        const int d = q * CF::SQ + u;
+        zl[u] = (1.f / (1.f + expf(-zl[u]))) * (high[d] - low[d]) + low[d];
+      }
+#pragma unroll
+      for (int u = 0; u < CF::DQ; ++u) {
+        const int d = CF::S + q * CF::DQ + u;
+        zu[u] = (1.f / (1.f + expf(-zu[u]))) * (high[d] - low[d]) + low[d];
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int u = 0; u < CF::SQ; ++u) yout[row * ldy + q * CF::SQ + u] = zl[u];
+#pragma unroll
+      for (int u = 0; u < CF::DQ; ++u) yout[row * ldy + CF::S + q * CF::DQ + u] = zu[u];
+    }
+    if (out_lp != nullptr) {
+      float v = ldsum;
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (q == 0 && valid) out_lp[row] = v;
+    }
+  }
+}
+
+}  // namespace naz

@@ -53,8 +53,10 @@ class _FusedCoupling:
         self._packed = None
 
     def set_mfma(self, mfma: str) -> None:
-        """"auto" (default: f16x3 when the GEMM2/3 weights fit fp16's range, else bf16x6),
-        "f16x3", "bf16x6" or "f32" (exact FP32 MFMA kernel); invalidates the packed weights."""
+        """"auto" (default: the 16-row-wave f16x3 kernel when the packed GEMM2/3 weights fit
+        fp16's range and the shape allows it, else the 32-row f16x3 kernel, else bf16x6),
+        "f16x3r16", "f16x3", "bf16x6" or "f32" (exact FP32 MFMA kernel); invalidates the
+        packed weights."""
         self.mfma = mfma
         self._sig, self._packed = None, None
 
@@ -63,7 +65,11 @@ class _FusedCoupling:
             return self.mfma
         big = max(float(t.nn.layers[i].weight.detach().abs().max()) * self.F16_PACK_SCALE[i]
                   for t in self.layers for i in (1, 2))
-        return "f16x3" if big < self.F16_WEIGHT_LIMIT else "bf16x6"
+        if big >= self.F16_WEIGHT_LIMIT:
+            return "bf16x6"
+        D, C, S, K, H, act, lower, bound = self.shape
+        r16 = ops.coupling_desc(D, C, S, K, len(self.layers), H, act, lower, bound, "f16x3r16")
+        return "f16x3r16" if ops.coupling_supported(r16) else "f16x3"
 
     def params(self) -> List[torch.Tensor]:
         out = []

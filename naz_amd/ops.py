@@ -315,13 +315,15 @@ def act_bwd(g_y: Tensor, y: Tensor, act: str) -> Tensor:
 # ----------------------------------------------------------------------------- a3 + a8 + a9 fused
 def coupling_desc(D: int, C: int, S: int, K: int, L: int, H: int, act: str = "tanh", has_lower: bool = True,
                   bound: float = 3.0, mfma: str = "bf16x6") -> CouplingDesc:
-    """``mfma``: "bf16x6" (FP32 GEMMs as six exact-split bf16 products), "f16x3" (GEMM1 bf16x6,
-    GEMM2/3 three exact-split fp16 products; needs |W1|,|W2| < 2^15) or "f32" (exact
+    """``mfma``: "bf16x6" (FP32 GEMMs as six exact-split bf16 products), "f16x3" (three
+    exact-split fp16 products; needs packed |W1|,|W2| < 2^15; GEMM1 bf16x6 for workgroups
+    outside fp16 range), "f16x3r16" (the same arithmetic on 16-row waves; S and D-S multiples
+    of 4; GEMM1 exact fp32 for workgroups outside fp16 range) or "f32" (exact
     v_mfma_f32_32x32x2_f32)."""
     d = CouplingDesc()
     d.D, d.C, d.S, d.K, d.L, d.H = D, C, S, K, L, H
     d.act, d.has_lower, d.bound = ACT.get(act, -1), int(has_lower), float(bound)
-    d.mfma_mode = {"bf16x6": 0, "f32": 1, "f16x3": 2}[mfma]
+    d.mfma_mode = {"bf16x6": 0, "f32": 1, "f16x3": 2, "f16x3r16": 3}[mfma]
     return d
 
 

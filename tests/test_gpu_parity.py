@@ -151,13 +151,19 @@ FLOWS = ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz", "nsa_d4c2
          "maf_twomoons.npz"]
 
 
+def _r16_ok(spec):
+    return spec["split"] % 4 == 0 and (spec["D"] - spec["split"]) % 4 == 0
+
+
 @pytest.mark.parametrize("name", FLOWS)
-@pytest.mark.parametrize("fused", ["auto", "bf16x6", "f32", False])
+@pytest.mark.parametrize("fused", ["auto", "f16x3", "f16x3r16", "bf16x6", "f32", False])
 def test_flow_log_prob_vs_golden(name, fused):
     fx = load_golden(name)
     f, spec, _ = _product_flow(fx)
     if spec["flow_type"] == "nsc":
         assert f.fused, "the nsc fixture shapes must hit a fused instantiation"
+        if fused == "f16x3r16" and not _r16_ok(spec):
+            pytest.skip("16-row-wave kernel needs S and D-S multiples of 4")
         f.set_fused(bool(fused))
         if fused:
             f._plan.set_mfma(fused)
@@ -171,11 +177,13 @@ def test_flow_log_prob_vs_golden(name, fused):
 
 
 @pytest.mark.parametrize("name", ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz", "nsc_d6c2_small.npz"])
-@pytest.mark.parametrize("fused", ["auto", "bf16x6", "f32", False])
+@pytest.mark.parametrize("fused", ["auto", "f16x3", "f16x3r16", "bf16x6", "f32", False])
 def test_flow_sample_transform_vs_golden(name, fused):
     from naz_amd import ops
     fx = load_golden(name)
     f, spec, _ = _product_flow(fx)
+    if fused == "f16x3r16" and not _r16_ok(spec):
+        pytest.skip("16-row-wave kernel needs S and D-S multiples of 4")
     f.set_fused(bool(fused))
     if fused:
         f._plan.set_mfma(fused)
@@ -195,7 +203,7 @@ def test_flow_sample_transform_vs_golden(name, fused):
     assert_parity(_np(ld), fx["ld_sample"], ld32.numpy(), what=f"{name} sample ld")
 
 
-@pytest.mark.parametrize("mfma", ["auto", "f16x3", "bf16x6", "f32"])
+@pytest.mark.parametrize("mfma", ["auto", "f16x3", "f16x3r16", "bf16x6", "f32"])
 def test_config3_full_flow_vs_live_oracle(mfma):
     """The metric configuration (D16|C32, K8, H[128,128], L=8) at 8192 rows vs the oracle."""
     from naz_amd.flows import NormalizingFlow
@@ -209,7 +217,7 @@ def test_config3_full_flow_vs_live_oracle(mfma):
     n = 8192
     if mfma == "auto":
         f._plan.packed()
-        assert f._plan.mode == "f16x3"
+        assert f._plan.mode == "f16x3r16"
     x = torch.as_tensor(O.gaussian_mixture(n, 16, seed=0))
     c = torch.as_tensor(O.context_normal(n, 32, seed=1))
     lp = f.log_prob(x.to(DEV), condition=c.to(DEV))
@@ -322,13 +330,14 @@ def test_native_library_is_the_path():
     assert str(_lib.LIB_PATH) in maps
 
 
+@pytest.mark.parametrize("mfma", ["f16x3", "f16x3r16"])
 @pytest.mark.parametrize("scale", [1.0, 5e4])
-def test_config3_gemm1_precision_paths(scale):
+def test_config3_gemm1_precision_paths(scale, mfma):
     """f16x3 picks GEMM1's fp16 path per 128-row workgroup only when every context / data value
     of its rows is below 2^15; rows 128..255 get context values x`scale` so that workgroup (and
     only it) takes the bf16x6 path at 5e4.  Both must match the oracle."""
     f, spec, state = _config3_flow()
-    f._plan.set_mfma("f16x3")
+    f._plan.set_mfma(mfma)
     n = 1024
     x = torch.as_tensor(O.gaussian_mixture(n, 16, seed=3))
     c = torch.as_tensor(O.context_normal(n, 32, seed=4))

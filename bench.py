@@ -248,6 +248,15 @@ def run_cnf(args, dev, rank, world, dist):
         elapsed, kern_s = float(tt[0]), float(tt[1])
     if rank == 0:
         achieved = cnf_flops_per_row() * B / kern_s / 1e12
+        mode = plan.mode or "f32"
+        if mode == "f16x3":
+            # layer 0 exact FP32, hidden + output layers on three fp16 products (FLOP-weighted)
+            w0 = CNF_D * CNF_H[0]
+            tot = w0 + sum(a * b for a, b in zip(CNF_H[:-1], CNF_H[1:])) + CNF_H[-1] * CNF_D
+            g0 = w0 / tot
+            peak = 1.0 / (g0 / FP32_PEAK_TFLOPS + (1 - g0) * 3 / BF16_PEAK_TFLOPS)
+        else:
+            peak = FP32_PEAK_TFLOPS
         rec = {
             "metric": "samples/sec through log_prob+log|detJ|, 16-dim CNF (FFJORD, Hutchinson trace)",
             "value": B * world * args.steps / elapsed, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -259,10 +268,13 @@ def run_cnf(args, dev, rank, world, dist):
                                    "RK4 x 8 (NFE 32, SURVEY.md §8d pin), log_prob (naz_cnf_integrate t 0->1)",
                        "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"dp{world} (independent row shards, no collective)"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "cnf_kernel<16,0,128,128,128,0,softplus>", "flop_per_row": cnf_flops_per_row(),
-                         "avg_kernel_ms": kern_s * 1e3},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": None, "mfma_mode": mode,
+                         "peak_note": "f16x3: layer 0 at the exact-FP32 MFMA peak, the rest at the dense fp16 "
+                                      "MFMA peak / 3 products, FLOP-weighted; f32: exact-FP32 MFMA peak "
+                                      f"{FP32_PEAK_TFLOPS}",
+                         "kernel": f"cnf_kernel<16,0,128,128,128,0,softplus,{mode}>",
+                         "flop_per_row": cnf_flops_per_row(), "avg_kernel_ms": kern_s * 1e3},
         }
         print(json.dumps(rec), flush=True)
     if dist is not None:

@@ -190,9 +190,14 @@ typedef struct naz_cnf_desc {
   int D, C;
   int n_hidden;
   int H[4];
-  int act; /* NAZ_ACT_* (softplus = naz default) */
-  int reserved[8];
+  int act;       /* NAZ_ACT_* (softplus = naz default) */
+  int mfma_mode; /* NAZ_CNF_F32 (0): exact FP32 MFMA; NAZ_CNF_F16X3 (1): layer 0 exact FP32, the
+                    hidden and output layers as 3 exact-split fp16 products (hidden widths multiples
+                    of 32; caller checks |W| < 2^15 at pack time); the packed layout depends on it */
+  int reserved[7];
 } naz_cnf_desc;
+#define NAZ_CNF_F32 0
+#define NAZ_CNF_F16X3 1
 int naz_cnf_supported(const naz_cnf_desc* d);
 int64_t naz_cnf_param_count(const naz_cnf_desc* d);
 int64_t naz_cnf_packed_bytes(const naz_cnf_desc* d);

@@ -27,7 +27,7 @@ class CouplingDesc(C.Structure):
 
 class CnfDesc(C.Structure):
     _fields_ = [("D", C.c_int), ("C", C.c_int), ("n_hidden", C.c_int), ("H", C.c_int * 4), ("act", C.c_int),
-                ("reserved", C.c_int * 8)]
+                ("mfma_mode", C.c_int), ("reserved", C.c_int * 7)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/naz_hip.h

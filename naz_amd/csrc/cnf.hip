@@ -31,8 +31,77 @@
 namespace naz {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef _Float16 cnf_half8 __attribute__((ext_vector_type(8)));
+typedef unsigned int cnf_u32x4 __attribute__((ext_vector_type(4)));
 
 NAZ_DEV floatx4 mfma16(float a, float b, floatx4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// ---- fp16x3 (NAZ_CNF_F16X3): W = Wh + Wl (round-to-nearest pieces, packed), v = vh + vl
+// (round-to-nearest pieces, exact residual, on the fly), W·v ≈ Wl·vh + Wh·vl + Wh·vh on
+// v_mfma_f32_16x16x32_f16 — fp32-grade products at 3 × 16 cycles per 16x16x32 block instead of
+// 8 × 32 cycles of v_mfma_f32_16x16x4_f32.  Activations/tangents whose wave maximum reaches
+// kCnfF16Limit are scaled by an exact power of two around the GEMM (rare path).
+struct CnfFrag2 {
+  cnf_half8 h, l;
+};
+
+NAZ_DEV floatx4 mfma16h(cnf_half8 a, cnf_half8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+NAZ_DEV floatx4 mfma16x3(const CnfFrag2& a, const CnfFrag2& b, floatx4 acc) {
+  acc = mfma16h(a.l, b.h, acc);
+  acc = mfma16h(a.h, b.l, acc);
+  acc = mfma16h(a.h, b.h, acc);
+  return acc;
+}
+
+template <bool HI>
+NAZ_DEV float cnf_sub_piece(float v, unsigned hp) {
+  float r;
+  if constexpr (HI)
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(v));
+  else
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(v));
+  return r;
+}
+
+typedef _Float16 cnf_half2 __attribute__((ext_vector_type(2)));
+
+// two floats -> packed fp16 pair, round-to-nearest-even (one v_cvt_pk_f16_f32 on gfx950).  The
+// activation/tangent split rounds to nearest on both pieces: the trace estimate accumulates
+// products over the whole solve, and round-toward-zero pieces bias it (measured: ld error
+// median 3.8e-6 with RTZ pieces on a [32, 32] field).
+NAZ_DEV unsigned cnf_pack2(float a, float b) {
+  const cnf_half2 h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+
+NAZ_DEV CnfFrag2 cnf_split8(const float (&v)[8]) {
+  cnf_u32x4 H, Lo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const unsigned hp = cnf_pack2(v[2 * q], v[2 * q + 1]);
+    const float r0 = cnf_sub_piece<false>(v[2 * q], hp), r1 = cnf_sub_piece<true>(v[2 * q + 1], hp);
+    H[q] = hp;
+    Lo[q] = cnf_pack2(r0, r1);
+  }
+  return CnfFrag2{__builtin_bit_cast(cnf_half8, H), __builtin_bit_cast(cnf_half8, Lo)};
+}
+
+// fp16 piece of a weight (0 = round-to-nearest hi, 1 = lo = fp16(W - hi))
+NAZ_DEV unsigned cnf_f16_piece(float v, int piece) {
+  const _Float16 hi = (_Float16)v;
+  if (piece == 0) return (unsigned)__builtin_bit_cast(unsigned short, hi);
+  const _Float16 lo = (_Float16)(v - (float)hi);
+  return (unsigned)__builtin_bit_cast(unsigned short, lo);
+}
+
+// input feature carried by k-slot 8q + j of 32-k step t: the lane's own accumulator registers
+// of blocks 2t, 2t + 1 (16x16 C layout: register i of block b on quarter q = feature 16b+4q+i)
+__host__ __device__ constexpr int cnf_feat32(int t, int q, int j) { return 32 * t + 16 * (j >> 2) + 4 * q + (j & 3); }
+
+constexpr float kCnfF16Limit = 16384.f;
 
 constexpr int cnf_up(int v, int m) { return (v + m - 1) / m * m; }
 constexpr int cnf_max(int a, int b) { return a > b ? a : b; }
@@ -100,11 +169,26 @@ NAZ_DEV void cnf_static_for(F&& f) {
 // ---------------------------------------------------------------------------
 // Packing: natural flat parameters -> the LDS image (one thread per image float)
 // ---------------------------------------------------------------------------
-template <class CF>
+template <class CF, bool X3>
 __global__ void cnf_pack_kernel(const float* __restrict__ flat, float* __restrict__ img) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= CF::TOTAL) return;
   float v = 0.f;
+  // f16x3 word of a weight chunk [ob][t][piece][lane][pair]: rows via row_of(ob, lane & 15),
+  // columns cnf_feat32(t, lane >> 4, j) of the layer's [rows, hin] weight at flat offset fo
+  auto x3_word = [&](int r, int nbi, int64_t fo, int hin, auto row_of) -> unsigned {
+    const int u = r & 255, chunk = r >> 8;
+    const int piece = chunk & 1, rest = chunk >> 1, t = rest % (nbi / 2), ob = rest / (nbi / 2);
+    const int lane = u >> 2, pair = u & 3;
+    const int orow = row_of(ob, lane & 15);
+    unsigned out = 0;
+    for (int e2 = 0; e2 < 2; ++e2) {
+      const int jj = 2 * pair + e2;
+      const float w = orow >= 0 ? flat[fo + (int64_t)orow * hin + cnf_feat32(t, lane >> 4, jj)] : 0.f;
+      out |= cnf_f16_piece(w, piece) << (16 * e2);
+    }
+    return out;
+  };
   // layer 0 weights: [ob][s4][lane][i], k-step s = 4 s4 + i carries x feature q + 4s (s < XS)
   // or context feature q + 4(s - XS) (XS <= s < XS + CS), q = lane >> 4
   constexpr int OB0 = CF::off_b(0);
@@ -124,7 +208,7 @@ __global__ void cnf_pack_kernel(const float* __restrict__ flat, float* __restric
     img[e] = v;
     return;
   }
-  bool done = false;
+  bool done = false, word = false;
   cnf_static_for<0, CF::NH>([&](auto J) {
     constexpr int j = decltype(J)::value;
     if (done) return;
@@ -134,6 +218,11 @@ __global__ void cnf_pack_kernel(const float* __restrict__ flat, float* __restric
     constexpr int64_t fo = CF::flat_off_w(j);
     if (j > 0 && e >= ow_ && e < ob_) {
       const int r = e - ow_;
+      if constexpr (X3) {
+        reinterpret_cast<unsigned*>(img)[e] = x3_word(r, nbi, fo, hin, [](int ob, int rl) { return 16 * ob + rl; });
+        done = word = true;
+        return;
+      }
       const int i = r & 3, lane = (r >> 2) & 63, rest = r >> 8;
       const int b = rest % nbi, ob = rest / nbi;
       const int o = 16 * ob + (lane & 15), k = 16 * b + 4 * (lane >> 4) + i;
@@ -144,9 +233,17 @@ __global__ void cnf_pack_kernel(const float* __restrict__ flat, float* __restric
       done = true;
     }
   });
+  if (word) return;
   if (!done) {
     constexpr int HL = CF::HL;
     constexpr int64_t fw = CF::flat_off_w(CF::NH);
+    if (X3 && e >= CF::OFF_WL && e < CF::OFF_BL) {
+      reinterpret_cast<unsigned*>(img)[e] = x3_word(e - CF::OFF_WL, HL / 16, fw, HL, [](int ob, int rl) {
+        const int nf = (rl >> 2) + 4 * (4 * ob + (rl & 3));
+        return nf < CF::D ? nf : -1;
+      });
+      return;
+    }
     if (e < CF::OFF_BL) {  // output layer: packed row r_local = lane & 15 <-> state feature q_r + 4(4 ob + i_r)
       const int r = e - CF::OFF_WL;
       const int i = r & 3, lane = (r >> 2) & 63, rest = r >> 8;
@@ -256,8 +353,86 @@ NAZ_DEV void cnf_linear(const float* __restrict__ W, const floatx4 (&iv)[8], con
   }
 }
 
+// the same Linear on the fp16x3 path: W chunks [NBO][NBI/2][piece][64 lanes][16 B]
+template <int NBI, int NBO>
+NAZ_DEV void cnf_linear_x3(const float* __restrict__ W, floatx4 (&iv)[8], floatx4 (&it)[8], floatx4 (&ov)[8],
+                           floatx4 (&ot)[8], int lane) {
+  // Exponent management for the fp16 pieces (exact powers of two, undone on the outputs):
+  //   * tangents, per batch row (= MFMA column, the 4 lanes l & 15 of that row): scaled so the
+  //     row's largest tangent lands in [2^14, 2^15).  Tangents span many decades and fp16's lo
+  //     piece goes subnormal below 2^-14 (absolute step 2^-24), which would cap their relative
+  //     precision; with the scaling every tangent within 2^-11 of its row maximum keeps ~22 bits;
+  //   * activations, per batch row, only in waves where one reaches kCnfF16Limit (rare; bias
+  //     pre-scaled).
+  float mv = 0.f, mt = 0.f;
+#pragma unroll
+  for (int b = 0; b < NBI; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      mv = fmaxf(mv, fabsf(iv[b][i]));
+      mt = fmaxf(mt, fabsf(it[b][i]));
+    }
+  mt = fmaxf(mt, __shfl_xor(mt, 16));
+  mt = fmaxf(mt, __shfl_xor(mt, 32));
+  int et = mt > 0.f ? 14 - ilogbf(mt) : 0;  // scaled row maximum in [2^14, 2^15)
+  et = et > 100 ? 100 : (et < -100 ? -100 : et);
+  const float st = ldexpf(1.f, et);
+#pragma unroll
+  for (int b = 0; b < NBI; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) it[b][i] *= st;
+  float sv = 1.f;
+  const bool scaled = __builtin_amdgcn_ballot_w64(mv >= kCnfF16Limit) != 0;
+  if (scaled) {  // per batch row, like the tangents (bias in the row's own accumulators)
+    mv = fmaxf(mv, __shfl_xor(mv, 16));
+    mv = fmaxf(mv, __shfl_xor(mv, 32));
+    const int ev = mv >= kCnfF16Limit ? (mv > 1e30f ? 100 : ilogbf(mv) - 13) : 0;
+    sv = ldexpf(1.f, -ev);
+#pragma unroll
+    for (int b = 0; b < NBI; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) iv[b][i] *= sv;
+#pragma unroll
+    for (int ob = 0; ob < NBO; ++ob) ov[ob] *= sv;
+  }
+  const cnf_u32x4* c4 = reinterpret_cast<const cnf_u32x4*>(W);
+#pragma unroll
+  for (int t = 0; t < NBI / 2; ++t) {
+    float v[8], tv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = iv[2 * t + (j >> 2)][j & 3];
+      tv[j] = it[2 * t + (j >> 2)][j & 3];
+    }
+    const CnfFrag2 bv = cnf_split8(v), bt = cnf_split8(tv);
+#pragma unroll
+    for (int ob = 0; ob < NBO; ++ob) {
+      const int base = ((ob * (NBI / 2) + t) * 2) * 64 + lane;
+      const CnfFrag2 a{__builtin_bit_cast(cnf_half8, c4[base]), __builtin_bit_cast(cnf_half8, c4[base + 64])};
+      ov[ob] = mfma16x3(a, bv, ov[ob]);
+      ot[ob] = mfma16x3(a, bt, ot[ob]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one k-step's fragment reads at a time (register budget)
+  }
+  const float it_ = ldexpf(1.f, -et);  // exact inverse scalings
+#pragma unroll
+  for (int ob = 0; ob < NBO; ++ob) ot[ob] *= it_;
+  if (scaled) {
+    const float iv_ = 1.f / sv;
+#pragma unroll
+    for (int ob = 0; ob < NBO; ++ob) ov[ob] *= iv_;
+  }
+}
+
+template <bool X3, int NBI, int NBO>
+NAZ_DEV void cnf_lin(const float* __restrict__ W, floatx4 (&iv)[8], floatx4 (&it)[8], floatx4 (&ov)[8],
+                     floatx4 (&ot)[8], int lane) {
+  if constexpr (X3) cnf_linear_x3<NBI, NBO>(W, iv, it, ov, ot, lane);
+  else cnf_linear<NBI, NBO>(W, iv, it, ov, ot, lane);
+}
+
 // f(x) in the state layout and g = -eps^T (df/dx) eps (row total on every lane of the row)
-template <class CF>
+template <class CF, bool X3>
 NAZ_DEV void cnf_rhs(const float* __restrict__ lds, const float (&xin)[CF::XS], const float (&e)[CF::XS],
                      const float (&c)[CF::CS > 0 ? CF::CS : 1], float (&f)[CF::XS], float& g, int lane) {
   const int q = lane >> 4;
@@ -291,11 +466,11 @@ NAZ_DEV void cnf_rhs(const float* __restrict__ lds, const float (&xin)[CF::XS], 
     constexpr int NBI = CF::NB(j - 1), NBO = CF::NB(j), OW = CF::off_w(j), OB = CF::off_b(j);
     if constexpr (j % 2 == 1) {
       init_bias4<NBO>(bv, bt, lds + OB, q);
-      cnf_linear<NBI, NBO>(lds + OW, av, at, bv, bt, lane);
+      cnf_lin<X3, NBI, NBO>(lds + OW, av, at, bv, bt, lane);
       act_all<CF::ACT, NBO>(bv, bt);
     } else {
       init_bias4<NBO>(av, at, lds + OB, q);
-      cnf_linear<NBI, NBO>(lds + OW, bv, bt, av, at, lane);
+      cnf_lin<X3, NBI, NBO>(lds + OW, bv, bt, av, at, lane);
       act_all<CF::ACT, NBO>(av, at);
     }
   });
@@ -304,9 +479,9 @@ NAZ_DEV void cnf_rhs(const float* __restrict__ lds, const float (&xin)[CF::XS], 
   floatx4 ov[8], ot[8];
   init_bias4<CF::NBL>(ov, ot, lds + CF::OFF_BL, q);
   if constexpr ((CF::NH - 1) % 2 == 0)
-    cnf_linear<NBI, CF::NBL>(lds + CF::OFF_WL, av, at, ov, ot, lane);
+    cnf_lin<X3, NBI, CF::NBL>(lds + CF::OFF_WL, av, at, ov, ot, lane);
   else
-    cnf_linear<NBI, CF::NBL>(lds + CF::OFF_WL, bv, bt, ov, ot, lane);
+    cnf_lin<X3, NBI, CF::NBL>(lds + CF::OFF_WL, bv, bt, ov, ot, lane);
   float tr = 0.f;
 #pragma unroll
   for (int s = 0; s < CF::XS; ++s) {
@@ -318,7 +493,7 @@ NAZ_DEV void cnf_rhs(const float* __restrict__ lds, const float (&xin)[CF::XS], 
   g = -tr;
 }
 
-template <class CF>
+template <class CF, bool X3>
 __global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_kernel(
     const float* __restrict__ packed, const float* __restrict__ x, int64_t ldx, const float* __restrict__ ctx,
     int64_t ldc, const float* __restrict__ eps, int64_t lde, float dt, int steps, float* __restrict__ y,
@@ -356,7 +531,7 @@ __global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_kernel(
     for (int it = 0; it < 4 * steps; ++it) {
       const int stage = it & 3;
       float g;
-      cnf_rhs<CF>(lds, xst, es, cs, f, g, lane);
+      cnf_rhs<CF, X3>(lds, xst, es, cs, f, g, lane);
       const float kg = dt * g;
       if (stage == 3) {
 #pragma unroll
@@ -397,14 +572,24 @@ __global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_kernel(
 // ---------------------------------------------------------------------------
 template <class CF>
 struct CnfOps {
+  // fp16x3 needs every hidden width (the GEMM k of the hidden and output layers) in 32-k steps
+  static constexpr bool kX3 = CF::NB(0) % 2 == 0 && CF::NB(CF::NH - 1) % 2 == 0 &&
+                              (CF::NH < 2 || CF::NB(1) % 2 == 0) && (CF::NH < 3 || CF::NB(2) % 2 == 0);
+  static bool supports(int mode) { return mode == NAZ_CNF_F32 || (mode == NAZ_CNF_F16X3 && kX3); }
   static int64_t packed_bytes() { return (int64_t)CF::TOTAL * 4; }
-  static int pack(const float* flat, void* packed, hipStream_t s) {
-    hipLaunchKernelGGL((cnf_pack_kernel<CF>), dim3((CF::TOTAL + 255) / 256), dim3(256), 0, s, flat,
-                       static_cast<float*>(packed));
+  static int pack(const float* flat, void* packed, int mode, hipStream_t s) {
+    if (mode == NAZ_CNF_F16X3) {
+      if constexpr (kX3)
+        hipLaunchKernelGGL((cnf_pack_kernel<CF, true>), dim3((CF::TOTAL + 255) / 256), dim3(256), 0, s, flat,
+                           static_cast<float*>(packed));
+    } else {
+      hipLaunchKernelGGL((cnf_pack_kernel<CF, false>), dim3((CF::TOTAL + 255) / 256), dim3(256), 0, s, flat,
+                         static_cast<float*>(packed));
+    }
     return check_launch("cnf_pack_kernel");
   }
   static int run(const void* packed, const float* x, int64_t ldx, const float* ctx, int64_t ldc, const float* eps,
-                 int64_t lde, float dt, int steps, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
+                 int64_t lde, float dt, int steps, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B, int mode,
                  hipStream_t s) {
     const int64_t tiles = (B + kCnfRows - 1) / kCnfRows;
     int dev = 0, cus = 256;
@@ -413,9 +598,16 @@ struct CnfOps {
       cus = 256;
     const int per_cu = (160 * 1024) / (CF::TOTAL * 4) >= 2 ? 2 : 1;
     const int64_t grid = tiles < (int64_t)cus * per_cu ? tiles : (int64_t)cus * per_cu;
-    hipLaunchKernelGGL((cnf_kernel<CF>), dim3((unsigned)grid), dim3(kCnfRows * 4), 0, s,
-                       static_cast<const float*>(packed), x, ldx, ctx, ldc, eps, lde, dt, steps, y, ldy, ld, ld_mode,
-                       B);
+    if (mode == NAZ_CNF_F16X3) {
+      if constexpr (kX3)
+        hipLaunchKernelGGL((cnf_kernel<CF, true>), dim3((unsigned)grid), dim3(kCnfRows * 4), 0, s,
+                           static_cast<const float*>(packed), x, ldx, ctx, ldc, eps, lde, dt, steps, y, ldy, ld,
+                           ld_mode, B);
+    } else {
+      hipLaunchKernelGGL((cnf_kernel<CF, false>), dim3((unsigned)grid), dim3(kCnfRows * 4), 0, s,
+                         static_cast<const float*>(packed), x, ldx, ctx, ldc, eps, lde, dt, steps, y, ldy, ld,
+                         ld_mode, B);
+    }
     return check_launch("cnf_kernel");
   }
 };
@@ -439,8 +631,12 @@ static int cnf_dispatch(const naz_cnf_desc* d, F&& f) {
   if (d->n_hidden < 1 || d->n_hidden > 4) return set_error("naz_cnf: n_hidden must be 1..4");
   for (int j = 0; j < d->n_hidden; ++j) H[j] = d->H[j];
 #define NAZ_CNF_CASE(D_, C_, H0, H1, H2, H3, A_)                                                              \
-  if (d->D == D_ && d->C == C_ && H[0] == H0 && H[1] == H1 && H[2] == H2 && H[3] == H3 && d->act == A_) \
-    return f(CnfOps<CnfCfg<D_, C_, H0, H1, H2, H3, A_>>{});
+  if (d->D == D_ && d->C == C_ && H[0] == H0 && H[1] == H1 && H[2] == H2 && H[3] == H3 && d->act == A_) {  \
+    using Ops = CnfOps<CnfCfg<D_, C_, H0, H1, H2, H3, A_>>;                                               \
+    if (!Ops::supports(d->mfma_mode))                                                                     \
+      return set_error("naz_cnf: mfma_mode %d is not available for this shape", d->mfma_mode);           \
+    return f(Ops{});                                                                                      \
+  }
   NAZ_CNF_CONFIGS(NAZ_CNF_CASE)
 #undef NAZ_CNF_CASE
   return set_error("naz_cnf: shape D=%d C=%d H=[%d,%d,%d,%d] act=%d is not instantiated (NAZ_CNF_CONFIGS)", d->D,
@@ -473,7 +669,7 @@ int64_t cnf_packed_bytes(const naz_cnf_desc* d) {
 }
 
 int cnf_pack(const naz_cnf_desc* d, const float* flat, void* packed, hipStream_t s) {
-  return cnf_dispatch(d, [&](auto ops) { return decltype(ops)::pack(flat, packed, s); });
+  return cnf_dispatch(d, [&](auto ops) { return decltype(ops)::pack(flat, packed, d->mfma_mode, s); });
 }
 
 int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
@@ -484,7 +680,8 @@ int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int
   // odeint.py:15-16: dt = t1 - t0 of consecutive grid points (a single value for a uniform grid)
   const float dt = (float)(((double)t1 - (double)t0) / (double)steps);
   return cnf_dispatch(d, [&](auto ops) {
-    return decltype(ops)::run(packed, x, ldx, ctx, ldc, eps, lde, dt, steps, y, ldy, ld, ld_mode, B, s);
+    return decltype(ops)::run(packed, x, ldx, ctx, ldc, eps, lde, dt, steps, y, ldy, ld, ld_mode, B, d->mfma_mode,
+                              s);
   });
 }
 

@@ -66,20 +66,44 @@ class FCNN(ConditionalFCNN):
 
 
 class _CnfPlan:
-    """The block's packed LDS image, re-packed when a parameter changes (version counters)."""
+    """The block's packed LDS image, re-packed when a parameter changes (version counters).
 
-    def __init__(self, net: ConditionalFCNN):
+    ``mfma``: "auto" (default: "f16x3" when the shape allows it and every hidden/output weight
+    fits fp16's range with margin, |W| < 2^15; else "f32"), "f16x3" or "f32"."""
+
+    F16_WEIGHT_LIMIT = 32768.0
+
+    def __init__(self, net: ConditionalFCNN, mfma: str = "auto"):
         self.net = net
+        self.mfma = mfma
+        self.mode = None
         self.desc = ops.cnf_desc(net.input_dim, net.context_dim, net.hidden_dims, net.act)
         if not ops.cnf_supported(self.desc):
             from .._lib import lib
             raise NotImplementedError(f"naz_amd CNF: {lib().naz_last_error().decode()}")
         self._sig, self._packed = None, None
 
+    def set_mfma(self, mfma: str) -> None:
+        self.mfma = mfma
+        self._sig, self._packed = None, None
+
+    def _resolve_mode(self) -> str:
+        if self.mfma != "auto":
+            return self.mfma
+        x3 = ops.cnf_desc(self.net.input_dim, self.net.context_dim, self.net.hidden_dims, self.net.act, "f16x3")
+        if not ops.cnf_supported(x3):
+            return "f32"
+        lins = self.net.linears()
+        big = max(float(lin.weight.detach().abs().max()) for lin in lins[1:])
+        return "f16x3" if big < self.F16_WEIGHT_LIMIT else "f32"
+
     def packed(self):
         ps = [t for lin in self.net.linears() for t in (lin.weight, lin.bias)]
         sig = tuple((p.data_ptr(), p._version) for p in ps)
         if sig != self._sig or self._packed is None:
+            self.mode = self._resolve_mode()
+            n = self.net
+            self.desc = ops.cnf_desc(n.input_dim, n.context_dim, n.hidden_dims, n.act, self.mode)
             flat = torch.cat([p.detach().reshape(-1) for p in ps])
             self._packed = ops.cnf_pack(self.desc, flat, self._packed)
             self._sig = sig
@@ -94,7 +118,8 @@ class _FFJORDCore:
             raise NotImplementedError("naz_amd CNF: differentiating through the ODE solve (adjoint) is SURVEY.md "
                                       "§8f rank 3; evaluate under torch.no_grad()")
         noise = self.noise if self.noise is not None else torch.randn(v.shape, device=v.device, dtype=torch.float32)
-        y, ld = ops.cnf_integrate(self._plan.desc, self._plan.packed(), v, noise, t0, t1, self.steps,
+        packed = self._plan.packed()  # may re-resolve the mode: read desc only after it
+        y, ld = ops.cnf_integrate(self._plan.desc, packed, v, noise, t0, t1, self.steps,
                                   context=self._context, ld_out=ld_buf, ld_mode=ld_mode)
         return y, ld
 

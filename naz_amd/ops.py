@@ -389,7 +389,10 @@ def coupling_sample(d: CouplingDesc, packed: Tensor, z: Tensor, context: Optiona
 
 
 # ----------------------------------------------------------------------------- a11 CNF
-def cnf_desc(D: int, C: int, hidden, act: str = "softplus") -> CnfDesc:
+def cnf_desc(D: int, C: int, hidden, act: str = "softplus", mfma: str = "f32") -> CnfDesc:
+    """``mfma``: "f32" (exact FP32 MFMA throughout) or "f16x3" (layer 0 exact FP32; hidden and
+    output layers as three exact-split fp16 products; hidden widths multiples of 32, packed
+    |W| < 2^15 — the caller checks)."""
     hidden = list(hidden)
     if not 1 <= len(hidden) <= 4:
         raise ValueError("naz_amd CNF: 1 to 4 hidden layers")
@@ -398,6 +401,7 @@ def cnf_desc(D: int, C: int, hidden, act: str = "softplus") -> CnfDesc:
     for j, h in enumerate(hidden):
         d.H[j] = int(h)
     d.act = ACT.get(act, -1)
+    d.mfma_mode = {"f32": 0, "f16x3": 1}[mfma]
     return d
 
 

@@ -568,14 +568,25 @@ NAZ_DEV float sub_f16_piece(float v, unsigned hp) {
   return r;
 }
 
+#ifdef NAZ_SPLIT_RTZ
+NAZ_DEV unsigned pack_f16x2(float a, float b) { return __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(a, b)); }
+#else
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+// round-to-nearest-even pair (one v_cvt_pk_f16_f32 on gfx950, same cost as the RTZ form)
+NAZ_DEV unsigned pack_f16x2(float a, float b) {
+  const half2v h = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+#endif
+
 NAZ_DEV Frag2 split8_f16(const float (&v)[8]) {
   u32x4 H, Lo;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const unsigned hp = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(v[2 * q], v[2 * q + 1]));
+    const unsigned hp = pack_f16x2(v[2 * q], v[2 * q + 1]);
     const float r0 = sub_f16_piece<false>(v[2 * q], hp), r1 = sub_f16_piece<true>(v[2 * q + 1], hp);
     H[q] = hp;
-    Lo[q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(r0, r1));
+    Lo[q] = pack_f16x2(r0, r1);
   }
   return Frag2{__builtin_bit_cast(half8, H), __builtin_bit_cast(half8, Lo)};
 }

@@ -15,6 +15,11 @@
 #include "naz_internal.h"
 #include "spline_bwd.h"
 
+// backward of the training walk on the hardware transcendentals (spline_bwd.h FAST)
+#ifndef NAZ_RQS_BWD_FAST
+#define NAZ_RQS_BWD_FAST true
+#endif
+
 namespace naz {
 
 // Copy `n` floats starting at src[0] into lds[0..n) with 16-B loads where aligned.
@@ -188,7 +193,7 @@ __global__ void __launch_bounds__(256) rqs_bwd_kernel(
     const float go = g_out != nullptr ? g_out[row * ldgo + i] : 0.f;
     const float gl = g_ld_mode == 1 ? g_ld[row] : (g_ld_mode == 2 ? g_ld[row * Dt + i] : 0.f);
     float gw[K], gh[K], gd[K - 1];
-    const float gi = rqs_vjp<K, INV>(uw, uh, ud, bound, x[row * ldx + i], go, gl, gw, gh, gd);
+    const float gi = rqs_vjp<K, INV, NAZ_RQS_BWD_FAST>(uw, uh, ud, bound, x[row * ldx + i], go, gl, gw, gh, gd);
     if (g_in != nullptr) g_in[row * ldgi + i] = gi;
     float* dst = BCAST ? gr_s + (size_t)r * P : g_raw + row * ldgr;
 #pragma unroll

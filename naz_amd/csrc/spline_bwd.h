@@ -17,10 +17,13 @@ namespace naz {
 // Returns dL/d(input); accumulates nothing else — writes dL/d(unnormalised params) into
 // gw[K], gh[K], gd[K-1].  g_out: upstream gradient on the map's output; g_ld: upstream gradient on
 // the log-det the kernel returns for this direction (forward ld, or the inverse map's ld).
-template <int K, bool INV>
+// FAST: hardware transcendentals / reciprocals (Math<true>) and fp32 knot prefix sums (the
+// training walk's backward, where gradients are compared statistically, not bitwise).
+template <int K, bool INV, bool FAST = false>
 NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float bound, float v, float g_out,
                       float g_ld, float* gw, float* gh, float* gd) {
-  using M = Math<false>;
+  using M = Math<FAST>;
+  auto rcp = [](float b) { return FAST ? Math<true>::rcp(b) : 1.f / b; };
 #pragma unroll
   for (int k = 0; k < K; ++k) { gw[k] = 0.f; gh[k] = 0.f; }
 #pragma unroll
@@ -28,15 +31,31 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
   if (!(v >= -bound && v <= bound)) return g_out;  // identity tails
 
   float fw[K], fh[K];
-  softmax_k<K>(uw, fw);
-  softmax_k<K>(uh, fh);
+  softmax_k<K, FAST>(uw, fw);
+  softmax_k<K, FAST>(uh, fh);
   SplineTables<K> t;
-  knots_from_fractions<K>(fw, kMinBinWidth, bound, t.cw);
-  knots_from_fractions<K>(fh, kMinBinHeight, bound, t.ch);
+  if constexpr (FAST) {
+    auto knots32 = [&](const float* frac, float minw, float* knots) {
+      const float scale = 1.f - minw * (float)K, two_b = 2.f * bound;
+      float acc = 0.f;
+      knots[0] = -bound;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        acc += minw + scale * frac[k];
+        knots[k + 1] = two_b * acc - bound;
+      }
+      knots[K] = bound;
+    };
+    knots32(fw, kMinBinWidth, t.cw);
+    knots32(fh, kMinBinHeight, t.ch);
+  } else {
+    knots_from_fractions<K>(fw, kMinBinWidth, bound, t.cw);
+    knots_from_fractions<K>(fh, kMinBinHeight, bound, t.ch);
+  }
   t.dv[0] = 1.f - kMinDerivative;
   t.dv[K] = 1.f - kMinDerivative;
 #pragma unroll
-  for (int k = 0; k < K - 1; ++k) t.dv[k + 1] = kMinDerivative + softplus(ud[k]);
+  for (int k = 0; k < K - 1; ++k) t.dv[k + 1] = kMinDerivative + softplus<FAST>(ud[k]);
 
   int cnt = 0;
 #pragma unroll
@@ -54,7 +73,7 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
     d0 = s ? t.dv[k] : d0;
     d1 = s ? t.dv[k + 1] : d1;
   }
-  const float W = cw1 - cw0, H = ch1 - ch0, delta = H / W;
+  const float W = cw1 - cw0, H = ch1 - ch0, iW = rcp(W), delta = H * iW;
   const float T1 = (d0 + d1) - 2.f * delta;
   float th;
   if constexpr (INV) {
@@ -62,15 +81,15 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
     const float a = dy * T1 + H * (delta - d0);
     const float b = H * d0 - dy * T1;
     const float c = -delta * dy;
-    th = (2.f * c) / (-b - M::sqrt(b * b - 4.f * a * c));
+    th = (2.f * c) * rcp(-b - M::sqrt(b * b - 4.f * a * c));
   } else {
-    th = (v - cw0) / W;
+    th = (v - cw0) * iW;
   }
   const float om = 1.f - th, tt = th * om;
   const float N = delta * th * th + d0 * tt;
   const float Dn = delta + T1 * tt;
   const float G = d1 * th * th + 2.f * delta * tt + d0 * om * om;
-  const float iDn = 1.f / Dn, iG = 1.f / G;
+  const float iDn = rcp(Dn), iG = rcp(G);
   // dF/dθ and the other partials of F and ldf
   const float Np = 2.f * delta * th + d0 * (1.f - 2.f * th);
   const float Dp = T1 * (1.f - 2.f * th);
@@ -81,7 +100,7 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
   const float F_d1 = -H * N * tt * iDn * iDn;
   const float Gp = 2.f * d1 * th + 2.f * delta * (1.f - 2.f * th) - 2.f * d0 * om;
   const float L_th = Gp * iG - 2.f * Dp * iDn;
-  const float L_dl = 2.f / delta + 2.f * tt * iG - 2.f * (1.f - 2.f * tt) * iDn;
+  const float L_dl = 2.f * rcp(delta) + 2.f * tt * iG - 2.f * (1.f - 2.f * tt) * iDn;
   const float L_d0 = om * om * iG - 2.f * tt * iDn;
   const float L_d1 = th * th * iG - 2.f * tt * iDn;
 
@@ -93,9 +112,9 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
     gdl = g_out * F_dl + g_ld * L_dl;
     gd0 = g_out * F_d0 + g_ld * L_d0;
     gd1 = g_out * F_d1 + g_ld * L_d1;
-    g_in = gth / W;
-    gcw0 = -gth / W;
-    gW = -gth * th / W;
+    g_in = gth * iW;
+    gcw0 = -gth * iW;
+    gW = -gth * th * iW;
   } else {
     // outputs x = cw0 + W·θ and ld_inv = −ldf(θ)
     const float gth = g_out * W - g_ld * L_th;
@@ -105,7 +124,7 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
     gd0 = -g_ld * L_d0;
     gd1 = -g_ld * L_d1;
     // implicit θ(y, p): dθ/dy = 1/F_θ, dθ/dp = −F_p/F_θ
-    const float r = gth / F_th;
+    const float r = gth * rcp(F_th);
     g_in = r;
     gch0 = -r;
     gH = -r * F_H;
@@ -114,8 +133,8 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
     gd1 += -r * F_d1;
   }
   // δ = H / W
-  gH += gdl / W;
-  gW += -gdl * delta / W;
+  gH += gdl * iW;
+  gW += -gdl * delta * iW;
   // bin quantities -> knot / slope arrays
   float gcw[K + 1], gch[K + 1], gdv[K + 1];
 #pragma unroll
@@ -150,7 +169,7 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
     gh[i] = fh[i] * (gfh[i] - doth);
   }
 #pragma unroll
-  for (int k = 0; k < K - 1; ++k) gd[k] = gdv[k + 1] / (1.f + M::exp(-ud[k]));  // softplus' = sigmoid
+  for (int k = 0; k < K - 1; ++k) gd[k] = gdv[k + 1] * rcp(1.f + M::exp(-ud[k]));  // softplus' = sigmoid
   return g_in;
 }
 

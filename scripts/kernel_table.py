@@ -11,6 +11,7 @@ def main():
     agg = collections.defaultdict(list)
     for r in rows:
         n = r["Kernel_Name"]
+        n = n.replace("(anonymous namespace)::", "")
         head = n.split("(")[0] if not n.startswith("void") else n[5:].split("(")[0]
         agg[(head[-60:], r["Grid_Size_X"], r["Grid_Size_Y"])].append(
             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)

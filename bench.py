@@ -282,6 +282,85 @@ def run_cnf(args, dev, rank, world, dist):
         dist.destroy_process_group()
 
 
+# --flow: the other §8 rows at the reference's own shapes, through the naz_amd NormalizingFlow API
+# (torch.no_grad, one log_prob call = one step).  (flow_type, D, C, hidden, L, extra args, batch)
+FLOW_CASES = {
+    # BASELINE configs[1]: 8-dim unconditional RQ-spline coupling flow, 6 layers, batch 2^18
+    "config2": ("nsc", 8, 0, [128, 128], 6, (8, 4), 1 << 18,
+                "BASELINE configs[1]: nsc D=8, C=0, K=8, L=6, H=[128,128], split 4 (fused kernel)"),
+    # naz's working MAF at the paper's 2-parameter shape (examples/papers/2506.05657/
+    # train_mle_all_data.py:62-70: D=2, C=2, hidden [150]*3, 16 layers); D-pass inverse per layer
+    "maf": ("maf", 2, 2, [150, 150, 150], 16, (), 1 << 18,
+            "naz maf (SURVEY.md §8a a5/a6) at train_mle_all_data.py:62-70's shape: D=2, C=2, H=[150]*3, L=16"),
+    # naz nsa (ConditionalSplineAutoregressive, D-pass inverse), pinned: D=4, C=2, H=[128,128], K=8, L=8
+    "nsa": ("nsa", 4, 2, [128, 128], 8, (8,), 1 << 18,
+            "naz nsa (SURVEY.md §8a a4/a6): D=4, C=2, K=8, L=8, H=[128,128], D-pass inverse per layer"),
+}
+
+
+def run_flow_case(args, dev, rank, world, dist):
+    from naz_amd.flows import NormalizingFlow
+    ftype, Dd, Cd, hid, Ld, extra, Bdef, desc = FLOW_CASES[args.flow]
+    torch.manual_seed(1234)
+    f = NormalizingFlow(ftype, None, Dd, Cd, hid, Ld, *extra).to(dev)
+    B = args.batch if args.batch != (1 << 20) else Bdef
+    x = torch.as_tensor(gaussian_mixture(B, Dd, seed=rank), device=dev)
+    c = (torch.as_tensor(np.random.default_rng(1 + rank).standard_normal(size=(B, Cd)).astype(np.float32),
+                         device=dev) if Cd else None)
+    # conditioner FLOPs per row: passes per layer (1 for coupling, D for autoregressive inverse)
+    if ftype == "nsc":
+        S = extra[1]
+        dims = [S + Cd] + hid + [(Dd - S) * (3 * extra[0] - 1)]
+        passes = 1
+    else:
+        mult = 2 if ftype == "maf" else 3 * extra[0] - 1
+        dims = [Dd + Cd] + hid + [Dd * mult]
+        passes = Dd
+    fl_row = 2 * passes * Ld * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            f.log_prob(x, condition=c)
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            lp = f.log_prob(x, condition=c)
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        assert bool(torch.isfinite(lp).all())
+    if dist is not None:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+    if rank == 0:
+        step_s = elapsed / args.steps
+        achieved = fl_row * B / step_s / 1e12
+        fused = getattr(f, "fused", False)
+        rec = {
+            "metric": f"samples/sec through log_prob+log|detJ|, naz {ftype} flow (NormalizingFlow API)",
+            "value": B * world / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
+            "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"dp{world} (independent row shards, no collective)",
+                       "path": "fused kernel" if fused else "per-layer HIP kernels (rowgemm + spline/affine)"},
+            "roofline": {"bound": "mfma", "achieved": achieved,
+                         "peak": FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3, "unit": "TFLOP/s",
+                         "frac": achieved / (FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3),
+                         "traffic": None, "kernel": "whole log_prob call", "flop_per_row": fl_row},
+        }
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -295,6 +374,8 @@ def main():
     ap.add_argument("--cnf", action="store_true",
                     help="BASELINE configs[4]: 16-dim FFJORD CNF (H=[128]*3, softplus, Hutchinson trace, RK4 x 8 "
                          "steps) log_prob at 2^18 rows per GPU")
+    ap.add_argument("--flow", choices=sorted(FLOW_CASES), default=None,
+                    help="time log_prob of another §8 flow through the NormalizingFlow API (see FLOW_CASES)")
     ap.add_argument("--mfma", choices=["auto", "f16x3", "f16x3r16", "bf16x6", "f32"], default="auto",
                     help="auto (default): f16x3r16 (16-row waves) when the packed hidden-layer weights fit fp16 and "
                          "the shape allows, else f16x3, else bf16x6; f32: exact FP32 MFMA")
@@ -315,6 +396,8 @@ def main():
         return run_train(args, dev, rank, world, dist)
     if args.cnf:
         return run_cnf(args, dev, rank, world, dist)
+    if args.flow:
+        return run_flow_case(args, dev, rank, world, dist)
 
     flow = build_flow()
     B = args.batch

@@ -58,7 +58,7 @@ struct RowGemmArgs {
   int act;
   int accumulate;
   int vec;  // A segments allow 16-byte loads of 8-k groups (set by rowgemm())
-  int vst;  // C rows allow 16-byte stores (N % 4 == 0, aligned; set by rowgemm())
+  int vst;  // C rows allow 16-byte stores (row stride % 4 == 0, aligned; set by rowgemm())
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -192,12 +192,20 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
         const int64_t m = m0 + wave * 32 + row;
         if (m >= p.M || col >= p.N) continue;
         float4 v = *reinterpret_cast<const float4*>(E + row * EP + 4 * c4);
-        float4* dst = reinterpret_cast<float4*>(p.c + m * p.ldc + col);
-        if (p.accumulate) {
-          const float4 o = *dst;
-          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        if (col + 4 <= p.N) {
+          float4* dst = reinterpret_cast<float4*>(p.c + m * p.ldc + col);
+          if (p.accumulate) {
+            const float4 o = *dst;
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *dst = v;
+        } else {  // row tail (N % 4 != 0): only the real columns (static indices: no scratch)
+          float* d1 = p.c + m * p.ldc + col;
+          const int nt = p.N - col;
+          d1[0] = p.accumulate ? d1[0] + v.x : v.x;
+          if (nt > 1) d1[1] = p.accumulate ? d1[1] + v.y : v.y;
+          if (nt > 2) d1[2] = p.accumulate ? d1[2] + v.z : v.z;
         }
-        *dst = v;
       }
     }
     return;
@@ -235,7 +243,7 @@ int rowgemm(RowGemmArgs p, hipStream_t s) {
     return 1;  // weights too large for the 32-bit buffer offsets: caller falls back
   p.vec = (p.ka0 % 8 == 0) && (p.ka0 == 0 || (al16(p.a0) && p.lda0 % 4 == 0)) &&
           (p.ka1 == 0 || (al16(p.a1) && p.lda1 % 4 == 0));
-  p.vst = p.N % 4 == 0 && p.ldc % 4 == 0 && al16(p.c);
+  p.vst = p.ldc % 4 == 0 && al16(p.c);  // 16-byte row pieces; a ragged row tail is stored per column
   const int nb = (p.N + 31) / 32;
   switch (nb > 8 ? 8 : nb) {
     case 1: rowgemm_launch<1>(p, s); break;

@@ -69,6 +69,19 @@ class MaskedLinear(nn.Linear):
     def forward(self, x):  # pragma: no cover - kept for API completeness; the nets call the fused kernel
         return ops.linear_act(x, self.weight, self.bias, "identity", mask=self.mask)
 
+    def masked_weight(self) -> torch.Tensor:
+        """W ⊙ mask, the weight MaskedLinear applies.  Formed once (a [out, in] tensor) instead of
+        per element inside every GEMM tile; under autograd it is a differentiable torch product,
+        so dW = mask ⊙ dWm exactly as pyro's F.linear(x, mask * W, b).  Cached across the D
+        passes of an autoregressive inverse while the weight is unchanged (version counter)."""
+        if torch.is_grad_enabled() and self.weight.requires_grad:
+            return self.weight * self.mask
+        key = (self.weight.data_ptr(), self.weight._version, self.mask.data_ptr(), self.mask._version)
+        if getattr(self, "_wm_key", None) != key:
+            self._wm = (self.weight * self.mask).detach()
+            self._wm_key = key
+        return self._wm
+
 
 def _slices(param_dims: Sequence[int]):
     ends = torch.cumsum(torch.tensor(param_dims), dim=0)
@@ -85,11 +98,11 @@ def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Ten
     h = None
     for i, layer in enumerate(layers):
         act = f_name if i < n - 1 else "identity"
-        m = layer.mask if masked else None
+        w = layer.masked_weight() if masked else layer.weight
         if i == 0:
-            h = lin(x, layer.weight, layer.bias, act, context=context, mask=m)
+            h = lin(x, w, layer.bias, act, context=context)
         else:
-            h = lin(h, layer.weight, layer.bias, act, mask=m)
+            h = lin(h, w, layer.bias, act)
     return h
 
 

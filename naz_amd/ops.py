@@ -135,7 +135,11 @@ def linear_act(x: Optional[Tensor], weight: Tensor, bias: Optional[Tensor], act:
     if mask is not None:
         mask = mask.to(torch.float32).contiguous()
     if out is None:
-        out = torch.empty((M, N), device=dev, dtype=torch.float32)
+        # rows padded to 16 bytes: the batch-row kernels then use 16-byte loads/stores on this
+        # activation here and in the next layer (the [M, N] view is what callers see)
+        npad = (N + 3) // 4 * 4
+        out = torch.empty((M, npad), device=dev, dtype=torch.float32)[:, :N] if npad != N else \
+            torch.empty((M, N), device=dev, dtype=torch.float32)
     check(lib().naz_linear_act(_p(context), ldc, C, _p(x), ldx, Kx, _p(weight), _p(mask), _p(bias), _p(out),
                                out.stride(0), M, N, ACT[act], _stream(dev)), "linear_act")
     return out

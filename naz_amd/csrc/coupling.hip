@@ -1025,6 +1025,7 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
 
   stage_issue<CF::A_SIZE, kX6Waves>(slot0, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER + a_off);
 
+  const RqsConsts<CF::K, DIR_INV> rc(bound);
   int g = 0;  // global stage counter: stage g lives in slot (g & 1)
   for (int li = 0; li < L; ++li) {
     const int l = DIR_INV ? (L - 1 - li) : li;
@@ -1151,7 +1152,7 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
         ud[k] = acc3[sd >> 4][sd & 15];
       }
       float ld;
-      zu[q] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[q], bound, ld);
+      zu[q] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[q], bound, rc, ld);
       ldsum += DIR_INV ? -ld : ld;
     }
   }

@@ -313,6 +313,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
 
   stage_issue<CF::A_SIZE, kR16Waves>(slot0, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER + a_off);
 
+  const RqsConsts<CF::K, DIR_INV> rc(bound);
   int g = 0;  // global stage counter: stage g lives in slot (g & 1)
   for (int li = 0; li < L; ++li) {
     const int l = DIR_INV ? (L - 1 - li) : li;
@@ -448,7 +449,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
         ud[k] = acc3[sd >> 2][sd & 3];
       }
       float ld;
-      zu[u] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[u], bound, ld);
+      zu[u] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[u], bound, rc, ld);
       ldsum += DIR_INV ? -ld : ld;
     }
   }

@@ -266,6 +266,36 @@ NAZ_DEV float rqs_bin(float x, float cw0, float w, float ch0, float h, float d0,
   }
 }
 
+// A wave-uniform float held in an SGPR: gfx950 has no scalar float ALU, so uniform float
+// constants otherwise occupy one VGPR each for the whole kernel (and were spilled).
+// The empty asm hides how the value was formed, so the combiner cannot push that arithmetic
+// back past the readfirstlane (into a VGPR) nor drop the readfirstlane as a no-op.
+NAZ_DEV float uniform_f(float v) {
+  asm volatile("" : "+v"(v));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+// rqs_select's bound-only constants, formed ONCE per kernel (before the layer loop) and held in
+// SGPRs.  Formed inside the loop, the compiler hoists their VALU part and holds ~K VGPRs.
+template <int K, bool INV>
+struct RqsConsts {
+  float key[K];  // key[k] = 2B·k·m_s − B + eps: interior search knot k without its softmax term
+  float cA;      // 2B·(1 − K·m)
+  float ms, mo;  // 2B·m of the searched / other table
+  float nb;      // −B
+  NAZ_DEV explicit RqsConsts(float bound) {
+    const float two_b = 2.f * bound;
+    ms = uniform_f(two_b * (INV ? kMinBinHeight : kMinBinWidth));
+    mo = uniform_f(two_b * (INV ? kMinBinWidth : kMinBinHeight));
+    cA = uniform_f(two_b * (1.f - kMinBinWidth * (float)K));
+    nb = uniform_f(-bound);
+    key[0] = 0.f;
+#pragma unroll
+    for (int k = 1; k < K; ++k) key[k] = uniform_f(__builtin_fmaf(ms, (float)k, -bound) + kSearchEps);
+  }
+};
+static_assert(kMinBinWidth == kMinBinHeight, "RqsConsts::cA serves both tables");
+
 // Select-first spline for the fused MFMA kernels: the same map as build_tables<K, true> +
 // rqs_apply<K, INV, true> (pyro _monotonic_rational_spline, quadratic), restated so that only
 // the selected bin's quantities are formed:
@@ -277,9 +307,11 @@ NAZ_DEV float rqs_bin(float x, float cw0, float w, float ch0, float h, float d0,
 //   * the other table's two knots and the two knot slopes (softplus) are formed only for that bin.
 // Knot positions agree with the cumsum form to a few ulp (fp32 prefix sums, fused multiply-add);
 // the map is C¹ across knots, so a bin flip at a knot changes y and ld only at rounding level.
-// Out-of-box inputs (|x| > B, NaN) pass through with ld = 0, branch-free.
+// Out-of-box inputs (|x| > B, NaN) pass through with ld = 0, branch-free.  `rc` holds the
+// bound-only constants (RqsConsts, built once per kernel).
 template <int K, bool INV>
-NAZ_DEV float rqs_select(const float* uw, const float* uh, const float* ud, float x, float bound, float& ld) {
+NAZ_DEV float rqs_select(const float* uw, const float* uh, const float* ud, float x, float bound,
+                         const RqsConsts<K, INV>& rc, float& ld) {
   constexpr float kL2E = 1.44269504088896341f;
   float Ew[K + 1], Eh[K + 1];
   {
@@ -298,18 +330,17 @@ NAZ_DEV float rqs_select(const float* uw, const float* uh, const float* ud, floa
       Eh[k + 1] = Eh[k] + __builtin_amdgcn_exp2f(__builtin_fmaf(uh[k], kL2E, -mhl));
     }
   }
-  const float two_b = 2.f * bound;
-  const float Aw = two_b * (1.f - kMinBinWidth * (float)K) * Math<true>::rcp(Ew[K]);
-  const float Ah = two_b * (1.f - kMinBinHeight * (float)K) * Math<true>::rcp(Eh[K]);
+  const float Aw = rc.cA * Math<true>::rcp(Ew[K]);
+  const float Ah = rc.cA * Math<true>::rcp(Eh[K]);
   const float* Es = INV ? Eh : Ew;  // searched table
   const float* Eo = INV ? Ew : Eh;
   const float As = INV ? Ah : Aw, Ao = INV ? Aw : Ah;
-  const float ms = two_b * (INV ? kMinBinHeight : kMinBinWidth), mo = two_b * (INV ? kMinBinWidth : kMinBinHeight);
+  const float ms = rc.ms, mo = rc.mo;
   float s0 = 0.f, s1 = Es[1], o0 = 0.f, o1 = Eo[1], udl = ud[0], udh = ud[0];
   int idx = 0;
 #pragma unroll
   for (int k = 1; k < K; ++k) {
-    const float key = __builtin_fmaf(As, Es[k], __builtin_fmaf(ms, (float)k, -bound) + kSearchEps);
+    const float key = __builtin_fmaf(As, Es[k], rc.key[k]);
     const bool s = x >= key;
     s0 = s ? Es[k] : s0;
     s1 = s ? Es[k + 1] : s1;
@@ -321,10 +352,10 @@ NAZ_DEV float rqs_select(const float* uw, const float* uh, const float* ud, floa
   }
   const bool first = idx == 0, last = idx == K - 1;
   const float fi = (float)idx;
-  const float cs0 = __builtin_fmaf(As, s0, __builtin_fmaf(ms, fi, -bound));
-  const float cs1 = last ? bound : __builtin_fmaf(As, s1, __builtin_fmaf(ms, fi + 1.f, -bound));
-  const float co0 = __builtin_fmaf(Ao, o0, __builtin_fmaf(mo, fi, -bound));
-  const float co1 = last ? bound : __builtin_fmaf(Ao, o1, __builtin_fmaf(mo, fi + 1.f, -bound));
+  const float cs0 = __builtin_fmaf(As, s0, __builtin_fmaf(ms, fi, rc.nb));
+  const float cs1 = last ? bound : __builtin_fmaf(As, s1, __builtin_fmaf(ms, fi + 1.f, rc.nb));
+  const float co0 = __builtin_fmaf(Ao, o0, __builtin_fmaf(mo, fi, rc.nb));
+  const float co1 = last ? bound : __builtin_fmaf(Ao, o1, __builtin_fmaf(mo, fi + 1.f, rc.nb));
   const float d0 = first ? 1.f - kMinDerivative : kMinDerivative + softplus<true>(udl);
   const float d1 = last ? 1.f - kMinDerivative : kMinDerivative + softplus<true>(udh);
   float lb;

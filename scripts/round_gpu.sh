@@ -5,6 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/round
+rm -rf $O/pmc $O/prof $O/prof_cnf
 mkdir -p $O
 step() {  # step <name> <timeout> <cmd...>; stop on crash / timeout
   local name=$1 t=$2; shift 2
@@ -21,4 +22,6 @@ step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc/p2 -o run --output-forma
 step pmc_sq 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc/p3 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step train 300 python bench.py --train --steps 5 --warmup 2
 step cnf 300 python bench.py --cnf --steps 10 --warmup 3
+step prof_cnf 240 rocprofv3 --kernel-trace --stats -d $O/prof_cnf -o run --output-format csv -- python3 bench.py --cnf --steps 10 --warmup 3
+for f in config2 maf nsa; do step flow_$f 240 python bench.py --flow $f --steps 10 --warmup 3; done
 exit 0

@@ -139,6 +139,20 @@ def inverse_bounding_transform(y, low, high):
 
 
 # ----------------------------------------------------------------------------- splines
+def _degree_plan(arn, v, ld_mode):
+    """The MADE net's degree-scheduled inverse (nn.ARInversePlan) when it applies: 2-D batch,
+    a row-sum log-det (each pass adds its own dim's term)."""
+    if ld_mode == ops.LD_PERDIM or v.dim() != 2:
+        return None
+    return arn.inverse_plan()
+
+
+def _pass_ld_mode(ld_mode, k):
+    """Row-sum mode of pass k's single-dim term: an overwriting mode overwrites on pass 1 only."""
+    return ops.LD_ROWSUM if (ld_mode == ops.LD_ROWSUM and k == 1) else (
+        ops.LD_ROWSUM_ADD if ld_mode == ops.LD_ROWSUM else ld_mode)
+
+
 def _zeros_rows(x):
     return torch.zeros(x.shape[:-1], device=x.device, dtype=torch.float32)
 
@@ -341,6 +355,12 @@ class _ConditionedSplineAutoregressive(_LDCache, Transform):
             raw = self.arn.raw(v, self.context)
             y, _ = ops.rqs(v, raw, self.count_bins, ops.LAYOUT_ARN, False, self.bound, ld_mode, ld_buf)
             return y
+        plan = _degree_plan(self.arn, v, ld_mode)
+        if plan is not None:
+            def step(k, i, raw, x):
+                ops.rqs(v[:, i:i + 1], raw, self.count_bins, ops.LAYOUT_ARN, True, self.bound,
+                        _pass_ld_mode(ld_mode, k), ld_buf, out=x[:, i:i + 1])
+            return plan.run(v, self.context, step)
         x = torch.zeros_like(v)
         D = v.shape[-1]
         scratch = _zeros_rows(v)
@@ -440,6 +460,11 @@ class _ConditionedAffineAutoregressive(_LDCache, Transform):
             raw = self.arn.raw(v, self.context)
             y, _ = ops.affine_ar(v, raw, False, ld_mode, ld_buf)
             return y
+        plan = _degree_plan(self.arn, v, ld_mode)
+        if plan is not None:
+            def step(k, i, raw, x):  # naz_affine_ar reports the FORWARD log-det in both directions
+                ops.affine_ar(v[:, i:i + 1], raw, True, _pass_ld_mode(ld_mode, k), ld_buf, out=x[:, i:i + 1])
+            return plan.run(v, self.context, step)
         # pyro loops over the permutation updating one dim per pass; updating every dim per
         # pass gives identical values (masked weights are exact zeros for non-predecessors)
         x = torch.zeros_like(v)
@@ -448,7 +473,6 @@ class _ConditionedAffineAutoregressive(_LDCache, Transform):
         for k in range(D):
             raw = self.arn.raw(x, self.context)
             last = k == D - 1
-            # naz_affine_ar reports the FORWARD log-det in both directions
             x, _ = ops.affine_ar(v, raw, True, ld_mode if last else ops.LD_ROWSUM, ld_buf if last else scratch)
         return x
 

@@ -182,6 +182,19 @@ class ConditionalAutoRegressiveNN(nn.Module):
         self.f = nonlinearity
         self.act = activation_name(nonlinearity)
 
+    # inverse passes run degree-scheduled (ARInversePlan); False = pyro's D full passes
+    degree_schedule = True
+
+    def inverse_plan(self) -> Optional["ARInversePlan"]:
+        """The cached degree-scheduled inverse (None when disabled)."""
+        if not self.degree_schedule:
+            return None
+        plan = self.__dict__.get("_inverse_plan")
+        if plan is None:
+            plan = ARInversePlan(self)
+            self.__dict__["_inverse_plan"] = plan
+        return plan
+
     def get_permutation(self):
         return self.permutation
 
@@ -211,6 +224,139 @@ class ConditionalAutoRegressiveNN(nn.Module):
 
     def forward(self, x, context=None):
         return self._shape(self.raw(x, context), x.shape[:-1])
+
+
+class _InverseBlock:
+    """One GEMM of the degree-scheduled inverse: columns [a, b) of a layer's (padded, degree-sorted)
+    activation from input columns [0, n) of the previous one (layer 0: the full [ctx | x])."""
+
+    __slots__ = ("a", "b", "n", "w", "bias")
+
+    def __init__(self, a, b, n, w, bias):
+        self.a, self.b, self.n, self.w, self.bias = a, b, n, w, bias
+
+
+class ARInversePlan:
+    """Degree-scheduled D-pass inverse of a MADE conditioner (pyro's AffineAutoregressive /
+    SplineAutoregressive ``_inverse``, naz/flows/transforms.py:133-198).
+
+    pyro runs the WHOLE network D times; pass k makes the dim of order k final.  A hidden unit's
+    value depends only on the inputs its masks reach, so a unit whose inputs all have order ≤ m
+    ("degree" m, read off the actual masks) has its final value from pass m + 1 on and never
+    changes afterwards.  Here every unit is computed exactly once, in pass (degree + 1):
+      * each layer's units are sorted by degree into groups, each group padded to a multiple of
+        4 columns (dummy units: zero weights and bias, zero weight in the next layer) so every
+        group is a 16-byte-aligned column slice of the activation buffer;
+      * pass k runs, per layer, the GEMM block [group k−1] × [prev-layer groups ≤ k−1] (masked
+        weights; the block is the non-zero part of that product), then only the output rows of
+        the dim of order k from last-layer groups ≤ k−1, then the elementwise map on that dim.
+    Same values as pyro's loop (the skipped products are exact zeros of the masks); the
+    conditioner work drops from D full networks to about one (triangular) network."""
+
+    def __init__(self, arn: "ConditionalAutoRegressiveNN"):
+        self.arn = arn
+        self._key = None
+
+    def _cache_key(self):
+        return tuple((l.weight.data_ptr(), l.weight._version, l.bias.data_ptr(), l.bias._version,
+                      l.mask.data_ptr(), l.mask._version) for l in self.arn.layers)
+
+    def _build(self):
+        arn = self.arn
+        D, C, mult = arn.input_dim, arn.context_dim, arn.output_multiplier
+        layers = list(arn.layers)
+        if len(layers) < 2:
+            raise ValueError("MADE conditioner without hidden layers")
+        perm = arn.permutation.cpu()
+        order = torch.empty(D, dtype=torch.float64)
+        order[perm] = torch.arange(1, D + 1, dtype=torch.float64)  # var perm[j] has order j + 1
+        prev_deg = torch.cat((torch.zeros(C, dtype=torch.float64), order))
+        prev_cols = None  # previous layer: padded column of each unit (None = natural [ctx | x])
+        prev_ends = None  # previous layer: padded column end of degree groups <= m
+        hidden = [[] for _ in range(D)]  # hidden[m] = blocks of degree m (run in pass m + 1)
+        widths = []
+        dev = layers[0].weight.device
+        for li, layer in enumerate(layers[:-1]):
+            m = layer.mask.detach().to("cpu", torch.float64)
+            deg = (m * prev_deg[None, :]).amax(dim=1)  # max order reached (0: context/bias only)
+            w = layer.masked_weight().detach().to("cpu", torch.float64)
+            bias = layer.bias.detach().to("cpu", torch.float64)
+            cols = torch.empty(layer.out_features, dtype=torch.int64)
+            ends, off = [], 0
+            for g in range(D):
+                units = torch.nonzero(deg == g).flatten()
+                a = off
+                cols[units] = torch.arange(a, a + units.numel())
+                off = a + (units.numel() + 3) // 4 * 4
+                ends.append(off)
+                if units.numel() == 0:
+                    continue
+                if prev_cols is None:
+                    n = C + D
+                    wb = torch.zeros(off - a, n, dtype=torch.float64)
+                    wb[:units.numel()] = w[units]
+                else:
+                    n = prev_ends[g]
+                    wb = torch.zeros(off - a, prev_ends[-1], dtype=torch.float64)
+                    wb[:units.numel(), prev_cols] = w[units]  # inputs scattered to padded columns
+                    wb = wb[:, :n]
+                bb = torch.zeros(off - a, dtype=torch.float64)
+                bb[:units.numel()] = bias[units]
+                hidden[g].append((li, a, off, n, wb, bb))
+            if deg.max() >= D:
+                raise RuntimeError("MADE masks: a hidden unit sees a variable of order D")
+            widths.append(off)
+            prev_deg, prev_cols, prev_ends = deg, cols, ends
+        # output rows of each dim (flat column p*D + i), from last-layer groups < order(i)
+        out = layers[-1]
+        m = out.mask.detach().to("cpu", torch.float64)
+        w = out.masked_weight().detach().to("cpu", torch.float64)
+        bias = out.bias.detach().to("cpu", torch.float64)
+        outs = []
+        for k in range(1, D + 1):
+            i = int(perm[k - 1])
+            rows = torch.tensor([p * D + i for p in range(mult)])
+            if ((m[rows] * prev_deg[None, :]).amax() if m.shape[1] else 0) >= k:
+                raise RuntimeError("MADE masks are not autoregressive in the permutation's order")
+            n = prev_ends[k - 1]
+            full = torch.zeros(mult, prev_ends[-1], dtype=torch.float64)
+            full[:, prev_cols] = w[rows]
+            outs.append((i, n, full[:, :max(n, 1)], bias[rows]))
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.widths = widths
+        self.hidden = [[(li, _InverseBlock(a, b, n, wb.to(**f32).contiguous(), bb.to(**f32)))
+                        for (li, a, b, n, wb, bb) in hidden[g]] for g in range(D)]
+        self.outs = [(i, n, wb.to(**f32).contiguous(), bb.to(**f32).contiguous()) for (i, n, wb, bb) in outs]
+
+    def plan(self):
+        key = self._cache_key()
+        if key != self._key:
+            self._build()
+            self._key = key
+        return self
+
+    def run(self, v: torch.Tensor, context: Optional[torch.Tensor], step) -> torch.Tensor:
+        """x with pass k's dim of order k set by step(k, dim, raw_k [B, mult], x) (raw_k is the
+        conditioner output of that dim only, pyro's column order p)."""
+        self.plan()
+        B, D = v.shape
+        x = torch.zeros_like(v)
+        hs = [torch.empty((B, w), device=v.device, dtype=torch.float32) for w in self.widths]
+        act = self.arn.act
+        for k in range(1, D + 1):
+            for li, blk in self.hidden[k - 1]:
+                dst = hs[li][:, blk.a:blk.b]
+                if li == 0:
+                    ops.linear_act(x, blk.w, blk.bias, act, context=context, out=dst)
+                else:
+                    ops.linear_act(hs[li - 1][:, :blk.n], blk.w, blk.bias, act, out=dst)
+            i, n, wb, bb = self.outs[k - 1]
+            if n:
+                raw = ops.linear_act(hs[-1][:, :n], wb, bb, "identity")
+            else:
+                raw = bb.reshape(1, -1).expand(B, -1)
+            step(k, i, raw, x)
+        return x
 
 
 class AutoRegressiveNN(ConditionalAutoRegressiveNN):

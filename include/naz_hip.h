@@ -156,7 +156,8 @@ typedef struct naz_coupling_desc {
   int act;                /* NAZ_ACT_* */
   int has_lower;          /* 1: lower (unconditional) spline on x1; 0: pyro identity=True */
   float bound;            /* spline box half-width (pyro default 3.0) */
-  int mfma_mode;          /* NAZ_MFMA_BF16X6 (0), NAZ_MFMA_F32 or NAZ_MFMA_F16X3; the packed layout depends on it */
+  int mfma_mode;          /* NAZ_MFMA_BF16X6 (0), NAZ_MFMA_F32, NAZ_MFMA_F16X3 or NAZ_MFMA_F16X3_R16; the packed
+                             layout depends on it (naz_amd's "auto" picks F16X3_R16 when supported)          */
   int reserved[6];
 } naz_coupling_desc;
 

@@ -17,7 +17,8 @@ IFS=';' read -r -a GROUP_LIST <<< "${PMC_GROUPS:-$DEFAULT_GROUPS}"
 for group in "${GROUP_LIST[@]}"; do
   i=$((i+1))
   echo "=== pass $i: $group"
-  timeout -k 10 300 rocprofv3 --pmc $group -d "$OUT/p$i" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
+  # CMD: the profiled program (default: the bench); e.g. CMD="scripts/gemm_bench.py --only fwd2"
+  timeout -k 10 300 rocprofv3 --pmc $group -d "$OUT/p$i" -o run --output-format csv -- python3 ${CMD:-bench.py $ARGS} > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ge 124 ]; then echo "stopping (rc=$rc)"; exit $rc; fi

@@ -68,36 +68,43 @@ def build_flow():
     return f
 
 
-def cpu_baseline(flow, x_host: np.ndarray, c_host: np.ndarray, budget_rows: int = 1 << 19):
+def cpu_baseline(flow, x_host: np.ndarray, c_host, budget_rows: int = 1 << 19, spec=None):
     """The reference's CPU path (the oracle: pure-torch restatement of pyro's eager per-layer
-    semantics, fp32) timed on this host's cores over a bounded sample of the same workload."""
+    semantics, fp32) timed on this host's cores over a bounded sample of the same workload.
+    ``spec`` names the flow (default: the bench's configs[2] nsc flow); ``c_host`` may be None."""
     from naz_amd.flows import io as fio
     from oracle import naz_oracle as O  # baseline + checker only
-    spec = dict(flow_type="nsc", D=D, C=C, hidden=[H, H], L=L, K=K, split=S)
+    if spec is None:
+        spec = dict(flow_type="nsc", D=D, C=C, hidden=[H, H], L=L, K=K, split=S)
     state = fio.export_state(flow)
     of = O.build_flow(spec, state, torch.float32)
     threads = torch.get_num_threads()
-    chunk = 1 << 16
+    chunk = min(1 << 16, budget_rows)
     xs = torch.as_tensor(x_host[:budget_rows])
-    cs = torch.as_tensor(c_host[:budget_rows])
+    cs = torch.as_tensor(c_host[:budget_rows]) if c_host is not None else None
+
+    def crows(i, j):  # the oracle's unconditional flows take ctx=None
+        return None if cs is None else cs[i:j]
+
     with torch.inference_mode():
-        of.log_prob(xs[:chunk], cs[:chunk])  # warm-up
+        of.log_prob(xs[:chunk], crows(0, chunk))  # warm-up
         runs = []
         for _ in range(3):
             t0 = time.perf_counter()
             for i in range(0, budget_rows, chunk):
-                of.log_prob(xs[i:i + chunk], cs[i:i + chunk])
+                of.log_prob(xs[i:i + chunk], crows(i, i + chunk))
             runs.append(time.perf_counter() - t0)
     med = statistics.median(runs)
     # parity spot check of the measured GPU path on the first 4096 rows (checker use)
     n = 4096
     of64 = O.build_flow(spec, state, torch.float64)
+    cond = c_host is not None
     with torch.inference_mode():
-        ref = of64.log_prob(xs[:n].double(), cs[:n].double()).numpy()
-        ref32 = of.log_prob(xs[:n], cs[:n]).numpy()
+        ref = of64.log_prob(xs[:n].double(), cs[:n].double() if cond else None).numpy()
+        ref32 = of.log_prob(xs[:n], crows(0, n)).numpy()
     with torch.no_grad():
         gpu = flow.log_prob(torch.as_tensor(x_host[:n], device="cuda"),
-                            condition=torch.as_tensor(c_host[:n], device="cuda")).cpu().numpy()
+                            condition=torch.as_tensor(c_host[:n], device="cuda") if cond else None).cpu().numpy()
     rel = np.abs(gpu - ref) / np.maximum(np.abs(ref), 1.0)
     rel32 = np.abs(ref32 - ref) / np.maximum(np.abs(ref), 1.0)
     return {
@@ -316,7 +323,14 @@ def run_flow_case(args, dev, rank, world, dist):
         mult = 2 if ftype == "maf" else 3 * extra[0] - 1
         dims = [Dd + Cd] + hid + [Dd * mult]
         passes = Dd
-    fl_row = 2 * passes * Ld * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    fl_ref = 2 * passes * Ld * sum(a * b for a, b in zip(dims[:-1], dims[1:]))  # the reference's work
+    fl_row = fl_ref
+    if ftype != "nsc":  # executed work of the degree-scheduled inverse (padded blocks included)
+        fl_row = 0
+        for net in f.nets:
+            plan = net.inverse_plan().plan()
+            fl_row += sum(2 * blk.w.shape[0] * blk.w.shape[1] for grp in plan.hidden for _, blk in grp)
+            fl_row += sum(2 * wb.shape[0] * n for _, n, wb, _ in plan.outs)
     with torch.no_grad():
         for _ in range(args.warmup):
             f.log_prob(x, condition=c)
@@ -353,8 +367,18 @@ def run_flow_case(args, dev, rank, world, dist):
             "roofline": {"bound": "mfma", "achieved": achieved,
                          "peak": FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3, "unit": "TFLOP/s",
                          "frac": achieved / (FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3),
-                         "traffic": None, "kernel": "whole log_prob call", "flop_per_row": fl_row},
+                         "traffic": None, "kernel": "whole log_prob call", "flop_per_row": fl_row,
+                         "reference_flop_per_row": fl_ref},
         }
+        if not args.no_cpu_baseline:
+            spec = dict(flow_type=ftype, D=Dd, C=Cd, hidden=list(hid), L=Ld)
+            if ftype == "nsc":
+                spec.update(K=extra[0], split=extra[1])
+            elif ftype == "nsa":
+                spec.update(K=extra[0])
+            xh = x[:1 << 17].cpu().numpy()
+            ch = c[:1 << 17].cpu().numpy() if c is not None else None
+            rec["cpu_baseline"], rec["parity_spot_check"] = cpu_baseline(f, xh, ch, budget_rows=1 << 17, spec=spec)
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()

@@ -40,6 +40,14 @@ NAZ_DEV floatx4 mfma3_16(const Frag2& a, const Frag2& b, floatx4 acc) {
   return acc;
 }
 
+// GEMM stages run at wave priority 1, the splines at 0: a SIMD's matrix pipe is fed first
+// and the spline VALU of the other waves fills the MFMA issue gaps (+0.5 %, same-box A/B).
+#ifndef NAZ_R16_NO_PRIO
+#define R16_PRIO(p) __builtin_amdgcn_s_setprio(p)
+#else
+#define R16_PRIO(p) ((void)0)
+#endif
+
 constexpr int kR16Waves = 8;                 // 8 waves x 16 rows = 128 rows per workgroup
 constexpr int kR16Rows = 16 * kR16Waves;
 
@@ -228,15 +236,19 @@ NAZ_DEV void gemm_r16_stage(floatx4 (&acc)[NB], const float* __restrict__ stage,
 }
 
 // k-steps [T0, T0 + KB) with each B fragment split from the activated accumulators just
-// before its MFMAs (blocks 2t, 2t + 1 hold the step's 8 values)
-template <int NB, int KB, int T0, int NX>
-NAZ_DEV void gemm_r16_lazy(floatx4 (&acc)[NB], const float* __restrict__ stage, int lane, const floatx4 (&x)[NX]) {
+// before its MFMAs (blocks 2t, 2t + 1 hold the step's 8 values).  ACT: the step's 8 values are
+// activated here too (sig_fold), so that work can fill the previous step's MFMA shadow.
+template <int NB, int KB, int T0, bool ACT, int NX>
+NAZ_DEV void gemm_r16_lazy(floatx4 (&acc)[NB], const float* __restrict__ stage, int lane, floatx4 (&x)[NX]) {
   const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
 #pragma unroll
   for (int t = 0; t < KB; ++t) {
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = x[2 * (T0 + t) + (j >> 2)][j & 3];
+    for (int j = 0; j < 8; ++j) {
+      v[j] = x[2 * (T0 + t) + (j >> 2)][j & 3];
+      if constexpr (ACT) v[j] = sig_fold(v[j]);
+    }
     const Frag2 b = split8_f16(v);
 #pragma unroll
     for (int o = 0; o < NB; ++o) {
@@ -375,7 +387,9 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
             for (int jj = 0; jj < 8; ++jj) v[jj] = in[8 * t + jj];
             bf[t] = split8_f16(v);
           }
+          R16_PRIO(1);
           gemm_r16_stage<CF::HB, CF::KS1>(acc1, cur, lane, bf);
+          R16_PRIO(0);
         } else {
           // exact fp32: 8 KS1 k-steps of 4; k-step s on this lane = slot (s / 8, s % 8)
           const float4* p4 = reinterpret_cast<const float4*>(cur);
@@ -401,10 +415,15 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
       } else if constexpr (j <= CF::NB2) {
         // ---------------- stage B_s: GEMM2 k-steps [T0, T0 + KB2)
         constexpr int s = j - 1, T0 = s * CF::KB2;
+#ifdef NAZ_R16_EAGER_ACT
 #pragma unroll
         for (int b = 2 * T0; b < 2 * (T0 + CF::KB2); ++b)  // activate the blocks these k-steps read
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc1[b][r] = sig_fold(acc1[b][r]);
+        constexpr bool kLazyAct = false;
+#else
+        constexpr bool kLazyAct = true;  // activated per k-step inside gemm_r16_lazy
+#endif
         if constexpr (s == 0) {
           const float4* b4 = reinterpret_cast<const float4*>(cur + CF::B_BIAS);
 #pragma unroll
@@ -413,14 +432,21 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
             acc2[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
           }
         }
-        gemm_r16_lazy<CF::HB, CF::KB2, T0>(acc2, cur, lane, acc1);
+        R16_PRIO(1);
+        gemm_r16_lazy<CF::HB, CF::KB2, T0, kLazyAct>(acc2, cur, lane, acc1);
+        R16_PRIO(0);
       } else {
         // ---------------- stage C_s: GEMM3 k-steps [T0, T0 + KB3) -> raw spline params
         constexpr int s = j - 1 - CF::NB2, T0 = s * CF::KB3;
+#ifdef NAZ_R16_EAGER_ACT
 #pragma unroll
         for (int b = 2 * T0; b < 2 * (T0 + CF::KB3); ++b)
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc2[b][r] = sig_fold(acc2[b][r]);
+        constexpr bool kLazyAct = false;
+#else
+        constexpr bool kLazyAct = true;
+#endif
         if constexpr (s == 0) {
           const float4* b4 = reinterpret_cast<const float4*>(cur + CF::C_BIAS);
 #pragma unroll
@@ -429,7 +455,9 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
             acc3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
           }
         }
-        gemm_r16_lazy<CF::NO, CF::KB3, T0>(acc3, cur, lane, acc2);
+        R16_PRIO(1);
+        gemm_r16_lazy<CF::NO, CF::KB3, T0, kLazyAct>(acc3, cur, lane, acc2);
+        R16_PRIO(0);
       }
     });
 

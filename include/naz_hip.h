@@ -27,6 +27,9 @@ extern "C" {
 /* ---- constants ---------------------------------------------------------- */
 #define NAZ_LAYOUT_DENSE 0 /* DenseNN hypernet output: [w(Dt*K) | h(Dt*K) | d(Dt*(K-1))]  */
 #define NAZ_LAYOUT_ARN 1   /* AutoRegressiveNN output: column p*Dt + i, p in [0, 3K-1)    */
+#define NAZ_RQS_FAST 16    /* OR into naz_rqs_fwd/inv's layout: hardware-transcendental
+                              select-first evaluation (fp32-grade, ~2x faster); default is the
+                              libm-grade evaluator that naz_rqs_bwd's VJP matches            */
 
 #define NAZ_LD_PERDIM 0      /* ld is [B, Dt], per dimension                                */
 #define NAZ_LD_ROWSUM 1      /* ld is [B], ld[r]  = sum_i ld[r, i]                          */

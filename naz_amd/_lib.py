@@ -12,6 +12,7 @@ from pathlib import Path
 LIB_PATH = Path(os.environ.get("NAZ_LIB", Path(__file__).resolve().parent / "lib" / "libnazhip.so"))
 
 LAYOUT_DENSE, LAYOUT_ARN = 0, 1
+RQS_FAST = 16  # NAZ_RQS_FAST: OR into the spline layout for the select-first hardware-math evaluator
 LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB = 0, 1, 2, 3
 ACT = {"identity": 0, "tanh": 1, "relu": 2, "softplus": 3, "sigmoid": 4}
 MFMA_BF16X6, MFMA_F32, MFMA_F16X3 = 0, 1, 2

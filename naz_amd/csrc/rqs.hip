@@ -10,7 +10,11 @@
 // stride equals the row length) are copied HBM→LDS with 16-byte loads, then each
 // thread evaluates one (row, dim) with its knots in registers.  The per-row
 // log-det sum is a fixed-order LDS reduction (dims 0..Dt−1, like torch's .sum(-1)).
-// HBM-bound: per (row, dim) 4·(3K−1) + 4 bytes in, 4 (+4) bytes out.
+// Two evaluators: the libm-grade one (knot cumsum in double, expf/logf, IEEE divides; what the
+// autograd walk and its VJP use) is VALU-bound at ~2.1 TB/s; `layout | NAZ_RQS_FAST` selects the
+// select-first evaluator of the fused kernels (rqs_select: hardware transcendentals, only the
+// selected bin formed), HBM-bound at ~4.4-4.7 TB/s algorithmic (2^20 rows, Dt=8, K=8), used by
+// the inference paths.  Per (row, dim) 4·(3K−1) + 4 bytes in, 4 (+4) bytes out.
 #include "naz_device.h"
 #include "naz_internal.h"
 #include "spline_bwd.h"
@@ -39,7 +43,7 @@ NAZ_DEV void block_copy_to_lds(float* lds, const float* __restrict__ src, int n,
   for (int i = head + 4 * nvec + tid; i < n; i += nthreads) lds[i] = src[i];
 }
 
-template <int K, bool INV>
+template <int K, bool INV, bool FAST>
 __global__ void __launch_bounds__(256) rqs_cond_kernel(
     const float* __restrict__ x, int64_t ldx, const float* __restrict__ raw, int64_t ldr,
     float* __restrict__ y, int64_t ldy, float* __restrict__ ld_out, int ld_mode, int64_t B, int Dt,
@@ -64,6 +68,7 @@ __global__ void __launch_bounds__(256) rqs_cond_kernel(
   }
   __syncthreads();
 
+  const RqsConsts<K, INV> rc(bound);
   for (int e = tid; e < rows * Dt; e += blockDim.x) {
     const int r = e / Dt, i = e - r * Dt;
     const float* pr = raw_s + (size_t)r * P;
@@ -79,11 +84,16 @@ __global__ void __launch_bounds__(256) rqs_cond_kernel(
 #pragma unroll
       for (int k = 0; k < K - 1; ++k) ud[k] = pr[(2 * K + k) * Dt + i];
     }
-    SplineTables<K> t;
-    build_tables<K>(uw, uh, ud, bound, t);
     const float xv = x[(r0 + r) * ldx + i];
     float ld;
-    const float yv = rqs_apply<K, INV>(t, xv, bound, ld);
+    float yv;
+    if constexpr (FAST) {
+      yv = rqs_select<K, INV>(uw, uh, ud, xv, bound, rc, ld);
+    } else {
+      SplineTables<K> t;
+      build_tables<K>(uw, uh, ud, bound, t);
+      yv = rqs_apply<K, INV>(t, xv, bound, ld);
+    }
     y[(r0 + r) * ldy + i] = yv;
     if (ld_mode == NAZ_LD_PERDIM) ld_out[(r0 + r) * Dt + i] = ld;
     else ld_s[r * Dt + i] = ld;
@@ -126,12 +136,18 @@ __global__ void __launch_bounds__(256) rqs_uncond_kernel(
 template <int K, bool INV>
 static int launch_rqs_cond(const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
                            float* ld, int ld_mode, int64_t B, int Dt, int layout, float bound, hipStream_t s) {
+  const bool fast = (layout & NAZ_RQS_FAST) != 0;
+  layout &= ~NAZ_RQS_FAST;
   const int R = (Dt >= 256) ? 1 : 256 / Dt;
   const size_t lds = ((size_t)R * Dt * (3 * K - 1) + (size_t)R * Dt) * sizeof(float);
   if (lds > 160 * 1024) return set_error("naz_rqs: Dt*K too large for one LDS block (%zu bytes)", lds);
   const int64_t grid = (B + R - 1) / R;
-  hipLaunchKernelGGL((rqs_cond_kernel<K, INV>), dim3((unsigned)grid), dim3(256), lds, s, x, ldx, raw, ldr, y, ldy,
-                     ld, ld_mode, B, Dt, layout, bound);
+  if (fast)
+    hipLaunchKernelGGL((rqs_cond_kernel<K, INV, true>), dim3((unsigned)grid), dim3(256), lds, s, x, ldx, raw, ldr, y,
+                       ldy, ld, ld_mode, B, Dt, layout, bound);
+  else
+    hipLaunchKernelGGL((rqs_cond_kernel<K, INV, false>), dim3((unsigned)grid), dim3(256), lds, s, x, ldx, raw, ldr,
+                       y, ldy, ld, ld_mode, B, Dt, layout, bound);
   return check_launch("rqs_cond_kernel");
 }
 

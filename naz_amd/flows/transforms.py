@@ -195,7 +195,7 @@ class Spline(TransformModule):
 
     def spline_apply(self, x, inverse, ld_mode, ld_out, out=None):
         return ops.rqs(x, self.flat_raw(), self.count_bins, ops.LAYOUT_DENSE, inverse, self.bound, ld_mode, ld_out,
-                       out=out, broadcast_raw=True)
+                       out=out, broadcast_raw=True, fast=True)
 
     def _call(self, x):
         y, ld = self.spline_apply(x, False, ops.LD_PERDIM, None)
@@ -242,7 +242,7 @@ class _ConditionedSplineCoupling(_LDCache, Transform):
         else:
             x1 = v1
         raw = m.nn.raw(x1, self.context)
-        ops.rqs(v2, raw, m.count_bins, ops.LAYOUT_DENSE, inverse, m.bound, ld_mode, ld_buf, out=out[:, s:])
+        ops.rqs(v2, raw, m.count_bins, ops.LAYOUT_DENSE, inverse, m.bound, ld_mode, ld_buf, out=out[:, s:], fast=True)
         if not inverse:
             if m.lower_spline is not None:
                 m.lower_spline.spline_apply(v1, False, ld_mode, ld_buf, out=out[:, :s])
@@ -353,13 +353,13 @@ class _ConditionedSplineAutoregressive(_LDCache, Transform):
     def _map(self, v, inverse, ld_buf, ld_mode):
         if not inverse:
             raw = self.arn.raw(v, self.context)
-            y, _ = ops.rqs(v, raw, self.count_bins, ops.LAYOUT_ARN, False, self.bound, ld_mode, ld_buf)
+            y, _ = ops.rqs(v, raw, self.count_bins, ops.LAYOUT_ARN, False, self.bound, ld_mode, ld_buf, fast=True)
             return y
         plan = _degree_plan(self.arn, v, ld_mode)
         if plan is not None:
             def step(k, i, raw, x):
                 ops.rqs(v[:, i:i + 1], raw, self.count_bins, ops.LAYOUT_ARN, True, self.bound,
-                        _pass_ld_mode(ld_mode, k), ld_buf, out=x[:, i:i + 1])
+                        _pass_ld_mode(ld_mode, k), ld_buf, out=x[:, i:i + 1], fast=True)
             return plan.run(v, self.context, step)
         x = torch.zeros_like(v)
         D = v.shape[-1]
@@ -368,7 +368,7 @@ class _ConditionedSplineAutoregressive(_LDCache, Transform):
             raw = self.arn.raw(x, self.context)
             last = k == D - 1
             x, _ = ops.rqs(v, raw, self.count_bins, ops.LAYOUT_ARN, True, self.bound,
-                           ld_mode if last else ops.LD_ROWSUM, ld_buf if last else scratch)
+                           ld_mode if last else ops.LD_ROWSUM, ld_buf if last else scratch, fast=True)
         return x
 
     def _call(self, x):

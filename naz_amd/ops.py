@@ -11,7 +11,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB, CnfDesc,
+from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, RQS_FAST, LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB, CnfDesc,
                    CouplingDesc, check, lib)
 
 Tensor = torch.Tensor
@@ -61,12 +61,14 @@ def _p(t: Optional[Tensor]) -> Optional[int]:
 # ----------------------------------------------------------------------------- a1 + a2
 def rqs(x: Tensor, raw: Tensor, count_bins: int, layout: int = LAYOUT_DENSE, inverse: bool = False,
         bound: float = 3.0, ld_mode: int = LD_PERDIM, ld_out: Optional[Tensor] = None,
-        out: Optional[Tensor] = None, broadcast_raw: bool = False) -> Tuple[Tensor, Tensor]:
+        out: Optional[Tensor] = None, broadcast_raw: bool = False, fast: bool = False) -> Tuple[Tensor, Tensor]:
     """Conditional RQ spline over a conditioner output (naz_rqs_fwd / naz_rqs_inv).
 
     ``out`` may be a strided 2-D view (unit last stride) to write into; ``broadcast_raw``
     passes a single parameter row (row stride 0) shared by every batch row, which is how
-    the unconditional lower spline of a coupling layer runs."""
+    the unconditional lower spline of a coupling layer runs.  ``fast`` selects the
+    select-first hardware-math evaluator (NAZ_RQS_FAST; fp32-grade, HBM-bound) instead of
+    the libm-grade one that ``rqs_bwd``'s VJP matches (the autograd walk keeps the latter)."""
     dev = _dev(x, raw, ld_out, out)
     x, ldx = _rows(x)
     B, Dt = x.shape
@@ -87,8 +89,8 @@ def rqs(x: Tensor, raw: Tensor, count_bins: int, layout: int = LAYOUT_DENSE, inv
     if ld_out is None:
         ld_out = torch.empty((B, Dt) if ld_mode == LD_PERDIM else (B,), device=dev, dtype=torch.float32)
     fn = lib().naz_rqs_inv if inverse else lib().naz_rqs_fwd
-    check(fn(_p(x), ldx, _p(raw), ldr, _p(out), out.stride(0), _p(ld_out), ld_mode, B, Dt, count_bins, layout,
-             float(bound), _stream(dev)), "rqs")
+    check(fn(_p(x), ldx, _p(raw), ldr, _p(out), out.stride(0), _p(ld_out), ld_mode, B, Dt, count_bins,
+             layout | (RQS_FAST if fast else 0), float(bound), _stream(dev)), "rqs")
     return out, ld_out
 
 

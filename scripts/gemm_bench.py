@@ -69,6 +69,17 @@ def main():
         t = timeit_(lambda: ops.gemm(G, W))
         fl = 2 * M * n_out * k_in
         out.append(f"{name:6s} rowgemm {t:8.1f} us  {fl / t / 1e6:6.1f} TF  {(G.numel() + M * k_in) * 4 / t / 1e3:6.0f} GB/s")
+    # standalone conditional spline (a1/a2): x [M, 8], DenseNN raw [M, 8 * 23], row-sum ld
+    for inv, fast, name in [(False, False, "rqsf"), (True, False, "rqsi"), (False, True, "rqsf_fast"),
+                            (True, True, "rqsi_fast")]:
+        if only and name not in only:
+            continue
+        X = torch.randn(M, 8, device=dev, generator=g)
+        R = torch.randn(M, 8 * 23, device=dev, generator=g)
+        ldb = torch.empty(M, device=dev)
+        t = timeit_(lambda: ops.rqs(X, R, 8, ops.LAYOUT_DENSE, inv, 3.0, ops.LD_ROWSUM, ldb, fast=fast))
+        nbytes = (X.numel() * 2 + R.numel() + M) * 4
+        out.append(f"{name:6s} spline  {t:8.1f} us  {nbytes / t / 1e3:6.0f} GB/s (algorithmic bytes)")
     print("\n".join(out))
 
 

@@ -58,12 +58,14 @@ def _product_flow(fx):
 # ------------------------------------------------------------------ a1 + a2 standalone spline
 @pytest.mark.parametrize("name", ["rqs_dense_k8.npz", "rqs_arn_k5.npz", "rqs_dense_k16.npz"])
 @pytest.mark.parametrize("inverse", [False, True])
-def test_rqs_kernel_vs_golden(name, inverse):
+@pytest.mark.parametrize("fast", [False, True], ids=["libm", "fast"])
+def test_rqs_kernel_vs_golden(name, inverse, fast):
+    """Both evaluators of naz_rqs_fwd/inv: libm-grade (the autograd walk) and NAZ_RQS_FAST."""
     from naz_amd import ops
     fx = load_golden(name)
     K, Dt, layout = int(fx["K"]), int(fx["Dt"]), int(fx["layout"])
     x, raw = _cuda(fx["x"]), _cuda(fx["raw"])
-    y, ld = ops.rqs(x, raw, K, layout, inverse=inverse)
+    y, ld = ops.rqs(x, raw, K, layout, inverse=inverse, fast=fast)
     ky, kl = ("y_inv", "ld_inv") if inverse else ("y_fwd", "ld_fwd")
     y32, ld32 = O.rqs_from_raw(torch.as_tensor(fx["x"]), torch.as_tensor(fx["raw"]), Dt, K, layout, inverse)
     assert_parity(_np(y), fx[ky], _np(y32), what=f"{name} y")

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/round
-rm -rf $O/pmc $O/prof $O/prof_cnf
+rm -rf $O/pmc $O/prof $O/prof_cnf $O/prof_train
 mkdir -p $O
 step() {  # step <name> <timeout> <cmd...>; stop on crash / timeout
   local name=$1 t=$2; shift 2
@@ -20,7 +20,10 @@ step prof 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format
 step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc/p1 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc/p2 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step pmc_sq 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc/p3 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+step pmc_wait 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU_TRANS_F32 -d $O/pmc/p4 -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 step train 300 python bench.py --train --steps 5 --warmup 2
+step prof_train 240 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run --output-format csv -- python3 bench.py --train --steps 3 --warmup 1 --no-cpu-baseline
+step gemm_bench 120 python scripts/gemm_bench.py
 step cnf 300 python bench.py --cnf --steps 10 --warmup 3
 step prof_cnf 240 rocprofv3 --kernel-trace --stats -d $O/prof_cnf -o run --output-format csv -- python3 bench.py --cnf --steps 10 --warmup 3
 for f in config2 maf nsa; do step flow_$f 240 python bench.py --flow $f --steps 10 --warmup 3; done

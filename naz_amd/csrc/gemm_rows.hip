@@ -379,10 +379,13 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WGradArgs p) {
 // VALU column sum of the G chunk, so it costs no MFMA block.  Loads of chunk i+1 are in flight
 // (registers) while chunk i's MFMAs run.
 // ------------------------------------------------------------------------------------------
-constexpr int WF_Q = 8;          // float4 prefetch slots per thread (32 KB per 256-thread chunk)
+#ifndef NAZ_WF_Q
+#define NAZ_WF_Q 8
+#endif
+constexpr int WF_Q = NAZ_WF_Q;   // float4 prefetch slots per thread (16 B x 256 x WF_Q per chunk)
 
 template <int MAXB>
-__global__ void __launch_bounds__(256, MAXB <= 2 ? 4 : (MAXB == 4 ? 3 : 2)) wgrad_flat_kernel(WGradArgs p, int R) {
+__global__ void __launch_bounds__(256, MAXB <= 1 ? 4 : (MAXB <= 2 ? 3 : 2)) wgrad_flat_kernel(WGradArgs p, int R) {
   extern __shared__ float wlds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N1 = p.N1, N2 = p.N2;
@@ -391,7 +394,9 @@ __global__ void __launch_bounds__(256, MAXB <= 2 ? 4 : (MAXB == 4 ? 3 : 2)) wgra
   const int NB1 = (N1 + 31) / 32, NB2 = (N2 + 31) / 32;
   const int64_t mb = (int64_t)blockIdx.x * p.rows_per_wg;
   const int64_t me = (mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M;
-  int bi[MAXB], bj[MAXB];
+  // this wave's output blocks q = blk0 + wave + 4j; past-the-end slots duplicate block 0 (their
+  // MFMAs run unconditionally so the k loop has no per-block branches; results are dropped)
+  int bi[MAXB], bj[MAXB], ga[MAXB], xb[MAXB];
   bool bv[MAXB];
 #pragma unroll
   for (int j = 0; j < MAXB; ++j) {
@@ -399,6 +404,8 @@ __global__ void __launch_bounds__(256, MAXB <= 2 ? 4 : (MAXB == 4 ? 3 : 2)) wgra
     bv[j] = q < NB1 * NB2;
     bi[j] = bv[j] ? q / NB2 : 0;
     bj[j] = bv[j] ? q - (q / NB2) * NB2 : 0;
+    ga[j] = 32 * bi[j] + (lane & 31);
+    xb[j] = 32 * bj[j] + (lane & 31);
   }
   floatx16 acc[MAXB];
 #pragma unroll
@@ -440,14 +447,20 @@ __global__ void __launch_bounds__(256, MAXB <= 2 ? 4 : (MAXB == 4 ? 3 : 2)) wgra
     store();
     __syncthreads();
     if (m0 + R < me) load(m0 + R);  // in flight during this chunk's MFMAs
-    for (int kk = 0; kk < R; kk += 2) {
-      const int k = kk + (lane >> 5);
+    // R is a multiple of 16; rows past the chunk's end were loaded as zeros
+    constexpr int U = MAXB >= 8 ? 2 : 4;  // k rows per unrolled group (8 blocks: no room to pipeline)
+    for (int kk = 0; kk < R; kk += U) {
 #pragma unroll
-      for (int j = 0; j < MAXB; ++j) {
-        if (!bv[j]) continue;
-        const float a = Gs[k * N1 + 32 * bi[j] + (lane & 31)];
-        const float b = Xs[k * N2 + 32 * bj[j] + (lane & 31)];
-        acc[j] = mfma_f32(a, b, acc[j]);
+      for (int u = 0; u < U; u += 2) {
+        const int k = kk + u + (lane >> 5);
+        float a[MAXB], b[MAXB];
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j) {
+          a[j] = Gs[k * N1 + ga[j]];
+          b[j] = Xs[k * N2 + xb[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j) acc[j] = mfma_f32(a[j], b[j], acc[j]);
       }
     }
     if (p.ones && tid < N1)
@@ -493,7 +506,7 @@ int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
                     p.N1 <= 256 && p.N2 <= 256;
   if (flat) {
     // rows per chunk: ~8192 floats of G + X (a multiple of 16, <= 128); ~1024 workgroups
-    int R = 8192 / (p.N1 + p.N2);
+    int R = 1024 * WF_Q / (p.N1 + p.N2);
     R = R > 128 ? 128 : (R / 16) * 16;
     if (R < 16) R = 16;
     while (R * (p.N1 + p.N2) / 4 > 256 * WF_Q) R -= 16;
@@ -502,7 +515,9 @@ int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
     if (rpw < 4 * R) rpw = 4 * R;
     p.rows_per_wg = rpw;
     const int nblk = ((p.N1 + 31) / 32) * ((p.N2 + 31) / 32);
-    const int maxb = nblk <= 4 ? 1 : (nblk <= 8 ? 2 : (nblk <= 16 ? 4 : 8));
+    const int per_wave = (nblk + 3) / 4;  // blocks per wave (4 waves): no idle MFMA slots for nblk % 4 == 0
+    const int maxb = per_wave <= 1 ? 1 : per_wave <= 2 ? 2 : per_wave <= 3 ? 3 : per_wave <= 4 ? 4
+                   : per_wave <= 6 ? 6 : 8;
     const size_t lds = sizeof(float) * (R * (p.N1 + p.N2) + 64);
     const unsigned gx = (unsigned)((p.M + rpw - 1) / rpw);
     for (int b0 = 0; b0 < nblk; b0 += 4 * maxb) {
@@ -512,7 +527,9 @@ int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
       switch (maxb) {
         case 1: hipLaunchKernelGGL(wgrad_flat_kernel<1>, dim3(gx), dim3(256), lds, s, q, R); break;
         case 2: hipLaunchKernelGGL(wgrad_flat_kernel<2>, dim3(gx), dim3(256), lds, s, q, R); break;
+        case 3: hipLaunchKernelGGL(wgrad_flat_kernel<3>, dim3(gx), dim3(256), lds, s, q, R); break;
         case 4: hipLaunchKernelGGL(wgrad_flat_kernel<4>, dim3(gx), dim3(256), lds, s, q, R); break;
+        case 6: hipLaunchKernelGGL(wgrad_flat_kernel<6>, dim3(gx), dim3(256), lds, s, q, R); break;
         default: hipLaunchKernelGGL(wgrad_flat_kernel<8>, dim3(gx), dim3(256), lds, s, q, R); break;
       }
     }

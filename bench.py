@@ -385,6 +385,128 @@ def run_flow_case(args, dev, rank, world, dist):
         dist.destroy_process_group()
 
 
+# --bayes: the Bayesian front end's per-draw loops at the paper shape
+# (examples/papers/2506.05657: D=2 (m1, m2), C=2 (chi_b, alpha), hidden [150]*3, 16 layers):
+# lp = density grid under P posterior draws (plot.py:192-204), sample = posterior-predictive
+# draws (calibrate.py:145-151).  One step = one batched call over all P draws.
+BAYES = dict(D=2, C=2, hidden=[150, 150, 150], L=16)
+
+
+def run_bayes(args, dev, rank, world, dist):
+    from naz_amd.flows import bflow_maf as BM
+    from oracle import jax_maf_np as J  # checker + cpu_baseline only
+    from oracle import naz_oracle as O
+    sp = dict(flow_type="maf", **BAYES)
+    D, C = sp["D"], sp["C"]
+    st = {k: v.numpy() for k, v in O.random_state(sp, seed=1234).items()}
+    layers = J.layers_from_state(sp, st)
+    lp_mode = args.bayes == "lp"
+    P = 64 if lp_mode else 16
+    B = args.batch if args.batch != (1 << 20) else (1 << 14 if lp_mode else 1 << 16)
+    rng = np.random.default_rng(100 + rank)
+    draws = [[[((W * (1 + 0.25 * rng.uniform(-1, 1, W.shape))).astype(np.float32),
+                (b * (1 + 0.25 * rng.uniform(-1, 1, b.shape))).astype(np.float32)) for (W, b) in params]
+              for params, _, _ in layers] for _ in range(P)]
+    params = [[(torch.tensor(np.stack([d[l][i][0] for d in draws]), device=dev),
+                torch.tensor(np.stack([d[l][i][1] for d in draws]), device=dev))
+               for i in range(len(BAYES["hidden"]) + 1)] for l in range(BAYES["L"])]
+    g = np.linspace(-3, 3, int(round(B ** 0.5)))
+    grid = np.stack(np.meshgrid(g, g), -1).reshape(-1, 2).astype(np.float32)
+    x = np.concatenate([grid, gaussian_mixture(B - grid.shape[0], D, seed=rank)]) if grid.shape[0] < B else grid[:B]
+    ctx = np.array([0.3, -1.2], dtype=np.float32)
+    nn_spec, _, _ = BM.make_conditional_autoregressive_nn(D, C, BAYES["hidden"])
+    tr = BM.make_masked_affine_autoregressive_transform(nn_spec, D)
+    flow = BM.make_normalizing_flow(tr, torch.tensor(x, device=dev),
+                                    [[torch.tensor(m, dtype=torch.float32) for m in ms] for _, _, ms in layers],
+                                    [None] * BAYES["L"], [torch.tensor(p) for _, p, _ in layers],
+                                    context=torch.tensor(ctx, device=dev))
+    if lp_mode:
+        def step():
+            return flow["lp_batched"](params)
+    else:
+        def step():
+            return flow["sampler_batched"](params, 7, B)[0]
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    assert bool(torch.isfinite(out).all())
+    if dist is not None:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+    if rank != 0:
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    step_s = elapsed / args.steps
+    dims = [D + C] + BAYES["hidden"] + [2 * D]
+    full = 2 * BAYES["L"] * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    if lp_mode:
+        fl_ref = D * full  # the reference's D full MADE passes per layer
+        fl_row = sum(2 * (b - a) * n for pl in flow["plans"] for grp in pl.hidden for (_, a, b, n, _, _) in grp)
+        fl_row += sum(2 * 2 * n for pl in flow["plans"] for (_, n, _, _) in pl.outs)
+    else:
+        fl_ref = fl_row = full
+    achieved = fl_row * P * B / step_s / 1e12
+    rec = {
+        "metric": ("draw-rows/sec through batched-over-parameters log_prob, naz Bayesian affine MAF"
+                   if lp_mode else "samples/sec through batched-over-parameters posterior-predictive sampling, "
+                                   "naz Bayesian affine MAF"),
+        "value": P * B * world / step_s, "unit": "draw-rows/s" if lp_mode else "samples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: rows = 2-D grid (+ Gaussian-mixture fill); P weight draws = MLE weights x (1 + 0.25 U(-1,1)) "
+                "(bflow_jax_maf.py:224-226); random-init MLE weights (torch seed 1234)",
+        "config": {"workload": f"SURVEY.md §8f rank {1 if lp_mode else 2}: naz JAX-MAF front end "
+                               f"({'lp' if lp_mode else 'sampler'}) at the 2506.05657 paper shape D=2, C=2, "
+                               f"H=[150]*3, L=16; {P} draws x {B} rows per step (pack included)",
+                   "draws": P, "rows_per_draw": B, "parallelism": f"dp{world} (independent draw sets, no collective)"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "whole batched call",
+                     "flop_per_row": fl_row, "reference_flop_per_row": fl_ref},
+    }
+    if not args.no_cpu_baseline:
+        # the reference's algorithm (numpy restatement of bflow_jax_maf.py, float32) per draw
+        nrow = min(B, 1 << 13)
+        ol = [(([(w.astype(np.float64), b.astype(np.float64)) for (w, b) in draws[0][l]]), perm, ms)
+              for l, (_, perm, ms) in enumerate(layers)]
+        ol32 = J.cast_layers(ol, np.float32)
+        times = []
+        for _ in range(2):
+            t1 = time.perf_counter()
+            if lp_mode:
+                J.log_prob(x[:nrow], ol32, ctx, np.float32)
+            else:
+                J.sample_from_z(np.random.default_rng(0).standard_normal((nrow, D)).astype(np.float32), ol32, ctx,
+                                np.float32)
+            times.append(time.perf_counter() - t1)
+        rec["cpu_baseline"] = {"value": nrow / min(times), "unit": rec["unit"],
+                               "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())), "kind": "port",
+                               "sample": f"one draw x {nrow} rows, numpy float32 restatement of the reference's JAX "
+                                         f"MAF (oracle/jax_maf_np.py), best of 2 ({min(times):.2f} s)"}
+        if lp_mode:
+            ref = J.log_prob(x[:4096], ol, ctx)
+            got = out[0, :4096].double().cpu().numpy()
+            r = np.abs(got - ref) / np.maximum(np.abs(ref), 1)
+            rec["parity_spot_check"] = {"rows": 4096, "draw": 0, "gpu_rel_median": float(np.median(r)),
+                                        "gpu_rel_max": float(r.max())}
+    print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -400,6 +522,9 @@ def main():
                          "steps) log_prob at 2^18 rows per GPU")
     ap.add_argument("--flow", choices=sorted(FLOW_CASES), default=None,
                     help="time log_prob of another §8 flow through the NormalizingFlow API (see FLOW_CASES)")
+    ap.add_argument("--bayes", choices=["lp", "sample"], default=None,
+                    help="§8f ranks 1-2: the Bayesian MAF front end batched over weight draws (lp over a grid, "
+                         "posterior-predictive sampling) at the paper shape")
     ap.add_argument("--mfma", choices=["auto", "f16x3", "f16x3r16", "bf16x6", "f32"], default="auto",
                     help="auto (default): f16x3r16 (16-row waves) when the packed hidden-layer weights fit fp16 and "
                          "the shape allows, else f16x3, else bf16x6; f32: exact FP32 MFMA")
@@ -422,6 +547,8 @@ def main():
         return run_cnf(args, dev, rank, world, dist)
     if args.flow:
         return run_flow_case(args, dev, rank, world, dist)
+    if args.bayes:
+        return run_bayes(args, dev, rank, world, dist)
 
     flow = build_flow()
     B = args.batch

@@ -85,6 +85,18 @@ int naz_spline_elementwise(int inverse, const float* x, int64_t ldx, const float
 int naz_linear_act(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx, int Kx, const float* W,
                    const float* mask, const float* b, float* y, int64_t ldy, int64_t M, int N, int act, void* stream);
 
+/* ---- §8f rank 1: conditioner layer batched over parameter draws -----------
+ * Replaces jax.vmap over the weights of bflow_jax_maf.py:113-116 (masked_linear), i.e. the
+ * per-draw evaluation loops of the Bayesian front end (plot.py:192-204, calibrate.py:145-151,
+ * hmc_maf_exact.py:128-133): nbatch independent problems
+ *   y_z = act(cat([ctx_z, x_z]) @ (W_z * mask)^T + b_z),  z = 0 .. nbatch-1,
+ * with problem z's operands at ctx + z*sctx, x + z*sx, W + z*sw, b + z*sb, y + z*sy (strides in
+ * floats; sctx = 0 / ldc = 0 broadcast a context). The mask [N, C+Kx] is shared. M rows each. */
+int naz_linear_act_batched(const float* ctx, int64_t ldc, int64_t sctx, int C, const float* x, int64_t ldx,
+                           int64_t sx, int Kx, const float* W, int64_t sw, const float* mask, const float* b,
+                           int64_t sb, float* y, int64_t ldy, int64_t sy, int64_t M, int N, int nbatch, int act,
+                           void* stream);
+
 /* ---- a5: affine autoregressive elementwise step --------------------------
  * Replaces the elementwise part of [pyro] AffineAutoregressive._call / ._inverse
  * (naz/flows/transforms.py:159; JAX restatement bflow_jax_maf.py:169-194):

@@ -68,6 +68,21 @@ int naz_linear_act(const float* ctx, int64_t ldc, int C, const float* x, int64_t
   return linear_act(ctx, ldc, C, x, ldx, Kx, W, mask, b, y, ldy, M, N, act, as_stream(stream));
 }
 
+int naz_linear_act_batched(const float* ctx, int64_t ldc, int64_t sctx, int C, const float* x, int64_t ldx,
+                           int64_t sx, int Kx, const float* W, int64_t sw, const float* mask, const float* b,
+                           int64_t sb, float* y, int64_t ldy, int64_t sy, int64_t M, int N, int nbatch, int act,
+                           void* stream) {
+  if (M < 0 || N < 0 || C < 0 || Kx < 0 || nbatch < 0) return set_error("naz_linear_act_batched: negative shape");
+  if (nbatch > 65535) return set_error("naz_linear_act_batched: nbatch %d > 65535 (grid z)", nbatch);
+  if (C > 0 && ctx == nullptr) return set_error("naz_linear_act_batched: C=%d but ctx is NULL", C);
+  if (Kx > 0 && x == nullptr) return set_error("naz_linear_act_batched: Kx=%d but x is NULL", Kx);
+  if (W == nullptr || y == nullptr) return set_error("naz_linear_act_batched: NULL W or y");
+  if (act < 0 || act > NAZ_ACT_SIGMOID) return set_error("naz_linear_act_batched: unknown activation %d", act);
+  if ((int64_t)N * (C + Kx) * 4 >= (1ll << 31)) return set_error("naz_linear_act_batched: weight block too large");
+  return rowgemm_linear_batched(ctx, ldc, sctx, C, x, ldx, sx, Kx, W, sw, mask, b, sb, y, ldy, sy, M, N, nbatch, act,
+                                as_stream(stream));
+}
+
 int naz_affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
                   float* ld, int ld_mode, int64_t B, int D, void* stream) {
   if (B < 0 || D <= 0) return set_error("naz_affine_ar: bad shape");

@@ -59,6 +59,10 @@ struct RowGemmArgs {
   int accumulate;
   int vec;  // A segments allow 16-byte loads of 8-k groups (set by rowgemm())
   int vst;  // C rows allow 16-byte stores (row stride % 4 == 0, aligned; set by rowgemm())
+  // batch of independent problems along blockIdx.z (per-draw weights, naz_linear_act_batched):
+  // problem z reads a0 + z*za0, a1 + z*za1, b + z*zb, bias + z*zbias and writes c + z*zc
+  // (the mask is shared); all zero for a single problem
+  int64_t za0, za1, zb, zbias, zc;
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -73,6 +77,14 @@ NAZ_DEV float rg_a(const RowGemmArgs& p, int64_t m, int k) {
 // waves per SIMD: up to 4 blocks of accumulators fit 128 VGPRs (4 waves/SIMD); wider tiles 2
 template <int NB>
 __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(RowGemmArgs p) {
+  {  // problem of this z slice (uniform: stays in SGPRs)
+    const int64_t z = blockIdx.z;
+    p.a0 += z * p.za0;
+    p.a1 += z * p.za1;
+    p.b += z * p.zb;
+    if (p.bias != nullptr) p.bias += z * p.zbias;
+    p.c += z * p.zc;
+  }
   constexpr int BN = 32 * NB;
   constexpr int AS_F = 2 * RG_BK * (RG_BM + RG_APAD), BS_F = 2 * RG_BK * (BN + RG_PAD);
   __shared__ float smem[AS_F + BS_F];
@@ -227,15 +239,15 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
 }
 
 template <int NB>
-void rowgemm_launch(const RowGemmArgs& p, hipStream_t s) {
-  dim3 grid((unsigned)((p.M + RG_BM - 1) / RG_BM), (unsigned)((p.N + 32 * NB - 1) / (32 * NB)));
+void rowgemm_launch(const RowGemmArgs& p, int nz, hipStream_t s) {
+  dim3 grid((unsigned)((p.M + RG_BM - 1) / RG_BM), (unsigned)((p.N + 32 * NB - 1) / (32 * NB)), (unsigned)nz);
   hipLaunchKernelGGL(rowgemm_kernel<NB>, grid, dim3(256), 0, s, p);
 }
 
 static bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
-int rowgemm(RowGemmArgs p, hipStream_t s) {
-  if (p.M <= 0 || p.N <= 0) return 0;
+int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
+  if (p.M <= 0 || p.N <= 0 || nz <= 0) return 0;
   const int64_t K = p.ka0 + p.ka1;
   const int64_t bspan = (K - 1) * (p.sbk < 0 ? -p.sbk : p.sbk) + (int64_t)(p.N - 1) * (p.sbn < 0 ? -p.sbn : p.sbn);
   const int64_t mspan = (K - 1) * (p.smk < 0 ? -p.smk : p.smk) + (int64_t)(p.N - 1) * (p.smn < 0 ? -p.smn : p.smn);
@@ -244,16 +256,20 @@ int rowgemm(RowGemmArgs p, hipStream_t s) {
   p.vec = (p.ka0 % 8 == 0) && (p.ka0 == 0 || (al16(p.a0) && p.lda0 % 4 == 0)) &&
           (p.ka1 == 0 || (al16(p.a1) && p.lda1 % 4 == 0));
   p.vst = p.ldc % 4 == 0 && al16(p.c);  // 16-byte row pieces; a ragged row tail is stored per column
+  if (nz > 1) {  // every problem's base keeps the alignment
+    p.vec = p.vec && p.za0 % 4 == 0 && p.za1 % 4 == 0;
+    p.vst = p.vst && p.zc % 4 == 0;
+  }
   const int nb = (p.N + 31) / 32;
   switch (nb > 8 ? 8 : nb) {
-    case 1: rowgemm_launch<1>(p, s); break;
-    case 2: rowgemm_launch<2>(p, s); break;
-    case 3: rowgemm_launch<3>(p, s); break;
-    case 4: rowgemm_launch<4>(p, s); break;
-    case 5: rowgemm_launch<5>(p, s); break;
-    case 6: rowgemm_launch<6>(p, s); break;
-    case 7: rowgemm_launch<7>(p, s); break;
-    default: rowgemm_launch<8>(p, s); break;
+    case 1: rowgemm_launch<1>(p, nz, s); break;
+    case 2: rowgemm_launch<2>(p, nz, s); break;
+    case 3: rowgemm_launch<3>(p, nz, s); break;
+    case 4: rowgemm_launch<4>(p, nz, s); break;
+    case 5: rowgemm_launch<5>(p, nz, s); break;
+    case 6: rowgemm_launch<6>(p, nz, s); break;
+    case 7: rowgemm_launch<7>(p, nz, s); break;
+    default: rowgemm_launch<8>(p, nz, s); break;
   }
   return check_launch("rowgemm_kernel");
 }
@@ -579,6 +595,38 @@ int rowgemm_linear(const float* ctx, int64_t ldc, int C, const float* x, int64_t
   p.act = act;
   p.accumulate = 0;
   return rowgemm(p, s);
+}
+
+// naz_linear_act_batched: nz problems with their own weights / bias over their own row blocks
+int rowgemm_linear_batched(const float* ctx, int64_t ldc, int64_t zc, int C, const float* x, int64_t ldx, int64_t zx,
+                           int Kx, const float* W, int64_t zw, const float* mask, const float* b, int64_t zb,
+                           float* y, int64_t ldy, int64_t zy, int64_t M, int N, int nz, int act, hipStream_t s) {
+  RowGemmArgs p{};
+  p.a0 = ctx;
+  p.lda0 = ldc;
+  p.ka0 = C;
+  p.za0 = zc;
+  p.a1 = x;
+  p.lda1 = ldx;
+  p.ka1 = Kx;
+  p.za1 = zx;
+  p.b = W;
+  p.sbk = 1;
+  p.sbn = C + Kx;
+  p.zb = zw;
+  p.mask = mask;
+  p.smk = 1;
+  p.smn = C + Kx;
+  p.bias = b;
+  p.zbias = zb;
+  p.c = y;
+  p.ldc = ldy;
+  p.zc = zy;
+  p.M = M;
+  p.N = N;
+  p.act = act;
+  p.accumulate = 0;
+  return rowgemm(p, s, nz);
 }
 
 // gemm() fast paths; return 1 when the shape was not taken (caller falls back)

@@ -35,6 +35,9 @@ int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, cons
 // gemm_rows.hip: batch-row GEMMs (forward linear layers, dX, dW)
 int rowgemm_linear(const float* ctx, int64_t ldc, int C, const float* x, int64_t ldx, int Kx, const float* W,
                    const float* mask, const float* b, float* y, int64_t ldy, int64_t M, int N, int act, hipStream_t s);
+int rowgemm_linear_batched(const float* ctx, int64_t ldc, int64_t zc, int C, const float* x, int64_t ldx, int64_t zx,
+                           int Kx, const float* W, int64_t zw, const float* mask, const float* b, int64_t zb,
+                           float* y, int64_t ldy, int64_t zy, int64_t M, int N, int nz, int act, hipStream_t s);
 int gemm_rows_try(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
                   int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
                   int mask_b, int accumulate, float* rowsum, hipStream_t s, int* rc);

@@ -1,0 +1,310 @@
+"""Batched-over-parameters affine MAF: the Bayesian front end's log_prob / sampler on MI355X
+(SURVEY.md §8f rank 1 and rank 2).
+
+naz's Bayesian flows (``naz/flows/bflow_jax_maf.py``) evaluate ONE trained affine MAF under
+many weight draws θ_p — HMC / SVI posterior and prior draws of ``flat_params * (1 + scale *
+standard_params)`` (``bflow_jax_maf.py:214-236``) — over the same rows: the density grid of
+``plot.py:192-204`` / ``plot_svi.py:184-196``, the training set inside NUTS
+(``hmc_maf_exact.py:128-133``), and 10^6 posterior-predictive samples per draw
+(``calibrate.py:145-151``).  The reference runs ``flow["lp"](θ_p)`` / ``flow["sampler"](θ_p,
+key, n)`` once per draw in a Python loop.  Here all draws of a chunk run together:
+
+* ``lp_batched(params) -> [P, B]``: the degree-scheduled D-pass inverse (``nn.ARInversePlan``)
+  with every GEMM one ``naz_linear_act_batched`` launch over (row tiles × column blocks ×
+  draws); the schedule depends only on the masks and permutation, so it is built once on
+  index-valued weights and each draw set is packed by one gather per block;
+* ``sampler_batched(params, key, size) -> ([P, size, D], log_j [P, size])``: one masked MADE
+  pass per layer (``naz_linear_act_batched`` with the shared mask) + ``naz_affine_ar``.
+
+``params`` is the reference's pytree (``torch_to_jax``: a list per layer of ``(W, b)`` per
+MADE linear) with a leading draw axis on every leaf, i.e. what ``jax.vmap(unravel_fn)`` of
+posterior draws gives (``plot.py:140``); ``unravel`` maps the flat ``[P, n]`` draws
+(``ravel_pytree`` order) to it.  Scope: ``bounds=None`` and no skip connections (what the
+examples use); the bounded branch raises ``NotImplementedError`` (it also carries the
+reference's sign bug, ``bflow_jax_maf.py:198-212``).  The sampler takes an integer seed or a
+``torch.Generator`` as ``rng_key``: JAX's PRNG stream is not reproduced, only its distribution.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+
+from .. import ops
+from ..nn import create_mask, degree_schedule
+
+__all__ = ["torch_to_jax", "make_conditional_autoregressive_nn", "make_masked_affine_autoregressive_transform",
+           "make_normalizing_flow", "ravel", "unravel", "MAFSpec"]
+
+Params = List[List[Tuple[Tensor, Tensor]]]
+
+
+def torch_to_jax(torch_maf):
+    """naz ``torch_to_jax`` (bflow_jax_maf.py:26-46) over a naz_amd ``maf`` flow: (params,
+    param_shapes, masks, mask_skips, permutations), tensors kept on the flow's device."""
+    params, shapes, masks, skips, perms = [], [], [], [], []
+    for t in torch_maf.flow_dist.transforms:
+        arn = t.nn
+        these = [(l.weight.detach().clone(), l.bias.detach().clone()) for l in arn.layers]
+        params.append(these)
+        shapes.append([(tuple(w.shape), tuple(b.shape)) for (w, b) in these])
+        masks.append([m.detach().to(torch.float32).clone() for m in arn.masks])
+        skips.append(arn.mask_skip.detach().to(torch.float32).clone())
+        perms.append(arn.permutation.detach().clone())
+    return params, shapes, masks, skips, perms
+
+
+class MAFSpec:
+    """What ``make_conditional_autoregressive_nn`` closes over (bflow_jax_maf.py:79-167)."""
+
+    def __init__(self, input_dim: int, context_dim: int, hidden_dims: Sequence[int], activation: str = "tanh"):
+        self.input_dim, self.context_dim = int(input_dim), int(context_dim)
+        self.hidden_dims = [int(h) for h in hidden_dims]
+        self.activation = activation
+        self.param_shapes = [((self.hidden_dims[0], self.input_dim + self.context_dim), (self.hidden_dims[0],))]
+        for i in range(1, len(self.hidden_dims)):
+            self.param_shapes.append(((self.hidden_dims[i], self.hidden_dims[i - 1]), (self.hidden_dims[i],)))
+        self.param_shapes.append(((2 * self.input_dim, self.hidden_dims[-1]), (2 * self.input_dim,)))
+
+
+def make_conditional_autoregressive_nn(input_dim: int, context_dim: int, hidden_dims: Sequence[int],
+                                       param_dims: Sequence[int] = (1, 1), permutation=None,
+                                       skip_connections: bool = False, activation_fn: str = "tanh",
+                                       simple_masking: bool = True):
+    """bflow_jax_maf.py:79-167: returns (nn_spec, param_shapes, generate_mask).  Affine MAF
+    conditioners only (param_dims [1, 1]), simple masking, no skip connections."""
+    if list(param_dims) != [1, 1]:
+        raise NotImplementedError("batched MAF: param_dims [1, 1] (affine) only")
+    if skip_connections or not simple_masking:
+        raise NotImplementedError("batched MAF: skip connections / random masking are not built")
+    if activation_fn not in ("tanh", "relu", "sigmoid", "identity"):
+        raise ValueError(f"unsupported activation {activation_fn!r}")
+    spec = MAFSpec(input_dim, context_dim, hidden_dims, activation_fn)
+
+    def generate_mask(permutation=permutation):
+        perm = torch.randperm(input_dim) if permutation is None else torch.as_tensor(permutation)
+        masks, mask_skip = create_mask(input_dim, context_dim, spec.hidden_dims, perm, 2)
+        return [m.to(torch.float32) for m in masks], mask_skip.to(torch.float32), perm
+
+    return spec, spec.param_shapes, generate_mask
+
+
+def make_masked_affine_autoregressive_transform(nn_fn: MAFSpec, input_dim: int, context=None):
+    """bflow_jax_maf.py:169-194: the (forward, inverse) pair is what ``make_normalizing_flow``
+    runs; here it is the spec it runs with."""
+    if nn_fn.input_dim != input_dim:
+        raise ValueError("input_dim does not match the conditioner")
+    return nn_fn
+
+
+def ravel(params: Params) -> Tensor:
+    """``ravel_pytree`` order (layer-major, (W, b) per linear, row-major) of a single-draw
+    ([o, i] leaves -> [n]) or batched ([P, o, i] leaves -> [P, n]) pytree."""
+    leaves = [t for layer in params for wb in layer for t in wb]
+    batched = leaves[0].dim() == 3
+    return torch.cat([t.reshape(t.shape[0], -1) if batched else t.reshape(-1) for t in leaves], dim=-1)
+
+
+def unravel(flat: Tensor, param_shapes) -> Params:
+    """Inverse of ``ravel`` (bflow_jax_maf.py:214-216's ``unravel_fn``, vmapped over a leading
+    draw axis when ``flat`` is [P, n])."""
+    lead = flat.shape[:-1]
+    need = sum(int(torch.tensor(ws).prod()) + int(torch.tensor(bs).prod()) for layer in param_shapes
+               for (ws, bs) in layer)
+    if need != flat.shape[-1]:
+        raise ValueError(f"flat params have {flat.shape[-1]} entries, the shapes need {need}")
+    out, off = [], 0
+    for layer in param_shapes:
+        these = []
+        for ws, bs in layer:
+            nw, nb = int(torch.tensor(ws).prod()), int(torch.tensor(bs).prod())
+            w = flat[..., off:off + nw].reshape(*lead, *ws)
+            b = flat[..., off + nw:off + nw + nb].reshape(*lead, *bs)
+            off += nw + nb
+            these.append((w, b))
+        out.append(these)
+    return out
+
+
+class _LayerPlan:
+    """Degree schedule of one MAF layer as gather maps into its per-draw flat buffer
+    ``F[p] = [0, W0.flat, b0, W1.flat, b1, ...]`` (index 0 = a structural zero)."""
+
+    def __init__(self, masks: List[Tensor], perm: Tensor, spec: MAFSpec):
+        D, C = spec.input_dim, spec.context_dim
+        cpu = dict(device="cpu", dtype=torch.float64)
+        wi, bi, off = [], [], 1
+        for (ws, bs) in spec.param_shapes:
+            nw, nb = ws[0] * ws[1], bs[0]
+            wi.append(torch.arange(off, off + nw, **cpu).reshape(ws))
+            bi.append(torch.arange(off + nw, off + nw + nb, **cpu))
+            off += nw + nb
+        self.size = off
+        self.masks = [m.to(**cpu) for m in masks]
+        widths, hidden, outs = degree_schedule(perm.cpu(), self.masks, wi, bi, D, C, 2)
+        self.widths = widths
+        self.hidden = [[(li, a, b, n, wb.round().long(), bb.round().long()) for (li, a, b, n, wb, bb) in g]
+                       for g in hidden]
+        self.outs = [(i, n, wb.round().long(), bb.round().long()) for (i, n, wb, bb) in outs]
+
+    def to(self, dev):
+        self.hidden = [[(li, a, b, n, w.to(dev), bb.to(dev)) for (li, a, b, n, w, bb) in g] for g in self.hidden]
+        self.outs = [(i, n, w.to(dev), bb.to(dev)) for (i, n, w, bb) in self.outs]
+        self.masks_dev = [m.to(dev, torch.float32) for m in self.masks]
+        return self
+
+
+def _draws(params: Params) -> int:
+    return params[0][0][0].shape[0]
+
+
+def _flat_layer(layer, P, dev):
+    """F[p] = [0, W0, b0, W1, b1, ...] for one layer of a batched pytree: [P, size]."""
+    parts = [torch.zeros((P, 1), device=dev, dtype=torch.float32)]
+    for (w, b) in layer:
+        parts += [w.reshape(P, -1).to(dev, torch.float32), b.reshape(P, -1).to(dev, torch.float32)]
+    return torch.cat(parts, dim=1)
+
+
+def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bounds=None, context=None,
+                          rows_per_chunk: int = 1 << 23) -> Dict[str, object]:
+    """naz ``make_normalizing_flow`` (bflow_jax_maf.py:196-225) on MI355X.  Returns
+    ``{"lp": f(params) -> [B], "sampler": f(params, rng_key, size) -> (y, log_j),
+    "lp_batched": f(params_P) -> [P, B], "sampler_batched": f(params_P, rng_key, size)}``.
+
+    ``x`` [B, D] are the evaluation rows; ``context`` None, [C] (broadcast) or [B, C].  The
+    single-draw functions are the batched ones at P = 1.  ``rows_per_chunk`` bounds the draws
+    evaluated together (activation memory ≈ 4·rows·Σwidths bytes)."""
+    if bounds is not None:
+        raise NotImplementedError("batched MAF: bounds=None only (see module docstring)")
+    spec = transform
+    D, C = spec.input_dim, spec.context_dim
+    x = torch.as_tensor(x)
+    dev = x.device
+    if dev.type != "cuda":
+        raise RuntimeError("naz_amd batched MAF runs on the GPU only; pass x on a cuda device")
+    x = x.to(torch.float32).contiguous()
+    if x.dim() != 2 or x.shape[1] != D:
+        raise ValueError(f"x must be [B, {D}]")
+    B = x.shape[0]
+    ctx = None
+    if C:
+        if context is None:
+            raise ValueError("conditional flow needs a context")
+        ctx = torch.as_tensor(context, device=dev, dtype=torch.float32).contiguous()
+        if ctx.shape[-1] != C or (ctx.dim() == 2 and ctx.shape[0] not in (1, B)):
+            raise ValueError(f"context must be [{C}] or [B, {C}]")
+    plans = [_LayerPlan(m, p, spec).to(dev) for (m, p) in zip(masks, perms)]
+    act = spec.activation
+    width_sum = max(sum(pl.widths) for pl in plans)
+
+    def _chunks(P, rows):
+        per = max(1, min(P, 65535, rows_per_chunk // max(rows, 1)))
+        return [(p0, min(P, p0 + per)) for p0 in range(0, P, per)]
+
+    def _pack(layer, plan, P):
+        F = _flat_layer(layer, P, dev)
+        hidden = [[(li, a, b, n, F[:, w], F[:, bb]) for (li, a, b, n, w, bb) in g] for g in plan.hidden]
+        outs = [(i, n, F[:, w], F[:, bb]) for (i, n, w, bb) in plan.outs]
+        return hidden, outs
+
+    def _lp_chunk(params: Params, out: Tensor):
+        """out [P, B] <- log p(x | θ_p): reversed layers, D degree-scheduled passes each."""
+        P = _draws(params)
+        z = x.expand(P, B, D).contiguous()
+        lp = out.reshape(P * B)
+        lp.zero_()
+        hs_all = torch.empty((P, B, width_sum), device=dev, dtype=torch.float32)
+        for l in reversed(range(len(plans))):
+            plan = plans[l]
+            hidden, outs = _pack(params[l], plan, P)
+            hs, o = [], 0
+            for w in plan.widths:
+                hs.append(hs_all[:, :, o:o + w])
+                o += w
+            xn = torch.zeros_like(z)
+            z2, x2 = z.view(P * B, D), xn.view(P * B, D)
+            for k in range(1, D + 1):
+                for (li, a, b, n, wb, bb) in hidden[k - 1]:
+                    dst = hs[li][:, :, a:b]
+                    if li == 0:
+                        ops.linear_act_batched(xn, wb, bb, act, context=ctx, out=dst)
+                    else:
+                        ops.linear_act_batched(hs[li - 1][:, :, :n], wb, bb, act, out=dst)
+                i, n, wb, bb = outs[k - 1]
+                if n:
+                    raw = ops.linear_act_batched(hs[-1][:, :, :n], wb, bb, "identity").reshape(P * B, 2)
+                else:  # the first dim in order sees only the bias (unconditional layer)
+                    raw = bb.reshape(P, 1, 2).expand(P, B, 2).reshape(P * B, 2)
+                ops.affine_ar(z2[:, i:i + 1], raw, True, ops.LD_ROWSUM_SUB, lp, out=x2[:, i:i + 1])
+            z = xn
+        ops.base_log_prob(z.view(P * B, D), out=lp, accumulate=True)
+
+    def lp_batched(params: Params) -> Tensor:
+        P = _draws(params)
+        out = torch.empty((P, B), device=dev, dtype=torch.float32)
+        for p0, p1 in _chunks(P, B * max(1, width_sum // 64)):
+            _lp_chunk([[(w[p0:p1], b[p0:p1]) for (w, b) in layer] for layer in params], out[p0:p1])
+        return out
+
+    def _sample_chunk(params: Params, z: Tensor, y_out: Tensor, lj_out: Tensor):
+        """JAX forward_fn composed in flow order (bflow_jax_maf.py:172-178, 218-222):
+        log_j = base(z) + Σ clip(ls) (the reference's returned quantity, sign as there)."""
+        P, S = z.shape[0], z.shape[1]
+        lj = lj_out.reshape(P * S)
+        ops.base_log_prob(z.reshape(P * S, D), out=lj)
+        cur = z
+        for l, plan in enumerate(plans):
+            h = None
+            layer = params[l]
+            nlin = len(layer)
+            for j, (w, b) in enumerate(layer):
+                m = plan.masks_dev[j]
+                a = "identity" if j == nlin - 1 else act
+                w, b = w.to(torch.float32), b.to(torch.float32)
+                if j == 0:
+                    h = ops.linear_act_batched(cur, w, b, a, context=ctx_s, mask=m)
+                else:
+                    h = ops.linear_act_batched(h, w, b, a, mask=m)
+            nxt = y_out if l == len(plans) - 1 else torch.empty_like(cur)
+            ops.affine_ar(cur.reshape(P * S, D), h.reshape(P * S, 2 * D), False, ops.LD_ROWSUM_ADD, lj,
+                          out=nxt.view(P * S, D))
+            cur = nxt
+
+    def sampler_batched(params: Params, rng_key: Union[int, torch.Generator, None] = None, size: int = 1,
+                        z: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+        nonlocal ctx_s
+        P = _draws(params)
+        S = int(size)
+        if z is None:
+            g = rng_key if isinstance(rng_key, torch.Generator) else \
+                torch.Generator(device=dev).manual_seed(int(rng_key or 0))
+            z = torch.randn((P, S, D), device=dev, dtype=torch.float32, generator=g)
+        else:
+            z = z.to(dev, torch.float32).reshape(P, S, D).contiguous()
+        if C:
+            if ctx.dim() != 1 and ctx.shape[0] != 1:
+                raise ValueError("sampler: the reference conditions on one context vector")
+            ctx_s = ctx.reshape(-1)
+        y = torch.empty((P, S, D), device=dev, dtype=torch.float32)
+        lj = torch.empty((P, S), device=dev, dtype=torch.float32)
+        for p0, p1 in _chunks(P, S * max(1, sum(spec.hidden_dims) // 64)):
+            _sample_chunk([[(w[p0:p1], b[p0:p1]) for (w, b) in layer] for layer in params], z[p0:p1], y[p0:p1],
+                          lj[p0:p1])
+        return y, lj
+
+    ctx_s = None
+
+    def _one(params):
+        return [[(w.unsqueeze(0), b.unsqueeze(0)) for (w, b) in layer] for layer in params]
+
+    def lp(params: Params) -> Tensor:
+        return lp_batched(_one(params))[0]
+
+    def sampler(params: Params, rng_key=None, size: int = 1):
+        y, lj = sampler_batched(_one(params), rng_key, size)
+        return y[0], lj[0]
+
+    return {"lp": lp, "sampler": sampler, "lp_batched": lp_batched, "sampler_batched": sampler_batched,
+            "plans": plans}

@@ -226,6 +226,70 @@ class ConditionalAutoRegressiveNN(nn.Module):
         return self._shape(self.raw(x, context), x.shape[:-1])
 
 
+def degree_schedule(perm: torch.Tensor, masks, weights, biases, D: int, C: int, mult: int):
+    """The degree schedule of ``ARInversePlan`` (see there) from float64 CPU tensors: per layer
+    mask, weight, bias (pyro's MaskedLinear order).  Returns (widths, hidden, outs):
+    hidden[g] = [(layer, a, b, n, w_block [b-a, n], bias_block [b-a])] run in pass g + 1,
+    outs[k-1] = (dim i, n, w_rows [mult, max(n, 1)], bias_rows [mult]) of pass k.  Every block
+    entry is one masked weight (or 0), so the schedule is linear in the weights: run on
+    index-valued weights it yields the gather map of a per-draw pack (flows/bflow_maf.py)."""
+    if len(weights) < 2:
+        raise ValueError("MADE conditioner without hidden layers")
+    order = torch.empty(D, dtype=torch.float64)
+    order[perm] = torch.arange(1, D + 1, dtype=torch.float64)  # var perm[j] has order j + 1
+    prev_deg = torch.cat((torch.zeros(C, dtype=torch.float64), order))
+    prev_cols = None  # previous layer: padded column of each unit (None = natural [ctx | x])
+    prev_ends = None  # previous layer: padded column end of degree groups <= m
+    hidden = [[] for _ in range(D)]  # hidden[m] = blocks of degree m (run in pass m + 1)
+    widths = []
+    for li in range(len(weights) - 1):
+        m = masks[li]
+        deg = (m * prev_deg[None, :]).amax(dim=1)  # max order reached (0: context/bias only)
+        w = weights[li] * m
+        bias = biases[li]
+        cols = torch.empty(w.shape[0], dtype=torch.int64)
+        ends, off = [], 0
+        for g in range(D):
+            units = torch.nonzero(deg == g).flatten()
+            a = off
+            cols[units] = torch.arange(a, a + units.numel())
+            off = a + (units.numel() + 3) // 4 * 4
+            ends.append(off)
+            if units.numel() == 0:
+                continue
+            if prev_cols is None:
+                n = C + D
+                wb = torch.zeros(off - a, n, dtype=torch.float64)
+                wb[:units.numel()] = w[units]
+            else:
+                n = prev_ends[g]
+                wb = torch.zeros(off - a, prev_ends[-1], dtype=torch.float64)
+                wb[:units.numel(), prev_cols] = w[units]  # inputs scattered to padded columns
+                wb = wb[:, :n]
+            bb = torch.zeros(off - a, dtype=torch.float64)
+            bb[:units.numel()] = bias[units]
+            hidden[g].append((li, a, off, n, wb, bb))
+        if deg.max() >= D:
+            raise RuntimeError("MADE masks: a hidden unit sees a variable of order D")
+        widths.append(off)
+        prev_deg, prev_cols, prev_ends = deg, cols, ends
+    # output rows of each dim (flat column p*D + i), from last-layer groups < order(i)
+    m = masks[-1]
+    w = weights[-1] * m
+    bias = biases[-1]
+    outs = []
+    for k in range(1, D + 1):
+        i = int(perm[k - 1])
+        rows = torch.tensor([p * D + i for p in range(mult)])
+        if ((m[rows] * prev_deg[None, :]).amax() if m.shape[1] else 0) >= k:
+            raise RuntimeError("MADE masks are not autoregressive in the permutation's order")
+        n = prev_ends[k - 1]
+        full = torch.zeros(mult, prev_ends[-1], dtype=torch.float64)
+        full[:, prev_cols] = w[rows]
+        outs.append((i, n, full[:, :max(n, 1)], bias[rows]))
+    return widths, hidden, outs
+
+
 class _InverseBlock:
     """One GEMM of the degree-scheduled inverse: columns [a, b) of a layer's (padded, degree-sorted)
     activation from input columns [0, n) of the previous one (layer 0: the full [ctx | x])."""
@@ -263,69 +327,17 @@ class ARInversePlan:
 
     def _build(self):
         arn = self.arn
-        D, C, mult = arn.input_dim, arn.context_dim, arn.output_multiplier
         layers = list(arn.layers)
-        if len(layers) < 2:
-            raise ValueError("MADE conditioner without hidden layers")
-        perm = arn.permutation.cpu()
-        order = torch.empty(D, dtype=torch.float64)
-        order[perm] = torch.arange(1, D + 1, dtype=torch.float64)  # var perm[j] has order j + 1
-        prev_deg = torch.cat((torch.zeros(C, dtype=torch.float64), order))
-        prev_cols = None  # previous layer: padded column of each unit (None = natural [ctx | x])
-        prev_ends = None  # previous layer: padded column end of degree groups <= m
-        hidden = [[] for _ in range(D)]  # hidden[m] = blocks of degree m (run in pass m + 1)
-        widths = []
         dev = layers[0].weight.device
-        for li, layer in enumerate(layers[:-1]):
-            m = layer.mask.detach().to("cpu", torch.float64)
-            deg = (m * prev_deg[None, :]).amax(dim=1)  # max order reached (0: context/bias only)
-            w = layer.masked_weight().detach().to("cpu", torch.float64)
-            bias = layer.bias.detach().to("cpu", torch.float64)
-            cols = torch.empty(layer.out_features, dtype=torch.int64)
-            ends, off = [], 0
-            for g in range(D):
-                units = torch.nonzero(deg == g).flatten()
-                a = off
-                cols[units] = torch.arange(a, a + units.numel())
-                off = a + (units.numel() + 3) // 4 * 4
-                ends.append(off)
-                if units.numel() == 0:
-                    continue
-                if prev_cols is None:
-                    n = C + D
-                    wb = torch.zeros(off - a, n, dtype=torch.float64)
-                    wb[:units.numel()] = w[units]
-                else:
-                    n = prev_ends[g]
-                    wb = torch.zeros(off - a, prev_ends[-1], dtype=torch.float64)
-                    wb[:units.numel(), prev_cols] = w[units]  # inputs scattered to padded columns
-                    wb = wb[:, :n]
-                bb = torch.zeros(off - a, dtype=torch.float64)
-                bb[:units.numel()] = bias[units]
-                hidden[g].append((li, a, off, n, wb, bb))
-            if deg.max() >= D:
-                raise RuntimeError("MADE masks: a hidden unit sees a variable of order D")
-            widths.append(off)
-            prev_deg, prev_cols, prev_ends = deg, cols, ends
-        # output rows of each dim (flat column p*D + i), from last-layer groups < order(i)
-        out = layers[-1]
-        m = out.mask.detach().to("cpu", torch.float64)
-        w = out.masked_weight().detach().to("cpu", torch.float64)
-        bias = out.bias.detach().to("cpu", torch.float64)
-        outs = []
-        for k in range(1, D + 1):
-            i = int(perm[k - 1])
-            rows = torch.tensor([p * D + i for p in range(mult)])
-            if ((m[rows] * prev_deg[None, :]).amax() if m.shape[1] else 0) >= k:
-                raise RuntimeError("MADE masks are not autoregressive in the permutation's order")
-            n = prev_ends[k - 1]
-            full = torch.zeros(mult, prev_ends[-1], dtype=torch.float64)
-            full[:, prev_cols] = w[rows]
-            outs.append((i, n, full[:, :max(n, 1)], bias[rows]))
+        cpu = dict(device="cpu", dtype=torch.float64)
+        widths, hidden, outs = degree_schedule(
+            arn.permutation.cpu(), [l.mask.detach().to(**cpu) for l in layers],
+            [l.weight.detach().to(**cpu) for l in layers], [l.bias.detach().to(**cpu) for l in layers],
+            arn.input_dim, arn.context_dim, arn.output_multiplier)
         f32 = dict(device=dev, dtype=torch.float32)
         self.widths = widths
         self.hidden = [[(li, _InverseBlock(a, b, n, wb.to(**f32).contiguous(), bb.to(**f32)))
-                        for (li, a, b, n, wb, bb) in hidden[g]] for g in range(D)]
+                        for (li, a, b, n, wb, bb) in hidden[g]] for g in range(arn.input_dim)]
         self.outs = [(i, n, wb.to(**f32).contiguous(), bb.to(**f32).contiguous()) for (i, n, wb, bb) in outs]
 
     def plan(self):

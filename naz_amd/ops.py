@@ -16,7 +16,7 @@ from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, RQS_FAST, LD_PERDIM, LD_ROWSUM
 
 Tensor = torch.Tensor
 
-__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "affine_ar", "affine_ar_bwd", "base_log_prob",
+__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
            "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate",
@@ -144,6 +144,57 @@ def linear_act(x: Optional[Tensor], weight: Tensor, bias: Optional[Tensor], act:
             torch.empty((M, N), device=dev, dtype=torch.float32)
     check(lib().naz_linear_act(_p(context), ldc, C, _p(x), ldx, Kx, _p(weight), _p(mask), _p(bias), _p(out),
                                out.stride(0), M, N, ACT[act], _stream(dev)), "linear_act")
+    return out
+
+
+def linear_act_batched(x: Optional[Tensor], weight: Tensor, bias: Optional[Tensor], act: str = "identity",
+                       context: Optional[Tensor] = None, mask: Optional[Tensor] = None,
+                       out: Optional[Tensor] = None) -> Tensor:
+    """Per-draw conditioner layer (naz_linear_act_batched):
+    out[z] = act(cat([context[z], x[z]]) @ (weight[z] * mask)^T + bias[z]) for z < P.
+
+    x / out: [P, M, *] with unit column stride (any row stride, draw stride); weight [P, N, C+Kx]
+    and bias [P, N] contiguous; context [C] / [M, C] (shared by every draw) or [P, M, C]."""
+    dev = _dev(x, weight, bias, context, mask)
+    P, N = weight.shape[0], weight.shape[1]
+    C = 0 if context is None else context.shape[-1]
+    Kx = 0 if x is None else x.shape[-1]
+    M = x.shape[1] if x is not None else (context.shape[-2] if context.dim() >= 2 else 1)
+
+    def _pm(t, what):  # (draw stride, row stride) of a [P, M, k] operand with unit column stride
+        if t.stride(-1) != 1 or t.shape[:2] != (P, M):
+            raise ValueError(f"{what} must be [P={P}, M={M}, *] with unit column stride, got "
+                             f"{tuple(t.shape)} / {t.stride()}")
+        return t.stride(0), t.stride(1)
+
+    sctx = ldc = 0
+    if context is not None:
+        if context.dim() == 3:
+            sctx, ldc = _pm(context, "context")
+        else:
+            context = context.reshape(-1, C).contiguous()
+            if context.shape[0] not in (1, M):
+                raise ValueError("context rows must match x rows (or be a single row)")
+            ldc = 0 if context.shape[0] == 1 else C
+    sx = ldx = 0
+    if x is not None:
+        sx, ldx = _pm(x, "x")
+    if weight.shape != (P, N, C + Kx):
+        raise ValueError(f"weight must be [P, N, {C + Kx}], got {tuple(weight.shape)}")
+    weight = weight.contiguous()
+    if bias is not None:
+        if bias.shape != (P, N):
+            raise ValueError(f"bias must be [P, N] = {(P, N)}, got {tuple(bias.shape)}")
+        bias = bias.contiguous()
+    if mask is not None:
+        mask = mask.to(torch.float32).contiguous()
+    if out is None:
+        npad = (N + 3) // 4 * 4
+        out = torch.empty((P, M, npad), device=dev, dtype=torch.float32)[:, :, :N]
+    sy, ldy = _pm(out, "out")
+    check(lib().naz_linear_act_batched(_p(context), ldc, sctx, C, _p(x), ldx, sx, Kx, _p(weight), N * (C + Kx),
+                                       _p(mask), _p(bias), N, _p(out), ldy, sy, M, N, P, ACT[act], _stream(dev)),
+          "linear_act_batched")
     return out
 
 

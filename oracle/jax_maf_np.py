@@ -66,12 +66,22 @@ def inverse_fn(y: np.ndarray, params, masks, perm, context=None):
     return x, np.sum(np.clip(log_scale, -5.0, 3.0), axis=-1)
 
 
-def log_prob(x: np.ndarray, layers, context=None):
+def cast_layers(layers, dtype):
+    """The same layers with weights, biases and masks in ``dtype`` (float32 = the reference's
+    own arithmetic precision, the ``ref32`` of tests/parity.py)."""
+    return [([(W.astype(dtype), b.astype(dtype)) for (W, b) in params], perm, [m.astype(dtype) for m in masks])
+            for params, perm, masks in layers]
+
+
+def log_prob(x: np.ndarray, layers, context=None, dtype=np.float64):
     """bflow_jax_maf.py:210-212 with bounds=None.  ``layers`` = list of (params, perm) in
-    flow order; reversed here as the reference's ``reduce(inv_transform, zip(reversed(...)))``."""
+    flow order; reversed here as the reference's ``reduce(inv_transform, zip(reversed(...)))``.
+    ``dtype`` float32 evaluates at the reference's precision (layers must be cast alike)."""
     D = x.shape[-1]
-    z = x.astype(np.float64)
-    log_det = np.zeros(x.shape[:-1])
+    z = x.astype(dtype)
+    if context is not None:
+        context = np.asarray(context).astype(dtype)
+    log_det = np.zeros(x.shape[:-1], dtype=dtype)
     for params, perm, masks in reversed(layers):
         z, ld = inverse_fn(z, params, masks, perm, context)
         log_det = log_det + ld
@@ -90,3 +100,25 @@ def layers_from_state(spec: dict, state: dict):
         masks = create_mask(spec["D"], spec["C"], hidden, perm, 2)
         out.append((params, perm, masks))
     return out
+
+
+def forward_fn(x: np.ndarray, params, masks, context=None):
+    """bflow_jax_maf.py:172-178: one MADE pass, y = mean + x * exp(clip(ls, -5, 3))."""
+    mean, log_scale = nn_fn(x, params, masks, context, x.shape[-1])
+    log_scale = np.clip(log_scale, -5.0, 3.0)
+    return mean + x * np.exp(log_scale), np.sum(log_scale, axis=-1)
+
+
+def sample_from_z(z: np.ndarray, layers, context=None, dtype=np.float64):
+    """bflow_jax_maf.py:214-222 (``sampler``) with the base draws ``z`` given (JAX's PRNG is not
+    restated) and bounds=None: layers in flow order; returns (y, log_j) with
+    log_j = base log-density of z + Σ clip(ls), the sign the reference returns."""
+    D = z.shape[-1]
+    y = z.astype(dtype)
+    if context is not None:
+        context = np.asarray(context).astype(dtype)
+    log_j = -np.sum(0.5 * y ** 2, axis=-1) - 0.5 * D * math.log(2 * math.pi)
+    for params, perm, masks in layers:
+        y, ld = forward_fn(y, params, masks, context)
+        log_j = log_j + ld
+    return y, log_j

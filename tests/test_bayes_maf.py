@@ -1,0 +1,193 @@
+"""Batched-over-parameters affine MAF (naz_amd.flows.bflow_maf): the
+Bayesian front end's ``make_normalizing_flow(...)["lp"]`` / ``["sampler"]`` (naz
+bflow_jax_maf.py:196-225) evaluated for P weight draws at once.
+
+CPU: the per-draw pack (gather map built from index-valued weights) reproduces the degree
+schedule of the real weights, and ravel/unravel follow ``ravel_pytree`` order.
+GPU: every draw's log_prob vs the numpy restatement of the reference's own JAX MAF
+(oracle/jax_maf_np.py) in float64, with its float32 run as ref32 (tests/parity.py); sampler
+vs the restated forward pass on the same base draws; the single-draw functions vs the
+batched ones; the sample -> log_prob round trip."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import jax_maf_np as J
+from oracle import naz_oracle as O
+from tests.parity import assert_parity
+
+CASES = [
+    dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=3, P=6, B=700, ctx="vec"),  # paper shape
+    dict(flow_type="maf", D=4, C=0, hidden=[32, 32], L=2, P=5, B=513, ctx=None),
+    dict(flow_type="maf", D=3, C=5, hidden=[40, 24], L=2, P=3, B=300, ctx="rows"),
+]
+
+
+def _setup(spec, seed=7):
+    """Base weights (the MLE flow), P perturbed draws as the Bayesian model makes them
+    (params = flat * (1 + scale * u), u ~ U(-1, 1), bflow_jax_maf.py:224-226), eval rows."""
+    st = {k: v.numpy() for k, v in O.random_state(spec, seed=seed).items()}
+    layers = J.layers_from_state(spec, st)  # [(params64, perm, masks64)] in flow order
+    rng = np.random.default_rng(seed)
+    P, B, D, C = spec["P"], spec["B"], spec["D"], spec["C"]
+    draws = []
+    for _ in range(P):
+        draws.append([[(W * (1 + 0.25 * rng.uniform(-1, 1, W.shape)), b * (1 + 0.25 * rng.uniform(-1, 1, b.shape)))
+                       for (W, b) in params] for params, _, _ in layers])
+    draws = [[[(W.astype(np.float32).astype(np.float64), b.astype(np.float32).astype(np.float64))
+               for (W, b) in lay] for lay in d] for d in draws]
+    x = (1.5 * rng.standard_normal((B, D))).astype(np.float32)
+    ctx = None
+    if spec["ctx"] == "vec":
+        ctx = rng.standard_normal(C).astype(np.float32)
+    elif spec["ctx"] == "rows":
+        ctx = rng.standard_normal((B, C)).astype(np.float32)
+    return layers, draws, x, ctx
+
+
+def _oracle_layers(layers, draw):
+    return [(draw[l], perm, masks) for l, (_, perm, masks) in enumerate(layers)]
+
+
+def _batched_params(draws, dev):
+    """[P] pytrees -> one pytree with a leading draw axis (what jax.vmap(unravel_fn) gives)."""
+    L, n = len(draws[0]), len(draws[0][0])
+    return [[(torch.tensor(np.stack([d[l][i][0] for d in draws]), dtype=torch.float32, device=dev),
+              torch.tensor(np.stack([d[l][i][1] for d in draws]), dtype=torch.float32, device=dev))
+             for i in range(n)] for l in range(L)]
+
+
+def _flow(spec, layers, x, ctx, dev):
+    from naz_amd.flows import bflow_maf as BM
+    nn_spec, _, _ = BM.make_conditional_autoregressive_nn(spec["D"], spec["C"], spec["hidden"])
+    tr = BM.make_masked_affine_autoregressive_transform(nn_spec, spec["D"])
+    masks = [[torch.tensor(m, dtype=torch.float32) for m in ms] for _, _, ms in layers]
+    perms = [torch.tensor(p) for _, p, _ in layers]
+    c = None if ctx is None else torch.tensor(ctx, device=dev)
+    return BM.make_normalizing_flow(tr, torch.tensor(x, device=dev), masks, [None] * len(layers), perms,
+                                    context=c)
+
+
+# ----------------------------------------------------------------------------- CPU
+@pytest.mark.parametrize("spec", CASES[:2], ids=lambda s: f"D{s['D']}C{s['C']}")
+def test_pack_gather_map_matches_schedule(spec):
+    """The gather map (schedule on index-valued weights) picks exactly the entries the degree
+    schedule places when run on the real weights (naz_amd.nn.degree_schedule)."""
+    from naz_amd.flows import bflow_maf as BM
+    from naz_amd.nn import degree_schedule
+    layers, draws, _, _ = _setup(spec)
+    nn_spec, _, _ = BM.make_conditional_autoregressive_nn(spec["D"], spec["C"], spec["hidden"])
+    for l, (_, perm, masks) in enumerate(layers):
+        plan = BM._LayerPlan([torch.tensor(m) for m in masks], torch.tensor(perm), nn_spec)
+        params = draws[0][l]
+        F = torch.cat([torch.zeros(1, dtype=torch.float64)] +
+                      [torch.cat((torch.tensor(W).reshape(-1), torch.tensor(b))) for (W, b) in params])
+        assert F.numel() == plan.size
+        widths, hidden, outs = degree_schedule(
+            torch.tensor(perm), [torch.tensor(m) for m in masks], [torch.tensor(W) for W, _ in params],
+            [torch.tensor(b) for _, b in params], spec["D"], spec["C"], 2)
+        assert widths == plan.widths
+        for g in range(spec["D"]):
+            assert len(hidden[g]) == len(plan.hidden[g])
+            for (li, a, b, n, wb, bb), (li2, a2, b2, n2, wi, bi) in zip(hidden[g], plan.hidden[g]):
+                assert (li, a, b, n) == (li2, a2, b2, n2)
+                assert torch.equal(F[wi], wb) and torch.equal(F[bi], bb)
+        for (i, n, wb, bb), (i2, n2, wi, bi) in zip(outs, plan.outs):
+            assert (i, n) == (i2, n2)
+            assert torch.equal(F[wi], wb) and torch.equal(F[bi], bb)
+
+
+def test_ravel_unravel_roundtrip():
+    from naz_amd.flows import bflow_maf as BM
+    spec = CASES[0]
+    _, shapes, _ = BM.make_conditional_autoregressive_nn(spec["D"], spec["C"], spec["hidden"])
+    shapes = [shapes] * 2
+    n = sum(int(np.prod(w)) + int(np.prod(b)) for layer in shapes for (w, b) in layer)
+    flat = torch.randn(3, n)
+    tree = BM.unravel(flat, shapes)
+    assert tree[0][0][0].shape == (3, 150, 4) and tree[1][-1][1].shape == (3, 4)
+    assert torch.equal(BM.ravel(tree), flat)
+    assert torch.equal(tree[0][0][0][1].reshape(-1), flat[1, :600])  # leaf order = ravel_pytree's
+    with pytest.raises(ValueError):
+        BM.unravel(flat[:, :-1], shapes)
+
+
+def test_rejects_unbuilt_options():
+    from naz_amd.flows import bflow_maf as BM
+    with pytest.raises(NotImplementedError):
+        BM.make_conditional_autoregressive_nn(2, 2, [8], skip_connections=True)
+    with pytest.raises(NotImplementedError):
+        BM.make_conditional_autoregressive_nn(2, 2, [8], param_dims=[1, 1, 1])
+
+
+# ----------------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", CASES, ids=lambda s: f"D{s['D']}C{s['C']}P{s['P']}")
+def test_lp_batched_vs_oracle(_gpu, spec):
+    layers, draws, x, ctx = _setup(spec)
+    flow = _flow(spec, layers, x, ctx, "cuda")
+    lp = flow["lp_batched"](_batched_params(draws, "cuda")).cpu().numpy()
+    assert lp.shape == (spec["P"], spec["B"])
+    for p, d in enumerate(draws):
+        ol = _oracle_layers(layers, d)
+        ref64 = J.log_prob(x, ol, ctx)
+        ref32 = J.log_prob(x, J.cast_layers(ol, np.float32), ctx, np.float32)
+        assert_parity(lp[p], ref64, ref32, what=f"lp_batched draw {p}")
+
+
+@pytest.mark.gpu
+def test_lp_single_equals_batched(_gpu):
+    spec = CASES[0]
+    layers, draws, x, ctx = _setup(spec)
+    flow = _flow(spec, layers, x, ctx, "cuda")
+    batched = flow["lp_batched"](_batched_params(draws, "cuda"))
+    one = _batched_params(draws[2:3], "cuda")
+    single = flow["lp"]([[(w[0], b[0]) for (w, b) in layer] for layer in one])
+    assert torch.equal(single, batched[2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [CASES[0], CASES[1]], ids=lambda s: f"D{s['D']}C{s['C']}")
+def test_sampler_batched_vs_oracle(_gpu, spec):
+    layers, draws, x, ctx = _setup(spec)
+    flow = _flow(spec, layers, x, ctx, "cuda")
+    S = 400
+    z = np.random.default_rng(3).standard_normal((spec["P"], S, spec["D"])).astype(np.float32)
+    y, lj = flow["sampler_batched"](_batched_params(draws, "cuda"), size=S, z=torch.tensor(z, device="cuda"))
+    y, lj = y.cpu().numpy(), lj.cpu().numpy()
+    for p, d in enumerate(draws):
+        ol = _oracle_layers(layers, d)
+        y64, lj64 = J.sample_from_z(z[p], ol, ctx)
+        y32, lj32 = J.sample_from_z(z[p], J.cast_layers(ol, np.float32), ctx, np.float32)
+        assert_parity(y[p], y64, y32, what=f"sampler y draw {p}")
+        assert_parity(lj[p], lj64, lj32, what=f"sampler log_j draw {p}")
+
+
+@pytest.mark.gpu
+def test_sample_logprob_roundtrip_and_rng(_gpu):
+    """log p(y) of the sampled y under the same draw = 2 base(z) - log_j (the sampler's log_j
+    is base(z) + Σ ls, bflow_jax_maf.py:220); seeded sampling is reproducible."""
+    spec = CASES[0]
+    layers, draws, x, ctx = _setup(spec)
+    flow = _flow(spec, layers, x, ctx, "cuda")
+    params = _batched_params(draws, "cuda")
+    S = 2048
+    z = torch.randn((spec["P"], S, spec["D"]), device="cuda", generator=torch.Generator("cuda").manual_seed(5))
+    y, lj = flow["sampler_batched"](params, size=S, z=z)
+    base = (-0.5 * (z.double() ** 2).sum(-1) - spec["D"] / 2 * np.log(2 * np.pi))
+    for p in range(spec["P"]):
+        f1 = _flow(spec, layers, y[p].cpu().numpy(), ctx, "cuda")
+        one = [[(w[p:p + 1], b[p:p + 1]) for (w, b) in layer] for layer in params]
+        lp = f1["lp_batched"](one)[0].double()
+        want = 2 * base[p] - lj[p].double()
+        err = ((lp - want).abs() / want.abs().clamp(min=1)).cpu().numpy()
+        assert np.quantile(err, 0.99) < 1e-4 and err.max() < 1e-3, (np.median(err), err.max())
+    y1, _ = flow["sampler_batched"](params, 11, S)
+    y2, _ = flow["sampler_batched"](params, 11, S)
+    assert torch.equal(y1, y2) and bool(torch.isfinite(y1).all())

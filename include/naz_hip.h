@@ -97,6 +97,21 @@ int naz_linear_act_batched(const float* ctx, int64_t ldc, int64_t sctx, int C, c
                            int64_t sb, float* y, int64_t ldy, int64_t sy, int64_t M, int N, int nbatch, int act,
                            void* stream);
 
+/* ---- a5/a6 forward + §8f rank 2: fused MADE conditioner + affine step ------
+ * One MAF layer in the sampling direction for P weight draws in one launch: replaces
+ * ConditionalAutoRegressiveNN.forward + AffineAutoregressive._call (naz/flows/transforms.py:
+ * 133-160) and the JAX front end's forward_fn (bflow_jax_maf.py:172-178):
+ *   raw = W_out·act(…act(W_0·[ctx|x] + b_0)…) + b_out;  y = raw[:D] + x·exp(clamp(raw[D:],-5,3));
+ *   ld  = / += / -= Σ clamp(raw[D:], -5, 3)   (ld_mode ROWSUM / ROWSUM_ADD / ROWSUM_SUB)
+ * packed: per-draw nets at packed + z*wstride in the layout documented in made.hip (masked
+ * weights, MFMA fragment order), naz_made_packed_floats() floats each; nh = hidden width in
+ * 32-blocks (1..5), nhid hidden layers, 2D <= 32, act tanh or relu. x/y/ld: S rows per draw,
+ * draw strides sx/sy/sld; ctx [C] (ldc = sctx = 0), rows at ldc, draw stride sctx. */
+int64_t naz_made_packed_floats(int nhid, int nh, int C, int D);
+int naz_made_affine_fwd(const float* packed, int64_t wstride, int nhid, int nh, int C, int D, const float* ctx,
+                        int64_t ldc, int64_t sctx, const float* x, int64_t ldx, int64_t sx, float* y, int64_t ldy,
+                        int64_t sy, float* ld, int64_t sld, int ld_mode, int64_t S, int P, int act, void* stream);
+
 /* ---- a5: affine autoregressive elementwise step --------------------------
  * Replaces the elementwise part of [pyro] AffineAutoregressive._call / ._inverse
  * (naz/flows/transforms.py:159; JAX restatement bflow_jax_maf.py:169-194):

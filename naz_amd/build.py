@@ -21,8 +21,9 @@ ARCH = os.environ.get("NAZ_OFFLOAD_ARCH", "gfx950")
 # Per-source flags.  The MFMA kernels are built without the SLP vectorizer: the packed f32 VALU
 # ops it forms (v_pk_add/mul/fma_f32) issue slower than scalar ones beside MFMAs, and the
 # packing moves add register pressure (spills in coupling_x6_kernel with it on).
-SOURCE_FLAGS = {"coupling.hip": ["-fno-slp-vectorize"], "cnf.hip": ["-fno-slp-vectorize"]}
-SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "gemm_rows.hip", "elementwise.hip", "coupling.hip", "cnf.hip", "capi.cpp"]
+SOURCE_FLAGS = {"coupling.hip": ["-fno-slp-vectorize"], "cnf.hip": ["-fno-slp-vectorize"],
+                "made.hip": ["-fno-slp-vectorize"]}
+SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "gemm_rows.hip", "elementwise.hip", "made.hip", "coupling.hip", "cnf.hip", "capi.cpp"]
 
 
 def hipcc() -> str:

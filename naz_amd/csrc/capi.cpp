@@ -83,6 +83,20 @@ int naz_linear_act_batched(const float* ctx, int64_t ldc, int64_t sctx, int C, c
                                 as_stream(stream));
 }
 
+int64_t naz_made_packed_floats(int nhid, int nh, int C, int D) {
+  if (nhid < 1 || nh < 1 || C < 0 || D < 1) return -1;
+  return made_packed_floats(nhid, nh, C, D);
+}
+
+int naz_made_affine_fwd(const float* packed, int64_t wstride, int nhid, int nh, int C, int D, const float* ctx,
+                        int64_t ldc, int64_t sctx, const float* x, int64_t ldx, int64_t sx, float* y, int64_t ldy,
+                        int64_t sy, float* ld, int64_t sld, int ld_mode, int64_t S, int P, int act, void* stream) {
+  if (S < 0 || P < 0 || x == nullptr || y == nullptr || packed == nullptr)
+    return set_error("naz_made_affine_fwd: bad arguments");
+  return made_affine_fwd(packed, wstride, nhid, nh, C, D, ctx, ldc, sctx, x, ldx, sx, y, ldy, sy, ld, sld, ld_mode, S,
+                         P, act, as_stream(stream));
+}
+
 int naz_affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
                   float* ld, int ld_mode, int64_t B, int D, void* stream) {
   if (B < 0 || D <= 0) return set_error("naz_affine_ar: bad shape");

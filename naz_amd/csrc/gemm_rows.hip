@@ -260,7 +260,12 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
     p.vec = p.vec && p.za0 % 4 == 0 && p.za1 % 4 == 0;
     p.vst = p.vst && p.zc % 4 == 0;
   }
-  const int nb = (p.N + 31) / 32;
+  int nb = (p.N + 31) / 32;
+  static const int split = [] {
+    const char* e = getenv("NAZ_RG_SPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  if (split && nb > 4) nb = (nb + 1) / 2;  // two column blocks of <= 4 x 32: 4 waves / SIMD
   switch (nb > 8 ? 8 : nb) {
     case 1: rowgemm_launch<1>(p, nz, s); break;
     case 2: rowgemm_launch<2>(p, nz, s); break;

@@ -155,6 +155,53 @@ class _LayerPlan:
         return self
 
 
+def _feat(o, r, lane):
+    """Feature held by accumulator register r of 32-block o in lane ``lane`` (made.hip)."""
+    return 32 * o + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+
+
+def made_pack_map(spec: MAFSpec, masks: List[Tensor], nh: int) -> Tensor:
+    """Gather map of naz_made_affine_fwd's packed net (layout in csrc/made.hip) into the per-draw
+    flat buffer F = [0, W0, b0, W1, b1, ...]: entry = 1-based flat index, 0 for a masked or
+    padded slot (so the gather applies the MADE masks)."""
+    D, C = spec.input_dim, spec.context_dim
+    Wi, Bi, off = [], [], 1
+    for (ws, bs), m in zip(spec.param_shapes, masks):
+        nw = ws[0] * ws[1]
+        Wi.append(torch.arange(off, off + nw).reshape(ws) * (m.cpu() != 0))
+        Bi.append(torch.arange(off + nw, off + nw + bs[0]))
+        off += nw + bs[0]
+
+    def gw(idx, of, kf):
+        ok = (of < idx.shape[0]) & (kf < idx.shape[1])
+        return torch.where(ok, idx[of.clamp(max=idx.shape[0] - 1), kf.clamp(max=idx.shape[1] - 1)], 0).reshape(-1)
+
+    def gb(idx, f):
+        return torch.where(f < idx.shape[0], idx[f.clamp(max=idx.shape[0] - 1)], 0).reshape(-1)
+
+    def grid(*n):
+        return torch.meshgrid(*[torch.arange(k) for k in n], indexing="ij")
+
+    s0 = ((C + D + 1) // 2 + 3) // 4 * 4
+    parts = []
+    o, t, l, q = grid(nh, s0 // 4, 64, 4)  # A0: W0[32o + l%32][2s + l//32], s = 4t + q
+    parts.append(gw(Wi[0], 32 * o + l % 32, 2 * (4 * t + q) + l // 32))
+    o, r, l = grid(nh, 16, 64)
+    parts.append(gb(Bi[0], _feat(o, r, l)))
+    for j in range(1, len(spec.hidden_dims)):
+        t, o, l, q = grid(nh * 4, nh, 64, 4)  # t-major: one input 32-block = one contiguous chunk
+        s = 4 * t + q
+        parts.append(gw(Wi[j], 32 * o + l % 32, _feat(s >> 4, s & 15, l)))
+        o, r, l = grid(nh, 16, 64)
+        parts.append(gb(Bi[j], _feat(o, r, l)))
+    t, l, q = grid(nh * 4, 64, 4)
+    s = 4 * t + q
+    parts.append(gw(Wi[-1], l % 32, _feat(s >> 4, s & 15, l)))
+    r, l = grid(16, 64)
+    parts.append(gb(Bi[-1], _feat(0, r, l)))
+    return torch.cat(parts)
+
+
 def _draws(params: Params) -> int:
     return params[0][0][0].shape[0]
 
@@ -196,6 +243,13 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         if ctx.shape[-1] != C or (ctx.dim() == 2 and ctx.shape[0] not in (1, B)):
             raise ValueError(f"context must be [{C}] or [B, {C}]")
     plans = [_LayerPlan(m, p, spec).to(dev) for (m, p) in zip(masks, perms)]
+    # fused forward (naz_made_affine_fwd): hidden widths <= 160, 2D <= 32, tanh / relu
+    nh = (max(spec.hidden_dims) + 31) // 32
+    fused_fwd = nh <= 5 and 2 * D <= 32 and spec.activation in ("tanh", "relu")
+    if fused_fwd:
+        made_maps = [made_pack_map(spec, m, nh).to(dev) for m in masks]
+        n_packed = ops.made_packed_floats(len(spec.hidden_dims), nh, C, D)
+        assert all(mp.numel() == n_packed for mp in made_maps), "made pack map out of sync with made.hip"
     act = spec.activation
     width_sum = max(sum(pl.widths) for pl in plans)
 
@@ -255,6 +309,14 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         lj = lj_out.reshape(P * S)
         ops.base_log_prob(z.reshape(P * S, D), out=lj)
         cur = z
+        if fused_fwd:
+            for l in range(len(plans)):
+                nxt = y_out if l == len(plans) - 1 else torch.empty_like(cur)
+                packed = _flat_layer(params[l], P, dev)[:, made_maps[l]]
+                ops.made_affine_fwd(packed, len(spec.hidden_dims), nh, cur, ctx_s, act, lj_out, ops.LD_ROWSUM_ADD,
+                                    out=nxt)
+                cur = nxt
+            return
         for l, plan in enumerate(plans):
             h = None
             layer = params[l]
@@ -307,4 +369,4 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         return y[0], lj[0]
 
     return {"lp": lp, "sampler": sampler, "lp_batched": lp_batched, "sampler_batched": sampler_batched,
-            "plans": plans}
+            "plans": plans, "fused_fwd": fused_fwd}

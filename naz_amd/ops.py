@@ -16,7 +16,7 @@ from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, RQS_FAST, LD_PERDIM, LD_ROWSUM
 
 Tensor = torch.Tensor
 
-__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "affine_ar", "affine_ar_bwd", "base_log_prob",
+__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
            "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate",
@@ -195,6 +195,36 @@ def linear_act_batched(x: Optional[Tensor], weight: Tensor, bias: Optional[Tenso
     check(lib().naz_linear_act_batched(_p(context), ldc, sctx, C, _p(x), ldx, sx, Kx, _p(weight), N * (C + Kx),
                                        _p(mask), _p(bias), N, _p(out), ldy, sy, M, N, P, ACT[act], _stream(dev)),
           "linear_act_batched")
+    return out
+
+
+def made_packed_floats(nhid: int, nh: int, C: int, D: int) -> int:
+    return int(lib().naz_made_packed_floats(nhid, nh, C, D))
+
+
+def made_affine_fwd(packed: Tensor, nhid: int, nh: int, x: Tensor, context: Optional[Tensor], act: str,
+                    ld: Tensor, ld_mode: int = LD_ROWSUM_ADD, out: Optional[Tensor] = None) -> Tensor:
+    """Fused MADE conditioner + affine forward step for P draws (naz_made_affine_fwd):
+    packed [P, n] (``flows.bflow_maf`` packer), x [P, S, D], ld [P, S]; context [C] or [S, C]."""
+    dev = _dev(packed, x, context, ld, out)
+    P, S, D = x.shape
+    C = 0 if context is None else context.shape[-1]
+    n = made_packed_floats(nhid, nh, C, D)
+    if packed.shape != (P, n) or not packed.is_contiguous():
+        raise ValueError(f"packed must be contiguous [P={P}, {n}], got {tuple(packed.shape)}")
+    if x.stride(-1) != 1 or ld.shape != (P, S) or ld.stride(-1) != 1:
+        raise ValueError("x needs unit column stride and ld must be [P, S]")
+    ldc = sctx = 0
+    if context is not None:
+        context = context.reshape(-1, C).contiguous()
+        if context.shape[0] not in (1, S):
+            raise ValueError("context must be [C] or [S, C]")
+        ldc = 0 if context.shape[0] == 1 else C
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib().naz_made_affine_fwd(_p(packed), n, nhid, nh, C, D, _p(context), ldc, sctx, _p(x), x.stride(1),
+                                    x.stride(0), _p(out), out.stride(1), out.stride(0), _p(ld), ld.stride(0), ld_mode,
+                                    S, P, ACT[act], _stream(dev)), "made_affine_fwd")
     return out
 
 

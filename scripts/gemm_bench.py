@@ -48,7 +48,7 @@ def main():
         fl = 2 * M * n1 * (n2 + 1)
         out.append(f"{name:6s} wgrad  {t:8.1f} us  {fl / t / 1e6:6.1f} TF  {(G.numel() + X.numel()) * 4 / t / 1e3:6.0f} GB/s")
     # rowgemm forward: act(X W^T + b)
-    for k, n, name in [(40, 128, "fwd1"), (128, 128, "fwd2"), (128, 184, "fwd3"), (152, 76, "ar152"), (76, 76, "ar76"),
+    for k, n, name in [(40, 128, "fwd1"), (128, 128, "fwd2"), (128, 184, "fwd3"), (152, 76, "ar152"), (76, 76, "ar76"), (150, 150, "s150"), (4, 150, "s4"), (152, 152, "s152"),
                        (128, 128, "fwd2id"), (128, 128, "fwd2relu")]:
         if only and name not in only:
             continue

@@ -191,3 +191,72 @@ def test_sample_logprob_roundtrip_and_rng(_gpu):
     y1, _ = flow["sampler_batched"](params, 11, S)
     y2, _ = flow["sampler_batched"](params, 11, S)
     assert torch.equal(y1, y2) and bool(torch.isfinite(y1).all())
+
+
+def _emulate_made_fwd(packed, nhid, nh, C, D, ctx, x):
+    """numpy model of made.hip's lane/register mapping (v_mfma_f32_32x32x2_f32: lane l supplies
+    A[l % 32][l // 32] and B[l // 32][l % 32]; D[m][n] sits in lane n + 32((m >> 2) & 1), register
+    (m & 3) + 4(m >> 3)) for one wave of 32 rows; returns y and Σ clamp(ls)."""
+    lane = np.arange(64)
+    regs_m = lambda r, l: (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)  # noqa: E731
+
+    def mfma_steps(A, Bsteps):  # A [steps][64] values, Bsteps [steps][64] -> acc [16][64]
+        acc = np.zeros((32, 32))
+        for a, b in zip(A, Bsteps):
+            Am = np.stack([a[:32], a[32:]], 1)  # [m][k]
+            Bm = np.stack([b[:32], b[32:]], 0)  # [k][n]
+            acc += Am @ Bm
+        r, l = np.meshgrid(np.arange(16), lane, indexing="ij")
+        return acc[regs_m(r, l), l % 32]
+
+    s0 = ((C + D + 1) // 2 + 3) // 4 * 4
+    pos = 0
+
+    def take(n):
+        nonlocal pos
+        v = packed[pos:pos + n]
+        pos += n
+        return v
+    inp = np.concatenate([np.broadcast_to(ctx, (32, C)), x], 1) if C else x
+    A0 = take(nh * s0 * 64).reshape(nh, s0 // 4, 64, 4).transpose(0, 1, 3, 2).reshape(nh, s0, 64)
+    B0 = np.zeros((s0, 64))
+    for s in range(s0):
+        k = 2 * s + lane // 32
+        B0[s] = np.where(k < C + D, inp[lane % 32, np.minimum(k, C + D - 1)], 0)
+    b = take(nh * 1024).reshape(nh, 16, 64)
+    hv = np.tanh(np.stack([mfma_steps(A0[o], B0) for o in range(nh)]) + b)
+    for _ in range(1, nhid):
+        A = take(nh * nh * 1024).reshape(nh * 4, nh, 64, 4).transpose(1, 0, 3, 2).reshape(nh, nh * 16, 64)
+        Bs = hv.reshape(nh * 16, 64)
+        b = take(nh * 1024).reshape(nh, 16, 64)
+        hv = np.tanh(np.stack([mfma_steps(A[o], Bs) for o in range(nh)]) + b)
+    A = take(nh * 1024).reshape(nh * 4, 64, 4).transpose(0, 2, 1).reshape(nh * 16, 64)
+    out = mfma_steps(A, hv.reshape(nh * 16, 64)) + take(1024).reshape(16, 64)
+    assert pos == packed.size
+    raw = np.zeros((32, 32))
+    r, l = np.meshgrid(np.arange(16), lane, indexing="ij")
+    raw[l % 32, regs_m(r, l)] = out
+    ls = np.clip(raw[:, D:2 * D], -5, 3)
+    return raw[:, :D] + x * np.exp(ls), ls.sum(1)
+
+
+@pytest.mark.parametrize("spec", CASES, ids=lambda s: f"D{s['D']}C{s['C']}")
+def test_made_pack_map_against_lane_model(spec):
+    """The fused forward kernel's packed layout, read the way made.hip reads it (numpy model of
+    the MFMA lane mapping), gives the reference's forward_fn (bflow_jax_maf.py:172-178)."""
+    from naz_amd.flows import bflow_maf as BM
+    layers, draws, _, _ = _setup(spec)
+    nn_spec, _, _ = BM.make_conditional_autoregressive_nn(spec["D"], spec["C"], spec["hidden"])
+    nh = (max(spec["hidden"]) + 31) // 32
+    D, C = spec["D"], spec["C"]
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((32, D))
+    ctx = rng.standard_normal(C) if C else None
+    for l, (_, perm, masks) in enumerate(layers[:2]):
+        mp = BM.made_pack_map(nn_spec, [torch.tensor(m) for m in masks], nh).numpy()
+        params = draws[0][l]
+        F = np.concatenate([[0.0]] + [np.concatenate((W.reshape(-1), b)) for (W, b) in params])
+        y, ld = _emulate_made_fwd(F[mp], len(spec["hidden"]), nh, C, D, ctx, x)
+        y64, ld64 = J.forward_fn(x, params, masks, ctx)
+        np.testing.assert_allclose(y, y64, rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(ld, ld64, rtol=1e-10, atol=1e-10)

@@ -44,7 +44,8 @@ def torch_to_jax(torch_maf):
     """naz ``torch_to_jax`` (bflow_jax_maf.py:26-46) over a naz_amd ``maf`` flow: (params,
     param_shapes, masks, mask_skips, permutations), tensors kept on the flow's device."""
     params, shapes, masks, skips, perms = [], [], [], [], []
-    for t in torch_maf.flow_dist.transforms:
+    # the layer list (an unconditional flow_dist holds one ComposeTransformModule)
+    for t in torch_maf.transforms:
         arn = t.nn
         these = [(l.weight.detach().clone(), l.bias.detach().clone()) for l in arn.layers]
         params.append(these)

@@ -352,6 +352,9 @@ class _ConditionedSplineAutoregressive(_LDCache, Transform):
 
     def _map(self, v, inverse, ld_buf, ld_mode):
         if not inverse:
+            y = _fused_made_forward(self.arn, v, self.context, ld_buf, ld_mode)
+            if y is not None:
+                return y
             raw = self.arn.raw(v, self.context)
             y, _ = ops.rqs(v, raw, self.count_bins, ops.LAYOUT_ARN, False, self.bound, ld_mode, ld_buf, fast=True)
             return y
@@ -435,6 +438,37 @@ class SplineAutoregressive(_ConditionedSplineAutoregressive, nn.Module):
 
     def __hash__(self):
         return nn.Module.__hash__(self)
+
+
+def _fused_made_forward(arn, v, context, ld_buf, ld_mode):
+    """AffineAutoregressive._call as ONE naz_made_affine_fwd launch (the whole masked MADE
+    conditioner + affine step, csrc/made.hip) when nothing is recorded for autograd and the
+    shape fits the kernel (hidden widths <= 160, 2D <= 32, tanh / relu, row-sum log-det);
+    None otherwise (the per-GEMM path runs)."""
+    from .bflow_maf import MAFSpec, made_pack_map
+    layers = list(arn.layers)
+    if (v.dim() != 2 or arn.output_multiplier != 2 or 2 * arn.input_dim > 32 or arn.act not in ("tanh", "relu")
+            or max(arn.hidden_dims) > 160 or ld_mode == ops.LD_PERDIM or v.requires_grad
+            or (torch.is_grad_enabled() and any(p.requires_grad for p in arn.parameters()))):
+        return None
+    C = arn.context_dim
+    if C and (context is None or context.dim() > 2 or (context.dim() == 2 and context.shape[0] not in (1, v.shape[0]))):
+        return None
+    nh = (max(arn.hidden_dims) + 31) // 32
+    key = tuple((l.weight.data_ptr(), l.weight._version, l.bias.data_ptr(), l.bias._version, l.mask._version)
+                for l in layers)
+    cache = arn.__dict__.get("_made_fwd")
+    if cache is None or cache[0] != key:
+        spec = MAFSpec(arn.input_dim, C, arn.hidden_dims, arn.act)
+        mp = made_pack_map(spec, [l.mask for l in layers], nh).to(v.device)
+        flat = torch.cat([torch.zeros(1, device=v.device)] +
+                         [t.detach().reshape(-1).float() for l in layers for t in (l.weight, l.bias)])
+        cache = (key, flat[mp].reshape(1, -1).contiguous())
+        arn.__dict__["_made_fwd"] = cache
+    x = v.contiguous().unsqueeze(0)
+    ctx = None if not C else context.reshape(-1, C)
+    y = ops.made_affine_fwd(cache[1], len(arn.hidden_dims), nh, x, ctx, arn.act, ld_buf.view(1, -1), ld_mode)
+    return y[0]
 
 
 class _ConditionedAffineAutoregressive(_LDCache, Transform):

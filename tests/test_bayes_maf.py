@@ -260,3 +260,57 @@ def test_made_pack_map_against_lane_model(spec):
         y64, ld64 = J.forward_fn(x, params, masks, ctx)
         np.testing.assert_allclose(y, y64, rtol=1e-10, atol=1e-10)
         np.testing.assert_allclose(ld, ld64, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,C,hidden,ctx_rows", [(2, 2, [150, 150, 150], False), (4, 3, [64, 40], True),
+                                                 (5, 0, [37], False)])
+def test_naz_maf_forward_uses_fused_kernel(_gpu, D, C, hidden, ctx_rows):
+    """naz_amd's NormalizingFlow("maf") forward direction (AffineAutoregressive._call, used by
+    sample) runs as one naz_made_affine_fwd launch per layer under no_grad; it matches the
+    per-GEMM path (naz_linear_act chain + naz_affine_ar) and the fp64 oracle layer."""
+    from naz_amd import ops
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    from naz_amd.flows.transforms import _fused_made_forward
+    spec = dict(flow_type="maf", D=D, C=C, hidden=hidden, L=2)
+    st = {k: v.float() for k, v in O.random_state(spec, seed=3).items()}
+    f = NormalizingFlow("maf", None, D, C, hidden, 2)
+    fio.load_state(f, {k: v.numpy() for k, v in st.items()})
+    rng = np.random.default_rng(1)
+    B = 1000
+    x = torch.tensor(rng.standard_normal((B, D)).astype(np.float32), device="cuda")
+    ctx = None
+    if C:
+        ctx = torch.tensor(rng.standard_normal((B, C) if ctx_rows else (C,)).astype(np.float32), device="cuda")
+    layers = J.layers_from_state(spec, {k: v.numpy() for k, v in st.items()})
+    with torch.no_grad():
+        for l, t in enumerate(f.transforms[:1]):
+            arn = t.nn
+            ld_f = torch.zeros(B, device="cuda")
+            y_f = _fused_made_forward(arn, x, ctx, ld_f, ops.LD_ROWSUM_ADD)
+            assert y_f is not None, "fused MADE forward not taken"
+            ld_g = torch.zeros(B, device="cuda")
+            y_g, _ = ops.affine_ar(x, arn.raw(x, ctx), False, ops.LD_ROWSUM_ADD, ld_g)
+            assert torch.allclose(y_f, y_g, rtol=1e-5, atol=1e-5) and torch.allclose(ld_f, ld_g, rtol=1e-5, atol=1e-5)
+            params, perm, masks = layers[l]
+            y64, ld64 = J.forward_fn(x.cpu().double().numpy(), params, masks,
+                                     None if ctx is None else ctx.cpu().double().numpy())
+            assert_parity(y_f.cpu().numpy(), y64, what="fused maf forward y", strict=True)
+            assert_parity(ld_f.cpu().numpy(), ld64, what="fused maf forward ld", strict=True)
+
+
+def test_torch_to_jax_layout():
+    """torch_to_jax (bflow_jax_maf.py:26-46) over a naz_amd maf flow: per layer (W, b) per MADE
+    linear in ravel order, the masks, mask_skip and permutation; shapes = the spec's."""
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import bflow_maf as BM
+    f = NormalizingFlow("maf", None, 2, 2, [150, 150, 150], 3)
+    params, shapes, masks, skips, perms = BM.torch_to_jax(f)
+    _, want, _ = BM.make_conditional_autoregressive_nn(2, 2, [150, 150, 150])
+    assert len(params) == 3 and all(sh == [(tuple(w), tuple(b)) for (w, b) in want] for sh in shapes)
+    arn = f.transforms[0].nn
+    assert torch.equal(params[0][1][0], arn.layers[1].weight.detach())
+    assert all(torch.equal(m, a.float()) for m, a in zip(masks[0], arn.masks))
+    assert torch.equal(perms[0], arn.permutation) and skips[0].shape == (4, 4)
+    assert BM.ravel(params).numel() == sum(p.numel() for p in f.parameters())

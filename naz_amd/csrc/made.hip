@@ -55,17 +55,19 @@ NAZ_DEV floatx16 mfma32(float a, float b, floatx16 c) { return __builtin_amdgcn_
 
 NAZ_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-template <int NH, int ACT>
-__global__ void __launch_bounds__(256, 2) made_affine_fwd_kernel(MadeArgs p) {
+template <int NH, int ACT, int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) made_affine_fwd_kernel(MadeArgs p) {
   // weight chunks of the hidden and output layers, double-buffered: one chunk = one input
   // 32-block of a hidden layer for all NH output blocks, or the whole output layer
   constexpr int CH4 = NH * 256;  // float4 per chunk
   __shared__ float4 Wl[2][CH4];
-  __shared__ float E[4][32][33];
+  constexpr int T = 64 * NW, PF = (CH4 + T - 1) / T;  // threads; prefetched float4 per thread
+  constexpr bool RAGGED = CH4 % T != 0;
+  __shared__ float E[NW][32][33];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int64_t z = blockIdx.z;
   const float* W = p.w + z * p.wstride;
-  const int64_t row = (int64_t)blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const int64_t row = (int64_t)blockIdx.x * (32 * NW) + wave * 32 + (lane & 31);
   const bool live = row < p.S;
   const float* xr = p.x + z * p.sx + row * p.ldx;
   const float* cr = p.ctx + z * p.sctx + row * p.ldc;
@@ -81,23 +83,27 @@ __global__ void __launch_bounds__(256, 2) made_affine_fwd_kernel(MadeArgs p) {
   };
   // the next chunk, in flight: named registers (an indexed array was kept in memory)
   float4 pf0, pf1, pf2, pf3, pf4;
-#define NAZ_MADE_FETCH(G)                                   \
-  {                                                         \
-    const float4* src_ = chunk_at(G);                       \
-    pf0 = src_[tid];                                        \
-    if constexpr (NH > 1) pf1 = src_[256 + tid];            \
-    if constexpr (NH > 2) pf2 = src_[512 + tid];            \
-    if constexpr (NH > 3) pf3 = src_[768 + tid];            \
-    if constexpr (NH > 4) pf4 = src_[1024 + tid];           \
+#define NAZ_MADE_PF(K, OP) \
+  if constexpr (PF > K) {  \
+    if (!RAGGED || K * T + tid < CH4) OP; \
   }
-#define NAZ_MADE_STASH(BUF)                                 \
-  {                                                         \
-    float4* dst_ = Wl[BUF];                                 \
-    dst_[tid] = pf0;                                        \
-    if constexpr (NH > 1) dst_[256 + tid] = pf1;            \
-    if constexpr (NH > 2) dst_[512 + tid] = pf2;            \
-    if constexpr (NH > 3) dst_[768 + tid] = pf3;            \
-    if constexpr (NH > 4) dst_[1024 + tid] = pf4;           \
+#define NAZ_MADE_FETCH(G)                             \
+  {                                                   \
+    const float4* src_ = chunk_at(G);                 \
+    NAZ_MADE_PF(0, pf0 = src_[tid])                   \
+    NAZ_MADE_PF(1, pf1 = src_[T + tid])               \
+    NAZ_MADE_PF(2, pf2 = src_[2 * T + tid])           \
+    NAZ_MADE_PF(3, pf3 = src_[3 * T + tid])           \
+    NAZ_MADE_PF(4, pf4 = src_[4 * T + tid])           \
+  }
+#define NAZ_MADE_STASH(BUF)                           \
+  {                                                   \
+    float4* dst_ = Wl[BUF];                           \
+    NAZ_MADE_PF(0, dst_[tid] = pf0)                   \
+    NAZ_MADE_PF(1, dst_[T + tid] = pf1)               \
+    NAZ_MADE_PF(2, dst_[2 * T + tid] = pf2)           \
+    NAZ_MADE_PF(3, dst_[3 * T + tid] = pf3)           \
+    NAZ_MADE_PF(4, dst_[4 * T + tid] = pf4)           \
   }
   NAZ_MADE_FETCH(0)
 
@@ -209,14 +215,26 @@ __global__ void __launch_bounds__(256, 2) made_affine_fwd_kernel(MadeArgs p) {
   }
 }
 
+#undef NAZ_MADE_PF
 #undef NAZ_MADE_FETCH
 #undef NAZ_MADE_STASH
 
+template <int NH, int NW>
+void launch_nw(const MadeArgs& a, int act, int P, hipStream_t s) {
+  dim3 grid((unsigned)((a.S + 32 * NW - 1) / (32 * NW)), 1, (unsigned)P);
+  if (act == ACT_TANH) hipLaunchKernelGGL((made_affine_fwd_kernel<NH, ACT_TANH, NW>), grid, dim3(64 * NW), 0, s, a);
+  else hipLaunchKernelGGL((made_affine_fwd_kernel<NH, ACT_RELU, NW>), grid, dim3(64 * NW), 0, s, a);
+}
+
+// waves per workgroup: rows sharing one staged weight chunk (NAZ_MADE_WAVES=4|8 overrides)
 template <int NH>
 void launch_nh(const MadeArgs& a, int act, int P, hipStream_t s) {
-  dim3 grid((unsigned)((a.S + 127) / 128), 1, (unsigned)P);
-  if (act == ACT_TANH) hipLaunchKernelGGL((made_affine_fwd_kernel<NH, ACT_TANH>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((made_affine_fwd_kernel<NH, ACT_RELU>), grid, dim3(256), 0, s, a);
+  static const int nw = [] {
+    const char* e = getenv("NAZ_MADE_WAVES");
+    return e ? atoi(e) : 4;
+  }();
+  if (nw == 8) launch_nw<NH, 8>(a, act, P, s);
+  else launch_nw<NH, 4>(a, act, P, s);
 }
 
 }  // namespace

@@ -236,6 +236,16 @@ int naz_cnf_pack(const naz_cnf_desc* d, const float* flat, void* packed, void* s
 int naz_cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
                       int64_t ldc, const float* eps, int64_t lde, float t0, float t1, int steps, float* y,
                       int64_t ldy, float* ld, int ld_mode, int64_t B, void* stream);
+/* §8f rank 3: the same block solve with adaptive Dormand-Prince 5(4) (naz FFJORDTransform
+ * solver='dopri5', atol = rtol = 1e-4: continuous_transforms.py:73-81; tableau as naz's
+ * odeint.py:136-160).  Step control per 16-row group (RMS error norm over the group's [x, a],
+ * accept at <= 1, h *= clamp(0.9 e^-1/5, 0.2 | 1 on accept, 10), Hairer initial step, FSAL, last
+ * step clipped to t1).  nfe (nullable, device int[ceil(B/16)]): RHS evaluations per group,
+ * negated when max_steps ran out before t1. */
+int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx,
+                             const float* ctx, int64_t ldc, const float* eps, int64_t lde, float t0, float t1,
+                             float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
+                             int* nfe, int64_t B, void* stream);
 
 #ifdef __cplusplus
 }

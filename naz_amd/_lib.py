@@ -64,6 +64,8 @@ SIGNATURES = {
     "naz_cnf_pack": (C.c_int, [C.POINTER(CnfDesc), _vp, _vp, _vp]),
     "naz_cnf_integrate": (C.c_int, [C.POINTER(CnfDesc), _vp, _vp, _i64, _vp, _i64, _vp, _i64, C.c_float, C.c_float,
                                     _i, _vp, _i64, _vp, _i, _i64, _vp]),
+    "naz_cnf_integrate_dopri5": (C.c_int, [C.POINTER(CnfDesc), _vp, _vp, _i64, _vp, _i64, _vp, _i64, C.c_float,
+                                           C.c_float, C.c_float, C.c_float, _i, _vp, _i64, _vp, _i, _vp, _i64, _vp]),
     "naz_coupling_supported": (C.c_int, [C.POINTER(CouplingDesc)]),
     "naz_coupling_param_count": (C.c_int64, [C.POINTER(CouplingDesc)]),
     "naz_coupling_packed_bytes": (C.c_int64, [C.POINTER(CouplingDesc)]),

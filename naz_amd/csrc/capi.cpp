@@ -177,6 +177,19 @@ int naz_cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x,
                        as_stream(stream));
 }
 
+int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx,
+                             const float* ctx, int64_t ldc, const float* eps, int64_t lde, float t0, float t1,
+                             float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
+                             int* nfe, int64_t B, void* stream) {
+  if (B < 0) return set_error("naz_cnf_integrate_dopri5: negative batch");
+  if (B > 0 && (packed == nullptr || x == nullptr || eps == nullptr || y == nullptr))
+    return set_error("naz_cnf_integrate_dopri5: null pointer");
+  if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
+    return set_error("naz_cnf_integrate_dopri5: context required");
+  return cnf_integrate_dopri5(d, packed, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy, ld,
+                              ld_mode, nfe, B, as_stream(stream));
+}
+
 int naz_coupling_supported(const naz_coupling_desc* d) { return coupling_supported(d); }
 int64_t naz_coupling_param_count(const naz_coupling_desc* d) { return coupling_param_count(d); }
 int64_t naz_coupling_packed_bytes(const naz_coupling_desc* d) { return coupling_packed_bytes(d); }

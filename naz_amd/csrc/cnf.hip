@@ -568,6 +568,206 @@ __global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Adaptive Dormand-Prince 5(4) solve (naz FFJORDTransform's
+// solver='dopri5', atol = rtol = 1e-4, continuous_transforms.py:73-81).  Same residency and
+// RHS as cnf_kernel; each WAVE (16 rows) integrates with its own step size: the controller
+// (RMS error norm over the wave's [x, a] elements, accept at <= 1, h *= clamp(0.9 e^-1/5,
+// 0.2 | 1 on accept, 10), Hairer's initial step, FSAL, last step clipped to t1) is restated in
+// oracle/naz_oracle.py::dopri5_augmented with the same 16-row groups.  The waves of a
+// workgroup never synchronise inside a tile (the weights are read-only LDS), so a wave that
+// needs more steps does not hold the others.  One RHS call site: the stage machine keeps
+// every k_i in named registers (no dynamically indexed arrays).
+// ---------------------------------------------------------------------------
+__constant__ float kDpA[15] = {1.f / 5,          3.f / 40,          9.f / 40,         44.f / 45,     -56.f / 15,
+                               32.f / 9,         19372.f / 6561,    -25360.f / 2187,  64448.f / 6561, -212.f / 729,
+                               9017.f / 3168,    -355.f / 33,       46732.f / 5247,   49.f / 176,    -5103.f / 18656};
+
+NAZ_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+template <class CF, bool X3>
+__global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_dopri5_kernel(
+    const float* __restrict__ packed, const float* __restrict__ x, int64_t ldx, const float* __restrict__ ctx,
+    int64_t ldc, const float* __restrict__ eps, int64_t lde, float t0, float t1, float atol, float rtol,
+    int max_steps, float* __restrict__ y, int64_t ldy, float* __restrict__ ld, int ld_mode, int* __restrict__ nfe_out,
+    int64_t B) {
+  __shared__ __attribute__((aligned(16))) float lds[CF::TOTAL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4;
+  for (int i = tid * 4; i < CF::TOTAL; i += blockDim.x * 4)
+    *reinterpret_cast<floatx4*>(lds + i) = *reinterpret_cast<const floatx4*>(packed + i);
+  __syncthreads();
+  constexpr int CSR = CF::CS > 0 ? CF::CS : 1;
+  constexpr int XS = CF::XS;
+  constexpr float b0 = 35.f / 384, b2 = 500.f / 1113, b3 = 125.f / 192, b4 = -2187.f / 6784, b5 = 11.f / 84;
+  constexpr float e0 = 35.f / 384 - 5179.f / 57600, e2 = 500.f / 1113 - 7571.f / 16695,
+                  e3 = 125.f / 192 - 393.f / 640, e4 = -2187.f / 6784 + 92097.f / 339200,
+                  e5 = 11.f / 84 - 187.f / 2100, e6 = -1.f / 40;
+  const float dir = t1 > t0 ? 1.f : -1.f;
+  for (int64_t tile = blockIdx.x; tile * kCnfRows < B; tile += gridDim.x) {
+    const int64_t row0 = tile * kCnfRows + wave * 16;
+    const int64_t row = row0 + (lane & 15);
+    const bool valid = row < B;
+    if (row0 >= B) continue;  // whole wave past the end (wave-uniform)
+    float xs[XS], es[XS], cs[CSR];
+    bool live[XS];
+#pragma unroll
+    for (int s = 0; s < XS; ++s) {
+      const int fi = q + 4 * s;
+      live[s] = valid && fi < CF::D;
+      xs[s] = live[s] ? x[row * ldx + fi] : 0.f;
+      es[s] = live[s] ? eps[row * lde + fi] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < CSR; ++s) {
+      const int fi = q + 4 * s;
+      cs[s] = (CF::CS > 0 && valid && fi < CF::C) ? ctx[(ldc ? row * ldc : 0) + fi] : 0.f;
+    }
+    const bool alive = valid && q == 0;  // the lane that owns a row's log-det element
+    const int64_t nrows = B - row0 < 16 ? B - row0 : 16;
+    const float inv_n = 1.f / (float)(nrows * (CF::D + 1));
+    // RMS over the wave's [x, a] elements of u / (atol + rtol * w)
+    auto rms2 = [&](const float (&u)[XS], float ua, const float (&w)[XS], float wa) {
+      float acc = 0.f;
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {
+        const float r = u[s] / (atol + rtol * fabsf(w[s]));
+        acc += live[s] ? r * r : 0.f;
+      }
+      const float ra = ua / (atol + rtol * wa);
+      acc += alive ? ra * ra : 0.f;
+      return sqrtf(wave_sum(acc) * inv_n);
+    };
+
+    float a = 0.f;
+    float k0[XS], k1[XS], k2[XS], k3[XS], k4[XS], k5[XS], xin[XS], x5[XS], f[XS];
+    float k0a = 0.f, k1a = 0.f, k2a = 0.f, k3a = 0.f, k4a = 0.f, k5a = 0.f, a5 = 0.f, g;
+#pragma unroll
+    for (int s = 0; s < XS; ++s) xin[s] = xs[s];
+    int phase = -2, steps = 0, nfe = 0;
+    float t = t0, h = 0.f, hh = 0.f, h0 = 0.f, d1 = 0.f;
+    bool last = false;
+    for (;;) {
+      cnf_rhs<CF, X3>(lds, xin, es, cs, f, g, lane);
+      ++nfe;
+      bool start_step = false;
+      if (phase == -2) {  // f(y0); initial-step heuristic part 1
+#pragma unroll
+        for (int s = 0; s < XS; ++s) k0[s] = f[s];
+        k0a = g;
+        const float d0 = rms2(xs, a, xs, 0.f);  // scale atol + rtol |y0|
+        d1 = rms2(k0, k0a, xs, 0.f);
+        h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : 0.01f * d0 / d1;
+#pragma unroll
+        for (int s = 0; s < XS; ++s) xin[s] = xs[s] + dir * h0 * k0[s];
+        phase = -1;
+      } else if (phase == -1) {  // part 2: h = min(100 h0, (0.01 / max(d1, d2))^(1/6))
+        float df[XS];
+#pragma unroll
+        for (int s = 0; s < XS; ++s) df[s] = f[s] - k0[s];
+        const float d2 = rms2(df, g - k0a, xs, 0.f) / h0;
+        const float dm = fmaxf(d1, d2);
+        const float h1 = dm <= 1e-15f ? fmaxf(1e-6f, h0 * 1e-3f) : powf(0.01f / dm, 1.f / 6.f);
+        h = fminf(100.f * h0, h1);
+        start_step = true;
+      } else if (phase == 1) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k1[s] = f[s];
+          xin[s] = xs[s] + hh * (kDpA[1] * k0[s] + kDpA[2] * k1[s]);
+        }
+        k1a = g;
+        phase = 2;
+      } else if (phase == 2) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k2[s] = f[s];
+          xin[s] = xs[s] + hh * (kDpA[3] * k0[s] + kDpA[4] * k1[s] + kDpA[5] * k2[s]);
+        }
+        k2a = g;
+        phase = 3;
+      } else if (phase == 3) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k3[s] = f[s];
+          xin[s] = xs[s] + hh * (kDpA[6] * k0[s] + kDpA[7] * k1[s] + kDpA[8] * k2[s] + kDpA[9] * k3[s]);
+        }
+        k3a = g;
+        phase = 4;
+      } else if (phase == 4) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k4[s] = f[s];
+          xin[s] = xs[s] + hh * (kDpA[10] * k0[s] + kDpA[11] * k1[s] + kDpA[12] * k2[s] + kDpA[13] * k3[s] +
+                                 kDpA[14] * k4[s]);
+        }
+        k4a = g;
+        phase = 5;
+      } else if (phase == 5) {  // 5th-order solution; its f is the FSAL stage k6
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k5[s] = f[s];
+          x5[s] = xs[s] + hh * (b0 * k0[s] + b2 * k2[s] + b3 * k3[s] + b4 * k4[s] + b5 * k5[s]);
+          xin[s] = x5[s];
+        }
+        k5a = g;
+        a5 = a + hh * (b0 * k0a + b2 * k2a + b3 * k3a + b4 * k4a + b5 * k5a);
+        phase = 6;
+      } else {  // phase 6: error estimate, accept / reject, next step size
+        float err[XS], w[XS];
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          err[s] = hh * (e0 * k0[s] + e2 * k2[s] + e3 * k3[s] + e4 * k4[s] + e5 * k5[s] + e6 * f[s]);
+          w[s] = fmaxf(fabsf(xs[s]), fabsf(x5[s]));
+        }
+        const float erra = hh * (e0 * k0a + e2 * k2a + e3 * k3a + e4 * k4a + e5 * k5a + e6 * g);
+        const float en = rms2(err, erra, w, fmaxf(fabsf(a), fabsf(a5)));
+        const bool accept = en <= 1.f;
+        if (accept) {
+#pragma unroll
+          for (int s = 0; s < XS; ++s) {
+            xs[s] = x5[s];
+            k0[s] = f[s];
+          }
+          a = a5;
+          k0a = g;
+          t = last ? t1 : t + hh;
+        }
+        const float fac = en == 0.f ? 10.f : fminf(10.f, fmaxf(0.9f * powf(en, -0.2f), accept ? 1.f : 0.2f));
+        h = fabsf(hh) * fac;
+        ++steps;
+        if (t == t1 || steps >= max_steps) break;
+        start_step = true;
+      }
+      if (start_step) {  // stage 1 input of the next step (clipped to end at t1)
+        const float rem = fabsf(t1 - t);
+        last = h >= rem;
+        hh = dir * (last ? rem : h);
+#pragma unroll
+        for (int s = 0; s < XS; ++s) xin[s] = xs[s] + hh * kDpA[0] * k0[s];
+        phase = 1;
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {
+        const int fi = q + 4 * s;
+        if (fi < CF::D) y[row * ldy + fi] = xs[s];
+      }
+      if (q == 0 && ld != nullptr) {
+        if (ld_mode == NAZ_LD_ROWSUM_ADD) ld[row] += a;
+        else if (ld_mode == NAZ_LD_ROWSUM_SUB) ld[row] -= a;
+        else ld[row] = a;
+      }
+    }
+    if (nfe_out != nullptr && lane == 0) nfe_out[row0 / 16] = steps >= max_steps && t != t1 ? -nfe : nfe;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Instantiations and dispatch
 // ---------------------------------------------------------------------------
 template <class CF>
@@ -609,6 +809,28 @@ struct CnfOps {
                          ld_mode, B);
     }
     return check_launch("cnf_kernel");
+  }
+  static int run_dopri5(const void* packed, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
+                        const float* eps, int64_t lde, float t0, float t1, float atol, float rtol, int max_steps,
+                        float* y, int64_t ldy, float* ld, int ld_mode, int* nfe, int64_t B, int mode, hipStream_t s) {
+    const int64_t tiles = (B + kCnfRows - 1) / kCnfRows;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess)
+      cus = 256;
+    const int per_cu = (160 * 1024) / (CF::TOTAL * 4) >= 2 ? 2 : 1;
+    const int64_t grid = tiles < (int64_t)cus * per_cu ? tiles : (int64_t)cus * per_cu;
+    if (mode == NAZ_CNF_F16X3) {
+      if constexpr (kX3)
+        hipLaunchKernelGGL((cnf_dopri5_kernel<CF, true>), dim3((unsigned)grid), dim3(kCnfRows * 4), 0, s,
+                           static_cast<const float*>(packed), x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol,
+                           max_steps, y, ldy, ld, ld_mode, nfe, B);
+    } else {
+      hipLaunchKernelGGL((cnf_dopri5_kernel<CF, false>), dim3((unsigned)grid), dim3(kCnfRows * 4), 0, s,
+                         static_cast<const float*>(packed), x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps,
+                         y, ldy, ld, ld_mode, nfe, B);
+    }
+    return check_launch("cnf_dopri5_kernel");
   }
 };
 
@@ -682,6 +904,20 @@ int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int
   return cnf_dispatch(d, [&](auto ops) {
     return decltype(ops)::run(packed, x, ldx, ctx, ldc, eps, lde, dt, steps, y, ldy, ld, ld_mode, B, d->mfma_mode,
                               s);
+  });
+}
+
+int cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                         int64_t ldc, const float* eps, int64_t lde, float t0, float t1, float atol, float rtol,
+                         int max_steps, float* y, int64_t ldy, float* ld, int ld_mode, int* nfe, int64_t B,
+                         hipStream_t s) {
+  if (B == 0) return 0;
+  if (!(atol > 0.f) || !(rtol >= 0.f)) return set_error("naz_cnf_integrate_dopri5: atol must be > 0, rtol >= 0");
+  if (max_steps < 1) return set_error("naz_cnf_integrate_dopri5: max_steps must be >= 1");
+  if (t0 == t1) return set_error("naz_cnf_integrate_dopri5: empty interval");
+  return cnf_dispatch(d, [&](auto ops) {
+    return decltype(ops)::run_dopri5(packed, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy, ld,
+                                     ld_mode, nfe, B, d->mfma_mode, s);
   });
 }
 

@@ -72,5 +72,9 @@ int cnf_pack(const naz_cnf_desc* d, const float* flat, void* packed, hipStream_t
 int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
                   int64_t ldc, const float* eps, int64_t lde, float t0, float t1, int steps, float* y, int64_t ldy,
                   float* ld, int ld_mode, int64_t B, hipStream_t s);
+int cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                         int64_t ldc, const float* eps, int64_t lde, float t0, float t1, float atol, float rtol,
+                         int max_steps, float* y, int64_t ldy, float* ld, int ld_mode, int* nfe, int64_t B,
+                         hipStream_t s);
 
 }  // namespace naz

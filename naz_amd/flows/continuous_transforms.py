@@ -9,8 +9,9 @@ registers, the MLP resident in LDS (csrc/cnf.hip).
 
 Solver: naz constructs torchdyn ``NeuralODE(solver='dopri5', atol=rtol=1e-4, sensitivity=
 'adjoint')`` (:73-81).  SURVEY.md §8d pins config 5 to fixed-step classical RK4 with 8 steps
-(NFE 32) — the default here (``solver='rk4', steps=8``); adaptive dopri5 and the adjoint
-backward are §8f rank 3 and raise NotImplementedError.  The Hutchinson probe eps ~ N(0, I)
+(NFE 32) — the default here (``solver='rk4', steps=8``); ``solver='dopri5'`` runs the adaptive
+Dormand-Prince solve (naz_cnf_integrate_dopri5, one step size per 16-row group); the adjoint
+backward is §8f rank 3 and raises NotImplementedError.  The Hutchinson probe eps ~ N(0, I)
 is drawn per solve on the device, as torchdyn does; assign ``transform.noise`` to fix it.
 """
 from __future__ import annotations
@@ -119,9 +120,20 @@ class _FFJORDCore:
                                       "§8f rank 3; evaluate under torch.no_grad()")
         noise = self.noise if self.noise is not None else torch.randn(v.shape, device=v.device, dtype=torch.float32)
         packed = self._plan.packed()  # may re-resolve the mode: read desc only after it
-        y, ld = ops.cnf_integrate(self._plan.desc, packed, v, noise, t0, t1, self.steps,
-                                  context=self._context, ld_out=ld_buf, ld_mode=ld_mode)
+        if self.solver == "dopri5":  # §8f rank 3: adaptive Dormand-Prince, per-16-row step control
+            y, ld = ops.cnf_integrate_dopri5(self._plan.desc, packed, v, noise, t0, t1, self.atol, self.rtol,
+                                             self.max_steps, context=self._context, ld_out=ld_buf, ld_mode=ld_mode,
+                                             nfe=self._nfe_buffer(v))
+        else:
+            y, ld = ops.cnf_integrate(self._plan.desc, packed, v, noise, t0, t1, self.steps,
+                                      context=self._context, ld_out=ld_buf, ld_mode=ld_mode)
         return y, ld
+
+    def _nfe_buffer(self, v):
+        """RHS evaluations per 16-row group of the last dopri5 solve (``last_nfe``)."""
+        n = (v.shape[0] + 15) // 16
+        self.last_nfe = torch.empty(n, device=v.device, dtype=torch.int32)
+        return self.last_nfe
 
     def _inverse(self, x):  # naz :91-95: integrate t 0 -> 1, cache int -tr J
         y, ld = self._solve(x, 0.0, 1.0, None, ops.LD_ROWSUM)
@@ -150,9 +162,9 @@ class _FFJORDCore:
 
 
 def _check_solver(solver, steps):
-    if solver != "rk4":
-        raise NotImplementedError(f"naz_amd CNF: solver {solver!r}: fixed-step 'rk4' is built (SURVEY.md §8d "
-                                  "config 5); adaptive dopri5 is §8f rank 3")
+    if solver not in ("rk4", "dopri5"):
+        raise NotImplementedError(f"naz_amd CNF: solver {solver!r}: fixed-step 'rk4' (SURVEY.md §8d config 5) and "
+                                  "adaptive 'dopri5' are built")
     if int(steps) < 1:
         raise ValueError("steps must be >= 1")
 
@@ -164,11 +176,14 @@ class FFJORDTransform(_FFJORDCore, TransformModule):
     codomain = constraints.real_vector
     bijective = True
 
-    def __init__(self, net, input_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4, steps=8):
+    def __init__(self, net, input_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4, steps=8,
+                 max_steps=1000):
         super().__init__()
         _check_solver(solver, steps)
         self.net, self.input_dim, self.steps = net, input_dim, int(steps)
         self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
+        self.max_steps = int(max_steps)
+        self.last_nfe = None
         self._plan = _CnfPlan(net)
         self._cached_logdet = None
         self._context = None
@@ -208,16 +223,23 @@ class _ConditionedFFJORD(_FFJORDCore, Transform):
     def noise(self):
         return self.module.noise
 
+    def __getattr__(self, name):  # solver settings live on the module
+        if name in ("solver", "atol", "rtol", "max_steps"):
+            return getattr(self.module, name)
+        raise AttributeError(name)
+
 
 class ConditionalFFJORDTransform(ConditionalTransformModule):
     """naz :109-121.  ``condition(ctx)`` returns a conditioned transform instead of naz's
     monkey-patch of the vector field's ``forward``."""
 
     def __init__(self, net, input_dim, context_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4,
-                 steps=8):
+                 steps=8, max_steps=1000):
         super().__init__()
         _check_solver(solver, steps)
         self.net, self.input_dim, self.context_dim, self.steps = net, input_dim, context_dim, int(steps)
+        self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
+        self.max_steps = int(max_steps)
         self._plan = _CnfPlan(net)
         self.noise: Optional[torch.Tensor] = None
 

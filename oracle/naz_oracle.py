@@ -410,6 +410,83 @@ def rk4_augmented(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor, t0: 
     return x, a
 
 
+# Dormand-Prince 5(4) tableau: naz's in-tree Dopri5 (neural_nets/__deprecated__/neural_odes/
+# odeint.py:136-160; c_x rows = a_ij, last row = b, c_err = b - b*)
+DOPRI5_A = [[1 / 5], [3 / 40, 9 / 40], [44 / 45, -56 / 15, 32 / 9],
+            [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729],
+            [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656]]
+DOPRI5_B = [35 / 384, 0.0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84]
+DOPRI5_E = [35 / 384 - 5179 / 57600, 0.0, 500 / 1113 - 7571 / 16695, 125 / 192 - 393 / 640,
+            -2187 / 6784 + 92097 / 339200, 11 / 84 - 187 / 2100, -1 / 40]
+
+
+def dopri5_augmented(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor, t0: float, t1: float,
+                     atol: float = 1e-4, rtol: float = 1e-4, group: int = 16, max_steps: int = 1000):
+    """Adaptive Dormand-Prince 5(4) on the augmented state [x, a] (naz
+    FFJORDTransform solver='dopri5', atol = rtol = 1e-4, continuous_transforms.py:73-81).
+
+    torchdyn (absent, unpinned) is restated by the standard embedded-RK controller it shares
+    with torchdiffeq: RMS error norm of err / (atol + rtol max(|y0|, |y1|)) over the state,
+    accept when <= 1, h *= clamp(0.9 norm^(-1/5), 0.2 (1 on accept), 10); Hairer's initial-step
+    heuristic (order 5); FSAL.  The last step is clipped to end exactly at t1 (no dense-output
+    interpolation).  One step size per GROUP of consecutive rows — the kernel's 16-row wave —
+    instead of torchdyn's single step size for the whole batch (a finer control; the same
+    tolerance).  Returns x(t1), a(t1) and the number of RHS evaluations per group."""
+    B = x.shape[0]
+    xs, as_, nfes = [], [], []
+    for g0 in range(0, B, group):
+        sl = slice(g0, min(B, g0 + group))
+        cg = None if ctx is None else (ctx[sl] if ctx.dim() == 2 and ctx.shape[0] == B else ctx)
+        y = x[sl].clone()
+        a = torch.zeros(y.shape[0], dtype=y.dtype)
+        e = eps[sl]
+
+        def f(v):
+            return hutchinson_rhs(net, v, cg, e)
+
+        def rms(u, ua):
+            return float(torch.sqrt((torch.sum(u ** 2) + torch.sum(ua ** 2)) / (u.numel() + ua.numel())))
+        direction = 1.0 if t1 > t0 else -1.0
+        k0, k0a = f(y)
+        sc, sca = atol + rtol * y.abs(), atol + rtol * a.abs()
+        d0, d1 = rms(y / sc, a / sca), rms(k0 / sc, k0a / sca)
+        h0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
+        f1, f1a = f(y + direction * h0 * k0)
+        d2 = rms((f1 - k0) / sc, (f1a - k0a) / sca) / h0
+        h1 = max(1e-6, h0 * 1e-3) if max(d1, d2) <= 1e-15 else (0.01 / max(d1, d2)) ** (1.0 / 6.0)
+        h = min(100 * h0, h1)
+        nfe, t, steps = 2, t0, 0
+        while steps < max_steps and t != t1:
+            rem = abs(t1 - t)
+            last = h >= rem
+            hh = direction * (rem if last else h)
+            ks, kas = [k0], [k0a]
+            for row in DOPRI5_A:
+                ki, kia = f(y + hh * sum(c * k for c, k in zip(row, ks)))
+                ks.append(ki)
+                kas.append(kia)
+            y5 = y + hh * sum(c * k for c, k in zip(DOPRI5_B, ks))
+            a5 = a + hh * sum(c * k for c, k in zip(DOPRI5_B, kas))
+            k6, k6a = f(y5)
+            ks.append(k6)
+            kas.append(k6a)
+            nfe += 6
+            err = hh * sum(c * k for c, k in zip(DOPRI5_E, ks))
+            erra = hh * sum(c * k for c, k in zip(DOPRI5_E, kas))
+            en = rms(err / (atol + rtol * torch.maximum(y.abs(), y5.abs())),
+                     erra / (atol + rtol * torch.maximum(a.abs(), a5.abs())))
+            if en <= 1.0:
+                y, a, k0, k0a = y5, a5, k6, k6a
+                t = t1 if last else t + hh
+            factor = 10.0 if en == 0 else min(10.0, max(0.9 / en ** 0.2, 1.0 if en <= 1.0 else 0.2))
+            h = abs(hh) * factor
+            steps += 1
+        xs.append(y)
+        as_.append(a)
+        nfes.append(nfe)
+    return torch.cat(xs), torch.cat(as_), nfes
+
+
 class FFJORD:
     """a11: naz ``FFJORDTransform`` (continuous_transforms.py:70-106).  ``inverse`` = its
     ``_inverse`` (integrate t 0 -> 1, the log_prob direction), ``forward`` = ``_call``

@@ -212,3 +212,72 @@ def test_cnf_f16x3_range_guard(scale):
     cf = 2.0 if scale == 1.0 else 4.0
     assert_parity(_np(y), y64, y32, what=f"range guard scale={scale} y", count_factor=cf)
     assert_parity(_np(a), a64, a32, what=f"range guard scale={scale} ld", count_factor=cf)
+
+
+def _oracle_dopri5(D, C, hidden, act, x, c, eps, t0, t1, atol, rtol, seed=3):
+    spec = dict(flow_type="cnf", D=D, C=C, hidden=hidden, L=1, activation=act)
+    st = {k: v.float() for k, v in O.random_state(spec, seed=seed, last_layer_scale=1.0).items()}
+    net = O.build_flow(spec, st, torch.float64).layers[0].nn
+    ct = None if c is None else torch.as_tensor(c).double()
+    y, a, nfe = O.dopri5_augmented(net, torch.as_tensor(x).double(), ct, torch.as_tensor(eps).double(), t0, t1,
+                                   atol, rtol)
+    yr, ar = O.rk4_augmented(net, torch.as_tensor(x).double(), ct, torch.as_tensor(eps).double(), t0, t1, 256)
+    return y.numpy(), a.numpy(), nfe, yr.numpy(), ar.numpy()
+
+
+@pytest.mark.parametrize("D,C,hidden,act", [(4, 2, [32, 32], "softplus"), (2, 2, [128, 64, 64], "softplus"),
+                                            (16, 0, [128, 128, 128], "softplus")])
+@pytest.mark.parametrize("direction", [(0.0, 1.0), (1.0, 0.0)])
+@pytest.mark.parametrize("mfma", ["f32", "f16x3"])
+def test_cnf_dopri5_vs_oracle(D, C, hidden, act, direction, mfma):
+    """§8f rank 3: adaptive dopri5 (per-16-row step control) vs the fp64 restatement with the same
+    groups and controller, and vs the converged solution (RK4, 256 steps): the error is at the
+    tolerance's scale and the step counts agree with the oracle's on (almost) every group."""
+    from naz_amd import ops
+    B, atol, rtol = 200, 1e-4, 1e-4
+    rng = np.random.default_rng(D * 10 + C + 1)
+    x = (rng.standard_normal((B, D)) * 0.8).astype(np.float32)
+    c = rng.standard_normal((B, C)).astype(np.float32) if C else None
+    eps = rng.standard_normal((B, D)).astype(np.float32)
+    t0, t1 = direction
+    y64, a64, nfe64, yr, ar = _oracle_dopri5(D, C, hidden, act, x, c, eps, t0, t1, atol, rtol)
+    _, _, flat = _oracle_block(D, C, hidden, act, x, c, eps, t0, t1, 1, torch.float64)
+    d = ops.cnf_desc(D, C, hidden, act, mfma)
+    if not ops.cnf_supported(d):
+        pytest.skip("mode not available for this shape")
+    packed = ops.cnf_pack(d, _cuda(flat))
+    nfe = torch.zeros((B + 15) // 16, device=DEV, dtype=torch.int32)
+    y, a = ops.cnf_integrate_dopri5(d, packed, _cuda(x), _cuda(eps), t0, t1, atol, rtol,
+                                    context=None if c is None else _cuda(c), nfe=nfe)
+    y, a, nfe = _np(y), _np(a), nfe.cpu().numpy()
+    assert (nfe > 0).all(), "a group ran out of steps"
+    # same step decisions on most groups (fp32 vs fp64 may flip a decision sitting at the threshold)
+    assert np.mean(nfe == np.asarray(nfe64)) >= 0.75, (nfe, nfe64)
+    # accuracy vs the converged solution: at the tolerance's scale
+    tol_y = 20 * (atol + rtol * np.abs(yr))
+    assert np.all(np.abs(y - yr) <= tol_y), np.abs(y - yr).max()
+    assert np.all(np.abs(a - ar) <= 20 * (atol + rtol * np.abs(ar))), np.abs(a - ar).max()
+    # vs the oracle's same-controller solve where the step sequence matched
+    same = np.repeat(nfe == np.asarray(nfe64), 16)[:B]
+    assert np.abs(y - y64)[same].max() <= 2e-4 and np.abs(a - a64)[same].max() <= 2e-4
+
+
+def test_cnf_dopri5_flow_api_and_ragged():
+    """NormalizingFlow("cnf", ..., solver="dopri5") log_prob runs the adaptive kernel; ragged
+    batches (the last wave partially filled) give the same per-row result as a full batch."""
+    from naz_amd.flows import NormalizingFlow
+    rng = np.random.default_rng(4)
+    f = NormalizingFlow("cnf", None, 4, 2, [32, 32], 2, solver="dopri5").to(DEV)
+    x = _cuda(rng.standard_normal((200, 4)) * 0.8)
+    c = _cuda(rng.standard_normal((200, 2)))
+    for t in f.transforms:
+        t.noise = _cuda(rng.standard_normal((200, 4)))
+    lp = f.log_prob(x, condition=c)
+    assert bool(torch.isfinite(lp).all())
+    nfe = f.transforms[0].last_nfe if hasattr(f.transforms[0], "last_nfe") else None
+    for t in f.transforms:
+        t.noise = t.noise[:37]
+    lp37 = f.log_prob(x[:37], condition=c[:37])
+    # rows 0..31 form the same two 16-row groups in both batches
+    assert torch.equal(lp37[:32], lp[:32])
+    assert nfe is None or int(nfe.min()) > 0

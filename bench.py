@@ -214,13 +214,21 @@ def run_cnf(args, dev, rank, world, dist):
     packed = plan.packed()
     eps = torch.randn(B, CNF_D, device=dev)
     lp = torch.empty(B, device=dev)
+    dopri5 = args.cnf_solver == "dopri5"
+    nfe = torch.zeros((B + 15) // 16, device=dev, dtype=torch.int32)
+
+    def solve():
+        if dopri5:  # §8f rank 3: adaptive Dormand-Prince, atol = rtol = 1e-4 (naz's setting)
+            return ops.cnf_integrate_dopri5(plan.desc, packed, x, eps, 0.0, 1.0, 1e-4, 1e-4, ld_out=lp,
+                                            ld_mode=ops.LD_ROWSUM_SUB, nfe=nfe)[0]
+        return ops.cnf_integrate(plan.desc, packed, x, eps, 0.0, 1.0, CNF_STEPS, ld_out=lp,
+                                 ld_mode=ops.LD_ROWSUM_SUB)[0]
 
     def step():
         # one log_prob: fresh Hutchinson probe, the solve (ld accumulated into lp), base density
         torch.randn(B, CNF_D, device=dev, out=eps)
         lp.zero_()
-        z, _ = ops.cnf_integrate(plan.desc, packed, x, eps, 0.0, 1.0, CNF_STEPS, ld_out=lp,
-                                 ld_mode=ops.LD_ROWSUM_SUB)
+        z = solve()
         ops.base_log_prob(z, out=lp, accumulate=True)
 
     stream = torch.cuda.current_stream(dev)
@@ -238,8 +246,7 @@ def run_cnf(args, dev, rank, world, dist):
             lp.zero_()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            z, _ = ops.cnf_integrate(plan.desc, packed, x, eps, 0.0, 1.0, CNF_STEPS, ld_out=lp,
-                                     ld_mode=ops.LD_ROWSUM_SUB)
+            z = solve()
             e1.record(stream)
             ops.base_log_prob(z, out=lp, accumulate=True)
             evs.append((e0, e1))
@@ -254,7 +261,11 @@ def run_cnf(args, dev, rank, world, dist):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_s = float(tt[0]), float(tt[1])
     if rank == 0:
-        achieved = cnf_flops_per_row() * B / kern_s / 1e12
+        flop_row = cnf_flops_per_row()
+        if dopri5:  # measured RHS evaluations per row (last step's solve) x FLOPs per RHS
+            nfe_mean = float(nfe.double().mean())
+            flop_row = int(flop_row / (4 * CNF_STEPS) * nfe_mean)
+        achieved = flop_row * B / kern_s / 1e12
         mode = plan.mode or "f32"
         if mode == "f16x3":
             # layer 0 exact FP32, hidden + output layers on three fp16 products (FLOP-weighted)
@@ -271,8 +282,11 @@ def run_cnf(args, dev, rank, world, dist):
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: x ~ 0.5 x 8-component Gaussian mixture; random-init weights (nn.Linear default, "
                     "torch seed 1234); eps ~ N(0, I) redrawn per step",
-            "config": {"workload": "BASELINE configs[4]: FFJORD block D=16, H=[128,128,128], softplus, fixed-step "
-                                   "RK4 x 8 (NFE 32, SURVEY.md §8d pin), log_prob (naz_cnf_integrate t 0->1)",
+            "config": {"workload": "BASELINE configs[4]: FFJORD block D=16, H=[128,128,128], softplus, " + (
+                                   "adaptive dopri5 atol=rtol=1e-4 per 16-row group (SURVEY.md §8f rank 3), "
+                                   "log_prob (naz_cnf_integrate_dopri5 t 0->1)" if dopri5 else
+                                   "fixed-step RK4 x 8 (NFE 32, SURVEY.md §8d pin), log_prob "
+                                   "(naz_cnf_integrate t 0->1)"),
                        "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"dp{world} (independent row shards, no collective)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -280,9 +294,34 @@ def run_cnf(args, dev, rank, world, dist):
                          "peak_note": "f16x3: layer 0 at the exact-FP32 MFMA peak, the rest at the dense fp16 "
                                       "MFMA peak / 3 products, FLOP-weighted; f32: exact-FP32 MFMA peak "
                                       f"{FP32_PEAK_TFLOPS}",
-                         "kernel": f"cnf_kernel<16,0,128,128,128,0,softplus,{mode}>",
-                         "flop_per_row": cnf_flops_per_row(), "avg_kernel_ms": kern_s * 1e3},
+                         "kernel": f"{'cnf_dopri5_kernel' if dopri5 else 'cnf_kernel'}"
+                                   f"<16,0,128,128,128,0,softplus,{mode}>",
+                         "flop_per_row": flop_row, "avg_kernel_ms": kern_s * 1e3},
         }
+        if dopri5:
+            rec["nfe_per_row"] = {"mean": nfe_mean, "min": int(nfe.min()), "max": int(nfe.max())}
+        if world == 1 and not args.no_cpu_baseline:
+            # the reference's arithmetic on the host: oracle FFJORD RHS (torch autograd VJP trace),
+            # same solver, fp32, all host threads, on a bounded row sample
+            from oracle import naz_oracle as O
+            lins = t.net.linears()
+            net = O.FCNN([l.weight.detach().cpu().float() for l in lins], [l.bias.detach().cpu().float() for l in lins])
+            nrow = 1 << 16
+            xs, es = x[:nrow].cpu(), eps[:nrow].cpu()
+            times = []
+            with torch.inference_mode(False):
+                for _ in range(2):
+                    c0 = time.perf_counter()
+                    if dopri5:
+                        O.dopri5_augmented(net, xs, None, es, 0.0, 1.0, 1e-4, 1e-4, group=nrow)
+                    else:
+                        O.rk4_augmented(net, xs, None, es, 0.0, 1.0, CNF_STEPS)
+                    times.append(time.perf_counter() - c0)
+            rec["cpu_baseline"] = {"value": nrow / min(times), "unit": "samples/s",
+                                   "cores": torch.get_num_threads(), "kind": "port",
+                                   "sample": f"{nrow} rows, oracle FFJORD (torch fp32, autograd VJP trace), "
+                                             f"{'dopri5 (one step size for the sample)' if dopri5 else 'RK4 x 8'}, "
+                                             f"best of 2 ({min(times):.2f} s)"}
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()
@@ -520,6 +559,8 @@ def main():
     ap.add_argument("--cnf", action="store_true",
                     help="BASELINE configs[4]: 16-dim FFJORD CNF (H=[128]*3, softplus, Hutchinson trace, RK4 x 8 "
                          "steps) log_prob at 2^18 rows per GPU")
+    ap.add_argument("--cnf-solver", choices=["rk4", "dopri5"], default="rk4",
+                    help="--cnf: pinned fixed-step RK4 x 8 (default) or adaptive dopri5 (atol = rtol = 1e-4)")
     ap.add_argument("--flow", choices=sorted(FLOW_CASES), default=None,
                     help="time log_prob of another §8 flow through the NormalizingFlow API (see FLOW_CASES)")
     ap.add_argument("--bayes", choices=["lp", "sample"], default=None,

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/round
-rm -rf $O/pmc $O/prof $O/prof_cnf $O/prof_train
+rm -rf $O/pmc $O/prof $O/prof_cnf $O/prof_train $O/prof_cnf_dopri5 $O/prof_bayes_sample
 mkdir -p $O
 step() {  # step <name> <timeout> <cmd...>; stop on crash / timeout
   local name=$1 t=$2; shift 2
@@ -27,4 +27,9 @@ step gemm_bench 120 python scripts/gemm_bench.py
 step cnf 300 python bench.py --cnf --steps 10 --warmup 3
 step prof_cnf 240 rocprofv3 --kernel-trace --stats -d $O/prof_cnf -o run --output-format csv -- python3 bench.py --cnf --steps 10 --warmup 3
 for f in config2 maf nsa; do step flow_$f 240 python bench.py --flow $f --steps 10 --warmup 3; done
+step cnf_dopri5 300 python bench.py --cnf --cnf-solver dopri5 --steps 10 --warmup 3
+step prof_cnf_dopri5 240 rocprofv3 --kernel-trace --stats -d $O/prof_cnf_dopri5 -o run --output-format csv -- python3 bench.py --cnf --cnf-solver dopri5 --steps 10 --warmup 3 --no-cpu-baseline
+step bayes_lp 240 python bench.py --bayes lp --steps 10 --warmup 3
+step bayes_sample 240 python bench.py --bayes sample --steps 10 --warmup 3
+step prof_bayes_sample 240 rocprofv3 --kernel-trace --stats -d $O/prof_bayes_sample -o run --output-format csv -- python3 bench.py --bayes sample --steps 5 --warmup 2 --no-cpu-baseline
 exit 0

@@ -97,6 +97,14 @@ int naz_linear_act_batched(const float* ctx, int64_t ldc, int64_t sctx, int C, c
                            int64_t sb, float* y, int64_t ldy, int64_t sy, int64_t M, int N, int nbatch, int act,
                            void* stream);
 
+/* ---- a10: chained input gradient of a Linear/act conditioner -------------------
+ * C[m, n] = (Σ_k A[m, k] · W[k, n] · mask[k, n]) · act'(dy[m, n]), act' taken from the
+ * post-activation value dy (tanh 1 - y², relu y > 0, softplus 1 - e^-y, sigmoid y(1 - y)):
+ * dPre_{l-1} = (dPre_l · (W_l ⊙ M_l)) ⊙ act'(h_{l-1}) in one batch-row GEMM (replaces the
+ * naz_gemm dX + naz_act_bwd pair of the autograd walk). mask nullable; W, mask rows at ldw, ldm. */
+int naz_gemm_dact(const float* A, int64_t lda, int K, const float* W, int64_t ldw, const float* mask, int64_t ldm,
+                  float* C, int64_t ldc, const float* dy, int64_t lddy, int dact, int64_t M, int N, void* stream);
+
 /* ---- a5/a6 forward + §8f rank 2: fused MADE conditioner + affine step ------
  * One MAF layer in the sampling direction for P weight draws in one launch: replaces
  * ConditionalAutoRegressiveNN.forward + AffineAutoregressive._call (naz/flows/transforms.py:

@@ -80,6 +80,85 @@ def linear_act(x, weight, bias, act="identity", context=None, mask=None):
     return LinearActFn.apply(x, context, weight, bias, mask, act)
 
 
+def _param_grads(gpre, x, c, W, need_W: bool, need_b: bool):
+    """dW (and db riding on it as an all-ones column) of one Linear layer: as LinearActFn."""
+    M = gpre.shape[0]
+    Cd = 0 if c is None else c.shape[-1]
+    g_W = g_b = None
+    if need_b:
+        g_b = torch.empty(W.shape[0], device=W.device, dtype=torch.float32)
+    gT = gpre.t()
+    if need_W:
+        g_W = torch.empty_like(W)
+        if Cd:
+            cc = c.reshape(1, -1).expand(M, Cd) if (c.dim() == 1 or c.shape[0] == 1) and M != 1 else c
+            ops.gemm(gT, cc, out=g_W[:, :Cd], rowsum=g_b)
+        if x is not None:
+            ops.gemm(gT, x, out=g_W[:, Cd:], rowsum=None if Cd else g_b)
+    elif need_b:
+        ops.gemm(gT, gT[:0].t(), out=torch.empty(W.shape[0], 0, device=W.device), rowsum=g_b)
+    return g_W, g_b
+
+
+class ChainFn(Function):
+    """A whole Linear/act conditioner chain (pyro DenseNN / MADE forward with masked weights
+    already applied) as ONE autograd node.  Backward walks the layers in reverse and forms each
+    hidden layer's pre-activation gradient with naz_gemm_dact: dPre_{l-1} = (dPre_l · W_l) ⊙
+    act'(h_{l-1}) in the dX GEMM's epilogue, so no separate naz_act_bwd pass reads and writes the
+    [B, H] gradient (values identical to the LinearActFn-per-layer walk)."""
+
+    @staticmethod
+    def forward(ctx, x, context, act: str, *wb):
+        n = len(wb) // 2
+        hs = []
+        h = x
+        for i in range(n):
+            a = act if i < n - 1 else "identity"
+            h = ops.linear_act(x if i == 0 else h, wb[2 * i], wb[2 * i + 1], a,
+                               context=context if i == 0 else None)
+            hs.append(h)
+        ctx.act, ctx.n = act, n
+        ctx.has_bias = [wb[2 * i + 1] is not None for i in range(n)]
+        ctx.save_for_backward(x, context, *[wb[2 * i] for i in range(n)], *hs[:-1])
+        return hs[-1]
+
+    @staticmethod
+    def backward(ctx, g_y):
+        n, act = ctx.n, ctx.act
+        saved = ctx.saved_tensors
+        x, c = saved[0], saved[1]
+        Ws = saved[2:2 + n]
+        hs = saved[2 + n:]
+        grads = [None] * (2 * n)
+        gpre = g_y.contiguous()
+        g_x = g_c = None
+        for i in reversed(range(n)):
+            W = Ws[i]
+            inp = x if i == 0 else hs[i - 1]
+            ci = c if i == 0 else None
+            gW, gb = _param_grads(gpre, inp, ci, W, _needs(ctx, 3 + 2 * i), ctx.has_bias[i] and _needs(ctx, 4 + 2 * i))
+            grads[2 * i], grads[2 * i + 1] = gW, gb
+            Cd = 0 if ci is None else ci.shape[-1]
+            if i > 0:
+                gpre = ops.gemm_dact(gpre, W, hs[i - 1], act)  # (gpre · W) ⊙ act'(h_{i-1})
+            else:
+                if x is not None and _needs(ctx, 0):
+                    g_x = ops.gemm(gpre, W[:, Cd:])
+                if Cd and _needs(ctx, 1):
+                    Wc = W[:, :Cd]
+                    if c.shape[0] == gpre.shape[0] and c.dim() == 2:
+                        g_c = ops.gemm(gpre, Wc)
+                    else:
+                        g_c = ops.gemm(ops.colsum(gpre).reshape(1, -1), Wc).reshape(c.shape)
+        return (g_x, g_c, None, *grads)
+
+
+def chain(x, weights, biases, act: str, context=None):
+    """Conditioner forward recorded as one ChainFn node (see there)."""
+    wb = [t for pair in zip(weights, biases) for t in pair]
+    return ChainFn.apply(x, context, act, *wb)
+
+
 class RqsFn(Function):
     """(y, ld_row) = RQ spline of x over conditioner output ``raw`` (row-sum log-det of THIS
     direction: the forward ldf, or the inverse's -ldf)."""

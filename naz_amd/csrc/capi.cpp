@@ -97,6 +97,17 @@ int naz_made_affine_fwd(const float* packed, int64_t wstride, int nhid, int nh, 
                          P, act, as_stream(stream));
 }
 
+int naz_gemm_dact(const float* A, int64_t lda, int K, const float* W, int64_t ldw, const float* mask, int64_t ldm,
+                  float* C, int64_t ldc, const float* dy, int64_t lddy, int dact, int64_t M, int N, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return set_error("naz_gemm_dact: negative shape");
+  if (M == 0 || N == 0) return 0;
+  if (A == nullptr || W == nullptr || C == nullptr || dy == nullptr) return set_error("naz_gemm_dact: null pointer");
+  if (dact < 0 || dact > NAZ_ACT_SIGMOID) return set_error("naz_gemm_dact: unknown activation %d", dact);
+  const int rc = rowgemm_dact(A, lda, K, W, ldw, mask, ldm, C, ldc, dy, lddy, dact, M, N, as_stream(stream));
+  if (rc == 1) return set_error("naz_gemm_dact: weights too large for the batch-row kernel");
+  return rc;
+}
+
 int naz_affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
                   float* ld, int ld_mode, int64_t B, int D, void* stream) {
   if (B < 0 || D <= 0) return set_error("naz_affine_ar: bad shape");

@@ -63,6 +63,11 @@ struct RowGemmArgs {
   // problem z reads a0 + z*za0, a1 + z*za1, b + z*zb, bias + z*zbias and writes c + z*zc
   // (the mask is shared); all zero for a single problem
   int64_t za0, za1, zb, zbias, zc;
+  // optional epilogue factor act'(dy[m, n]) from a post-activation value (the chained dX of a
+  // Linear/act conditioner: dPre_{l-1} = (dPre_l · W_l) ⊙ act'(h_{l-1})); null = none
+  const float* dy;
+  int64_t lddy;
+  int dact;
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -191,7 +196,12 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          E[row * EP + 32 * oo + (lane & 31)] = activate_rt(p.act, acc[o0 + oo][r] + bn);
+          float v = activate_rt(p.act, acc[o0 + oo][r] + bn);
+          if (p.dy != nullptr) {
+            const int64_t m = m0 + wave * 32 + row;
+            if (m < p.M && n < p.N) v *= activate_grad_from_out(p.dact, p.dy[m * p.lddy + n]);
+          }
+          E[row * EP + 32 * oo + (lane & 31)] = v;
         }
       }
       // 8 EG float4 per row; 64 / (8 EG) rows per wave-instruction
@@ -232,7 +242,8 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
       const int64_t m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m >= p.M) continue;
       float* dst = p.c + m * p.ldc + n;
-      const float v = activate_rt(p.act, acc[o][r] + bn);
+      float v = activate_rt(p.act, acc[o][r] + bn);
+      if (p.dy != nullptr) v *= activate_grad_from_out(p.dact, p.dy[m * p.lddy + n]);
       *dst = p.accumulate ? *dst + v : v;
     }
   }
@@ -632,6 +643,30 @@ int rowgemm_linear_batched(const float* ctx, int64_t ldc, int64_t zc, int C, con
   p.act = act;
   p.accumulate = 0;
   return rowgemm(p, s, nz);
+}
+
+// naz_gemm_dact: C[m, n] = (Σ_k A[m, k] W[k, n] mask[k, n]) · act'(dy[m, n])   (A rows at lda)
+int rowgemm_dact(const float* A, int64_t lda, int K, const float* W, int64_t ldw, const float* mask, int64_t ldm,
+                 float* C, int64_t ldc, const float* dy, int64_t lddy, int dact, int64_t M, int N, hipStream_t s) {
+  RowGemmArgs p{};
+  p.a1 = A;
+  p.lda1 = lda;
+  p.ka1 = K;
+  p.b = W;  // B(k, n) = W[k, n]
+  p.sbk = ldw;
+  p.sbn = 1;
+  p.mask = mask;
+  p.smk = ldm;
+  p.smn = 1;
+  p.c = C;
+  p.ldc = ldc;
+  p.M = M;
+  p.N = N;
+  p.act = NAZ_ACT_IDENTITY;
+  p.dy = dy;
+  p.lddy = lddy;
+  p.dact = dact;
+  return rowgemm(p, s);
 }
 
 // gemm() fast paths; return 1 when the shape was not taken (caller falls back)

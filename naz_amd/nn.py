@@ -9,6 +9,8 @@ Every forward runs ``naz_linear_act`` (fused concat + mask + bias + activation).
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Sequence
 
 import torch
@@ -89,11 +91,19 @@ def _slices(param_dims: Sequence[int]):
     return [slice(int(s), int(e)) for s, e in zip(starts, ends)]
 
 
+# conditioner chains under autograd run as one ChainFn node (act' fused into the dX GEMMs);
+# NAZ_CHAIN_NODE=0 selects the LinearActFn-per-layer walk (A/B, tests)
+_CHAIN_NODE = os.environ.get("NAZ_CHAIN_NODE", "1") != "0"
+
+
 def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Tensor], masked: bool) -> torch.Tensor:
     """The conditioner pass; recorded for autograd (HIP backward kernels) when grad mode is on
     and a weight, the input or the context requires grad."""
     n = len(layers)
     grad = ag.params_require_grad(layers) or ag.tensor_requires_grad(x, context)
+    if grad and n >= 2 and x is not None and _CHAIN_NODE:  # one autograd node, act' fused into dX
+        ws = [layer.masked_weight() if masked else layer.weight for layer in layers]
+        return ag.chain(x, ws, [layer.bias for layer in layers], f_name, context=context)
     lin = ag.linear_act if grad else ops.linear_act
     h = None
     for i, layer in enumerate(layers):

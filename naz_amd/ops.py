@@ -16,7 +16,7 @@ from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, RQS_FAST, LD_PERDIM, LD_ROWSUM
 
 Tensor = torch.Tensor
 
-__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "affine_ar", "affine_ar_bwd", "base_log_prob",
+__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "gemm_dact", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
            "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5",
@@ -374,6 +374,31 @@ def gemm(a: Tensor, b: Tensor, out: Optional[Tensor] = None, mask: Optional[Tens
     check(lib().naz_gemm(M, N, K, _p(a), a.stride(0), a.stride(1), _p(b), b.stride(0), b.stride(1), _p(out),
                          out.stride(0), out.stride(1), _p(mask), smm, smn, int(mask_b), int(accumulate), sk,
                          _p(rowsum), _stream(dev)), "gemm")
+    return out
+
+
+def gemm_dact(a: Tensor, weight: Tensor, y: Tensor, act: str, mask: Optional[Tensor] = None,
+              out: Optional[Tensor] = None) -> Tensor:
+    """(a @ (weight * mask)) * act'(y) in one batch-row GEMM (naz_gemm_dact): the input
+    gradient of a Linear layer chained with the derivative of the activation that produced its
+    input (``y`` = that activation's output)."""
+    dev = _dev(a, weight, y, mask, out)
+    a, lda = _rows(a)
+    M, K = a.shape
+    if weight.shape[0] != K or weight.stride(1) != 1:
+        raise ValueError("gemm_dact: weight must be [K, N] with unit column stride")
+    N = weight.shape[1]
+    y, lddy = _rows(y)
+    if y.shape != (M, N):
+        raise ValueError(f"gemm_dact: y must be {(M, N)}")
+    if mask is not None and (mask.shape != weight.shape or mask.stride(1) != 1):
+        raise ValueError("gemm_dact: mask must match weight")
+    if out is None:
+        npad = (N + 3) // 4 * 4
+        out = torch.empty((M, npad), device=dev, dtype=torch.float32)[:, :N]
+    check(lib().naz_gemm_dact(_p(a), lda, K, _p(weight), weight.stride(0), _p(mask),
+                              0 if mask is None else mask.stride(0), _p(out), out.stride(0), _p(y), lddy, ACT[act], M, N,
+                              _stream(dev)), "gemm_dact")
     return out
 
 

@@ -280,3 +280,25 @@ def test_graph_walk_matches_fused_inference():
     assert lp_graph.requires_grad and not lp_fused.requires_grad
     assert_parity(_np(lp_graph), fx["lp64"], fx["lp32"], what="graph walk")
     assert_parity(_np(lp_fused), fx["lp64"], fx["lp32"], what="fused")
+
+
+@pytest.mark.parametrize("ftype,extra,C", [("nsc", (8, 8), 32), ("maf", (), 2), ("nsa", (8,), 2)])
+def test_chain_node_matches_per_layer_walk(monkeypatch, ftype, extra, C):
+    """The conditioner chain as one autograd node (ChainFn: act' fused into the dX GEMM
+    epilogue by naz_gemm_dact) gives the per-layer LinearActFn walk's gradients."""
+    from naz_amd import nn as nnmod
+    from naz_amd.flows import NormalizingFlow
+    D = 16 if ftype == "nsc" else 4
+    torch.manual_seed(0)
+    f = NormalizingFlow(ftype, None, D, C, [64, 64], 2, *extra).to(DEV)
+    x = torch.randn(2048, D, device=DEV)
+    c = torch.randn(2048, C, device=DEV)
+    grads = {}
+    for node in (True, False):
+        monkeypatch.setattr(nnmod, "_CHAIN_NODE", node)
+        f.zero_grad()
+        (-f.log_prob(x, condition=c).mean()).backward()
+        grads[node] = [p.grad.detach().clone() for p in f.parameters() if p.grad is not None]
+    assert len(grads[True]) == len(grads[False]) > 0
+    for a, b in zip(grads[True], grads[False]):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-7 * float(b.abs().max()) + 1e-12), (a - b).abs().max()

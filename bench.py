@@ -493,8 +493,7 @@ def run_bayes(args, dev, rank, world, dist):
     full = 2 * BAYES["L"] * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
     if lp_mode:
         fl_ref = D * full  # the reference's D full MADE passes per layer
-        fl_row = sum(2 * (b - a) * n for pl in flow["plans"] for grp in pl.hidden for (_, a, b, n, _, _) in grp)
-        fl_row += sum(2 * 2 * n for pl in flow["plans"] for (_, n, _, _) in pl.outs)
+        fl_row = flow["lp_flops_per_row"]()  # executed: context-only units folded into per-draw biases
     else:
         fl_ref = fl_row = full
     achieved = fl_row * P * B / step_s / 1e12

@@ -120,6 +120,14 @@ int naz_made_affine_fwd(const float* packed, int64_t wstride, int nhid, int nh, 
                         int64_t ldc, int64_t sctx, const float* x, int64_t ldx, int64_t sx, float* y, int64_t ldy,
                         int64_t sy, float* ld, int64_t sld, int ld_mode, int64_t S, int P, int act, void* stream);
 
+/* Inverse single-dim variant (the last pass of a 2-dim MAF inverse, §8f rank 1): a context-free
+ * MADE chain on x (C = 0) whose output rows 0, 1 are (mean, log_scale) of dim `dim`; then
+ * y = x except y[dim] = (v[dim] - mean)·exp(-clamp(ls, -5, 3)), ld op= clamp(ls). v (the data
+ * being inverted) rows at ldv, draw stride sv; packed as naz_made_packed_floats(nhid, nh, 0, D). */
+int naz_made_affine_inv1(const float* packed, int64_t wstride, int nhid, int nh, int D, const float* x, int64_t ldx,
+                         int64_t sx, const float* v, int64_t ldv, int64_t sv, int dim, float* y, int64_t ldy,
+                         int64_t sy, float* ld, int64_t sld, int ld_mode, int64_t S, int P, int act, void* stream);
+
 /* ---- a5: affine autoregressive elementwise step --------------------------
  * Replaces the elementwise part of [pyro] AffineAutoregressive._call / ._inverse
  * (naz/flows/transforms.py:159; JAX restatement bflow_jax_maf.py:169-194):

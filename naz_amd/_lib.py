@@ -41,6 +41,8 @@ SIGNATURES = {
                                          _vp]),
     "naz_linear_act": (C.c_int, [_vp, _i64, _i, _vp, _i64, _i, _vp, _vp, _vp, _vp, _i64, _i64, _i, _i, _vp]),
     "naz_gemm_dact": (C.c_int, [_vp, _i64, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i, _i64, _i, _vp]),
+    "naz_made_affine_inv1": (C.c_int, [_vp, _i64, _i, _i, _i, _vp, _i64, _i64, _vp, _i64, _i64, _i, _vp, _i64, _i64,
+                                       _vp, _i64, _i, _i64, _i, _i, _vp]),
     "naz_made_packed_floats": (_i64, [_i, _i, _i, _i]),
     "naz_made_affine_fwd": (C.c_int, [_vp, _i64, _i, _i, _i, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64,
                                       _vp, _i64, _i, _i64, _i, _i, _vp]),

@@ -108,6 +108,15 @@ int naz_gemm_dact(const float* A, int64_t lda, int K, const float* W, int64_t ld
   return rc;
 }
 
+int naz_made_affine_inv1(const float* packed, int64_t wstride, int nhid, int nh, int D, const float* x, int64_t ldx,
+                         int64_t sx, const float* v, int64_t ldv, int64_t sv, int dim, float* y, int64_t ldy,
+                         int64_t sy, float* ld, int64_t sld, int ld_mode, int64_t S, int P, int act, void* stream) {
+  if (S < 0 || P < 0 || x == nullptr || y == nullptr || packed == nullptr)
+    return set_error("naz_made_affine_inv1: bad arguments");
+  return made_affine_inv1(packed, wstride, nhid, nh, D, x, ldx, sx, v, ldv, sv, dim, y, ldy, sy, ld, sld, ld_mode, S,
+                          P, act, as_stream(stream));
+}
+
 int naz_affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
                   float* ld, int ld_mode, int64_t B, int D, void* stream) {
   if (B < 0 || D <= 0) return set_error("naz_affine_ar: bad shape");

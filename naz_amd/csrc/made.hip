@@ -49,6 +49,11 @@ struct MadeArgs {
   int64_t sld;
   int ld_mode;
   int64_t S;  // rows per draw
+  // inverse single-dim mode (naz_made_affine_inv1, inv_dim >= 0): raw rows 0, 1 = (mean, ls)
+  // of dim inv_dim; y = x except y[inv_dim] = (v[inv_dim] - mean) exp(-clamp(ls))
+  int inv_dim;
+  const float* v;
+  int64_t ldv, sv;
 };
 
 NAZ_DEV floatx16 mfma32(float a, float b, floatx16 c) { return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0); }
@@ -199,7 +204,16 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) made_affine_fwd_kernel(MadeAr
   __syncthreads();
 
   // affine step, one lane per row
-  if (h == 0 && live) {
+  if (h == 0 && live && p.inv_dim >= 0) {
+    float* yr = p.y + z * p.sy + row * p.ldy;
+    const float ls = fminf(fmaxf(E[wave][lane][1], -5.f), 3.f);
+    for (int i = 0; i < p.D; ++i)
+      yr[i] = i == p.inv_dim ? (p.v[z * p.sv + row * p.ldv + i] - E[wave][lane][0]) * expf(-ls) : xr[i];
+    float* l = p.ld + z * p.sld + row;
+    if (p.ld_mode == NAZ_LD_ROWSUM) *l = ls;
+    else if (p.ld_mode == NAZ_LD_ROWSUM_ADD) *l += ls;
+    else if (p.ld_mode == NAZ_LD_ROWSUM_SUB) *l -= ls;
+  } else if (h == 0 && live) {
     float s = 0.f;
     float* yr = p.y + z * p.sy + row * p.ldy;
     for (int i = 0; i < p.D; ++i) {
@@ -238,6 +252,8 @@ void launch_nh(const MadeArgs& a, int act, int P, hipStream_t s) {
 }
 
 }  // namespace
+
+static int made_launch(const MadeArgs& a, int nh, int act, int P, hipStream_t s);
 
 int64_t made_packed_floats(int nhid, int nh, int C, int D) {
   const int s0 = ((C + D + 1) / 2 + 3) / 4 * 4;
@@ -280,6 +296,51 @@ int made_affine_fwd(const float* packed, int64_t wstride, int nhid, int nh, int 
   a.sld = sld;
   a.ld_mode = ld_mode;
   a.S = S;
+  a.inv_dim = -1;
+  a.v = nullptr;
+  return made_launch(a, nh, act, P, s);
+}
+
+int made_affine_inv1(const float* packed, int64_t wstride, int nhid, int nh, int D, const float* x, int64_t ldx,
+                     int64_t sx, const float* v, int64_t ldv, int64_t sv, int dim, float* y, int64_t ldy, int64_t sy,
+                     float* ld, int64_t sld, int ld_mode, int64_t S, int P, int act, hipStream_t s) {
+  if (S == 0 || P == 0) return 0;
+  if (nh < 1 || nh > 5) return set_error("naz_made_affine_inv1: hidden blocks %d not in 1..5 (width <= 160)", nh);
+  if (nhid < 1) return set_error("naz_made_affine_inv1: needs >= 1 hidden layer");
+  if (D < 1 || dim < 0 || dim >= D) return set_error("naz_made_affine_inv1: dim %d not in [0, D=%d)", dim, D);
+  if (act != ACT_TANH && act != ACT_RELU) return set_error("naz_made_affine_inv1: activation %d not built", act);
+  if (P > 65535) return set_error("naz_made_affine_inv1: P=%d > 65535", P);
+  if (ld == nullptr || v == nullptr || ld_mode < NAZ_LD_ROWSUM || ld_mode > NAZ_LD_ROWSUM_SUB)
+    return set_error("naz_made_affine_inv1: v and a row-sum ld buffer are required");
+  if ((reinterpret_cast<uintptr_t>(packed) & 15) || (wstride & 3))
+    return set_error("naz_made_affine_inv1: packed nets must be 16-byte aligned");
+  if (wstride < made_packed_floats(nhid, nh, 0, D)) return set_error("naz_made_affine_inv1: wstride too small");
+  MadeArgs a{};
+  a.w = packed;
+  a.wstride = wstride;
+  a.nhid = nhid;
+  a.C = 0;
+  a.D = D;
+  a.s0 = ((D + 1) / 2 + 3) / 4 * 4;
+  a.ctx = x;
+  a.x = x;
+  a.ldx = ldx;
+  a.sx = sx;
+  a.y = y;
+  a.ldy = ldy;
+  a.sy = sy;
+  a.ld = ld;
+  a.sld = sld;
+  a.ld_mode = ld_mode;
+  a.S = S;
+  a.inv_dim = dim;
+  a.v = v;
+  a.ldv = ldv;
+  a.sv = sv;
+  return made_launch(a, nh, act, P, s);
+}
+
+static int made_launch(const MadeArgs& a, int nh, int act, int P, hipStream_t s) {
   switch (nh) {
     case 1: launch_nh<1>(a, act, P, s); break;
     case 2: launch_nh<2>(a, act, P, s); break;

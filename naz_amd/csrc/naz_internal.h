@@ -45,6 +45,9 @@ int made_affine_fwd(const float* packed, int64_t wstride, int nhid, int nh, int 
                     int64_t sy, float* ld, int64_t sld, int ld_mode, int64_t S, int P, int act, hipStream_t s);
 int rowgemm_dact(const float* A, int64_t lda, int K, const float* W, int64_t ldw, const float* mask, int64_t ldm,
                  float* C, int64_t ldc, const float* dy, int64_t lddy, int dact, int64_t M, int N, hipStream_t s);
+int made_affine_inv1(const float* packed, int64_t wstride, int nhid, int nh, int D, const float* x, int64_t ldx,
+                     int64_t sx, const float* v, int64_t ldv, int64_t sv, int dim, float* y, int64_t ldy, int64_t sy,
+                     float* ld, int64_t sld, int ld_mode, int64_t S, int P, int act, hipStream_t s);
 int gemm_rows_try(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
                   int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
                   int mask_b, int accumulate, float* rowsum, hipStream_t s, int* rc);

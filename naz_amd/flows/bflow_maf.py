@@ -216,13 +216,16 @@ def _flat_layer(layer, P, dev):
 
 
 def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bounds=None, context=None,
-                          rows_per_chunk: int = 1 << 23) -> Dict[str, object]:
+                          rows_per_chunk: int = 1 << 23, fold_context: bool = True,
+                          fuse_pass2: bool = True) -> Dict[str, object]:
     """naz ``make_normalizing_flow`` (bflow_jax_maf.py:196-225) on MI355X.  Returns
     ``{"lp": f(params) -> [B], "sampler": f(params, rng_key, size) -> (y, log_j),
     "lp_batched": f(params_P) -> [P, B], "sampler_batched": f(params_P, rng_key, size)}``.
 
     ``x`` [B, D] are the evaluation rows; ``context`` None, [C] (broadcast) or [B, C].  The
-    single-draw functions are the batched ones at P = 1.  ``rows_per_chunk`` bounds the draws
+    single-draw functions are the batched ones at P = 1.  With one context vector,
+    ``fold_context`` evaluates the context-only (degree-0) MADE units once per draw and folds
+    them into biases (same values up to fp32 reassociation; False = the plain schedule).  ``rows_per_chunk`` bounds the draws
     evaluated together (activation memory ≈ 4·rows·Σwidths bytes)."""
     if bounds is not None:
         raise NotImplementedError("batched MAF: bounds=None only (see module docstring)")
@@ -296,11 +299,130 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             z = xn
         ops.base_log_prob(z.view(P * B, D), out=lp, accumulate=True)
 
+    # ---- one context vector for every row (the density-grid case, plot.py:189-204): every
+    # degree-0 hidden unit (masks reach only the context) is a per-draw constant.  Those units
+    # are computed once per draw (M = 1 launches) and their products with the later groups'
+    # weights fold into those groups' biases; the per-row GEMMs only see the x-dependent groups.
+    const_ctx = C > 0 and ctx.dim() == 1
+
+    def _split_maps(plan):
+        """Per block: (index maps of the constant columns, of the per-row columns, split e)."""
+        if hasattr(plan, "split"):
+            return plan.split
+        e_out = {}  # layer -> width of its degree-0 group (its constant columns)
+        for (li, a, b, n, w, bb) in plan.hidden[0]:
+            e_out[li] = b
+        split = []
+        for g in plan.hidden:
+            row = []
+            for (li, a, b, n, w, bb) in g:
+                e = C if li == 0 else e_out.get(li - 1, 0)
+                row.append((e, w[:, :e].contiguous(), w[:, e:].contiguous()))
+            split.append(row)
+        e_last = e_out.get(len(plan.widths) - 1, 0)
+        outs = [(e_last, w[:, :e_last].contiguous(), w[:, e_last:].contiguous()) for (i, n, w, bb) in plan.outs]
+        plan.split = (split, outs)
+        return plan.split
+
+    def _lp_chunk_const(params: Params, out: Tensor):
+        """_lp_chunk with the context's degree-0 units folded into per-draw biases."""
+        P = _draws(params)
+        z = x.expand(P, B, D).contiguous()
+        lp = out.reshape(P * B)
+        lp.zero_()
+        hs_all = torch.empty((P, B, width_sum), device=dev, dtype=torch.float32)
+        c1 = ctx.reshape(1, 1, C).expand(P, 1, C)
+        for l in reversed(range(len(plans))):
+            plan = plans[l]
+            F = _flat_layer(params[l], P, dev)
+            split, osplit = _split_maps(plan)
+            hs, o = [], 0
+            for w in plan.widths:
+                hs.append(hs_all[:, :, o:o + w])
+                o += w
+            # per-draw constants: the degree-0 group of every hidden layer ([P, 1, e])
+            hc = {}
+            for (li, a, b, n, w, bb) in plan.hidden[0]:
+                src = torch.cat((c1, torch.zeros((P, 1, D), device=dev)), 2) if li == 0 else hc[li - 1]
+                hc[li] = ops.linear_act_batched(src[:, :, :n].contiguous(), F[:, w], F[:, bb], act)
+            xn = torch.zeros_like(z)
+            z2, x2 = z.view(P * B, D), xn.view(P * B, D)
+            for k in range(1, D + 1):
+                if k == 2 and _fused_pass2(plan, split):
+                    # D = 2: pass 2 is one context-free MADE chain on x -> one fused launch
+                    z = _pass2_fused(plan, split, osplit, F, hc, c1, xn, z, lp.view(P, B))
+                    break
+                for (li, a, b, n, w, bb), (e, wc, wr) in zip(plan.hidden[k - 1], split[k - 1]):
+                    if k == 1:
+                        continue  # degree-0 groups: the constants above
+                    bias = F[:, bb]
+                    if e:  # constant columns -> bias (one row per draw)
+                        src = c1.contiguous() if li == 0 else hc[li - 1]
+                        bias = ops.linear_act_batched(src, F[:, wc], bias, "identity")[:, 0, :].contiguous()
+                    dst = hs[li][:, :, a:b]
+                    inp = xn if li == 0 else hs[li - 1][:, :, e:n]
+                    ops.linear_act_batched(inp, F[:, wr], bias, act, out=dst)
+                i, n, wb, bb = plan.outs[k - 1]
+                e, wc, wr = osplit[k - 1]
+                bias = F[:, bb]
+                if e:
+                    bias = ops.linear_act_batched(hc[len(plan.widths) - 1], F[:, wc], bias, "identity")[:, 0, :]
+                if n > e:
+                    raw = ops.linear_act_batched(hs[-1][:, :, e:n], F[:, wr], bias.contiguous(), "identity")
+                    raw = raw.reshape(P * B, 2)
+                else:  # only constant inputs: one raw row per draw
+                    raw = bias.reshape(P, 1, 2).expand(P, B, 2).reshape(P * B, 2)
+                ops.affine_ar(z2[:, i:i + 1], raw, True, ops.LD_ROWSUM_SUB, lp, out=x2[:, i:i + 1])
+            else:
+                z = xn
+        ops.base_log_prob(z.reshape(P * B, D), out=lp, accumulate=True)
+
+    def _fused_pass2(plan, split):
+        """D = 2 with every layer's degree-1 group in one block of <= 160 units (tanh / relu)."""
+        if D != 2 or act not in ("tanh", "relu") or not fuse_pass2:
+            return False
+        g1 = plan.hidden[1]
+        nl = len(plan.widths)
+        return (len(g1) == nl and [blk[0] for blk in g1] == list(range(nl)) and
+                all(b - a <= 160 for (li, a, b, n, w, bb) in g1))
+
+    def _pass2_fused(plan, split, osplit, F, hc, c1, xn, z, lp2):
+        """The order-2 dim of a 2-dim MAF layer: layer 0's degree-1 units from x, each later
+        layer's from the previous layer's (context / degree-0 parts folded into per-draw biases),
+        its two output rows, the inverse affine step — one naz_made_affine_inv1 launch."""
+        P = z.shape[0]
+        g1, s1 = plan.hidden[1], split[1]
+        rows = [b - a for (li, a, b, n, w, bb) in g1]
+        key = tuple(rows)
+        if getattr(plan, "p2_key", None) != key:
+            sp = MAFSpec(D, 0, rows, act)
+            sp.param_shapes[-1] = ((2, rows[-1]), (2,))
+            ones = [torch.ones(ws) for (ws, _) in sp.param_shapes]
+            plan.p2_nh = (max(rows) + 31) // 32
+            plan.p2_map = made_pack_map(sp, ones, plan.p2_nh).to(dev)
+            plan.p2_key = key
+        parts = [torch.zeros((P, 1), device=dev)]
+        for (li, a, b, n, w, bb), (e, wc, wr) in zip(g1, s1):
+            bias = F[:, bb]
+            if e:
+                src = c1.contiguous() if li == 0 else hc[li - 1]
+                bias = ops.linear_act_batched(src, F[:, wc], bias, "identity")[:, 0, :]
+            parts += [F[:, wr].reshape(P, -1), bias.reshape(P, -1)]
+        i, n, wb, bb = plan.outs[1]
+        e, wc, wr = osplit[1]
+        bias = F[:, bb]
+        if e:
+            bias = ops.linear_act_batched(hc[len(plan.widths) - 1], F[:, wc], bias, "identity")[:, 0, :]
+        parts += [F[:, wr].reshape(P, -1), bias.reshape(P, -1)]
+        packed = torch.cat(parts, 1)[:, plan.p2_map].contiguous()
+        return ops.made_affine_inv1(packed, len(rows), plan.p2_nh, xn, z, i, act, lp2, ops.LD_ROWSUM_SUB)
+
     def lp_batched(params: Params) -> Tensor:
         P = _draws(params)
         out = torch.empty((P, B), device=dev, dtype=torch.float32)
+        run = _lp_chunk_const if (const_ctx and fold_context) else _lp_chunk
         for p0, p1 in _chunks(P, B * max(1, width_sum // 64)):
-            _lp_chunk([[(w[p0:p1], b[p0:p1]) for (w, b) in layer] for layer in params], out[p0:p1])
+            run([[(w[p0:p1], b[p0:p1]) for (w, b) in layer] for layer in params], out[p0:p1])
         return out
 
     def _sample_chunk(params: Params, z: Tensor, y_out: Tensor, lj_out: Tensor):
@@ -369,5 +491,21 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         y, lj = sampler_batched(_one(params), rng_key, size)
         return y[0], lj[0]
 
+    def lp_flops_per_row() -> int:
+        """Executed GEMM FLOPs per (draw, row) of lp_batched (padded blocks included)."""
+        tot = 0
+        for plan in plans:
+            if const_ctx and fold_context:
+                split, osplit = _split_maps(plan)
+                for g in range(1, D):
+                    for (li, a, b, n, w, bb), (e, wc, wr) in zip(plan.hidden[g], split[g]):
+                        tot += 2 * (b - a) * (n - e)
+                tot += sum(2 * 2 * max(n - e, 0) for (i, n, w, bb), (e, wc, wr) in zip(plan.outs, osplit))
+            else:
+                tot += sum(2 * (b - a) * n for g in plan.hidden for (li, a, b, n, w, bb) in g)
+                tot += sum(2 * 2 * n for (i, n, w, bb) in plan.outs)
+        return tot
+
     return {"lp": lp, "sampler": sampler, "lp_batched": lp_batched, "sampler_batched": sampler_batched,
+            "lp_flops_per_row": lp_flops_per_row,
             "plans": plans, "fused_fwd": fused_fwd}

@@ -16,7 +16,7 @@ from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, RQS_FAST, LD_PERDIM, LD_ROWSUM
 
 Tensor = torch.Tensor
 
-__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "gemm_dact", "affine_ar", "affine_ar_bwd", "base_log_prob",
+__all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "made_affine_inv1", "gemm_dact", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
            "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5",
@@ -225,6 +225,25 @@ def made_affine_fwd(packed: Tensor, nhid: int, nh: int, x: Tensor, context: Opti
     check(lib().naz_made_affine_fwd(_p(packed), n, nhid, nh, C, D, _p(context), ldc, sctx, _p(x), x.stride(1),
                                     x.stride(0), _p(out), out.stride(1), out.stride(0), _p(ld), ld.stride(0), ld_mode,
                                     S, P, ACT[act], _stream(dev)), "made_affine_fwd")
+    return out
+
+
+def made_affine_inv1(packed: Tensor, nhid: int, nh: int, x: Tensor, v: Tensor, dim: int, act: str, ld: Tensor,
+                     ld_mode: int = LD_ROWSUM_SUB, out: Optional[Tensor] = None) -> Tensor:
+    """Context-free MADE chain + inverse affine step of one dim (naz_made_affine_inv1):
+    x, v [P, S, D] (unit column stride), ld [P, S], packed [P, naz_made_packed_floats(nhid, nh, 0, D)]."""
+    dev = _dev(packed, x, v, ld, out)
+    P, S, D = x.shape
+    n = made_packed_floats(nhid, nh, 0, D)
+    if packed.shape != (P, n) or not packed.is_contiguous():
+        raise ValueError(f"packed must be contiguous [P={P}, {n}], got {tuple(packed.shape)}")
+    if v.shape != x.shape or x.stride(-1) != 1 or v.stride(-1) != 1 or ld.shape != (P, S) or ld.stride(-1) != 1:
+        raise ValueError("x, v must be [P, S, D] with unit column stride and ld [P, S]")
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib().naz_made_affine_inv1(_p(packed), n, nhid, nh, D, _p(x), x.stride(1), x.stride(0), _p(v), v.stride(1),
+                                     v.stride(0), int(dim), _p(out), out.stride(1), out.stride(0), _p(ld), ld.stride(0),
+                                     ld_mode, S, P, ACT[act], _stream(dev)), "made_affine_inv1")
     return out
 
 

@@ -57,7 +57,7 @@ def _batched_params(draws, dev):
              for i in range(n)] for l in range(L)]
 
 
-def _flow(spec, layers, x, ctx, dev):
+def _flow(spec, layers, x, ctx, dev, **kw):
     from naz_amd.flows import bflow_maf as BM
     nn_spec, _, _ = BM.make_conditional_autoregressive_nn(spec["D"], spec["C"], spec["hidden"])
     tr = BM.make_masked_affine_autoregressive_transform(nn_spec, spec["D"])
@@ -65,7 +65,7 @@ def _flow(spec, layers, x, ctx, dev):
     perms = [torch.tensor(p) for _, p, _ in layers]
     c = None if ctx is None else torch.tensor(ctx, device=dev)
     return BM.make_normalizing_flow(tr, torch.tensor(x, device=dev), masks, [None] * len(layers), perms,
-                                    context=c)
+                                    context=c, **kw)
 
 
 # ----------------------------------------------------------------------------- CPU
@@ -314,3 +314,20 @@ def test_torch_to_jax_layout():
     assert all(torch.equal(m, a.float()) for m, a in zip(masks[0], arn.masks))
     assert torch.equal(perms[0], arn.permutation) and skips[0].shape == (4, 4)
     assert BM.ravel(params).numel() == sum(p.numel() for p in f.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,C,hidden", [(2, 2, [150, 150, 150]), (4, 3, [64, 40]), (3, 5, [33, 20, 17])])
+def test_lp_context_folding(_gpu, D, C, hidden):
+    """One context vector: the degree-0 (context-only) MADE units evaluated once per draw and
+    folded into biases give the plain degree schedule's log_prob and the oracle's."""
+    spec = dict(flow_type="maf", D=D, C=C, hidden=hidden, L=2, P=4, B=600, ctx="vec")
+    layers, draws, x, ctx = _setup(spec)
+    params = _batched_params(draws, "cuda")
+    a = _flow(spec, layers, x, ctx, "cuda")["lp_batched"](params)
+    b = _flow(spec, layers, x, ctx, "cuda", fold_context=False)["lp_batched"](params)
+    assert torch.allclose(a, b, rtol=2e-5, atol=2e-5), (a - b).abs().max()
+    for p, d in enumerate(draws):
+        ol = _oracle_layers(layers, d)
+        assert_parity(a[p].cpu().numpy(), J.log_prob(x, ol, ctx),
+                      J.log_prob(x, J.cast_layers(ol, np.float32), ctx, np.float32), what=f"folded lp draw {p}")

@@ -341,6 +341,10 @@ FLOW_CASES = {
     # naz nsa (ConditionalSplineAutoregressive, D-pass inverse), pinned: D=4, C=2, H=[128,128], K=8, L=8
     "nsa": ("nsa", 4, 2, [128, 128], 8, (8,), 1 << 18,
             "naz nsa (SURVEY.md §8a a4/a6): D=4, C=2, K=8, L=8, H=[128,128], D-pass inverse per layer"),
+    # the density-grid use (plot.py:126-127): one context vector for every row
+    "maf_grid": ("maf", 2, 2, [150, 150, 150], 16, (), 1 << 18,
+                 "naz maf at the paper shape with ONE context vector (density grid, plot.py:126-127): "
+                 "context-only MADE units folded into biases"),
 }
 
 
@@ -353,6 +357,9 @@ def run_flow_case(args, dev, rank, world, dist):
     x = torch.as_tensor(gaussian_mixture(B, Dd, seed=rank), device=dev)
     c = (torch.as_tensor(np.random.default_rng(1 + rank).standard_normal(size=(B, Cd)).astype(np.float32),
                          device=dev) if Cd else None)
+    grid = args.flow.endswith("_grid")
+    if grid:  # one context vector, broadcast (naz: condition=[C])
+        c = c[0].contiguous()
     # conditioner FLOPs per row: passes per layer (1 for coupling, D for autoregressive inverse)
     if ftype == "nsc":
         S = extra[1]
@@ -368,8 +375,14 @@ def run_flow_case(args, dev, rank, world, dist):
         fl_row = 0
         for net in f.nets:
             plan = net.inverse_plan().plan()
-            fl_row += sum(2 * blk.w.shape[0] * blk.w.shape[1] for grp in plan.hidden for _, blk in grp)
-            fl_row += sum(2 * wb.shape[0] * n for _, n, wb, _ in plan.outs)
+            if grid:  # degree-0 units folded: only the x-dependent columns run per row
+                split, osplit = plan._splits()
+                fl_row += sum(2 * blk.w.shape[0] * (blk.n - e) for grp, sp in zip(plan.hidden[1:], split[1:])
+                              for (_, blk), (e, _, _) in zip(grp, sp))
+                fl_row += sum(2 * wb.shape[0] * max(n - e, 0) for (_, n, wb, _), (e, _, _) in zip(plan.outs, osplit))
+            else:
+                fl_row += sum(2 * blk.w.shape[0] * blk.w.shape[1] for grp in plan.hidden for _, blk in grp)
+                fl_row += sum(2 * wb.shape[0] * n for _, n, wb, _ in plan.outs)
     with torch.no_grad():
         for _ in range(args.warmup):
             f.log_prob(x, condition=c)
@@ -416,7 +429,9 @@ def run_flow_case(args, dev, rank, world, dist):
             elif ftype == "nsa":
                 spec.update(K=extra[0])
             xh = x[:1 << 17].cpu().numpy()
-            ch = c[:1 << 17].cpu().numpy() if c is not None else None
+            ch = None
+            if c is not None:
+                ch = (c.reshape(1, -1).expand(1 << 17, -1) if grid else c[:1 << 17]).cpu().numpy()
             rec["cpu_baseline"], rec["parity_spot_check"] = cpu_baseline(f, xh, ch, budget_rows=1 << 17, spec=spec)
         print(json.dumps(rec), flush=True)
     if dist is not None:

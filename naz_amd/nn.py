@@ -362,6 +362,9 @@ class ARInversePlan:
         conditioner output of that dim only, pyro's column order p)."""
         self.plan()
         B, D = v.shape
+        if context is not None and self.fold_context and (
+                context.dim() == 1 or context.shape[0] == 1 or context.stride(0) == 0):
+            return self._run_folded(v, context.reshape(-1, context.shape[-1])[0], step)
         x = torch.zeros_like(v)
         hs = [torch.empty((B, w), device=v.device, dtype=torch.float32) for w in self.widths]
         act = self.arn.act
@@ -377,6 +380,57 @@ class ARInversePlan:
                 raw = ops.linear_act(hs[-1][:, :n], wb, bb, "identity")
             else:
                 raw = bb.reshape(1, -1).expand(B, -1)
+            step(k, i, raw, x)
+        return x
+
+
+    # one context vector for all rows: evaluate the context-only (degree-0) units once and fold
+    # them into the later groups' biases (flows/bflow_maf.py does the same per weight draw)
+    fold_context = True
+
+    def _splits(self):
+        """Per block (e, W[:, :e], W[:, e:]): e = the input columns that are constant under a
+        broadcast context (layer 0: the context; later layers: the previous degree-0 group)."""
+        key = self._key
+        if getattr(self, "_split_key", None) == key:
+            return self._split
+        C = self.arn.context_dim
+        e_out = {li: blk.b for li, blk in self.hidden[0]}
+        split = [[(e, blk.w[:, :e].contiguous(), blk.w[:, e:].contiguous())
+                  for li, blk in g for e in [C if li == 0 else e_out.get(li - 1, 0)]] for g in self.hidden]
+        e_last = e_out.get(len(self.widths) - 1, 0)
+        outs = [(e_last, wb[:, :e_last].contiguous(), wb[:, e_last:].contiguous()) for (_, _, wb, _) in self.outs]
+        self._split, self._split_key = (split, outs), key
+        return self._split
+
+    def _run_folded(self, v: torch.Tensor, c: torch.Tensor, step) -> torch.Tensor:
+        B, D = v.shape
+        C = c.shape[0]
+        act = self.arn.act
+        split, osplit = self._splits()
+        hc = {}  # layer -> [1, e] constant activations of its degree-0 group
+        for li, blk in self.hidden[0]:
+            src = torch.cat((c, torch.zeros(D, device=v.device))).reshape(1, -1) if li == 0 else hc[li - 1]
+            hc[li] = ops.linear_act(src[:, :blk.n].contiguous(), blk.w, blk.bias, act)
+        x = torch.zeros_like(v)
+        hs = [torch.empty((B, w), device=v.device, dtype=torch.float32) for w in self.widths]
+        c1 = c.reshape(1, C)
+        for k in range(1, D + 1):
+            if k > 1:
+                for (li, blk), (e, wc, wr) in zip(self.hidden[k - 1], split[k - 1]):
+                    bias = blk.bias
+                    if e:
+                        src = c1 if li == 0 else hc[li - 1]
+                        bias = ops.linear_act(src, wc, bias, "identity").reshape(-1)
+                    inp = x if li == 0 else hs[li - 1][:, e:blk.n]
+                    ops.linear_act(inp, wr, bias, act, out=hs[li][:, blk.a:blk.b])
+            i, n, wb, bb = self.outs[k - 1]
+            e, wc, wr = osplit[k - 1]
+            bias = bb if not e else ops.linear_act(hc[len(self.widths) - 1], wc, bb, "identity").reshape(-1)
+            if n > e:
+                raw = ops.linear_act(hs[-1][:, e:n], wr, bias, "identity")
+            else:
+                raw = bias.reshape(1, -1).expand(B, -1)
             step(k, i, raw, x)
         return x
 

@@ -87,3 +87,27 @@ def test_scheduled_inverse_sample_round_trip(spec):
         lp_full = f.log_prob(xs, condition=cond)
     assert torch.isfinite(lp).all()
     torch.testing.assert_close(lp, lp_full, rtol=1e-5, atol=2e-4)
+
+
+@pytest.mark.parametrize("spec", [s for s in CASES if s["C"]], ids=_id)
+def test_broadcast_context_folding(spec):
+    """log_prob(x, condition=<one context vector>): the context-only (degree-0) MADE units are
+    evaluated once and folded into biases (ARInversePlan._run_folded); same values as the plain
+    schedule and the oracle."""
+    from naz_amd.nn import ARInversePlan
+    f, state = _flow(spec)
+    n = 2048
+    x = torch.as_tensor(O.gaussian_mixture(n, spec["D"], seed=5))
+    c1 = torch.as_tensor(O.context_normal(1, spec["C"], seed=6))[0]
+    with torch.no_grad():
+        lp = f.log_prob(x.to(DEV), condition=c1.to(DEV)).cpu().numpy()
+        ARInversePlan.fold_context = False
+        try:
+            lp_plain = f.log_prob(x.to(DEV), condition=c1.to(DEV)).cpu().numpy()
+        finally:
+            ARInversePlan.fold_context = True
+    cn = c1.expand(n, -1)
+    lp64 = O.build_flow(spec, state, torch.float64).log_prob(x.double(), cn.double()).numpy()
+    lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, cn).numpy()
+    assert_parity(lp, lp64, lp32, what=f"{_id(spec)} folded")
+    np.testing.assert_allclose(lp, lp_plain, rtol=1e-5, atol=1e-4)

@@ -498,6 +498,10 @@ class _ConditionedAffineAutoregressive(_LDCache, Transform):
         if plan is not None:
             def step(k, i, raw, x):  # naz_affine_ar reports the FORWARD log-det in both directions
                 ops.affine_ar(v[:, i:i + 1], raw, True, _pass_ld_mode(ld_mode, k), ld_buf, out=x[:, i:i + 1])
+            if ld_mode != ops.LD_PERDIM:  # D = 2, one context vector: pass 2 fused
+                y = plan.run_affine2(v, self.context, step, ld_buf, _pass_ld_mode(ld_mode, 2))
+                if y is not None:
+                    return y
             return plan.run(v, self.context, step)
         # pyro loops over the permutation updating one dim per pass; updating every dim per
         # pass gives identical values (masked weights are exact zeros for non-predecessors)

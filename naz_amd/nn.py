@@ -435,6 +435,59 @@ class ARInversePlan:
         return x
 
 
+    def run_affine2(self, v: torch.Tensor, context: Optional[torch.Tensor], step, ld_buf: torch.Tensor,
+                    ld_mode2: int) -> Optional[torch.Tensor]:
+        """Affine MAF inverse for D = 2 with one context vector: pass 1 as in ``run`` (folded),
+        pass 2 = the context-free chain of degree-1 units + the inverse affine step of the order-2
+        dim in ONE naz_made_affine_inv1 launch (csrc/made.hip).  None when not applicable."""
+        self.plan()
+        B, D = v.shape
+        arn = self.arn
+        if (D != 2 or context is None or not self.fold_context or arn.output_multiplier != 2
+                or arn.act not in ("tanh", "relu") or ld_buf is None or not ld_buf.is_contiguous()
+                or not (context.dim() == 1 or context.shape[0] == 1 or context.stride(0) == 0)):
+            return None
+        g1 = self.hidden[1]
+        nl = len(self.widths)
+        if [li for li, _ in g1] != list(range(nl)) or any(blk.b - blk.a > 160 for _, blk in g1):
+            return None
+        from .flows.bflow_maf import MAFSpec, made_pack_map
+        c = context.reshape(-1, context.shape[-1])[0]
+        C = c.shape[0]
+        split, osplit = self._splits()
+        act = arn.act
+        hc = {}
+        for li, blk in self.hidden[0]:
+            src = torch.cat((c, torch.zeros(D, device=v.device))).reshape(1, -1) if li == 0 else hc[li - 1]
+            hc[li] = ops.linear_act(src[:, :blk.n].contiguous(), blk.w, blk.bias, act)
+        x = torch.zeros_like(v)
+        i, n, wb, bb = self.outs[0]
+        e, wc, wr = osplit[0]
+        raw = bb if not e else ops.linear_act(hc[nl - 1], wc, bb, "identity").reshape(-1)
+        step(1, i, raw.reshape(1, -1).expand(B, -1), x)  # order-1 dim: constant conditioner output
+        rows = [blk.b - blk.a for _, blk in g1]
+        if getattr(self, "_p2_key", None) != (self._key, tuple(rows)):
+            sp = MAFSpec(D, 0, rows, act)
+            sp.param_shapes[-1] = ((2, rows[-1]), (2,))
+            self._p2_nh = (max(rows) + 31) // 32
+            self._p2_map = made_pack_map(sp, [torch.ones(ws) for (ws, _) in sp.param_shapes], self._p2_nh).to(v.device)
+            self._p2_key = (self._key, tuple(rows))
+        c1 = c.reshape(1, C)
+        parts = [torch.zeros(1, device=v.device)]
+        for (li, blk), (e, wc, wr) in zip(g1, split[1]):
+            bias = blk.bias if not e else ops.linear_act(c1 if li == 0 else hc[li - 1], wc, blk.bias,
+                                                         "identity").reshape(-1)
+            parts += [wr.reshape(-1), bias.reshape(-1)]
+        i2, n2, wb2, bb2 = self.outs[1]
+        e, wc, wr = osplit[1]
+        bias = bb2 if not e else ops.linear_act(hc[nl - 1], wc, bb2, "identity").reshape(-1)
+        parts += [wr.reshape(-1), bias.reshape(-1)]
+        packed = torch.cat(parts)[self._p2_map].reshape(1, -1).contiguous()
+        y = ops.made_affine_inv1(packed, nl, self._p2_nh, x.unsqueeze(0), v.contiguous().unsqueeze(0), i2, act,
+                                 ld_buf.view(1, -1), ld_mode2)
+        return y[0]
+
+
 class AutoRegressiveNN(ConditionalAutoRegressiveNN):
     """[pyro] nn/auto_reg_nn.py::AutoRegressiveNN."""
 

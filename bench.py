@@ -455,7 +455,8 @@ def run_bayes(args, dev, rank, world, dist):
     st = {k: v.numpy() for k, v in O.random_state(sp, seed=1234).items()}
     layers = J.layers_from_state(sp, st)
     lp_mode = args.bayes == "lp"
-    P = 64 if lp_mode else 16
+    grad_mode = args.bayes == "grad"
+    P = 64 if lp_mode else (1 if grad_mode else 16)
     B = args.batch if args.batch != (1 << 20) else (1 << 14 if lp_mode else 1 << 16)
     rng = np.random.default_rng(100 + rank)
     draws = [[[((W * (1 + 0.25 * rng.uniform(-1, 1, W.shape))).astype(np.float32),
@@ -468,6 +469,8 @@ def run_bayes(args, dev, rank, world, dist):
     grid = np.stack(np.meshgrid(g, g), -1).reshape(-1, 2).astype(np.float32)
     x = np.concatenate([grid, gaussian_mixture(B - grid.shape[0], D, seed=rank)]) if grid.shape[0] < B else grid[:B]
     ctx = np.array([0.3, -1.2], dtype=np.float32)
+    if grad_mode:  # NUTS over the training set: per-row contexts (hmc_maf_exact.py:128)
+        ctx = np.random.default_rng(7).standard_normal((B, C)).astype(np.float32)
     nn_spec, _, _ = BM.make_conditional_autoregressive_nn(D, C, BAYES["hidden"])
     tr = BM.make_masked_affine_autoregressive_transform(nn_spec, D)
     flow = BM.make_normalizing_flow(tr, torch.tensor(x, device=dev),
@@ -477,6 +480,11 @@ def run_bayes(args, dev, rank, world, dist):
     if lp_mode:
         def step():
             return flow["lp_batched"](params)
+    elif grad_mode:
+        one = [[(w[0], b[0]) for (w, b) in layer] for layer in params]
+
+        def step():
+            return flow["lp_and_grad"](one)[1]
     else:
         def step():
             return flow["sampler_batched"](params, 7, B)[0]
@@ -509,27 +517,52 @@ def run_bayes(args, dev, rank, world, dist):
     if lp_mode:
         fl_ref = D * full  # the reference's D full MADE passes per layer
         fl_row = flow["lp_flops_per_row"]()  # executed: context-only units folded into per-draw biases
+    elif grad_mode:  # forward D passes + backward (2x the GEMM work of the forward)
+        fl_ref = fl_row = 3 * D * full
     else:
         fl_ref = fl_row = full
     achieved = fl_row * P * B / step_s / 1e12
     rec = {
         "metric": ("draw-rows/sec through batched-over-parameters log_prob, naz Bayesian affine MAF"
-                   if lp_mode else "samples/sec through batched-over-parameters posterior-predictive sampling, "
-                                   "naz Bayesian affine MAF"),
-        "value": P * B * world / step_s, "unit": "draw-rows/s" if lp_mode else "samples/s", "n_gpus": world,
+                   if lp_mode else ("rows/sec through the NUTS potential and its gradient (sum lp, d/dtheta), "
+                                    "naz Bayesian affine MAF" if grad_mode else
+                                    "samples/sec through batched-over-parameters posterior-predictive sampling, "
+                                    "naz Bayesian affine MAF")),
+        "value": P * B * world / step_s, "unit": "draw-rows/s" if lp_mode else ("rows/s" if grad_mode else "samples/s"),
+        "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: rows = 2-D grid (+ Gaussian-mixture fill); P weight draws = MLE weights x (1 + 0.25 U(-1,1)) "
                 "(bflow_jax_maf.py:224-226); random-init MLE weights (torch seed 1234)",
-        "config": {"workload": f"SURVEY.md §8f rank {1 if lp_mode else 2}: naz JAX-MAF front end "
-                               f"({'lp' if lp_mode else 'sampler'}) at the 2506.05657 paper shape D=2, C=2, "
+        "config": {"workload": f"SURVEY.md §8f rank {2 if args.bayes == 'sample' else 1}: naz JAX-MAF front end "
+                               f"({ {'lp': 'lp', 'grad': 'NUTS potential + gradient', 'sample': 'sampler'}[args.bayes] })"
+                               f" at the 2506.05657 paper shape D=2, C=2, "
                                f"H=[150]*3, L=16; {P} draws x {B} rows per step (pack included)",
                    "draws": P, "rows_per_draw": B, "parallelism": f"dp{world} (independent draw sets, no collective)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "whole batched call",
                      "flop_per_row": fl_row, "reference_flop_per_row": fl_ref},
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and grad_mode:
+        # the reference's NLL gradient on the host: oracle flow (pyro semantics, torch fp32 autograd)
+        st = {}
+        for l, lay in enumerate(draws[0]):
+            for i, (W, b) in enumerate(lay):
+                st[f"layers.{l}.nn.layers.{i}.weight"] = torch.tensor(W, requires_grad=True)
+                st[f"layers.{l}.nn.layers.{i}.bias"] = torch.tensor(b, requires_grad=True)
+            st[f"layers.{l}.nn.permutation"] = torch.tensor(layers[l][1])
+        of = O.build_flow(sp, st, torch.float32)
+        nrow = min(B, 1 << 13)
+        xs, cs = torch.tensor(x[:nrow]), torch.tensor(ctx[:nrow])
+        times = []
+        for _ in range(2):
+            t1 = time.perf_counter()
+            of.log_prob(xs, cs).sum().backward()
+            times.append(time.perf_counter() - t1)
+        rec["cpu_baseline"] = {"value": nrow / min(times), "unit": "rows/s", "cores": torch.get_num_threads(),
+                               "kind": "port", "sample": f"{nrow} rows, oracle maf (torch fp32 autograd, D-pass "
+                                                         f"inverse), best of 2 ({min(times):.2f} s)"}
+    if not args.no_cpu_baseline and not grad_mode:
         # the reference's algorithm (numpy restatement of bflow_jax_maf.py, float32) per draw
         nrow = min(B, 1 << 13)
         ol = [(([(w.astype(np.float64), b.astype(np.float64)) for (w, b) in draws[0][l]]), perm, ms)
@@ -577,7 +610,7 @@ def main():
                     help="--cnf: pinned fixed-step RK4 x 8 (default) or adaptive dopri5 (atol = rtol = 1e-4)")
     ap.add_argument("--flow", choices=sorted(FLOW_CASES), default=None,
                     help="time log_prob of another §8 flow through the NormalizingFlow API (see FLOW_CASES)")
-    ap.add_argument("--bayes", choices=["lp", "sample"], default=None,
+    ap.add_argument("--bayes", choices=["lp", "sample", "grad"], default=None,
                     help="§8f ranks 1-2: the Bayesian MAF front end batched over weight draws (lp over a grid, "
                          "posterior-predictive sampling) at the paper shape")
     ap.add_argument("--mfma", choices=["auto", "f16x3", "f16x3r16", "bf16x6", "f32"], default="auto",

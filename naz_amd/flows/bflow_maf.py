@@ -481,6 +481,36 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
 
     ctx_s = None
 
+    grad_flow = {}
+
+    def lp_and_grad(params) -> Tuple[Tensor, Tensor]:
+        """(Σ_rows log p(x | θ), ∇θ of it in ``ravel`` order): the NUTS / HMC potential of
+        ``bayesian_normalizing_flow`` (bflow_jax_maf.py:233-235: ``flow_lp(unravel(p)).sum()``
+        and its gradient).  One draw (pytree or flat [n]); runs the NLL training walk (HIP
+        forward + backward kernels, nn autograd) on a naz_amd maf with these weights."""
+        from torch import nn as tnn
+        from .flow import NormalizingFlow
+        if torch.is_tensor(params):
+            params = unravel(params, [spec.param_shapes] * len(plans))
+        f = grad_flow.get("f")
+        if f is None:
+            acts = {"tanh": tnn.Tanh(), "relu": tnn.ReLU(), "sigmoid": tnn.Sigmoid(), "identity": tnn.Identity()}
+            f = NormalizingFlow("maf", None, D, C, spec.hidden_dims, len(plans), activation=acts[act]).to(dev)
+            for t, perm in zip(f.transforms, perms):
+                t.nn.set_permutation(torch.as_tensor(perm))
+            grad_flow["f"] = f
+        with torch.no_grad():
+            for t, layer in zip(f.transforms, params):
+                for lin, (w, b) in zip(t.nn.layers, layer):
+                    lin.weight.copy_(w)
+                    lin.bias.copy_(b)
+        f.zero_grad(set_to_none=True)
+        with torch.enable_grad():
+            total = f.log_prob(x, condition=ctx).sum()
+            total.backward()
+        g = [[(lin.weight.grad, lin.bias.grad) for lin in t.nn.layers] for t in f.transforms]
+        return total.detach(), ravel(g)
+
     def _one(params):
         return [[(w.unsqueeze(0), b.unsqueeze(0)) for (w, b) in layer] for layer in params]
 
@@ -507,5 +537,5 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         return tot
 
     return {"lp": lp, "sampler": sampler, "lp_batched": lp_batched, "sampler_batched": sampler_batched,
-            "lp_flops_per_row": lp_flops_per_row,
+            "lp_and_grad": lp_and_grad, "lp_flops_per_row": lp_flops_per_row,
             "plans": plans, "fused_fwd": fused_fwd}

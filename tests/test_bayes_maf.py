@@ -331,3 +331,45 @@ def test_lp_context_folding(_gpu, D, C, hidden):
         ol = _oracle_layers(layers, d)
         assert_parity(a[p].cpu().numpy(), J.log_prob(x, ol, ctx),
                       J.log_prob(x, J.cast_layers(ol, np.float32), ctx, np.float32), what=f"folded lp draw {p}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ctx_kind", ["vec", "rows"])
+def test_lp_and_grad_vs_oracle_autograd(_gpu, ctx_kind):
+    """The NUTS potential Σ_rows lp(θ) and its gradient (bflow_jax_maf.py:233-235) from the HIP
+    training walk vs the fp64 oracle's torch autograd (and its fp32 run as ref32)."""
+    from naz_amd.flows import bflow_maf as BM
+    spec = dict(flow_type="maf", D=2, C=2, hidden=[48, 48], L=3, P=1, B=1500, ctx=ctx_kind)
+    layers, draws, x, ctx = _setup(spec)
+    flow = _flow(spec, layers, x, ctx, "cuda")
+    d = draws[0]
+    params = [[(torch.tensor(W, dtype=torch.float32, device="cuda"), torch.tensor(b, dtype=torch.float32,
+                                                                                   device="cuda"))
+               for (W, b) in lay] for lay in d]
+    total, grad = flow["lp_and_grad"](params)
+    total2, grad2 = flow["lp_and_grad"](BM.ravel(params))  # flat draw, second call reuses the flow
+    # the dW reductions accumulate with fp32 atomics: equal up to summation order
+    assert torch.equal(total, total2) and torch.allclose(grad, grad2, rtol=1e-5, atol=1e-6 * float(grad.abs().max()))
+
+    def oracle(dtype):
+        st = {}
+        for l, lay in enumerate(d):
+            for i, (W, b) in enumerate(lay):
+                st[f"layers.{l}.nn.layers.{i}.weight"] = torch.tensor(W, dtype=dtype, requires_grad=True)
+                st[f"layers.{l}.nn.layers.{i}.bias"] = torch.tensor(b, dtype=dtype, requires_grad=True)
+            st[f"layers.{l}.nn.permutation"] = torch.tensor(layers[l][1])
+        f = O.build_flow(spec, st, dtype)
+        xc = torch.tensor(x, dtype=dtype)
+        cc = torch.tensor(ctx, dtype=dtype)
+        cc = cc.expand(len(x), -1) if cc.dim() == 1 else cc
+        lp = f.log_prob(xc, cc).sum()
+        lp.backward()
+        g = torch.cat([t.grad.reshape(-1) for l in range(len(d)) for i in range(len(d[0]))
+                       for t in (st[f"layers.{l}.nn.layers.{i}.weight"], st[f"layers.{l}.nn.layers.{i}.bias"])])
+        return lp.item(), g.numpy()
+    lp64, g64 = oracle(torch.float64)
+    lp32, g32 = oracle(torch.float32)
+    assert abs(total.item() - lp64) / abs(lp64) < 1e-5
+    from tests.parity import grad_floor
+    assert_parity(grad.cpu().numpy(), g64, g32, what="NUTS potential gradient", floor=grad_floor(g64),
+                  count_factor=None)

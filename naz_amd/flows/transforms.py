@@ -533,7 +533,12 @@ class _ConditionedAffineAutoregressive(_LDCache, Transform):
         return self._map(x, False, ld, ops.LD_ROWSUM_ADD)
 
     def _inv_ld(self, y):
-        """Differentiable D-pass inverse; the affine kernel reports the forward log-det."""
+        """Differentiable inverse; the affine kernel reports the forward log-det.  Degree-
+        scheduled (every MADE unit once, ARInversePlan.run_grad) unless the conditioner's
+        degree_schedule is off, then pyro's D full passes."""
+        plan = self.arn.inverse_plan() if y.dim() == 2 else None
+        if plan is not None:
+            return plan.run_grad(y, self.context, lambda k, i, raw: ag.affine_ar(y[:, i:i + 1], raw, True))
         x = torch.zeros_like(y)
         ld = None
         for _ in range(y.shape[-1]):

@@ -435,6 +435,62 @@ class ARInversePlan:
         return x
 
 
+    def index_maps(self):
+        """The schedule as gather maps into F = [0, W0, b0, W1, b1, ...] (flat, unmasked): the
+        schedule is linear in the weights, so running it on index-valued weights (1-based, masks
+        applied) gives, per block, the flat index of every entry (0 = masked / padding)."""
+        arn = self.arn
+        layers = list(arn.layers)
+        key = tuple((l.mask.data_ptr(), l.mask._version) for l in layers) + (tuple(arn.permutation.tolist()),)
+        if getattr(self, "_imap_key", None) == key:
+            return self._imap
+        cpu = dict(device="cpu", dtype=torch.float64)
+        wi, bi, off = [], [], 1
+        for l in layers:
+            nw = l.weight.numel()
+            wi.append(torch.arange(off, off + nw, **cpu).reshape(l.weight.shape))
+            bi.append(torch.arange(off + nw, off + nw + l.bias.numel(), **cpu))
+            off += nw + l.bias.numel()
+        widths, hidden, outs = degree_schedule(arn.permutation.cpu(), [l.mask.detach().to(**cpu) for l in layers],
+                                               wi, bi, arn.input_dim, arn.context_dim, arn.output_multiplier)
+        dev = layers[0].weight.device
+        hidden = [[(li, a, b, n, w.round().long().to(dev), bb.round().long().to(dev)) for (li, a, b, n, w, bb) in g]
+                  for g in hidden]
+        outs = [(i, n, w.round().long().to(dev), bb.round().long().to(dev)) for (i, n, w, bb) in outs]
+        self._imap, self._imap_key = (widths, hidden, outs), key
+        return self._imap
+
+    def run_grad(self, v: torch.Tensor, context: Optional[torch.Tensor], step):
+        """Differentiable degree-scheduled inverse (training walk, a10): the blocks are gathered
+        from the live parameters (torch indexing, so autograd scatters their gradients back) and
+        run through LinearActFn; step(k, dim, raw_k) -> (x_dim [B, 1], forward ld [B]).  Same
+        values as pyro's D-pass loop with every hidden unit computed once."""
+        B, D = v.shape
+        widths, hidden, outs = self.index_maps()
+        layers = list(self.arn.layers)
+        F = torch.cat([v.new_zeros(1)] + [t.reshape(-1) for l in layers for t in (l.weight, l.bias)])
+        act = self.arn.act
+        cols = [v.new_zeros(B, 1) for _ in range(D)]
+        done = [[] for _ in widths]  # per hidden layer: its group outputs in degree order
+        ld = None
+        for k in range(1, D + 1):
+            x = torch.cat(cols, 1)
+            for (li, a, b, n, wi, bi) in hidden[k - 1]:
+                if li == 0:
+                    h = ag.linear_act(x, F[wi], F[bi], act, context=context)
+                else:
+                    h = ag.linear_act(torch.cat(done[li - 1], 1)[:, :n], F[wi], F[bi], act)
+                done[li].append(h)
+            i, n, wi, bi = outs[k - 1]
+            if n:
+                raw = ag.linear_act(torch.cat(done[-1], 1)[:, :n], F[wi], F[bi], "identity")
+            else:
+                raw = F[bi].reshape(1, -1).expand(B, -1)
+            xi, ldi = step(k, i, raw)
+            cols[i] = xi
+            ld = ldi if ld is None else ld + ldi
+        return torch.cat(cols, 1), ld
+
     def run_affine2(self, v: torch.Tensor, context: Optional[torch.Tensor], step, ld_buf: torch.Tensor,
                     ld_mode2: int) -> Optional[torch.Tensor]:
         """Affine MAF inverse for D = 2 with one context vector: pass 1 as in ``run`` (folded),

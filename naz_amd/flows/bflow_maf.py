@@ -483,15 +483,9 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
 
     grad_flow = {}
 
-    def lp_and_grad(params) -> Tuple[Tensor, Tensor]:
-        """(Σ_rows log p(x | θ), ∇θ of it in ``ravel`` order): the NUTS / HMC potential of
-        ``bayesian_normalizing_flow`` (bflow_jax_maf.py:233-235: ``flow_lp(unravel(p)).sum()``
-        and its gradient).  One draw (pytree or flat [n]); runs the NLL training walk (HIP
-        forward + backward kernels, nn autograd) on a naz_amd maf with these weights."""
+    def _grad_model():
         from torch import nn as tnn
         from .flow import NormalizingFlow
-        if torch.is_tensor(params):
-            params = unravel(params, [spec.param_shapes] * len(plans))
         f = grad_flow.get("f")
         if f is None:
             acts = {"tanh": tnn.Tanh(), "relu": tnn.ReLU(), "sigmoid": tnn.Sigmoid(), "identity": tnn.Identity()}
@@ -499,17 +493,63 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             for t, perm in zip(f.transforms, perms):
                 t.nn.set_permutation(torch.as_tensor(perm))
             grad_flow["f"] = f
+        return f
+
+    def _grad_step(flat: Tensor):
+        """flat θ -> (Σ lp, ∇θ): weights copied in, the NLL training walk forward + backward."""
+        f = _grad_model()
+        params = unravel(flat, [spec.param_shapes] * len(plans))
         with torch.no_grad():
             for t, layer in zip(f.transforms, params):
                 for lin, (w, b) in zip(t.nn.layers, layer):
                     lin.weight.copy_(w)
                     lin.bias.copy_(b)
-        f.zero_grad(set_to_none=True)
         with torch.enable_grad():
             total = f.log_prob(x, condition=ctx).sum()
             total.backward()
         g = [[(lin.weight.grad, lin.bias.grad) for lin in t.nn.layers] for t in f.transforms]
         return total.detach(), ravel(g)
+
+    def _capture():
+        """The whole gradient step as one HIP graph (it is ~1,000 small launches eager)."""
+        f = _grad_model()
+        n = sum(p.numel() for p in f.parameters())
+        static = torch.zeros(n, device=dev, dtype=torch.float32)
+        static.copy_(ravel([[(lin.weight.detach(), lin.bias.detach()) for lin in t.nn.layers] for t in f.transforms]))
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # warm the caches (schedules, packs) outside the capture
+                f.zero_grad(set_to_none=True)
+                _grad_step(static)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        f.zero_grad(set_to_none=True)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = _grad_step(static)
+        grad_flow["graph"] = (graph, static, out)
+
+    def lp_and_grad(params, use_graph: bool = True) -> Tuple[Tensor, Tensor]:
+        """(Σ_rows log p(x | θ), ∇θ of it in ``ravel`` order): the NUTS / HMC potential of
+        ``bayesian_normalizing_flow`` (bflow_jax_maf.py:233-235: ``flow_lp(unravel(p)).sum()``
+        and its gradient).  One draw (pytree or flat [n]); runs the NLL training walk (HIP
+        forward + backward kernels, nn autograd) on a naz_amd maf with these weights, replayed as
+        one captured HIP graph after the first call (``use_graph=False``: eager launches)."""
+        flat = params if torch.is_tensor(params) else ravel(params)
+        flat = flat.to(dev, torch.float32).reshape(-1)
+        if use_graph and "graph" not in grad_flow and not grad_flow.get("no_graph"):
+            try:
+                _capture()
+            except RuntimeError:  # capture unsupported here: eager launches (same kernels)
+                grad_flow["no_graph"] = True
+                torch.cuda.synchronize(dev)
+        if use_graph and "graph" in grad_flow:
+            graph, static, (total, grad) = grad_flow["graph"]
+            static.copy_(flat)
+            graph.replay()
+            return total.clone(), grad.clone()
+        _grad_model().zero_grad(set_to_none=True)
+        return _grad_step(flat)
 
     def _one(params):
         return [[(w.unsqueeze(0), b.unsqueeze(0)) for (w, b) in layer] for layer in params]
@@ -537,5 +577,5 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         return tot
 
     return {"lp": lp, "sampler": sampler, "lp_batched": lp_batched, "sampler_batched": sampler_batched,
-            "lp_and_grad": lp_and_grad, "lp_flops_per_row": lp_flops_per_row,
+            "lp_and_grad": lp_and_grad, "grad_state": grad_flow, "lp_flops_per_row": lp_flops_per_row,
             "plans": plans, "fused_fwd": fused_fwd}

@@ -441,7 +441,8 @@ class ARInversePlan:
         applied) gives, per block, the flat index of every entry (0 = masked / padding)."""
         arn = self.arn
         layers = list(arn.layers)
-        key = tuple((l.mask.data_ptr(), l.mask._version) for l in layers) + (tuple(arn.permutation.tolist()),)
+        key = tuple((l.mask.data_ptr(), l.mask._version) for l in layers) + (
+            arn.permutation.data_ptr(), arn.permutation._version)  # no device sync (graph capture)
         if getattr(self, "_imap_key", None) == key:
             return self._imap
         cpu = dict(device="cpu", dtype=torch.float64)

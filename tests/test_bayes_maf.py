@@ -339,7 +339,7 @@ def test_lp_and_grad_vs_oracle_autograd(_gpu, ctx_kind):
     """The NUTS potential Σ_rows lp(θ) and its gradient (bflow_jax_maf.py:233-235) from the HIP
     training walk vs the fp64 oracle's torch autograd (and its fp32 run as ref32)."""
     from naz_amd.flows import bflow_maf as BM
-    spec = dict(flow_type="maf", D=2, C=2, hidden=[48, 48], L=3, P=1, B=1500, ctx=ctx_kind)
+    spec = dict(flow_type="maf", D=2, C=2, hidden=[48, 48], L=3, P=2, B=1500, ctx=ctx_kind)
     layers, draws, x, ctx = _setup(spec)
     flow = _flow(spec, layers, x, ctx, "cuda")
     d = draws[0]
@@ -350,6 +350,17 @@ def test_lp_and_grad_vs_oracle_autograd(_gpu, ctx_kind):
     total2, grad2 = flow["lp_and_grad"](BM.ravel(params))  # flat draw, second call reuses the flow
     # the dW reductions accumulate with fp32 atomics: equal up to summation order
     assert torch.equal(total, total2) and torch.allclose(grad, grad2, rtol=1e-5, atol=1e-6 * float(grad.abs().max()))
+    assert "graph" in flow["grad_state"], "the gradient step was not captured as a HIP graph"
+    total3, grad3 = flow["lp_and_grad"](params, use_graph=False)  # eager launches
+    assert torch.allclose(total, total3, rtol=1e-6) and torch.allclose(grad, grad3, rtol=1e-5,
+                                                                        atol=1e-6 * float(grad.abs().max()))
+    d2 = draws[1] if len(draws) > 1 else d  # replay with new weights follows them
+    p2 = BM.ravel([[(torch.tensor(W, dtype=torch.float32, device="cuda"), torch.tensor(b, dtype=torch.float32,
+                                                                                        device="cuda"))
+                    for (W, b) in lay] for lay in d2])
+    t_g, g_g = flow["lp_and_grad"](p2)
+    t_e, g_e = flow["lp_and_grad"](p2, use_graph=False)
+    assert torch.allclose(t_g, t_e, rtol=1e-6) and torch.allclose(g_g, g_e, rtol=1e-5, atol=1e-6 * float(g_e.abs().max()))
 
     def oracle(dtype):
         st = {}

@@ -56,13 +56,38 @@ class LinearActFn(Function):
         gT = gpre.t()  # [N, M] view
         if _needs(ctx, 2):
             g_W = torch.empty_like(W)
-            if Cd:  # db rides on the first dW GEMM as an all-ones column
-                cc = c.reshape(1, -1).expand(M, Cd) if (c.dim() == 1 or c.shape[0] == 1) and M != 1 else c
-                ops.gemm(gT, cc, out=g_W[:, :Cd], mask=None if mask is None else mask[:, :Cd],
-                         rowsum=g_b)
-            if x is not None:
-                ops.gemm(gT, x, out=g_W[:, Cd:], mask=None if mask is None else mask[:, Cd:],
-                         rowsum=None if Cd else g_b)
+            N, Kx = W.shape[0], (0 if x is None else x.shape[-1])
+            thin = M >= 1024 and mask is None and bool(N % 4 or Cd % 4 or Kx % 4)
+            if thin and (Cd + Kx) <= 256 and N <= 256:
+                # the batch-row dW kernel (wgrad_flat) wants both widths in multiples of 4 and
+                # one contiguous input: [ctx | x] concatenated, dPre padded with zero columns
+                parts = []
+                if Cd:
+                    parts.append(c.reshape(1, -1).expand(M, Cd) if (c.dim() == 1 or c.shape[0] == 1) and M != 1
+                                 else c)
+                if Kx:
+                    parts.append(x)
+                K4, N4 = (Cd + Kx + 3) // 4 * 4, (N + 3) // 4 * 4
+                xin = torch.zeros((M, K4), device=W.device, dtype=torch.float32)
+                xin[:, :Cd + Kx] = torch.cat(parts, 1) if len(parts) > 1 else parts[0]
+                gp = gpre
+                if N4 != N:
+                    gp = torch.zeros((M, N4), device=W.device, dtype=torch.float32)
+                    gp[:, :N] = gpre
+                gw4 = torch.empty((N4, K4), device=W.device, dtype=torch.float32)
+                gb4 = torch.empty(N4, device=W.device, dtype=torch.float32) if want_b else None
+                ops.gemm(gp.t(), xin, out=gw4, rowsum=gb4)
+                g_W.copy_(gw4[:N, :Cd + Kx])
+                if want_b:
+                    g_b.copy_(gb4[:N])
+            else:
+                if Cd:  # db rides on the first dW GEMM as an all-ones column
+                    cc = c.reshape(1, -1).expand(M, Cd) if (c.dim() == 1 or c.shape[0] == 1) and M != 1 else c
+                    ops.gemm(gT, cc, out=g_W[:, :Cd], mask=None if mask is None else mask[:, :Cd],
+                             rowsum=g_b)
+                if x is not None:
+                    ops.gemm(gT, x, out=g_W[:, Cd:], mask=None if mask is None else mask[:, Cd:],
+                             rowsum=None if Cd else g_b)
         elif want_b:
             ops.gemm(gT, gT[:0].t(), out=torch.empty(W.shape[0], 0, device=W.device), rowsum=g_b)
         if x is not None and _needs(ctx, 0):

@@ -26,10 +26,11 @@ step prof_train 240 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run --o
 step gemm_bench 120 python scripts/gemm_bench.py
 step cnf 300 python bench.py --cnf --steps 10 --warmup 3
 step prof_cnf 240 rocprofv3 --kernel-trace --stats -d $O/prof_cnf -o run --output-format csv -- python3 bench.py --cnf --steps 10 --warmup 3
-for f in config2 maf nsa; do step flow_$f 240 python bench.py --flow $f --steps 10 --warmup 3; done
+for f in config2 maf nsa maf_grid; do step flow_$f 240 python bench.py --flow $f --steps 10 --warmup 3; done
 step cnf_dopri5 300 python bench.py --cnf --cnf-solver dopri5 --steps 10 --warmup 3
 step prof_cnf_dopri5 240 rocprofv3 --kernel-trace --stats -d $O/prof_cnf_dopri5 -o run --output-format csv -- python3 bench.py --cnf --cnf-solver dopri5 --steps 10 --warmup 3 --no-cpu-baseline
 step bayes_lp 240 python bench.py --bayes lp --steps 10 --warmup 3
 step bayes_sample 240 python bench.py --bayes sample --steps 10 --warmup 3
+step bayes_grad 240 python bench.py --bayes grad --steps 5 --warmup 2
 step prof_bayes_sample 240 rocprofv3 --kernel-trace --stats -d $O/prof_bayes_sample -o run --output-format csv -- python3 bench.py --bayes sample --steps 5 --warmup 2 --no-cpu-baseline
 exit 0

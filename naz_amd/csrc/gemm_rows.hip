@@ -196,12 +196,7 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          float v = activate_rt(p.act, acc[o0 + oo][r] + bn);
-          if (p.dy != nullptr) {
-            const int64_t m = m0 + wave * 32 + row;
-            if (m < p.M && n < p.N) v *= activate_grad_from_out(p.dact, p.dy[m * p.lddy + n]);
-          }
-          E[row * EP + 32 * oo + (lane & 31)] = v;
+          E[row * EP + 32 * oo + (lane & 31)] = activate_rt(p.act, acc[o0 + oo][r] + bn);
         }
       }
       // 8 EG float4 per row; 64 / (8 EG) rows per wave-instruction
@@ -214,6 +209,13 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
         const int64_t m = m0 + wave * 32 + row;
         if (m >= p.M || col >= p.N) continue;
         float4 v = *reinterpret_cast<const float4*>(E + row * EP + 4 * c4);
+        if (p.dy != nullptr) {  // chained act' (naz_gemm_dact), applied on the 16-byte row piece
+          const float* dyr = p.dy + m * p.lddy + col;
+          v.x *= activate_grad_from_out(p.dact, dyr[0]);
+          if (col + 1 < p.N) v.y *= activate_grad_from_out(p.dact, dyr[1]);
+          if (col + 2 < p.N) v.z *= activate_grad_from_out(p.dact, dyr[2]);
+          if (col + 3 < p.N) v.w *= activate_grad_from_out(p.dact, dyr[3]);
+        }
         if (col + 4 <= p.N) {
           float4* dst = reinterpret_cast<float4*>(p.c + m * p.ldc + col);
           if (p.accumulate) {
@@ -242,8 +244,7 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
       const int64_t m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m >= p.M) continue;
       float* dst = p.c + m * p.ldc + n;
-      float v = activate_rt(p.act, acc[o][r] + bn);
-      if (p.dy != nullptr) v *= activate_grad_from_out(p.dact, p.dy[m * p.lddy + n]);
+      const float v = activate_rt(p.act, acc[o][r] + bn);  // (dy: vst path only, see rowgemm_dact)
       *dst = p.accumulate ? *dst + v : v;
     }
   }
@@ -648,6 +649,10 @@ int rowgemm_linear_batched(const float* ctx, int64_t ldc, int64_t zc, int C, con
 // naz_gemm_dact: C[m, n] = (Σ_k A[m, k] W[k, n] mask[k, n]) · act'(dy[m, n])   (A rows at lda)
 int rowgemm_dact(const float* A, int64_t lda, int K, const float* W, int64_t ldw, const float* mask, int64_t ldm,
                  float* C, int64_t ldc, const float* dy, int64_t lddy, int dact, int64_t M, int N, hipStream_t s) {
+  // the act' factor is applied in the 16-byte row-piece epilogue only (in the per-element one it
+  // pushed the accumulators to scratch): C rows must allow it
+  if (ldc % 4 != 0 || (reinterpret_cast<uintptr_t>(C) & 15) != 0)
+    return set_error("naz_gemm_dact: C needs 16-byte aligned rows (ldc %% 4 == 0)");
   RowGemmArgs p{};
   p.a1 = A;
   p.lda1 = lda;

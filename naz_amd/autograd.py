@@ -17,6 +17,7 @@ Autograd only sequences the kernels; no torch arithmetic runs on the batch excep
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -105,6 +106,9 @@ def linear_act(x, weight, bias, act="identity", context=None, mask=None):
     return LinearActFn.apply(x, context, weight, bias, mask, act)
 
 
+_DW_CONCAT = os.environ.get("NAZ_DW_CONCAT", "1") != "0"
+
+
 def _param_grads(gpre, x, c, W, need_W: bool, need_b: bool):
     """dW (and db riding on it as an all-ones column) of one Linear layer: as LinearActFn."""
     M = gpre.shape[0]
@@ -115,11 +119,18 @@ def _param_grads(gpre, x, c, W, need_W: bool, need_b: bool):
     gT = gpre.t()
     if need_W:
         g_W = torch.empty_like(W)
-        if Cd:
-            cc = c.reshape(1, -1).expand(M, Cd) if (c.dim() == 1 or c.shape[0] == 1) and M != 1 else c
-            ops.gemm(gT, cc, out=g_W[:, :Cd], rowsum=g_b)
-        if x is not None:
-            ops.gemm(gT, x, out=g_W[:, Cd:], rowsum=None if Cd else g_b)
+        Kx = 0 if x is None else x.shape[-1]
+        if _DW_CONCAT and Cd and Kx and M >= 1024 and (Cd + Kx) % 4 == 0 and Cd + Kx <= 255 and c.dim() == 2 \
+                and c.shape[0] == M:
+            # per-row [ctx | x]: one dW GEMM over the concatenated input (one pass over dPre, the
+            # flat wgrad kernel on a 16-byte multiple width instead of a narrow x-only GEMM)
+            ops.gemm(gT, torch.cat((c, x), 1), out=g_W, rowsum=g_b)
+        else:
+            if Cd:
+                cc = c.reshape(1, -1).expand(M, Cd) if (c.dim() == 1 or c.shape[0] == 1) and M != 1 else c
+                ops.gemm(gT, cc, out=g_W[:, :Cd], rowsum=g_b)
+            if x is not None:
+                ops.gemm(gT, x, out=g_W[:, Cd:], rowsum=None if Cd else g_b)
     elif need_b:
         ops.gemm(gT, gT[:0].t(), out=torch.empty(W.shape[0], 0, device=W.device), rowsum=g_b)
     return g_W, g_b

@@ -217,7 +217,7 @@ def _flat_layer(layer, P, dev):
 
 def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bounds=None, context=None,
                           rows_per_chunk: int = 1 << 23, fold_context: bool = True,
-                          fuse_pass2: bool = True) -> Dict[str, object]:
+                          fuse_pass2: bool = True, batch_layers: bool = True) -> Dict[str, object]:
     """naz ``make_normalizing_flow`` (bflow_jax_maf.py:196-225) on MI355X.  Returns
     ``{"lp": f(params) -> [B], "sampler": f(params, rng_key, size) -> (y, log_j),
     "lp_batched": f(params_P) -> [P, B], "sampler_batched": f(params_P, rng_key, size)}``.
@@ -386,13 +386,8 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         return (len(g1) == nl and [blk[0] for blk in g1] == list(range(nl)) and
                 all(b - a <= 160 for (li, a, b, n, w, bb) in g1))
 
-    def _pass2_fused(plan, split, osplit, F, hc, c1, xn, z, lp2):
-        """The order-2 dim of a 2-dim MAF layer: layer 0's degree-1 units from x, each later
-        layer's from the previous layer's (context / degree-0 parts folded into per-draw biases),
-        its two output rows, the inverse affine step — one naz_made_affine_inv1 launch."""
-        P = z.shape[0]
-        g1, s1 = plan.hidden[1], split[1]
-        rows = [b - a for (li, a, b, n, w, bb) in g1]
+    def _p2_map(plan, rows):
+        """made.hip pack map of the pass-2 chain (context-free, degree-1 widths ``rows``)."""
         key = tuple(rows)
         if getattr(plan, "p2_key", None) != key:
             sp = MAFSpec(D, 0, rows, act)
@@ -401,6 +396,15 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             plan.p2_nh = (max(rows) + 31) // 32
             plan.p2_map = made_pack_map(sp, ones, plan.p2_nh).to(dev)
             plan.p2_key = key
+
+    def _pass2_fused(plan, split, osplit, F, hc, c1, xn, z, lp2):
+        """The order-2 dim of a 2-dim MAF layer: layer 0's degree-1 units from x, each later
+        layer's from the previous layer's (context / degree-0 parts folded into per-draw biases),
+        its two output rows, the inverse affine step — one naz_made_affine_inv1 launch."""
+        P = z.shape[0]
+        g1, s1 = plan.hidden[1], split[1]
+        rows = [b - a for (li, a, b, n, w, bb) in g1]
+        _p2_map(plan, rows)
         parts = [torch.zeros((P, 1), device=dev)]
         for (li, a, b, n, w, bb), (e, wc, wr) in zip(g1, s1):
             bias = F[:, bb]
@@ -417,10 +421,75 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         packed = torch.cat(parts, 1)[:, plan.p2_map].contiguous()
         return ops.made_affine_inv1(packed, len(rows), plan.p2_nh, xn, z, i, act, lp2, ops.LD_ROWSUM_SUB)
 
+    def _same_structure():
+        """Every layer's schedule has the same block shapes (only the permutation's dims differ):
+        then the per-draw constants and packs of ALL layers run as single launches."""
+        def sig(pl):
+            split, osplit = _split_maps(pl)
+            return (tuple(blk[:4] for blk in pl.hidden[0]), tuple(blk[:4] for blk in pl.hidden[1]),
+                    tuple(t[0] for t in split[1]), tuple((o[1], t[0]) for o, t in zip(pl.outs, osplit)))
+        s0 = sig(plans[0])
+        return all(_fused_pass2(pl, None) and sig(pl) == s0 for pl in plans)
+
+    def _lp_chunk_const2(params: Params, out: Tensor):
+        """D = 2, one context vector, identical layer structure: the degree-0 constants, bias
+        folds and pass-2 packs of all L layers x P draws in one launch each (Q = L P problems),
+        then per layer only the order-1 affine step and the fused pass-2 kernel."""
+        P = _draws(params)
+        L = len(plans)
+        Q = L * P
+        z = x.expand(P, B, D).contiguous()
+        lp = out.reshape(P * B)
+        lp.zero_()
+        Fa = torch.stack([_flat_layer(params[l], P, dev) for l in range(L)])  # [L, P, size]
+
+        def gat(get):  # per-layer index maps of one shape -> [Q, *shape] (one gather)
+            idx = torch.stack([get(l) for l in range(L)])
+            return torch.gather(Fa, 2, idx.reshape(L, 1, -1).expand(L, P, -1)).reshape(Q, *idx.shape[1:])
+        pl0 = plans[0]
+        nl = len(pl0.widths)
+        sp = [_split_maps(pl) for pl in plans]
+        c1 = ctx.reshape(1, 1, C).expand(Q, 1, C).contiguous()
+        hc = {}
+        for j, (li, a, b, n, w, bb) in enumerate(pl0.hidden[0]):
+            src = torch.cat((c1, torch.zeros((Q, 1, D), device=dev)), 2) if li == 0 else hc[li - 1]
+            hc[li] = ops.linear_act_batched(src[:, :, :n].contiguous(), gat(lambda l: plans[l].hidden[0][j][4]),
+                                            gat(lambda l: plans[l].hidden[0][j][5]), act)
+        parts = [torch.zeros((Q, 1), device=dev)]
+        for j, (li, a, b, n, w, bb) in enumerate(pl0.hidden[1]):
+            e = sp[0][0][1][j][0]
+            bias = gat(lambda l: plans[l].hidden[1][j][5])
+            if e:
+                bias = ops.linear_act_batched(c1 if li == 0 else hc[li - 1], gat(lambda l: sp[l][0][1][j][1]), bias,
+                                              "identity")[:, 0, :]
+            parts += [gat(lambda l: sp[l][0][1][j][2]).reshape(Q, -1), bias.reshape(Q, -1)]
+        raws = []
+        for k in range(2):
+            e = sp[0][1][k][0]
+            bias = gat(lambda l: plans[l].outs[k][3])
+            if e:
+                bias = ops.linear_act_batched(hc[nl - 1], gat(lambda l: sp[l][1][k][1]), bias, "identity")[:, 0, :]
+            raws.append(bias)
+        parts += [gat(lambda l: sp[l][1][1][2]).reshape(Q, -1), raws[1].reshape(Q, -1)]
+        rows = [blk[2] - blk[1] for blk in pl0.hidden[1]]
+        _p2_map(pl0, rows)
+        packed = torch.cat(parts, 1)[:, pl0.p2_map].contiguous()  # [Q, made_packed_floats]
+        for l in reversed(range(L)):
+            i1, i2 = plans[l].outs[0][0], plans[l].outs[1][0]
+            r1 = raws[0][l * P:(l + 1) * P].reshape(P, 1, 2).expand(P, B, 2).reshape(P * B, 2)
+            xn = torch.zeros_like(z)
+            ops.affine_ar(z.view(P * B, D)[:, i1:i1 + 1], r1, True, ops.LD_ROWSUM_SUB, lp,
+                          out=xn.view(P * B, D)[:, i1:i1 + 1])
+            z = ops.made_affine_inv1(packed[l * P:(l + 1) * P], nl, pl0.p2_nh, xn, z, i2, act, lp.view(P, B),
+                                     ops.LD_ROWSUM_SUB)
+        ops.base_log_prob(z.reshape(P * B, D), out=lp, accumulate=True)
+
     def lp_batched(params: Params) -> Tensor:
         P = _draws(params)
         out = torch.empty((P, B), device=dev, dtype=torch.float32)
         run = _lp_chunk_const if (const_ctx and fold_context) else _lp_chunk
+        if run is _lp_chunk_const and batch_layers and _same_structure():
+            run = _lp_chunk_const2
         for p0, p1 in _chunks(P, B * max(1, width_sum // 64)):
             run([[(w[p0:p1], b[p0:p1]) for (w, b) in layer] for layer in params], out[p0:p1])
         return out

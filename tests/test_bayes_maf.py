@@ -384,3 +384,21 @@ def test_lp_and_grad_vs_oracle_autograd(_gpu, ctx_kind):
     from tests.parity import grad_floor
     assert_parity(grad.cpu().numpy(), g64, g32, what="NUTS potential gradient", floor=grad_floor(g64),
                   count_factor=None)
+
+
+@pytest.mark.gpu
+def test_lp_layer_batched_constants():
+    """D = 2, one context vector: the per-draw constants / packs of all layers in single
+    launches (_lp_chunk_const2) give the per-layer folded path's log_prob."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    spec = dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=4, P=5, B=700, ctx="vec")
+    layers, draws, x, ctx = _setup(spec)
+    params = _batched_params(draws, "cuda")
+    a = _flow(spec, layers, x, ctx, "cuda")["lp_batched"](params)
+    b = _flow(spec, layers, x, ctx, "cuda", batch_layers=False)["lp_batched"](params)
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-5), (a - b).abs().max()
+    for p, d in enumerate(draws):
+        ol = _oracle_layers(layers, d)
+        assert_parity(a[p].cpu().numpy(), J.log_prob(x, ol, ctx),
+                      J.log_prob(x, J.cast_layers(ol, np.float32), ctx, np.float32), what=f"layer-batched lp {p}")

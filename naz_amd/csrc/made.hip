@@ -155,6 +155,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) made_affine_fwd_kernel(MadeAr
     for (int c = 0; c < NH; ++c) {  // input 32-block c of hidden layer j
       const float4* Wb = Wl[g & 1];
       if (g + 1 < nchunk) NAZ_MADE_FETCH(g + 1)  // in flight during this chunk's MFMAs
+#ifndef NAZ_MADE_NO_PRIO  // MFMA chunk at wave priority 1 (same-box A/B: lp -1 %, sample -0.3 %)
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
 #pragma unroll
@@ -166,6 +169,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) made_affine_fwd_kernel(MadeAr
           acc[o] = mfma32(a.w, hv[c][t * 4 + 3], acc[o]);
         }
       }
+#ifndef NAZ_MADE_NO_PRIO  // MFMA chunk at wave priority 1 (same-box A/B: lp -1 %, sample -0.3 %)
+      __builtin_amdgcn_s_setprio(0);
+#endif
       if (g + 1 < nchunk) {  // hand the prefetched chunk to the other buffer
         NAZ_MADE_STASH((g & 1) ^ 1)
       }

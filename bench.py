@@ -3,13 +3,18 @@ coupling flow (BASELINE.json metric, configs[2] = "Conditional SBI flow: 16-dim 
 context, RQ-spline, batch 2^20, 1 MI355X"; shapes pinned in SURVEY.md §8: K=8, L=8, H=[128,128],
 split 8, tanh, bound 3).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--scaling strong|weak]
+                    [--no-cpu-baseline] [--train | --cnf | --flow F | --bayes M]
 
-One step = one fused log_prob launch over one batch of 2^20 rows per GPU, inputs resident in
-HBM.  N > 1 runs under torch.distributed.run, one process per GPU: each rank owns an
-independent shard of 2^20 rows (log_prob has no cross-row term: SURVEY.md §8e) — no data-path
-collective, "weak" scaling.  The timed region is bracketed by barrier + synchronize on both
-sides; the max over ranks is reported.  Rank 0 prints ONE JSON line.
+One step = one fused log_prob launch over this rank's rows, inputs resident in HBM.  N > 1
+runs one process per GPU: under torch.distributed.run (RANK/WORLD_SIZE set by the driver), or,
+when ``--gpus N`` is given without that environment, by starting torch.distributed.run itself as
+a child process before anything touches the GPU.  Rows are independent (log_prob has no
+cross-row term: SURVEY.md §8e), so the ranks run with no data-path collective.  Default
+``--scaling strong``: ONE global batch of 2^20 rows (the metric's batch) split over the ranks —
+north_star's ">=6x strong scaling at 8 GPUs"; ``--scaling weak``: --batch rows per rank.  The
+timed region is bracketed by barrier + synchronize on both sides; the max over ranks is
+reported and ``value`` = global rows per step / that time.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -56,6 +61,46 @@ def gaussian_mixture(n: int, dim: int, seed: int) -> np.ndarray:
     return (means[comp] + sig[comp] * rng.standard_normal(size=(n, dim))).astype(np.float32)
 
 
+def mixture_rows(lo: int, hi: int, dim: int, seed: int = 0, chunk: int = 1 << 16) -> np.ndarray:
+    """Rows [lo, hi) of ONE global synthetic batch (the mixture above), generated in fixed 2^16-row
+    chunks, each from its own seeded stream, so a rank's shard holds the same rows whatever the
+    number of ranks (strong scaling splits one global batch)."""
+    rng = np.random.default_rng(seed)
+    means = rng.normal(0.0, 2.0, size=(8, dim))
+    sig = rng.uniform(0.3, 1.0, size=(8, dim))
+    out = np.empty((hi - lo, dim), dtype=np.float32)
+    for c0 in range(lo - lo % chunk, hi, chunk):
+        r = np.random.default_rng([seed, c0 // chunk])
+        comp = r.integers(0, 8, size=chunk)
+        blk = means[comp] + sig[comp] * r.standard_normal(size=(chunk, dim))
+        a, b = max(lo, c0), min(hi, c0 + chunk)
+        out[a - lo:b - lo] = blk[a - c0:b - c0]
+    return out
+
+
+def normal_rows(lo: int, hi: int, dim: int, seed: int = 1, chunk: int = 1 << 16) -> np.ndarray:
+    """Rows [lo, hi) of one global N(0, I) context batch, chunked like mixture_rows."""
+    out = np.empty((hi - lo, dim), dtype=np.float32)
+    for c0 in range(lo - lo % chunk, hi, chunk):
+        blk = np.random.default_rng([seed, c0 // chunk]).standard_normal(size=(chunk, dim))
+        a, b = max(lo, c0), min(hi, c0 + chunk)
+        out[a - lo:b - lo] = blk[a - c0:b - c0]
+    return out
+
+
+def shard(args, rank: int, world: int, default_global: int):
+    """(lo, hi, global_rows) of this rank.  strong: one global batch (--batch, default the
+    config's) split contiguously over the ranks; weak: --batch rows per rank."""
+    per = args.batch if args.batch is not None else None
+    if args.scaling == "weak":
+        n = per if per is not None else default_global
+        return rank * n, (rank + 1) * n, n * world
+    g = per if per is not None else default_global
+    base, rem = divmod(g, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0), g
+
+
 def build_flow():
     from naz_amd.flows import NormalizingFlow
     torch.manual_seed(1234)
@@ -78,7 +123,9 @@ def cpu_baseline(flow, x_host: np.ndarray, c_host, budget_rows: int = 1 << 19, s
         spec = dict(flow_type="nsc", D=D, C=C, hidden=[H, H], L=L, K=K, split=S)
     state = fio.export_state(flow)
     of = O.build_flow(spec, state, torch.float32)
-    threads = torch.get_num_threads()
+    cores = host_cores()
+    torch.set_num_threads(cores["threads"])
+    threads = cores["threads"]
     chunk = min(1 << 16, budget_rows)
     xs = torch.as_tensor(x_host[:budget_rows])
     cs = torch.as_tensor(c_host[:budget_rows]) if c_host is not None else None
@@ -89,7 +136,7 @@ def cpu_baseline(flow, x_host: np.ndarray, c_host, budget_rows: int = 1 << 19, s
     with torch.inference_mode():
         of.log_prob(xs[:chunk], crows(0, chunk))  # warm-up
         runs = []
-        for _ in range(3):
+        for _ in range(5):  # 1 warm-up, median of 5
             t0 = time.perf_counter()
             for i in range(0, budget_rows, chunk):
                 of.log_prob(xs[i:i + chunk], crows(i, i + chunk))
@@ -105,14 +152,62 @@ def cpu_baseline(flow, x_host: np.ndarray, c_host, budget_rows: int = 1 << 19, s
     with torch.no_grad():
         gpu = flow.log_prob(torch.as_tensor(x_host[:n], device="cuda"),
                             condition=torch.as_tensor(c_host[:n], device="cuda") if cond else None).cpu().numpy()
-    rel = np.abs(gpu - ref) / np.maximum(np.abs(ref), 1.0)
-    rel32 = np.abs(ref32 - ref) / np.maximum(np.abs(ref), 1.0)
     return {
         "value": budget_rows / med, "unit": "samples/s", "cores": threads, "kind": "port",
         "sample": f"{budget_rows} rows of the same workload in 2^16-row chunks, torch.inference_mode, "
-                  f"{threads} threads, median of 3 after 1 warm-up chunk ({med:.2f} s)",
-    }, {"rows": n, "gpu_rel_median": float(np.median(rel)), "gpu_rel_q99": float(np.quantile(rel, 0.99)),
-        "gpu_rel_max": float(rel.max()), "ref_fp32_rel_max": float(rel32.max())}
+                  f"{threads} threads, median of 5 after 1 warm-up chunk ({med:.2f} s)",
+        "host": cores,
+    }, parity_record(gpu, ref, ref32)
+
+
+def host_cores() -> dict:
+    """Host CPUs the baseline may use: os.sched_getaffinity(0), the physical cores lscpu lists
+    for them, and the cgroup CPU quota (the GPU box gives a job a 16-CPU share of a larger
+    host, which OMP_NUM_THREADS states).  Threads used = the smallest of these."""
+    aff = sorted(os.sched_getaffinity(0))
+    phys = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        cores = {(ln.split(",")[2], ln.split(",")[1]) for ln in out.splitlines()
+                 if ln and not ln.startswith("#") and int(ln.split(",")[0]) in set(aff)}
+        phys = len(cores) or None
+    except Exception:
+        pass
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    omp = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    threads = min(v for v in (len(aff), phys, quota, omp) if v)
+    return {"threads": threads, "sched_getaffinity": len(aff), "lscpu_physical_cores": phys,
+            "cgroup_cpu_quota": quota, "OMP_NUM_THREADS": omp}
+
+
+def parity_record(gpu, ref64, ref32) -> dict:
+    """The spot check against the fp64 oracle, judged by the tests' criterion (tests/parity.py):
+    rel = |v - ref64| / max(|ref64|, 1); median <= max(1e-6, 4 x ref32's), q99 <= max(1e-5,
+    4 x ref32's), max <= max(1e-5, 32 x ref32's), #(rel > 1e-5) <= 2 x ref32's + 2."""
+    from tests import parity as P
+    rec = {"rows": int(np.asarray(gpu).size)}
+    try:
+        st = P.assert_parity(gpu, ref64, ref32, what="bench spot check")
+        rec["pass"] = True
+    except AssertionError as e:
+        st, rec["pass"], rec["failure"] = None, False, str(e)[:300]
+    r = P.rel_err(gpu, ref64).ravel()
+    r32 = P.rel_err(ref32, ref64).ravel()
+    rec.update({"gpu_rel_median": float(np.median(r)), "gpu_rel_q99": float(np.quantile(r, 0.99)),
+                "gpu_rel_max": float(r.max()), "n_above_1e-5": int((r > P.RTOL).sum()),
+                "ref_fp32_rel_median": float(np.median(r32)), "ref_fp32_rel_q99": float(np.quantile(r32, 0.99)),
+                "ref_fp32_rel_max": float(r32.max()), "ref_fp32_n_above_1e-5": int((r32 > P.RTOL).sum())})
+    rec.update(tolerance="rel=|v-ref64|/max(|ref64|,1) vs the fp64 oracle; median<=max(1e-6,4*ref32), "
+                         "q99<=max(1e-5,4*ref32), max<=max(1e-5,32*ref32), n_above_1e-5<=2*ref32+2 "
+                         "(ref32 = the reference algorithm in fp32; tests/parity.py)")
+    return rec
 
 
 def load_traffic(mode: str):
@@ -129,23 +224,27 @@ def load_traffic(mode: str):
 
 
 def run_train(args, dev, rank, world, dist):
-    """configs[3]: the NLL step of naz's train (train_flows.py:194-213), 2^20 rows per GPU,
-    one process per GPU, gradients all-reduced over RCCL in one flat bucket."""
+    """configs[3]: the NLL step of naz's train (train_flows.py:194-213) on one global batch of
+    2^23 rows (strong scaling, the default: split over the ranks) or --batch rows per rank
+    (weak), one process per GPU, gradients all-reduced over RCCL in one flat bucket.  A rank's
+    rows are processed in --micro-batch chunks whose gradients accumulate before the one
+    all-reduce (the same gradient as one pass; bounds the activation memory)."""
     from naz_amd.trainers import DataParallel, nll_step
     from naz_amd.trainers.train_flows import _flow_parameters
     flow = build_flow()
     flow.set_fused(False)
-    B = args.batch
-    x = torch.as_tensor(gaussian_mixture(B, D, seed=rank), device=dev)
-    c = torch.as_tensor(np.random.default_rng(1 + 1000 * rank).standard_normal(size=(B, C)).astype(np.float32),
-                        device=dev)
+    lo, hi, G = shard(args, rank, world, 1 << 23)
+    B = hi - lo
+    x = torch.as_tensor(mixture_rows(lo, hi, D, seed=0), device=dev)
+    c = torch.as_tensor(normal_rows(lo, hi, C, seed=1), device=dev)
     dp = DataParallel()
     params = _flow_parameters(flow)
     dp.broadcast_params(params)
     opt = torch.optim.Adam(params, lr=1e-4)
+    mb = args.micro_batch
 
     def step():
-        return nll_step(flow, x, c, opt, params, dp, B * world, clip_val=1.0)
+        return nll_step(flow, x, c, opt, params, dp, G, clip_val=1.0, micro_batch=mb)
 
     for _ in range(args.warmup):
         step()
@@ -167,26 +266,65 @@ def run_train(args, dev, rank, world, dist):
         elapsed = float(t[0])
     if rank == 0:
         step_s = elapsed / args.steps
-        flop = 3 * flops_per_row() * B  # fwd GEMMs + dX + dW
+        flop = 3 * flops_per_row() * B  # per rank: fwd GEMMs + dX + dW
         achieved = flop / step_s / 1e12
+        traffic, traffic_src = load_traffic("train")
         rec = {
             "metric": "samples/sec through the NLL training step (log_prob fwd + backward + grad all-reduce + "
                       "clip + Adam), 16-dim RQ-spline flow",
-            "value": B * world / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+            "value": G / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
             "config": {"workload": "BASELINE configs[3]: the configs[2] flow's NLL step, data parallel",
-                       "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world} (RCCL all-reduce)"},
+                       "batch_per_gpu": B, "global_batch": G, "micro_batch": mb,
+                       "parallelism": f"dp{world} (RCCL all-reduce, one flat bucket)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "whole step",
-                         "flop_per_row": 3 * flops_per_row()},
+                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "whole step", "flop_per_row": 3 * flops_per_row()},
             "final_loss": float(loss),
         }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = train_cpu_baseline(flow)
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def train_cpu_baseline(flow, rows: int = 1 << 14) -> dict:
+    """The reference's NLL step on the host: the oracle flow (pyro semantics, torch fp32) forward
+    + autograd backward + clip + Adam over a bounded sample of the same workload."""
+    from naz_amd.flows import io as fio
+    from oracle import naz_oracle as O  # baseline only
+    spec = dict(flow_type="nsc", D=D, C=C, hidden=[H, H], L=L, K=K, split=S)
+    state = {k: torch.as_tensor(v).clone() for k, v in fio.export_state(flow).items()}
+    of = O.build_flow(spec, state, torch.float32)
+    ps = [v.requires_grad_(True) for v in state.values() if v.is_floating_point()]
+    cores = host_cores()
+    torch.set_num_threads(cores["threads"])
+    xs = torch.as_tensor(mixture_rows(0, rows, D, seed=0))
+    cs = torch.as_tensor(normal_rows(0, rows, C, seed=1))
+    opt = torch.optim.Adam(ps, lr=1e-4)
+
+    def step():
+        opt.zero_grad()
+        loss = -of.log_prob(xs, cs).mean()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(ps, 1.0)
+        opt.step()
+
+    step()  # warm-up
+    runs = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        step()
+        runs.append(time.perf_counter() - t0)
+    med = statistics.median(runs)
+    return {"value": rows / med, "unit": "samples/s", "cores": cores["threads"], "kind": "port",
+            "sample": f"{rows} rows, oracle nsc flow (torch fp32) forward + autograd backward + clip + Adam, "
+                      f"{cores['threads']} threads, median of 5 after 1 warm-up ({med:.2f} s)",
+            "host": cores}
 
 
 CNF_D, CNF_H, CNF_STEPS = 16, [128, 128, 128], 8
@@ -207,8 +345,9 @@ def run_cnf(args, dev, rank, world, dist):
     from naz_amd.flows import NormalizingFlow
     torch.manual_seed(1234)
     f = NormalizingFlow("cnf", None, CNF_D, 0, CNF_H, 1, steps=CNF_STEPS)
-    B = args.batch if args.batch != (1 << 20) else (1 << 18)
-    x = torch.as_tensor(gaussian_mixture(B, CNF_D, seed=rank), device=dev) * 0.5
+    lo, hi, G = shard(args, rank, world, 1 << 18)
+    B = hi - lo
+    x = torch.as_tensor(mixture_rows(lo, hi, CNF_D, seed=0), device=dev) * 0.5
     t = f.transforms[0]
     plan = t._plan
     packed = plan.packed()
@@ -277,9 +416,9 @@ def run_cnf(args, dev, rank, world, dist):
             peak = FP32_PEAK_TFLOPS
         rec = {
             "metric": "samples/sec through log_prob+log|detJ|, 16-dim CNF (FFJORD, Hutchinson trace)",
-            "value": B * world * args.steps / elapsed, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "value": G * args.steps / elapsed, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: x ~ 0.5 x 8-component Gaussian mixture; random-init weights (nn.Linear default, "
                     "torch seed 1234); eps ~ N(0, I) redrawn per step",
             "config": {"workload": "BASELINE configs[4]: FFJORD block D=16, H=[128,128,128], softplus, " + (
@@ -287,7 +426,7 @@ def run_cnf(args, dev, rank, world, dist):
                                    "log_prob (naz_cnf_integrate_dopri5 t 0->1)" if dopri5 else
                                    "fixed-step RK4 x 8 (NFE 32, SURVEY.md §8d pin), log_prob "
                                    "(naz_cnf_integrate t 0->1)"),
-                       "batch_per_gpu": B, "global_batch": B * world,
+                       "batch_per_gpu": B, "global_batch": G,
                        "parallelism": f"dp{world} (independent row shards, no collective)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": None, "mfma_mode": mode,
@@ -353,10 +492,10 @@ def run_flow_case(args, dev, rank, world, dist):
     ftype, Dd, Cd, hid, Ld, extra, Bdef, desc = FLOW_CASES[args.flow]
     torch.manual_seed(1234)
     f = NormalizingFlow(ftype, None, Dd, Cd, hid, Ld, *extra).to(dev)
-    B = args.batch if args.batch != (1 << 20) else Bdef
-    x = torch.as_tensor(gaussian_mixture(B, Dd, seed=rank), device=dev)
-    c = (torch.as_tensor(np.random.default_rng(1 + rank).standard_normal(size=(B, Cd)).astype(np.float32),
-                         device=dev) if Cd else None)
+    lo, hi, G = shard(args, rank, world, Bdef)
+    B = hi - lo
+    x = torch.as_tensor(mixture_rows(lo, hi, Dd, seed=0), device=dev)
+    c = torch.as_tensor(normal_rows(lo, hi, Cd, seed=1), device=dev) if Cd else None
     grid = args.flow.endswith("_grid")
     if grid:  # one context vector, broadcast (naz: condition=[C])
         c = c[0].contiguous()
@@ -409,11 +548,11 @@ def run_flow_case(args, dev, rank, world, dist):
         fused = getattr(f, "fused", False)
         rec = {
             "metric": f"samples/sec through log_prob+log|detJ|, naz {ftype} flow (NormalizingFlow API)",
-            "value": B * world / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+            "value": G / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
-            "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B * world,
+            "config": {"workload": desc, "batch_per_gpu": B, "global_batch": G,
                        "parallelism": f"dp{world} (independent row shards, no collective)",
                        "path": "fused kernel" if fused else "per-layer HIP kernels (rowgemm + spline/affine)"},
             "roofline": {"bound": "mfma", "achieved": achieved,
@@ -457,7 +596,7 @@ def run_bayes(args, dev, rank, world, dist):
     lp_mode = args.bayes == "lp"
     grad_mode = args.bayes == "grad"
     P = 64 if lp_mode else (1 if grad_mode else 16)
-    B = args.batch if args.batch != (1 << 20) else (1 << 14 if lp_mode else 1 << 16)
+    B = args.batch if args.batch is not None else (1 << 14 if lp_mode else 1 << 16)
     rng = np.random.default_rng(100 + rank)
     draws = [[[((W * (1 + 0.25 * rng.uniform(-1, 1, W.shape))).astype(np.float32),
                 (b * (1 + 0.25 * rng.uniform(-1, 1, b.shape))).astype(np.float32)) for (W, b) in params]
@@ -593,19 +732,42 @@ def run_bayes(args, dev, rank, world, dist):
         dist.destroy_process_group()
 
 
+def launch_ranks(n: int) -> int:
+    """``bench.py --gpus N`` without a torch.distributed environment: start N ranks (one process
+    per GPU) under torch.distributed.run as a CHILD process and return its exit code.  Nothing in
+    this parent touches the GPU (no HIP call before the fork/exec of the launcher)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="rows per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="strong: the GLOBAL batch (default: the config's — 2^20 log_prob, 2^23 --train, 2^18 "
+                         "--cnf); weak: rows per GPU")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong (default, north_star's '>=6x strong scaling at 8 GPUs'): one global batch split "
+                         "over the ranks; weak: --batch rows on every rank")
+    ap.add_argument("--micro-batch", type=int, default=1 << 20,
+                    help="--train: rows per forward+backward chunk (gradients accumulate before the all-reduce)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train", action="store_true",
                     help="time the data-parallel NLL training step instead (BASELINE configs[3]: fwd + HIP "
-                         "backward + flat-bucket RCCL all-reduce + clip + Adam) on the same flow and batch")
+                         "backward + flat-bucket RCCL all-reduce + clip + Adam) on the same flow")
     ap.add_argument("--cnf", action="store_true",
                     help="BASELINE configs[4]: 16-dim FFJORD CNF (H=[128]*3, softplus, Hutchinson trace, RK4 x 8 "
-                         "steps) log_prob at 2^18 rows per GPU")
+                         "steps) log_prob at 2^18 rows")
     ap.add_argument("--cnf-solver", choices=["rk4", "dopri5"], default="rk4",
                     help="--cnf: pinned fixed-step RK4 x 8 (default) or adaptive dopri5 (atol = rtol = 1e-4)")
     ap.add_argument("--flow", choices=sorted(FLOW_CASES), default=None,
@@ -618,6 +780,9 @@ def main():
                          "the shape allows, else f16x3, else bf16x6; f32: exact FP32 MFMA")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -626,6 +791,11 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        world = dist.get_world_size()  # n_gpus = the ranks RCCL actually formed
+        rank = dist.get_rank()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but {world} rank(s) formed; reporting n_gpus = {world}",
+              file=sys.stderr, flush=True)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
@@ -637,11 +807,17 @@ def main():
         return run_flow_case(args, dev, rank, world, dist)
     if args.bayes:
         return run_bayes(args, dev, rank, world, dist)
+    return run_log_prob(args, dev, rank, world, dist)
 
+
+def run_log_prob(args, dev, rank, world, dist):
+    """The headline: BASELINE's metric on configs[2], one fused naz_coupling_log_prob launch per
+    step over this rank's rows of the global batch."""
     flow = build_flow()
-    B = args.batch
-    x_host = gaussian_mixture(B, D, seed=0 + rank)
-    c_host = np.random.default_rng(1 + 1000 * rank).standard_normal(size=(B, C)).astype(np.float32)
+    lo, hi, G = shard(args, rank, world, 1 << 20)
+    B = hi - lo
+    x_host = mixture_rows(lo, hi, D, seed=0)
+    c_host = normal_rows(lo, hi, C, seed=1)
     x = torch.as_tensor(x_host, device=dev)
     c = torch.as_tensor(c_host, device=dev)
     out = torch.empty(B, device=dev)
@@ -684,7 +860,7 @@ def main():
         elapsed, avg_kern_s = float(t[0]), float(t[1])
 
     if rank == 0:
-        total_rows = B * world * args.steps
+        total_rows = G * args.steps
         flop_launch = flops_per_row() * B
         achieved = flop_launch / avg_kern_s / 1e12
         # ceiling for algorithmic FP32 FLOPs on the pipe the kernel actually uses: bf16/fp16 dense
@@ -706,12 +882,13 @@ def main():
         rec = {
             "metric": METRIC, "value": total_rows / elapsed, "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: x ~ 8-component Gaussian mixture (numpy rng(rank)), context ~ N(0, I); "
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I) (one global batch, 2^16-row "
+                    "seeded chunks); "
                     "random-init weights (nn.Linear default, torch seed 1234, last layer x3)",
             "config": {"workload": "BASELINE configs[2]: conditional RQ-spline coupling flow D=16 | C=32, K=8, "
                                    "L=8, H=[128,128], split 8, tanh; fused log_prob (naz_coupling_log_prob)",
-                       "batch_per_gpu": B, "global_batch": B * world,
+                       "batch_per_gpu": B, "global_batch": G,
                        "parallelism": f"dp{world} (independent row shards, no collective)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,

@@ -207,6 +207,11 @@ def _draws(params: Params) -> int:
     return params[0][0][0].shape[0]
 
 
+def _flat_layer_size(layer) -> int:
+    """Floats per draw of one layer's flat parameter row (_flat_layer)."""
+    return 1 + sum(w[0].numel() + b[0].numel() for (w, b) in layer)
+
+
 def _flat_layer(layer, P, dev):
     """F[p] = [0, W0, b0, W1, b1, ...] for one layer of a batched pytree: [P, size]."""
     parts = [torch.zeros((P, 1), device=dev, dtype=torch.float32)]
@@ -257,8 +262,10 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
     act = spec.activation
     width_sum = max(sum(pl.widths) for pl in plans)
 
-    def _chunks(P, rows):
-        per = max(1, min(P, 65535, rows_per_chunk // max(rows, 1)))
+    def _chunks(P, rows, max_draws=65535):
+        """Draw ranges per launch set: at most ``max_draws`` (the grid-z limit of the batched
+        launches) and ``rows_per_chunk`` budget units (~64 floats each) per chunk."""
+        per = max(1, min(P, max_draws, rows_per_chunk // max(rows, 1)))
         return [(p0, min(P, p0 + per)) for p0 in range(0, P, per)]
 
     def _pack(layer, plan, P):
@@ -488,9 +495,17 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         P = _draws(params)
         out = torch.empty((P, B), device=dev, dtype=torch.float32)
         run = _lp_chunk_const if (const_ctx and fold_context) else _lp_chunk
+        per_draw, max_draws = B * max(1, width_sum // 64), 65535
         if run is _lp_chunk_const and batch_layers and _same_structure():
             run = _lp_chunk_const2
-        for p0, p1 in _chunks(P, B * max(1, width_sum // 64)):
+            # its launches run over Q = L * P problems (grid z), and it holds every layer's
+            # flat parameters and pass-2 pack per draw: cap P and budget those bytes too
+            L = len(plans)
+            max_draws = max(1, 65535 // L)
+            rows2 = [blk[2] - blk[1] for blk in plans[0].hidden[1]]
+            pack = ops.made_packed_floats(len(rows2), (max(rows2) + 31) // 32, 0, D)
+            per_draw += (L * (pack + _flat_layer_size(params[0]))) // 64 + 1
+        for p0, p1 in _chunks(P, per_draw, max_draws):
             run([[(w[p0:p1], b[p0:p1]) for (w, b) in layer] for layer in params], out[p0:p1])
         return out
 

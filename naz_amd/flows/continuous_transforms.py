@@ -121,9 +121,17 @@ class _FFJORDCore:
         noise = self.noise if self.noise is not None else torch.randn(v.shape, device=v.device, dtype=torch.float32)
         packed = self._plan.packed()  # may re-resolve the mode: read desc only after it
         if self.solver == "dopri5":  # §8f rank 3: adaptive Dormand-Prince, per-16-row step control
+            nfe = self._nfe_buffer(v)
             y, ld = ops.cnf_integrate_dopri5(self._plan.desc, packed, v, noise, t0, t1, self.atol, self.rtol,
                                              self.max_steps, context=self._context, ld_out=ld_buf, ld_mode=ld_mode,
-                                             nfe=self._nfe_buffer(v))
+                                             nfe=nfe)
+            # a group that hit max_steps before t1 writes a negative count (cnf.hip): its state and
+            # log-det are from partway through the interval, so fail loudly (strict, the default)
+            if self.strict and nfe.numel() and bool((nfe < 0).any()):
+                bad = int((nfe < 0).sum())
+                raise RuntimeError(f"naz_amd CNF dopri5: {bad} of {nfe.numel()} 16-row groups reached max_steps="
+                                   f"{self.max_steps} before t1 (step size collapsed or non-finite state); "
+                                   "raise max_steps, loosen atol/rtol, or set strict=False to accept partial solves")
         else:
             y, ld = ops.cnf_integrate(self._plan.desc, packed, v, noise, t0, t1, self.steps,
                                       context=self._context, ld_out=ld_buf, ld_mode=ld_mode)
@@ -177,12 +185,13 @@ class FFJORDTransform(_FFJORDCore, TransformModule):
     bijective = True
 
     def __init__(self, net, input_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4, steps=8,
-                 max_steps=1000):
+                 max_steps=1000, strict=True):
         super().__init__()
         _check_solver(solver, steps)
         self.net, self.input_dim, self.steps = net, input_dim, int(steps)
         self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
         self.max_steps = int(max_steps)
+        self.strict = bool(strict)
         self.last_nfe = None
         self._plan = _CnfPlan(net)
         self._cached_logdet = None
@@ -224,7 +233,7 @@ class _ConditionedFFJORD(_FFJORDCore, Transform):
         return self.module.noise
 
     def __getattr__(self, name):  # solver settings live on the module
-        if name in ("solver", "atol", "rtol", "max_steps"):
+        if name in ("solver", "atol", "rtol", "max_steps", "strict"):
             return getattr(self.module, name)
         raise AttributeError(name)
 
@@ -234,12 +243,13 @@ class ConditionalFFJORDTransform(ConditionalTransformModule):
     monkey-patch of the vector field's ``forward``."""
 
     def __init__(self, net, input_dim, context_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4,
-                 steps=8, max_steps=1000):
+                 steps=8, max_steps=1000, strict=True):
         super().__init__()
         _check_solver(solver, steps)
         self.net, self.input_dim, self.context_dim, self.steps = net, input_dim, context_dim, int(steps)
         self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
         self.max_steps = int(max_steps)
+        self.strict = bool(strict)
         self._plan = _CnfPlan(net)
         self.noise: Optional[torch.Tensor] = None
 

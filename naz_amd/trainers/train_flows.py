@@ -118,25 +118,37 @@ class DataParallel:
 
 def nll_step(flow, x_b: torch.Tensor, y_b: Optional[torch.Tensor], optimizer, params: List[torch.Tensor],
              dp: DataParallel, global_batch: int, clip_val: Optional[float] = 1.0,
-             lambda_l1: float = 0.0) -> torch.Tensor:
+             lambda_l1: float = 0.0, micro_batch: Optional[int] = None) -> torch.Tensor:
     """One NLL training step on this rank's slice (x_b, y_b) of a global minibatch of
     ``global_batch`` rows (train_flows.py:194-213).  Returns the GLOBAL mean NLL (+ L1) as a
-    0-dim tensor on the device (no host sync)."""
+    0-dim tensor on the device (no host sync).
+
+    ``micro_batch``: the slice runs forward + backward in chunks of that many rows whose
+    gradients accumulate in ``.grad`` before the single all-reduce — the same gradient as one
+    pass over the slice (up to fp32 summation order), with activation memory bounded by the
+    chunk (a 2^23-row global batch on one GPU)."""
     optimizer.zero_grad(set_to_none=False)
-    lp = flow.log_prob(x_b, condition=y_b)
-    loss = -lp.sum() / global_batch
+    n = x_b.shape[0]
+    step = max(1, n if not micro_batch or micro_batch >= n else int(micro_batch))
+    loss = torch.zeros((), device=x_b.device)
     if lambda_l1 > 0.0:
         reg = 0.0
         for name, p in flow.named_parameters():
             if name.endswith("weight"):
                 reg = reg + lambda_l1 * p.abs().sum()
-        loss = loss + reg / dp.world  # every rank adds its share; the SUM reduce restores one copy
-    loss.backward()
+        part = reg / dp.world  # every rank adds its share; the SUM reduce restores one copy
+        part.backward()
+        loss = loss + part.detach()
+    for s in range(0, n, step):
+        cond = y_b if y_b is None or y_b.dim() == 1 else y_b[s:s + step]
+        part = -flow.log_prob(x_b[s:s + step], condition=cond).sum() / global_batch
+        part.backward()
+        loss = loss + part.detach()
     dp.all_reduce_grads(params)
     if clip_val is not None:
         nn.utils.clip_grad_norm_(params, clip_val)
     optimizer.step()
-    return dp.all_reduce_sum(loss.detach().clone())
+    return dp.all_reduce_sum(loss)
 
 
 def train(flow, x, y, opt=optim.Adam, lr=0.001, num_epochs=1024, train_frac=0.7, batch_frac=0.005,

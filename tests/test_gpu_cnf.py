@@ -281,3 +281,18 @@ def test_cnf_dopri5_flow_api_and_ragged():
     # rows 0..31 form the same two 16-row groups in both batches
     assert torch.equal(lp37[:32], lp[:32])
     assert nfe is None or int(nfe.min()) > 0
+
+
+def test_cnf_dopri5_max_steps_raises():
+    """A dopri5 solve that reaches max_steps before t1 returns a partial state; the transform
+    fails loudly (strict=True, the default) instead of handing it to log_prob."""
+    from naz_amd.flows import NormalizingFlow
+    rng = np.random.default_rng(5)
+    x = _cuda(rng.standard_normal((64, 4)) * 0.8)
+    c = _cuda(rng.standard_normal((64, 2)))
+    f = NormalizingFlow("cnf", None, 4, 2, [32, 32], 1, solver="dopri5", atol=1e-9, rtol=1e-9,
+                        max_steps=1).to(DEV)
+    with pytest.raises(RuntimeError, match="max_steps"):
+        f.log_prob(x, condition=c)
+    f.transforms[0].strict = False
+    assert f.log_prob(x, condition=c).shape == (64,)

@@ -23,7 +23,7 @@ from torch import nn
 from torch.distributions import Transform, constraints
 
 from .. import ops
-from ..nn import activation_name
+from ..nn import activation_name, cache_epoch
 from .transforms import ComposeTransformModule, ConditionalComposeTransformModule, ConditionalTransformModule, \
     TransformModule
 
@@ -100,7 +100,7 @@ class _CnfPlan:
 
     def packed(self):
         ps = [t for lin in self.net.linears() for t in (lin.weight, lin.bias)]
-        sig = tuple((p.data_ptr(), p._version) for p in ps)
+        sig = tuple((p.data_ptr(), p._version) for p in ps) + (cache_epoch(),)
         if sig != self._sig or self._packed is None:
             self.mode = self._resolve_mode()
             n = self.net

@@ -18,7 +18,7 @@ from torch import nn
 from torch.distributions import Normal
 
 from .. import ops
-from ..nn import activation_name
+from ..nn import activation_name, cache_epoch
 from ..utils import device
 from .continuous_transforms import continuous_free_form
 from .distributions import ConditionalTransformedDistribution, TransformedDistribution
@@ -84,7 +84,7 @@ class _FusedCoupling:
 
     def packed(self) -> torch.Tensor:
         ps = self.params()
-        sig = tuple((p.data_ptr(), p._version) for p in ps)
+        sig = tuple((p.data_ptr(), p._version) for p in ps) + (cache_epoch(),)
         if sig != self._sig or self._packed is None:
             D, C, S, K, H, act, lower, bound = self.shape
             self.mode = self._resolve_mode()

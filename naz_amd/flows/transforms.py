@@ -24,7 +24,7 @@ import torch.nn.functional as F
 
 from .. import autograd as ag
 from .. import ops
-from ..nn import (AutoRegressiveNN, ConditionalAutoRegressiveNN, ConditionalDenseNN, DenseNN)
+from ..nn import (AutoRegressiveNN, ConditionalAutoRegressiveNN, ConditionalDenseNN, DenseNN, cache_epoch)
 from ..utils import device, set_device
 
 __all__ = ["TransformModule", "ConditionalTransformModule", "ComposeTransformModule",
@@ -456,7 +456,7 @@ def _fused_made_forward(arn, v, context, ld_buf, ld_mode):
         return None
     nh = (max(arn.hidden_dims) + 31) // 32
     key = tuple((l.weight.data_ptr(), l.weight._version, l.bias.data_ptr(), l.bias._version, l.mask._version)
-                for l in layers)
+                for l in layers) + (cache_epoch(),)
     cache = arn.__dict__.get("_made_fwd")
     if cache is None or cache[0] != key:
         spec = MAFSpec(arn.input_dim, C, arn.hidden_dims, arn.act)

@@ -61,6 +61,22 @@ def create_mask(input_dim: int, context_dim: int, hidden_dims: Sequence[int], pe
     return masks, mask_skip
 
 
+# Weight-derived caches (masked weights, degree schedules, packed kernel images) are keyed on
+# (data_ptr, _version) of the tensors they come from plus this epoch.  An in-place write through
+# ``param.data`` does not bump ``_version``: call ``invalidate_caches()`` after one (io.load_state
+# and trainers.set_params do), or update weights with in-place ops under torch.no_grad().
+_CACHE_EPOCH = [0]
+
+
+def invalidate_caches() -> None:
+    """Drop every weight-derived cache (see _CACHE_EPOCH)."""
+    _CACHE_EPOCH[0] += 1
+
+
+def cache_epoch() -> int:
+    return _CACHE_EPOCH[0]
+
+
 class MaskedLinear(nn.Linear):
     """[pyro] nn.auto_reg_nn.MaskedLinear: F.linear(x, mask * W, b); mask is a buffer."""
 
@@ -78,7 +94,7 @@ class MaskedLinear(nn.Linear):
         passes of an autoregressive inverse while the weight is unchanged (version counter)."""
         if torch.is_grad_enabled() and self.weight.requires_grad:
             return self.weight * self.mask
-        key = (self.weight.data_ptr(), self.weight._version, self.mask.data_ptr(), self.mask._version)
+        key = (self.weight.data_ptr(), self.weight._version, self.mask.data_ptr(), self.mask._version, cache_epoch())
         if getattr(self, "_wm_key", None) != key:
             self._wm = (self.weight * self.mask).detach()
             self._wm_key = key
@@ -333,7 +349,7 @@ class ARInversePlan:
 
     def _cache_key(self):
         return tuple((l.weight.data_ptr(), l.weight._version, l.bias.data_ptr(), l.bias._version,
-                      l.mask.data_ptr(), l.mask._version) for l in self.arn.layers)
+                      l.mask.data_ptr(), l.mask._version) for l in self.arn.layers) + (cache_epoch(),)
 
     def _build(self):
         arn = self.arn
@@ -442,7 +458,7 @@ class ARInversePlan:
         arn = self.arn
         layers = list(arn.layers)
         key = tuple((l.mask.data_ptr(), l.mask._version) for l in layers) + (
-            arn.permutation.data_ptr(), arn.permutation._version)  # no device sync (graph capture)
+            arn.permutation.data_ptr(), arn.permutation._version, cache_epoch())  # no device sync (graph capture)
         if getattr(self, "_imap_key", None) == key:
             return self._imap
         cpu = dict(device="cpu", dtype=torch.float64)

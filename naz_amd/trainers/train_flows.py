@@ -23,7 +23,7 @@ import torch
 import torch.optim as optim
 from torch import nn
 
-__all__ = ["DataParallel", "get_params", "set_params", "nll_step", "train"]
+__all__ = ["DataParallel", "get_params", "set_params", "nll_step", "train", "train_lightning", "predict"]
 
 
 def _transforms(flow):
@@ -43,6 +43,8 @@ def get_params(flow) -> List[dict]:
 
 def set_params(flow, params, sample_idx: Optional[int] = None) -> None:
     """naz/trainers/train_flows.py:47-71."""
+    from ..nn import invalidate_caches
+    invalidate_caches()
     for i, t in enumerate(_transforms(flow)):
         if not isinstance(t, nn.Module):
             continue
@@ -222,3 +224,97 @@ def train(flow, x, y, opt=optim.Adam, lr=0.001, num_epochs=1024, train_frac=0.7,
     if not return_final and best_weights is not None:
         set_params(flow, best_weights)
     return flow, history, history_val, best_mse, best_epoch
+
+
+def train_lightning(flow, theta_train, condition_train, opt=optim.AdamW, lr=2e-3, lambda_l2=1e-5, batch_size=10240,
+                    num_epochs=600, seed: int = 0, group=None):
+    """naz/trainers/train_flows.py:244-278 without PyTorch-Lightning (not a dependency here):
+    the same loop its ``Learner`` defines — per epoch a shuffled pass in minibatches of
+    ``batch_size`` rows (DataLoader(shuffle=True), last batch partial), loss = -mean log_prob,
+    ``opt(params, lr, weight_decay=lambda_l2)``, no clipping (Lightning's default) — as the
+    data-parallel NLL step (one process per GPU under torch.distributed).  Returns the flow."""
+    dp = DataParallel(group)
+    params = _flow_parameters(flow)
+    dp.broadcast_params(params)
+    optimizer = opt(params, lr=lr, weight_decay=lambda_l2)
+    gen = torch.Generator().manual_seed(seed)
+    dev = next(iter(params)).device if params else theta_train.device
+    x = theta_train.to(dev)
+    y = condition_train.to(dev) if condition_train is not None else None
+    n = x.shape[0]
+    flow.train()
+    for _ in range(num_epochs):
+        order = torch.randperm(n, generator=gen).to(dev)
+        for s in range(0, n, batch_size):
+            idx = order[s:s + batch_size]
+            lo, hi = dp.shard(len(idx))
+            mine = idx[lo:hi]
+            nll_step(flow, x[mine], y[mine] if y is not None else None, optimizer, params, dp, len(idx),
+                     clip_val=None)
+    flow.flow_dist.clear_cache()
+    return flow
+
+
+def _draw_params(posterior_samples, l: int, names: List[str], p0: int, p1: int, dev):
+    """One flow layer's (W, b) pairs for draws [p0, p1) from naz's posterior dict
+    (keys ``flow_{l}_{name}``, a leading draw axis; bflow.py:66-78 / train_flows.py:414)."""
+    out = []
+    for i in range(len(names) // 2):
+        w = torch.as_tensor(posterior_samples[f"flow_{l}_nn.layers.{i}.weight"][p0:p1])
+        b = torch.as_tensor(posterior_samples[f"flow_{l}_nn.layers.{i}.bias"][p0:p1])
+        out.append((w.to(dev, torch.float32), b.to(dev, torch.float32)))
+    return out
+
+
+def predict(flow, cond, posterior_samples, Nsamples, seed: Optional[int] = None,
+            rows_per_launch: int = 1 << 25):
+    """naz/trainers/train_flows.py:384-422: ``Nsamples`` draws of theta ~ p(theta | cond) under
+    every posterior sample of the flow parameters -> numpy [N_posterior, Nsamples, D].
+
+    The reference loops over posterior samples, ``set_params`` then ``flow.sample(cond,
+    [Nsamples])`` (a positional ``cond`` that its conditional ``sample`` asserts against; the
+    evident intent ``sample([Nsamples], condition=cond)`` is what runs here).  For naz's affine
+    MAF (``maf``, the Bayesian flows of bflow.py) all draws of a chunk run together: one batched
+    masked-MADE forward + affine launch per layer over (draws × samples) — the fused
+    ``naz_made_affine_fwd`` kernel when the shape fits it, else ``naz_linear_act_batched`` GEMMs
+    (``flows.bflow_maf.sampler_batched``).  Other flow types take the reference's per-draw loop
+    over the HIP sampling path.  The flow's own parameters are left at the last posterior sample,
+    as the reference's loop leaves them."""
+    import numpy as np
+    key0 = "flow_0_nn.layers.0.weight"
+    P = len(posterior_samples[key0])
+    if getattr(flow, "flow_type", None) == "maf" and flow.embedding_net.__class__.__name__ == "Identity":
+        from ..flows import bflow_maf as BM
+        ts = list(flow.flow_dist.transforms)
+        arn0 = ts[0].nn
+        dev = arn0.layers[0].weight.device
+        spec = BM.MAFSpec(arn0.input_dim, arn0.context_dim, arn0.hidden_dims, arn0.act)
+        _, _, masks, _, perms = BM.torch_to_jax(flow)
+        D = arn0.input_dim
+        ctx = None
+        if arn0.context_dim:
+            ctx = torch.as_tensor(cond, dtype=torch.float32, device=dev).reshape(-1)
+        bm = BM.make_normalizing_flow(spec, torch.zeros((1, D), device=dev), masks, [None] * len(ts), perms,
+                                      context=ctx)
+        names = [n for n, _ in ts[0].named_parameters()]
+        out = np.empty((P, int(Nsamples), D), dtype=np.float32)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(int(torch.randint(0, 2 ** 62, ()).item()) if seed is None else int(seed))
+        per = max(1, rows_per_launch // max(int(Nsamples), 1))
+        for p0 in range(0, P, per):
+            p1 = min(P, p0 + per)
+            params = [_draw_params(posterior_samples, l, names, p0, p1, dev) for l in range(len(ts))]
+            y = bm["sampler_batched"](params, gen, int(Nsamples))[0]
+            if flow.bounds is not None:
+                from ..flows.transforms import inverse_bounding_transform
+                b = flow._bounds_dev(y)
+                y = inverse_bounding_transform(y, b["low"], b["high"])
+            out[p0:p1] = y.cpu().numpy()
+        set_params(flow, posterior_samples, sample_idx=P - 1)
+        return out
+    samples = []
+    for i in range(P):
+        set_params(flow, posterior_samples, sample_idx=i)
+        with torch.no_grad():
+            samples.append(flow.sample([int(Nsamples)], condition=cond).cpu().numpy())
+    return np.array(samples)

@@ -1,0 +1,210 @@
+"""GPU: the config-3/4 NLL training step end to end — full-size flow
+gradient parity, micro-batching, data parallelism over two ranks on one device (gloo), the
+``naz`` import-compatible trainers, and posterior-predictive ``predict``."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import naz_oracle as O
+from tests.parity import assert_parity, grad_floor
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from naz_amd import _lib
+    _lib.lib()
+
+
+def _np(t):
+    return t.detach().double().cpu().numpy()
+
+
+CFG3 = dict(flow_type="nsc", D=16, C=32, hidden=[128, 128], L=8, K=8, split=8)
+
+
+def _cfg3_flow(state):
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    f = NormalizingFlow("nsc", None, 16, 32, [128, 128], 8, 8, 8)
+    fio.load_state(f, state)
+    return f
+
+
+def _oracle_grads(spec, state, x, ctx, dt):
+    st = {k: (torch.as_tensor(np.asarray(v)) if np.asarray(v).dtype.kind in "iu" else
+              torch.as_tensor(np.asarray(v)).to(dt).requires_grad_(True)) for k, v in state.items()}
+    of = O.build_flow(spec, st, dt)
+    lp = of.log_prob(torch.as_tensor(x).to(dt), torch.as_tensor(ctx).to(dt))
+    keys = [k for k in st if st[k].requires_grad]
+    return lp.detach(), dict(zip(keys, torch.autograd.grad(-lp.mean(), [st[k] for k in keys])))
+
+
+def test_config3_full_flow_gradient_vs_oracle():
+    """BASELINE configs[2]/[3] flow at full depth (L=8, D=16|C=32, K=8, H=[128,128]) on 4096
+    rows: every parameter's NLL gradient against the oracle's float64 autograd."""
+    from naz_amd.flows import io as fio
+    state = {k: v.numpy() for k, v in O.random_state(CFG3, seed=1234).items()}
+    x = O.gaussian_mixture(4096, 16, seed=0)
+    c = O.context_normal(4096, 32, seed=1)
+    f = _cfg3_flow(state)
+    lp = f.log_prob(torch.as_tensor(x, device=DEV), condition=torch.as_tensor(c, device=DEV))
+    (-lp.mean()).backward()
+    lp64, g64 = _oracle_grads(CFG3, state, x, c, torch.float64)
+    lp32, g32 = _oracle_grads(CFG3, state, x, c, torch.float32)
+    assert_parity(_np(lp), _np(lp64), _np(lp32), what="config-3 L=8 walk log_prob")
+    params = fio.named_state_params(f)
+    assert set(params) == set(g64)
+    for k, p in params.items():
+        g = _np(g64[k])
+        assert_parity(_np(p.grad), g, _np(g32[k]), what=f"config-3 L=8 d/d{k}", floor=grad_floor(g),
+                      count_factor=None)
+
+
+def test_nll_step_micro_batch_matches_one_pass():
+    """nll_step(micro_batch=m) accumulates the same gradient as one pass over the slice."""
+    from naz_amd.trainers import DataParallel, nll_step
+    from naz_amd.trainers.train_flows import _flow_parameters
+    state = {k: v.numpy() for k, v in O.random_state(CFG3, seed=7).items()}
+    x = torch.as_tensor(O.gaussian_mixture(6000, 16, seed=3), device=DEV)
+    c = torch.as_tensor(O.context_normal(6000, 32, seed=4), device=DEV)
+    grads = []
+    for mb in (None, 2048):
+        f = _cfg3_flow(state)
+        f.set_fused(False)
+        ps = _flow_parameters(f)
+        opt = torch.optim.SGD(ps, lr=0.0)
+        nll_step(f, x, c, opt, ps, DataParallel(), 6000, clip_val=None, micro_batch=mb)
+        grads.append([p.grad.detach().clone() for p in ps])
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=1e-6 * float(b.abs().max()) + 1e-12)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _dp_steps(rank, world, steps=3):
+    """`steps` nll_steps of the HIP nsc flow on this rank's slice of fixed global batches."""
+    from naz_amd.trainers import DataParallel, nll_step
+    from naz_amd.trainers.train_flows import _flow_parameters
+    state = {k: v.numpy() for k, v in O.random_state(CFG3, seed=99).items()}
+    f = _cfg3_flow(state)
+    if rank > 0:  # replicas start different: the DP path must broadcast rank 0's weights
+        with torch.no_grad():
+            for p in f.parameters():
+                p.add_(0.01)
+    dp = DataParallel()
+    ps = _flow_parameters(f)
+    dp.broadcast_params(ps)
+    opt = torch.optim.Adam(ps, lr=1e-3)
+    G = 3001  # ragged over 2 ranks
+    x = torch.as_tensor(O.gaussian_mixture(G * steps, 16, seed=5), device=DEV)
+    c = torch.as_tensor(O.context_normal(G * steps, 32, seed=6), device=DEV)
+    losses = []
+    for s in range(steps):
+        lo, hi = dp.shard(G)
+        rows = slice(s * G + lo, s * G + hi)
+        losses.append(float(nll_step(f, x[rows], c[rows], opt, ps, dp, G, clip_val=1.0)))
+    return losses, [p.detach().cpu().numpy() for p in ps]
+
+
+def _dp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank,) + _dp_steps(rank, world))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_two_ranks_on_one_gpu_match_single_process():
+    """Config 4's DP step with the real HIP flow: two gloo ranks sharing cuda:0, each on its
+    ragged slice, one flat gradient all-reduce, clip, Adam == one process on the whole batch;
+    the replicas stay bitwise identical."""
+    import torch.multiprocessing as mp
+    ref_losses, ref_params = _dp_steps(0, 1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, losses, params in res:
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        for a, b in zip(params, ref_params):
+            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6)
+    for a, b in zip(res[0][2], res[1][2]):
+        assert np.array_equal(a, b), "replicas diverged"
+
+
+def test_naz_compat_front_end_runs_unchanged():
+    """The import paths and calls of examples/papers/2506.05657/train_mle_all_data.py:1-20,
+    62-89 (at a toy size): construction, train(), sample(), log_prob; train_lightning too."""
+    from naz.flows.flow import NormalizingFlow
+    from naz.trainers.train_flows import train, train_lightning
+    from naz.utils import set_device
+    rng = np.random.default_rng(0)
+    lam = rng.standard_normal((2000, 2)).astype(np.float32)
+    th = (lam[:, :1] + 0.3 * rng.standard_normal((2000, 2))).astype(np.float32)
+    flow = NormalizingFlow('maf', None, 2, 2, [32, 32], 3)
+    model, history, history_val, best_mse, best_epoch = train(flow, set_device(th), set_device(lam), train_frac=0.89,
+                                                              patience=64, lr=1e-3, min_lr=1e-9, num_epochs=2,
+                                                              batch_frac=0.05, lr_decay=0.5, verbose=False)
+    assert len(history_val) == 2 and np.isfinite(best_mse)
+    s = model.sample([500], condition=set_device(lam[0]))
+    assert s.shape == (500, 2) and bool(torch.isfinite(s).all())
+    lp = model.log_prob(set_device(th[:64]), condition=set_device(lam[:64]))
+    assert lp.shape == (64,) and bool(torch.isfinite(lp).all())
+    before = [p.detach().clone() for p in model.parameters()]
+    train_lightning(model, set_device(th), set_device(lam), num_epochs=1, batch_size=512)
+    assert any(not torch.equal(a, p.detach()) for a, p in zip(before, model.parameters()))
+
+
+def test_predict_batched_matches_oracle_per_draw():
+    """predict (train_flows.py:384-422) for a maf: all posterior draws in one batched sampler
+    call; draw p's samples equal the oracle flow under draw p's weights applied to the same
+    base draws z (regenerated from the seed)."""
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    from naz_amd.trainers import predict
+    spec = dict(flow_type="maf", D=2, C=2, hidden=[48, 48], L=4)
+    state = {k: v.numpy() for k, v in O.random_state(spec, seed=3).items()}
+    f = NormalizingFlow("maf", None, 2, 2, [48, 48], 4)
+    fio.load_state(f, state)
+    P, N = 5, 700
+    rng = np.random.default_rng(1)
+    post = {}
+    for l in range(4):
+        for i in range(3):
+            for n in ("weight", "bias"):
+                v = state[f"layers.{l}.nn.layers.{i}.{n}"]
+                post[f"flow_{l}_nn.layers.{i}.{n}"] = (v * (1 + 0.2 * rng.uniform(-1, 1, (P,) + v.shape))).astype(
+                    np.float32)
+    cond = np.array([0.4, -1.1], dtype=np.float32)
+    y = predict(f, torch.as_tensor(cond, device=DEV), post, N, seed=17)
+    assert y.shape == (P, N, 2)
+    g = torch.Generator(device=DEV).manual_seed(17)
+    z = torch.randn((P, N, 2), device=DEV, generator=g).double().cpu()
+    for p in range(P):
+        st = dict(state)
+        for k, v in post.items():
+            l, rest = k[5:].split("_", 1)
+            st[f"layers.{l}.{rest}"] = v[p]
+        of = O.build_flow(spec, st, torch.float64)
+        ref = of.sample_from_base(z[p], torch.as_tensor(cond).double().expand(N, 2)).numpy()
+        np.testing.assert_allclose(y[p], ref, rtol=1e-4, atol=2e-4, err_msg=f"draw {p}")

@@ -50,10 +50,8 @@ def set_params(flow, params, sample_idx: Optional[int] = None) -> None:
             continue
         for name, param in t.named_parameters():
             with torch.no_grad():
-                if sample_idx is None:
-                    param.copy_(params[i][name])
-                else:
-                    param.copy_(params[f"flow_{i}_{name}"][sample_idx])
+                src = params[i][name] if sample_idx is None else params[f"flow_{i}_{name}"][sample_idx]
+                param.copy_(torch.as_tensor(src))
 
 
 def _flow_parameters(flow) -> List[torch.Tensor]:

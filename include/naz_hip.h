@@ -181,6 +181,13 @@ int naz_colsum(const float* A, int64_t lda, int64_t M, int N, float* out, void* 
 /* gpre = gy * act'(pre) computed from the post-activation y (tanh, relu, softplus, sigmoid) */
 int naz_act_bwd(const float* gy, int64_t ldg, const float* y, int64_t ldy, float* gpre, int64_t ldp, int64_t M, int N,
                 int act, void* stream);
+/* MC dropout on a conditioner activation [M, N] (naz transforms.py:29-95, the Dropout
+ * conditioners behind dropout_p; mcdpflow.py:39-56 samples with them active):
+ *   y[m, n] = keep(seed, m, n) ? x[m, n] / (1 - p) : 0,   P(keep) = 1 - p,  0 <= p < 1.
+ * keep is a hash of (seed, m, n): the backward applies the same call (same seed) to the
+ * gradient. y may alias x.                                                                */
+int naz_dropout(const float* x, int64_t ldx, float* y, int64_t ldy, int64_t M, int N, float p, uint64_t seed,
+                void* stream);
 /* g_z[r, i] = -z[r, i] * g_lp[r]   (VJP of naz_base_log_prob)                             */
 int naz_base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float* g_z, int64_t ldgz, int64_t B, int D,
                           void* stream);

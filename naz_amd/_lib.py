@@ -61,6 +61,7 @@ SIGNATURES = {
     "naz_colsum": (C.c_int, [_vp, _i64, _i64, _i, _vp, _vp]),
     "naz_act_bwd": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i, _i, _vp]),
     "naz_base_log_prob_bwd": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _i64, _i, _vp]),
+    "naz_dropout": (C.c_int, [_vp, _i64, _vp, _i64, _i64, _i, C.c_float, C.c_uint64, _vp]),
     "naz_cnf_supported": (C.c_int, [C.POINTER(CnfDesc)]),
     "naz_cnf_param_count": (C.c_int64, [C.POINTER(CnfDesc)]),
     "naz_cnf_packed_bytes": (C.c_int64, [C.POINTER(CnfDesc)]),

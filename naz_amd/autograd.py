@@ -144,39 +144,45 @@ class ChainFn(Function):
     [B, H] gradient (values identical to the LinearActFn-per-layer walk)."""
 
     @staticmethod
-    def forward(ctx, x, context, act: str, *wb):
+    def forward(ctx, x, context, act: str, drop, *wb):
         n = len(wb) // 2
-        hs = []
+        hs, ins = [], []  # post-activation (act') / next layer's input (post-dropout)
         h = x
         for i in range(n):
             a = act if i < n - 1 else "identity"
-            h = ops.linear_act(x if i == 0 else h, wb[2 * i], wb[2 * i + 1], a,
+            h = ops.linear_act(x if i == 0 else ins[-1], wb[2 * i], wb[2 * i + 1], a,
                                context=context if i == 0 else None)
             hs.append(h)
-        ctx.act, ctx.n = act, n
+            if i < n - 1:
+                ins.append(ops.dropout(h, drop[0], drop[1][i]) if drop is not None else h)
+        ctx.act, ctx.n, ctx.drop = act, n, drop
         ctx.has_bias = [wb[2 * i + 1] is not None for i in range(n)]
-        ctx.save_for_backward(x, context, *[wb[2 * i] for i in range(n)], *hs[:-1])
+        extra = ins if drop is not None else []
+        ctx.save_for_backward(x, context, *[wb[2 * i] for i in range(n)], *hs[:-1], *extra)
         return hs[-1]
 
     @staticmethod
     def backward(ctx, g_y):
-        n, act = ctx.n, ctx.act
+        n, act, drop = ctx.n, ctx.act, ctx.drop
         saved = ctx.saved_tensors
         x, c = saved[0], saved[1]
         Ws = saved[2:2 + n]
-        hs = saved[2 + n:]
+        hs = saved[2 + n:2 + 2 * n - 1]
+        ins = saved[2 + 2 * n - 1:] if drop is not None else hs
         grads = [None] * (2 * n)
         gpre = g_y.contiguous()
         g_x = g_c = None
         for i in reversed(range(n)):
             W = Ws[i]
-            inp = x if i == 0 else hs[i - 1]
+            inp = x if i == 0 else ins[i - 1]
             ci = c if i == 0 else None
-            gW, gb = _param_grads(gpre, inp, ci, W, _needs(ctx, 3 + 2 * i), ctx.has_bias[i] and _needs(ctx, 4 + 2 * i))
+            gW, gb = _param_grads(gpre, inp, ci, W, _needs(ctx, 4 + 2 * i), ctx.has_bias[i] and _needs(ctx, 5 + 2 * i))
             grads[2 * i], grads[2 * i + 1] = gW, gb
             Cd = 0 if ci is None else ci.shape[-1]
             if i > 0:
                 gpre = ops.gemm_dact(gpre, W, hs[i - 1], act)  # (gpre · W) ⊙ act'(h_{i-1})
+                if drop is not None:  # ⊙ the forward's dropout mask / (1 - p)
+                    ops.dropout(gpre, drop[0], drop[1][i - 1], out=gpre)
             else:
                 if x is not None and _needs(ctx, 0):
                     g_x = ops.gemm(gpre, W[:, Cd:])
@@ -186,13 +192,13 @@ class ChainFn(Function):
                         g_c = ops.gemm(gpre, Wc)
                     else:
                         g_c = ops.gemm(ops.colsum(gpre).reshape(1, -1), Wc).reshape(c.shape)
-        return (g_x, g_c, None, *grads)
+        return (g_x, g_c, None, None, *grads)
 
 
-def chain(x, weights, biases, act: str, context=None):
-    """Conditioner forward recorded as one ChainFn node (see there)."""
+def chain(x, weights, biases, act: str, context=None, drop=None):
+    """Conditioner forward recorded as one ChainFn node (see there); ``drop`` = (p, seeds)."""
     wb = [t for pair in zip(weights, biases) for t in pair]
-    return ChainFn.apply(x, context, act, *wb)
+    return ChainFn.apply(x, context, act, drop, *wb)
 
 
 class RqsFn(Function):

@@ -174,6 +174,13 @@ int naz_act_bwd(const float* gy, int64_t ldg, const float* y, int64_t ldy, float
   return act_bwd(gy, ldg, y, ldy, gpre, ldp, M, N, act, as_stream(stream));
 }
 
+int naz_dropout(const float* x, int64_t ldx, float* y, int64_t ldy, int64_t M, int N, float p, uint64_t seed,
+                void* stream) {
+  if (M < 0 || N < 0) return set_error("naz_dropout: negative shape");
+  if (!(p >= 0.f && p < 1.f)) return set_error("naz_dropout: p must be in [0, 1)");
+  return dropout(x, ldx, y, ldy, M, N, p, seed, as_stream(stream));
+}
+
 int naz_base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float* g_z, int64_t ldgz, int64_t B, int D,
                           void* stream) {
   return base_log_prob_bwd(z, ldz, g_lp, g_z, ldgz, B, D, as_stream(stream));

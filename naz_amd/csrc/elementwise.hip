@@ -134,6 +134,42 @@ int base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float* g_z
   return check_launch("base_log_prob_bwd_kernel");
 }
 
+// MC dropout on a conditioner activation (naz ConditionalAutoRegressiveNNDropout /
+// ConditionalDenseNNDropout, transforms.py:29-95: nn.Dropout(p) after every hidden activation):
+//   y[m, n] = keep(seed, m, n) ? x[m, n] / (1 - p) : 0,   P(keep) = 1 - p.
+// keep is a counter-based hash of (seed, m, n) — no mask tensor in HBM, and the backward
+// (the same call on the gradient) regenerates exactly the forward's mask.  In place allowed.
+NAZ_DEV uint32_t drop_hash(uint64_t seed, int64_t m, int n) {
+  uint64_t h = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(m + 1)) ^ (0xC2B2AE3D27D4EB4Full * (uint64_t)(n + 1));
+  h ^= h >> 33;  // murmur3 fmix64
+  h *= 0xFF51AFD7ED558CCDull;
+  h ^= h >> 33;
+  h *= 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 33;
+  return (uint32_t)h;
+}
+
+__global__ void dropout_kernel(const float* __restrict__ x, int64_t ldx, float* y, int64_t ldy, int64_t M, int N,
+                               uint32_t thresh, float scale, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * N) return;
+  const int64_t m = i / N;
+  const int n = (int)(i - m * N);
+  const float v = x[m * ldx + n];
+  y[m * ldy + n] = drop_hash(seed, m, n) >= thresh ? v * scale : 0.f;
+}
+
+int dropout(const float* x, int64_t ldx, float* y, int64_t ldy, int64_t M, int N, float p, uint64_t seed,
+            hipStream_t s) {
+  if (M == 0 || N == 0) return 0;
+  const double t = (double)p * 4294967296.0;
+  const uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  const float scale = p >= 1.f ? 0.f : 1.f / (1.f - p);
+  hipLaunchKernelGGL(dropout_kernel, dim3(blocks_for(M * N)), dim3(256), 0, s, x, ldx, y, ldy, M, N, thresh, scale,
+                     seed);
+  return check_launch("dropout_kernel");
+}
+
 int affine_ar(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy,
               float* ld, int ld_mode, int64_t B, int D, hipStream_t s) {
   if (B == 0) return 0;

@@ -57,6 +57,8 @@ int affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, in
 int colsum(const float* A, int64_t lda, int64_t M, int N, float* out, hipStream_t s);
 int act_bwd(const float* gy, int64_t ldg, const float* y, int64_t ldy, float* gp, int64_t ldp, int64_t M, int N, int act,
             hipStream_t s);
+int dropout(const float* x, int64_t ldx, float* y, int64_t ldy, int64_t M, int N, float p, uint64_t seed,
+            hipStream_t s);
 int base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float* g_z, int64_t ldgz, int64_t B, int D,
                       hipStream_t s);
 

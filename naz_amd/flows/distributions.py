@@ -68,8 +68,11 @@ class TransformedDistribution:
         lp = ag.base_log_prob(y)
         return lp if acc is None else lp + acc
 
+    def _fused_ok(self) -> bool:
+        return self._fused is not None and self._fused.usable()
+
     def _log_prob_into(self, y: torch.Tensor, lp: torch.Tensor, bounds=None) -> torch.Tensor:
-        if self._fused is not None:
+        if self._fused_ok():
             return self._fused.log_prob(y, self._context, bounds=bounds, out=lp)
         if bounds is not None:
             y, lj = ops.bounding_fwd(y, bounds["low"], bounds["high"])
@@ -87,7 +90,7 @@ class TransformedDistribution:
         return self._log_prob_into(y, lp, bounds).reshape(lead)
 
     def _transform_z(self, z: torch.Tensor, bounds=None) -> torch.Tensor:
-        if self._fused is not None:
+        if self._fused_ok():
             y, _ = self._fused.sample(z, self._context, bounds=bounds)
             return y
         ld = torch.zeros(z.shape[0], device=z.device, dtype=torch.float32)

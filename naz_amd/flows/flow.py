@@ -71,6 +71,11 @@ class _FusedCoupling:
         r16 = ops.coupling_desc(D, C, S, K, len(self.layers), H, act, lower, bound, "f16x3r16")
         return "f16x3r16" if ops.coupling_supported(r16) else "f16x3"
 
+    def usable(self) -> bool:
+        """False while a conditioner's MC dropout is active (train mode, dropout_p > 0): the
+        fused kernel has no dropout, so the per-layer kernels run."""
+        return not any(t.nn.dropout_active() for t in self.layers)
+
     def params(self) -> List[torch.Tensor]:
         out = []
         for t in self.layers:

@@ -447,7 +447,8 @@ def _fused_made_forward(arn, v, context, ld_buf, ld_mode):
     None otherwise (the per-GEMM path runs)."""
     from .bflow_maf import MAFSpec, made_pack_map
     layers = list(arn.layers)
-    if (v.dim() != 2 or arn.output_multiplier != 2 or 2 * arn.input_dim > 32 or arn.act not in ("tanh", "relu")
+    if (v.dim() != 2 or arn.dropout_active() or arn.output_multiplier != 2 or 2 * arn.input_dim > 32
+            or arn.act not in ("tanh", "relu")
             or max(arn.hidden_dims) > 160 or ld_mode == ops.LD_PERDIM or v.requires_grad
             or (torch.is_grad_enabled() and any(p.requires_grad for p in arn.parameters()))):
         return None
@@ -618,22 +619,26 @@ def _hidden(hidden_dim):
 
 
 def _unsupported(use_batchnorm, dropout_p):
+    """use_batchnorm is rejected; returns the conditioners' dropout probability (naz's
+    *Dropout conditioners when dropout_p is not None, transforms.py:141-147,178-184,224-227)."""
     if use_batchnorm:
         raise NotImplementedError("naz_amd: use_batchnorm is outside the log_prob hot path (SURVEY.md §8)")
-    if dropout_p is not None:
-        raise NotImplementedError("naz_amd: MC-dropout conditioners are SURVEY.md §8f rank 2, not yet built")
+    if dropout_p is not None and not 0.0 <= float(dropout_p) < 1.0:
+        raise ValueError("dropout_p must be in [0, 1)")
+    return 0.0 if dropout_p is None else float(dropout_p)
 
 
 def masked_affine_autoregressive(theta_dim, condition_dim, hidden_dim, num_layers, activation=nn.Tanh(),
                                  use_batchnorm=False, random_mask=True, random_perm=False, dropout_p=None):
     """naz/flows/transforms.py:133-160."""
-    _unsupported(use_batchnorm, dropout_p)
+    p = _unsupported(use_batchnorm, dropout_p)
     transforms, nets = [], []
     for _ in range(num_layers):
         perm = None if random_mask else torch.arange(theta_dim)
         arn = (ConditionalAutoRegressiveNN(theta_dim, condition_dim, _hidden(hidden_dim), nonlinearity=activation,
-                                           permutation=perm) if condition_dim > 0 else
-               AutoRegressiveNN(theta_dim, _hidden(hidden_dim), nonlinearity=activation, permutation=perm))
+                                           permutation=perm, dropout_p=p) if condition_dim > 0 else
+               AutoRegressiveNN(theta_dim, _hidden(hidden_dim), nonlinearity=activation, permutation=perm,
+                                dropout_p=p))
         nets.append(arn)
         t = ConditionalAffineAutoregressive(arn) if condition_dim > 0 else AffineAutoregressive(arn)
         transforms.append(t)
@@ -647,7 +652,7 @@ def neural_spline_autoregressive(theta_dim, condition_dim, hidden_dim, num_layer
                                  activation=nn.Tanh(), use_batchnorm=False, random_mask=True, random_perm=False,
                                  dropout_p=None):
     """naz/flows/transforms.py:165-198."""
-    _unsupported(use_batchnorm, dropout_p)
+    p = _unsupported(use_batchnorm, dropout_p)
     if order != "quadratic":
         raise NotImplementedError("naz_amd: only order='quadratic' (naz's default) is implemented")
     paramdim = [count_bins, count_bins, count_bins - 1]
@@ -655,9 +660,10 @@ def neural_spline_autoregressive(theta_dim, condition_dim, hidden_dim, num_layer
     for _ in range(num_layers):
         perm = None if random_mask else torch.arange(theta_dim)
         arn = (ConditionalAutoRegressiveNN(theta_dim, condition_dim, _hidden(hidden_dim), param_dims=paramdim,
-                                           nonlinearity=activation, permutation=perm) if condition_dim > 0 else
+                                           nonlinearity=activation, permutation=perm, dropout_p=p)
+               if condition_dim > 0 else
                AutoRegressiveNN(theta_dim, _hidden(hidden_dim), param_dims=paramdim, nonlinearity=activation,
-                                permutation=perm))
+                                permutation=perm, dropout_p=p))
         nets.append(arn)
         t = (ConditionalSplineAutoregressive(theta_dim, arn, count_bins=count_bins, order=order)
              if condition_dim > 0 else SplineAutoregressive(theta_dim, arn, count_bins=count_bins, order=order))
@@ -672,8 +678,10 @@ def neural_spline_coupling(theta_dim, condition_dim, hidden_dim, num_layers, cou
                            order="quadratic", activation=nn.Tanh(), use_batchnorm=False, random_perm=False,
                            dropout_p=None, identity=False):
     """naz/flows/transforms.py:201-236 (intent): DenseNN hypernet input cat([ctx, x1]),
-    param_dims [(D-s)K, (D-s)K, (D-s)(K-1)], SplineCoupling per layer."""
-    _unsupported(use_batchnorm, dropout_p)
+    param_dims [(D-s)K, (D-s)K, (D-s)(K-1)], SplineCoupling per layer.  dropout_p: the
+    ConditionalDenseNNDropout intent (the reference's _forward indexes an undefined
+    ``self.dropout_layers[i]``, transforms.py:82): dropout after every hidden activation."""
+    p = _unsupported(use_batchnorm, dropout_p)
     if order != "quadratic":
         raise NotImplementedError("naz_amd: only order='quadratic' (naz's default) is implemented")
     Dt = theta_dim - split_dim
@@ -681,8 +689,8 @@ def neural_spline_coupling(theta_dim, condition_dim, hidden_dim, num_layers, cou
     transforms, nets = [], []
     for _ in range(num_layers):
         net = (ConditionalDenseNN(split_dim, condition_dim, _hidden(hidden_dim), param_dims=param_dims,
-                                  nonlinearity=activation) if condition_dim > 0 else
-               DenseNN(split_dim, _hidden(hidden_dim), param_dims=param_dims, nonlinearity=activation))
+                                  nonlinearity=activation, dropout_p=p) if condition_dim > 0 else
+               DenseNN(split_dim, _hidden(hidden_dim), param_dims=param_dims, nonlinearity=activation, dropout_p=p))
         nets.append(net)
         t = (ConditionalSplineCoupling(theta_dim, split_dim, net, count_bins=count_bins, order=order,
                                        identity=identity) if condition_dim > 0 else

@@ -112,14 +112,19 @@ def _slices(param_dims: Sequence[int]):
 _CHAIN_NODE = os.environ.get("NAZ_CHAIN_NODE", "1") != "0"
 
 
-def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Tensor], masked: bool) -> torch.Tensor:
+def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Tensor], masked: bool,
+               drop=None) -> torch.Tensor:
     """The conditioner pass; recorded for autograd (HIP backward kernels) when grad mode is on
-    and a weight, the input or the context requires grad."""
+    and a weight, the input or the context requires grad.  ``drop`` = (p, seeds): MC dropout
+    after every hidden activation (naz_dropout, one seed per hidden layer)."""
     n = len(layers)
     grad = ag.params_require_grad(layers) or ag.tensor_requires_grad(x, context)
-    if grad and n >= 2 and x is not None and _CHAIN_NODE:  # one autograd node, act' fused into dX
+    if grad and n >= 2 and x is not None and (_CHAIN_NODE or drop is not None):
+        # one autograd node, act' fused into dX (and the dropout mask re-applied to it)
         ws = [layer.masked_weight() if masked else layer.weight for layer in layers]
-        return ag.chain(x, ws, [layer.bias for layer in layers], f_name, context=context)
+        return ag.chain(x, ws, [layer.bias for layer in layers], f_name, context=context, drop=drop)
+    if grad and drop is not None:
+        raise NotImplementedError("naz_amd: dropout under autograd needs a conditioner with hidden layers and an input")
     lin = ag.linear_act if grad else ops.linear_act
     h = None
     for i, layer in enumerate(layers):
@@ -129,15 +134,38 @@ def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Ten
             h = lin(x, w, layer.bias, act, context=context)
         else:
             h = lin(h, w, layer.bias, act)
+        if drop is not None and i < n - 1:
+            h = ops.dropout(h, drop[0], drop[1][i], out=h)
     return h
 
 
-class ConditionalDenseNN(nn.Module):
+class _DropoutMixin:
+    """naz's MC-dropout conditioners (ConditionalAutoRegressiveNNDropout /
+    ConditionalDenseNNDropout, naz/flows/transforms.py:29-95): nn.Dropout(dropout_p) after every
+    hidden activation, active in train mode only (torch semantics).  Each conditioner pass draws
+    fresh masks: one 64-bit seed per hidden layer from torch's CPU generator (so
+    torch.manual_seed makes a run reproducible); the kernel hashes (seed, row, column)."""
+
+    dropout_p = 0.0
+
+    def dropout_active(self) -> bool:
+        return bool(self.dropout_p) and self.training
+
+    def _drop_args(self):
+        if not self.dropout_active():
+            return None
+        n_hidden = len(self.layers) - 1
+        seeds = torch.randint(0, 2 ** 62, (max(n_hidden, 1),), dtype=torch.int64).tolist()
+        return float(self.dropout_p), seeds
+
+
+class ConditionalDenseNN(_DropoutMixin, nn.Module):
     """[pyro] nn/dense_nn.py::ConditionalDenseNN — input cat([context, x])."""
 
     def __init__(self, input_dim: int, context_dim: int, hidden_dims: Sequence[int],
-                 param_dims: Sequence[int] = (1, 1), nonlinearity: nn.Module = nn.ReLU()):
+                 param_dims: Sequence[int] = (1, 1), nonlinearity: nn.Module = nn.ReLU(), dropout_p: float = 0.0):
         super().__init__()
+        self.dropout_p = float(dropout_p or 0.0)
         self.input_dim, self.context_dim = input_dim, context_dim
         self.hidden_dims = list(hidden_dims)
         self.param_dims = list(param_dims)
@@ -151,7 +179,7 @@ class ConditionalDenseNN(nn.Module):
 
     def raw(self, x: torch.Tensor, context: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Flat conditioner output [B, sum(param_dims)] (what the spline kernels consume)."""
-        return _run_chain(self.layers, self.act, x, context, masked=False)
+        return _run_chain(self.layers, self.act, x, context, masked=False, drop=self._drop_args())
 
     def _shape(self, h, lead):
         if self.output_multiplier == 1:
@@ -168,20 +196,21 @@ class ConditionalDenseNN(nn.Module):
 class DenseNN(ConditionalDenseNN):
     """[pyro] nn/dense_nn.py::DenseNN."""
 
-    def __init__(self, input_dim, hidden_dims, param_dims=(1, 1), nonlinearity=nn.ReLU()):
-        super().__init__(input_dim, 0, hidden_dims, param_dims, nonlinearity)
+    def __init__(self, input_dim, hidden_dims, param_dims=(1, 1), nonlinearity=nn.ReLU(), dropout_p=0.0):
+        super().__init__(input_dim, 0, hidden_dims, param_dims, nonlinearity, dropout_p)
 
     def forward(self, x):
         return self._shape(self.raw(x, None), x.shape[:-1])
 
 
-class ConditionalAutoRegressiveNN(nn.Module):
+class ConditionalAutoRegressiveNN(_DropoutMixin, nn.Module):
     """[pyro] nn/auto_reg_nn.py::ConditionalAutoRegressiveNN (MADE, Germain et al. 2015)."""
 
     def __init__(self, input_dim: int, context_dim: int, hidden_dims: Sequence[int],
                  param_dims: Sequence[int] = (1, 1), permutation: Optional[torch.Tensor] = None,
-                 skip_connections: bool = False, nonlinearity: nn.Module = nn.ReLU()):
+                 skip_connections: bool = False, nonlinearity: nn.Module = nn.ReLU(), dropout_p: float = 0.0):
         super().__init__()
+        self.dropout_p = float(dropout_p or 0.0)
         if skip_connections:
             raise NotImplementedError("naz_amd: MADE skip connections are not on naz's path (transforms.py:142,180)")
         self.input_dim, self.context_dim = input_dim, context_dim
@@ -212,8 +241,10 @@ class ConditionalAutoRegressiveNN(nn.Module):
     degree_schedule = True
 
     def inverse_plan(self) -> Optional["ARInversePlan"]:
-        """The cached degree-scheduled inverse (None when disabled)."""
-        if not self.degree_schedule:
+        """The cached degree-scheduled inverse (None when disabled, or while MC dropout is active:
+        pyro's D-pass inverse then draws fresh dropout masks on every pass, which the schedule's
+        compute-each-unit-once cannot reproduce)."""
+        if not self.degree_schedule or self.dropout_active():
             return None
         plan = self.__dict__.get("_inverse_plan")
         if plan is None:
@@ -236,7 +267,7 @@ class ConditionalAutoRegressiveNN(nn.Module):
 
     def raw(self, x: torch.Tensor, context: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Flat MADE output [B, mult*D], column p*D + i (pyro's reshape to [mult, D])."""
-        return _run_chain(self.layers, self.act, x, context, masked=True)
+        return _run_chain(self.layers, self.act, x, context, masked=True, drop=self._drop_args())
 
     def _shape(self, h, lead):
         if self.output_multiplier == 1:
@@ -565,8 +596,9 @@ class AutoRegressiveNN(ConditionalAutoRegressiveNN):
     """[pyro] nn/auto_reg_nn.py::AutoRegressiveNN."""
 
     def __init__(self, input_dim, hidden_dims, param_dims=(1, 1), permutation=None, skip_connections=False,
-                 nonlinearity=nn.ReLU()):
-        super().__init__(input_dim, 0, hidden_dims, param_dims, permutation, skip_connections, nonlinearity)
+                 nonlinearity=nn.ReLU(), dropout_p=0.0):
+        super().__init__(input_dim, 0, hidden_dims, param_dims, permutation, skip_connections, nonlinearity,
+                         dropout_p)
 
     def forward(self, x):
         return self._shape(self.raw(x, None), x.shape[:-1])

@@ -443,6 +443,23 @@ def act_bwd(g_y: Tensor, y: Tensor, act: str) -> Tensor:
     return gp
 
 
+def dropout(x: Tensor, p: float, seed: int, out: Optional[Tensor] = None) -> Tensor:
+    """MC dropout of a conditioner activation (naz_dropout): x / (1 - p) where the hash of
+    (seed, row, col) keeps it, else 0.  The same (p, seed) on a same-shape gradient applies
+    the forward's mask (the backward).  ``out`` may be ``x`` (in place)."""
+    dev = _dev(x, out)
+    x, ldx = _rows(x)
+    M, N = x.shape
+    if out is None:
+        out = torch.empty((M, N), device=dev, dtype=torch.float32)
+    o, ldo = _rows(out)
+    if o.data_ptr() != out.data_ptr():
+        raise ValueError("dropout: out must be a row-strided 2-D tensor")
+    check(lib().naz_dropout(_p(x), ldx, _p(o), ldo, M, N, float(p), int(seed) & (2 ** 64 - 1), _stream(dev)),
+          "dropout")
+    return out
+
+
 # ----------------------------------------------------------------------------- a3 + a8 + a9 fused
 def coupling_desc(D: int, C: int, S: int, K: int, L: int, H: int, act: str = "tanh", has_lower: bool = True,
                   bound: float = 3.0, mfma: str = "bf16x6") -> CouplingDesc:

@@ -232,7 +232,9 @@ def run_train(args, dev, rank, world, dist):
     from naz_amd.trainers import DataParallel, nll_step
     from naz_amd.trainers.train_flows import _flow_parameters
     flow = build_flow()
-    flow.set_fused(False)
+    if args.train_walk:  # A/B: the per-node autograd walk instead of the fused training path
+        from naz_amd.flows import flow as flow_mod
+        flow_mod._TRAIN_FUSED = "0"
     lo, hi, G = shard(args, rank, world, 1 << 23)
     B = hi - lo
     x = torch.as_tensor(mixture_rows(lo, hi, D, seed=0), device=dev)
@@ -762,6 +764,8 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=1 << 20,
                     help="--train: rows per forward+backward chunk (gradients accumulate before the all-reduce)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train-walk", action="store_true",
+                    help="--train: run the per-node autograd walk instead of the fused NLL step (A/B)")
     ap.add_argument("--train", action="store_true",
                     help="time the data-parallel NLL training step instead (BASELINE configs[3]: fwd + HIP "
                          "backward + flat-bucket RCCL all-reduce + clip + Adam) on the same flow")

@@ -231,6 +231,34 @@ int naz_coupling_sample(const naz_coupling_desc* d, const void* packed, const fl
                         const float* ctx, int64_t ldc, const float* low, const float* high, float* y, int64_t ldy,
                         float* out_ld, int64_t B, void* stream);
 
+/* ---- a10 over a3: the fused NLL training step of the coupling flow ----------------
+ * Replaces the autograd walk of train's loss.backward() (naz/trainers/train_flows.py:195,208)
+ * through NormalizingFlow.log_prob (flow.py:45-79) for the spline-coupling flow.  Requires a
+ * packed image of mode NAZ_MFMA_F16X3_R16 (naz_coupling_pack) plus the backward image:
+ *   naz_coupling_pack_bwd: per-layer fp32 transposed-weight images (size
+ *     naz_coupling_bwd_packed_bytes) from the same flat parameters; re-pack after updates.
+ *   naz_coupling_log_prob_train: out_lp as naz_coupling_log_prob, computed with libm-grade
+ *     activations / splines (the reference walk's precision), and states [L+1][B][D] with
+ *     states[l+1] = layer l's input in the log_prob direction, states[0] = z.
+ *   naz_coupling_bwd_layer: for layer l (call l = 0 .. L-1), given g_in = dLoss/dstates[l]
+ *     and g_lp[r] = dLoss/dlog p_r, writes g_out = dLoss/dstates[l+1], adds the lower
+ *     spline's parameter gradients into g_low [S(3K-1)] (zero it first), and writes the
+ *     weight-gradient operands: h1, h2 [B,H] (tanh activations), dp1, dp2 [B,H] (dLoss/d
+ *     pre-activation), dp3 [B, naz_coupling_dp3_columns] (dLoss/d GEMM3 output, column c
+ *     holding DenseNN output row rows[c], -1 = zero padding), x0 [B, C+S] = [ctx | x1].
+ *     Then dW2 = dp3ᵀ·h2, dW1 = dp2ᵀ·h1, dW0 = dp1ᵀ·x0, db = column sums (naz_gemm).       */
+int64_t naz_coupling_bwd_packed_bytes(const naz_coupling_desc* d);
+int naz_coupling_pack_bwd(const naz_coupling_desc* d, const float* flat_params, void* packed_bwd, void* stream);
+int naz_coupling_log_prob_train(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx,
+                                const float* ctx, int64_t ldc, const float* low, const float* high, float* out_lp,
+                                float* states, int64_t B, void* stream);
+int naz_coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const void* packed_bwd, const float* flat,
+                           int layer, const float* state, const float* ctx, int64_t ldc, const float* g_in,
+                           const float* g_lp, float* h1, float* h2, float* dp1, float* dp2, float* dp3, float* x0,
+                           float* g_out, float* g_low, int64_t B, void* stream);
+/* writes the DenseNN output row of every dp3 column into rows (may be NULL); returns the count */
+int naz_coupling_dp3_columns(const naz_coupling_desc* d, int* rows);
+
 /* ---- a11: continuous normalizing flow (FFJORD block, Hutchinson trace) --------
  * naz FFJORDTransform (naz/flows/continuous_transforms.py:70-106) over ConditionalFCNN
  * (:38-60, input cat([x, ctx]), Softplus default).  One call integrates ONE block

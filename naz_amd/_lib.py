@@ -62,6 +62,12 @@ SIGNATURES = {
     "naz_act_bwd": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i, _i, _vp]),
     "naz_base_log_prob_bwd": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _i64, _i, _vp]),
     "naz_dropout": (C.c_int, [_vp, _i64, _vp, _i64, _i64, _i, C.c_float, C.c_uint64, _vp]),
+    "naz_coupling_bwd_packed_bytes": (C.c_int64, [C.POINTER(CouplingDesc)]),
+    "naz_coupling_pack_bwd": (C.c_int, [C.POINTER(CouplingDesc), _vp, _vp, _vp]),
+    "naz_coupling_log_prob_train": (C.c_int, [C.POINTER(CouplingDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "naz_coupling_bwd_layer": (C.c_int, [C.POINTER(CouplingDesc), _vp, _vp, _vp, _i, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                         _vp, _vp, _vp, _i64, _vp]),
+    "naz_coupling_dp3_columns": (C.c_int, [C.POINTER(CouplingDesc), _vp]),
     "naz_cnf_supported": (C.c_int, [C.POINTER(CnfDesc)]),
     "naz_cnf_param_count": (C.c_int64, [C.POINTER(CnfDesc)]),
     "naz_cnf_packed_bytes": (C.c_int64, [C.POINTER(CnfDesc)]),

@@ -239,4 +239,28 @@ int naz_coupling_sample(const naz_coupling_desc* d, const void* packed, const fl
   return coupling_sample(d, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, as_stream(stream));
 }
 
+int64_t naz_coupling_bwd_packed_bytes(const naz_coupling_desc* d) { return coupling_bwd_packed_bytes(d); }
+
+int naz_coupling_pack_bwd(const naz_coupling_desc* d, const float* flat_params, void* packed_bwd, void* stream) {
+  return coupling_pack_bwd(d, flat_params, packed_bwd, as_stream(stream));
+}
+
+int naz_coupling_log_prob_train(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx,
+                                const float* ctx, int64_t ldc, const float* low, const float* high, float* out_lp,
+                                float* states, int64_t B, void* stream) {
+  if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_log_prob_train: conditional flow needs ctx");
+  return coupling_log_prob_train(d, packed, x, ldx, ctx, ldc, low, high, out_lp, states, B, as_stream(stream));
+}
+
+int naz_coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const void* packed_bwd, const float* flat,
+                           int layer, const float* state, const float* ctx, int64_t ldc, const float* g_in,
+                           const float* g_lp, float* h1, float* h2, float* dp1, float* dp2, float* dp3, float* x0,
+                           float* g_out, float* g_low, int64_t B, void* stream) {
+  if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_bwd_layer: conditional flow needs ctx");
+  return coupling_bwd_layer(d, packed, packed_bwd, flat, layer, state, ctx, ldc, g_in, g_lp, h1, h2, dp1, dp2, dp3,
+                            x0, g_out, g_low, B, as_stream(stream));
+}
+
+int naz_coupling_dp3_columns(const naz_coupling_desc* d, int* rows) { return coupling_dp3_columns(d, rows); }
+
 }  // extern "C"

@@ -26,6 +26,7 @@
 #include "naz_device.h"
 #include "naz_internal.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace naz {
@@ -1196,6 +1197,7 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
 }  // namespace naz
 
 #include "coupling_r16.h"
+#include "coupling_train.h"
 
 namespace naz {
 
@@ -1243,6 +1245,63 @@ struct CouplingOps {
       const int64_t grid = (B + kRowsPerWG - 1) / kRowsPerWG;
       hipLaunchKernelGGL((coupling_flow_kernel<G, INV>), dim3((unsigned)grid), dim3(256), lds, s, pk, L, x, ldx,
                          ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+    }
+  }
+  // ---- NLL training path (r16 instantiations only; the packed image must be F16X3_R16)
+  static int64_t bwd_layer_floats() {
+    if constexpr (R16OK) return BwdR16<CR>::LAYER;
+    else return -1;
+  }
+  static int pack_bwd(const float* flat, void* packed, int L, hipStream_t s) {
+    if constexpr (R16OK) {
+      const int64_t n = (int64_t)L * BwdR16<CR>::LAYER;
+      const int64_t grid = std::min<int64_t>((n + 255) / 256, 8192);
+      hipLaunchKernelGGL((coupling_pack_bwd_r16_kernel<CR>), dim3((unsigned)grid), dim3(256), 0, s, flat,
+                         reinterpret_cast<float*>(packed), L);
+      return check_launch("coupling_pack_bwd_r16_kernel");
+    } else {
+      return -2;
+    }
+  }
+  static int log_prob_train(const void* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
+                            const float* low, const float* high, float* out_lp, float* states, int64_t B, float bound,
+                            hipStream_t s) {
+    if constexpr (R16OK) {
+      if (B == 0) return 0;
+      const int64_t grid = (B + kR16Rows - 1) / kR16Rows;
+      hipLaunchKernelGGL((coupling_r16_kernel<CR, true, 1>), dim3((unsigned)grid), dim3(kR16Rows * 4),
+                         (size_t)CR::MAXSTAGE * 4, s, reinterpret_cast<const float*>(packed), L, x, ldx, ctx, ldc, low,
+                         high, out_lp, nullptr, 0, B, bound, states);
+      return check_launch("coupling_r16_kernel<train>");
+    } else {
+      return -2;
+    }
+  }
+  static int bwd_layer(const void* packed, const void* bwd, const float* flat, int l, const float* state,
+                       const float* ctx, int64_t ldc, const float* g_in, const float* g_lp, const BwdOut& o, int64_t B,
+                       float bound, hipStream_t s) {
+    if constexpr (R16OK) {
+      if (B == 0) return 0;
+      const int64_t ntiles = (B + kR16Rows - 1) / kR16Rows;
+      const int64_t grid = std::min<int64_t>(ntiles, 1024);
+      const size_t lds = (size_t)(2 * kX6Slot + CR::S * (3 * CR::K - 1) + kR16Waves) * 4;
+      hipLaunchKernelGGL((coupling_bwd_r16_kernel<CR>), dim3((unsigned)grid), dim3(kR16Rows * 4), lds, s,
+                         reinterpret_cast<const float*>(packed), reinterpret_cast<const float*>(bwd), flat, l, state,
+                         ctx, ldc, g_in, g_lp, o, B, bound);
+      return check_launch("coupling_bwd_r16_kernel");
+    } else {
+      return -2;
+    }
+  }
+  static int dp3_columns(int* rows) {
+    if constexpr (R16OK) {
+      using BW = BwdR16<CR>;
+      if (rows != nullptr)
+        for (int q = 0; q < 4; ++q)
+          for (int sl = 0; sl < BW::NS3; ++sl) rows[q * BW::NS3 + sl] = BW::slot_row(q, sl);
+      return 4 * BW::NS3;
+    } else {
+      return -2;
     }
   }
   static int run(bool inv, int mode, const void* packed, int L, const float* x, int64_t ldx, const float* ctx,
@@ -1345,6 +1404,61 @@ int coupling_sample(const naz_coupling_desc* d, const void* packed, const float*
     return decltype(ops)::run(false, d->mfma_mode, packed, d->L, z, ldz, ctx, ldc, low, high, out_ld, y, ldy, B,
                               d->bound, s);
   });
+  return rc == -2 ? unsupported(d) : rc;
+}
+
+// ---- NLL training path (coupling_train.h) ----------------------------------------------
+static int train_mode_ok(const naz_coupling_desc* d) {
+  if (d == nullptr) return set_error("naz_coupling: null descriptor");
+  if (d->mfma_mode != NAZ_MFMA_F16X3_R16)
+    return set_error("naz_coupling training path: the packed image must be NAZ_MFMA_F16X3_R16 (mode %d)", d->mfma_mode);
+  return 0;
+}
+
+int64_t coupling_bwd_packed_bytes(const naz_coupling_desc* d) {
+  int64_t v = -1;
+  coupling_dispatch(d, [&](auto ops) {
+    const int64_t f = decltype(ops)::bwd_layer_floats();
+    v = f < 0 ? -1 : f * d->L * 4;
+    return 0;
+  });
+  return v;
+}
+
+int coupling_pack_bwd(const naz_coupling_desc* d, const float* flat, void* packed, hipStream_t s) {
+  if (int rc = train_mode_ok(d)) return rc;
+  int rc = coupling_dispatch(d, [&](auto ops) { return decltype(ops)::pack_bwd(flat, packed, d->L, s); });
+  return rc == -2 ? unsupported(d) : rc;
+}
+
+int coupling_log_prob_train(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx,
+                            const float* ctx, int64_t ldc, const float* low, const float* high, float* out_lp,
+                            float* states, int64_t B, hipStream_t s) {
+  if (int rc = train_mode_ok(d)) return rc;
+  if ((low == nullptr) != (high == nullptr)) return set_error("naz_coupling_log_prob_train: low/high must both be set");
+  if (states == nullptr) return set_error("naz_coupling_log_prob_train: states buffer required");
+  int rc = coupling_dispatch(d, [&](auto ops) {
+    return decltype(ops)::log_prob_train(packed, d->L, x, ldx, ctx, ldc, low, high, out_lp, states, B, d->bound, s);
+  });
+  return rc == -2 ? unsupported(d) : rc;
+}
+
+int coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const void* packed_bwd, const float* flat,
+                       int layer, const float* state, const float* ctx, int64_t ldc, const float* g_in,
+                       const float* g_lp, float* h1, float* h2, float* dp1, float* dp2, float* dp3, float* x0,
+                       float* g_out, float* g_low, int64_t B, hipStream_t s) {
+  if (int rc = train_mode_ok(d)) return rc;
+  if (layer < 0 || layer >= d->L) return set_error("naz_coupling_bwd_layer: layer %d out of range", layer);
+  if (d->has_lower && g_low == nullptr) return set_error("naz_coupling_bwd_layer: g_low required with a lower spline");
+  const BwdOut o{h1, h2, dp1, dp2, dp3, x0, g_out, g_low};
+  int rc = coupling_dispatch(d, [&](auto ops) {
+    return decltype(ops)::bwd_layer(packed, packed_bwd, flat, layer, state, ctx, ldc, g_in, g_lp, o, B, d->bound, s);
+  });
+  return rc == -2 ? unsupported(d) : rc;
+}
+
+int coupling_dp3_columns(const naz_coupling_desc* d, int* rows) {
+  int rc = coupling_dispatch(d, [&](auto ops) { return decltype(ops)::dp3_columns(rows); });
   return rc == -2 ? unsupported(d) : rc;
 }
 

@@ -259,11 +259,27 @@ NAZ_DEV void gemm_r16_lazy(floatx4 (&acc)[NB], const float* __restrict__ stage, 
   }
 }
 
-template <class CF, bool DIR_INV>
-__global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
+// Training forward (VAR = 1, coupling_train.h): the log_prob walk of the NLL step with the
+// reference walk's libm-grade activation and spline (tanh_f / build_tables + rqs_apply, not
+// the hardware-transcendental fold and select-first spline) and every layer's input state
+// written to states[l + 1][row][:] (states[0] = z), for the backward kernel to recompute from.
+// The GEMMs keep the f16x3 split.  Activated values are -tanh/2 (the fold's convention), so the
+// packed image is the same.
+constexpr float kInvSigScale = 0.34657359027997264f;  // 1 / kSigScale = ln 2 / 2
+// NAZ_TRAIN_FAST: hardware transcendentals in the training kernels' activations and splines
+#ifdef NAZ_TRAIN_FAST
+constexpr bool kTrainFast = true;
+#else
+constexpr bool kTrainFast = false;
+#endif
+NAZ_DEV float acc_fold(float v) { return -0.5f * tanh_f<kTrainFast>(v * kInvSigScale); }
+
+template <class CF, bool DIR_INV, int VAR = 0>
+__global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
-    float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound) {
+    float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound,
+    float* __restrict__ states = nullptr) {
   extern __shared__ float4 lds4[];
   float* const slot0 = reinterpret_cast<float*>(lds4);
   float* const slot1 = slot0 + kX6Slot;
@@ -329,6 +345,15 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
   int g = 0;  // global stage counter: stage g lives in slot (g & 1)
   for (int li = 0; li < L; ++li) {
     const int l = DIR_INV ? (L - 1 - li) : li;
+    if constexpr (VAR == 1) {  // layer l's input state P[l + 1]
+      if (valid) {
+        float* st = states + ((int64_t)(l + 1) * B + row) * CF::D;
+#pragma unroll
+        for (int u = 0; u < CF::SQ; ++u) st[q * CF::SQ + u] = zl[u];
+#pragma unroll
+        for (int u = 0; u < CF::DQ; ++u) st[CF::S + q * CF::DQ + u] = zu[u];
+      }
+    }
     const float* lp = packed + (int64_t)l * CF::LAYER;
     const float* lnext = packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER;
     floatx4 acc1[CF::HB], acc2[CF::HB], acc3[CF::NO];
@@ -351,8 +376,21 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
         for (int u = 0; u < CF::SQ; ++u) {
           if constexpr (DIR_INV && CF::LOWER) {
             float ld;
-            zl[u] = rqs_table<CF::K, true>(cur + CF::A_TBL + (q * CF::SQ + u) * CF::TBL, zl[u], bound, ld);
-            ldsum -= ld;
+            if constexpr (VAR == 1) {
+              SplineTables<CF::K> tb;
+              const float* tp = cur + CF::A_TBL + (q * CF::SQ + u) * CF::TBL;
+#pragma unroll
+              for (int k = 0; k <= CF::K; ++k) {
+                tb.cw[k] = tp[k];
+                tb.ch[k] = tp[CF::K + 1 + k];
+                tb.dv[k] = tp[2 * (CF::K + 1) + k];
+              }
+              zl[u] = rqs_apply<CF::K, true, kTrainFast>(tb, zl[u], bound, ld);
+              ldsum -= ld;  // ldsum carries the forward maps' log-dets (rqs_apply: the inverse's)
+            } else {
+              zl[u] = rqs_table<CF::K, true>(cur + CF::A_TBL + (q * CF::SQ + u) * CF::TBL, zl[u], bound, ld);
+              ldsum -= ld;
+            }
           }
         }
         float in[CF::KS1 * 8];
@@ -422,7 +460,13 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
           for (int r = 0; r < 4; ++r) acc1[b][r] = sig_fold(acc1[b][r]);
         constexpr bool kLazyAct = false;
 #else
-        constexpr bool kLazyAct = true;  // activated per k-step inside gemm_r16_lazy
+        constexpr bool kLazyAct = VAR == 0;  // activated per k-step inside gemm_r16_lazy
+        if constexpr (VAR == 1) {
+#pragma unroll
+          for (int b = 2 * T0; b < 2 * (T0 + CF::KB2); ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc1[b][r] = acc_fold(acc1[b][r]);
+        }
 #endif
         if constexpr (s == 0) {
           const float4* b4 = reinterpret_cast<const float4*>(cur + CF::B_BIAS);
@@ -445,7 +489,13 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
           for (int r = 0; r < 4; ++r) acc2[b][r] = sig_fold(acc2[b][r]);
         constexpr bool kLazyAct = false;
 #else
-        constexpr bool kLazyAct = true;
+        constexpr bool kLazyAct = VAR == 0;
+        if constexpr (VAR == 1) {
+#pragma unroll
+          for (int b = 2 * T0; b < 2 * (T0 + CF::KB3); ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc2[b][r] = acc_fold(acc2[b][r]);
+        }
 #endif
         if constexpr (s == 0) {
           const float4* b4 = reinterpret_cast<const float4*>(cur + CF::C_BIAS);
@@ -477,8 +527,24 @@ __global__ void __launch_bounds__(kR16Rows * 4, 4) coupling_r16_kernel(
         ud[k] = acc3[sd >> 2][sd & 3];
       }
       float ld;
-      zu[u] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[u], bound, rc, ld);
-      ldsum += DIR_INV ? -ld : ld;
+      if constexpr (VAR == 1) {
+        SplineTables<CF::K> tb;
+        build_tables<CF::K, kTrainFast>(uw, uh, ud, bound, tb);
+        zu[u] = rqs_apply<CF::K, DIR_INV, kTrainFast>(tb, zu[u], bound, ld);
+        ldsum += DIR_INV ? -ld : ld;
+      } else {
+        zu[u] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[u], bound, rc, ld);
+        ldsum += DIR_INV ? -ld : ld;
+      }
+    }
+  }
+  if constexpr (VAR == 1) {  // P[0] = z
+    if (valid) {
+      float* st = states + row * CF::D;
+#pragma unroll
+      for (int u = 0; u < CF::SQ; ++u) st[q * CF::SQ + u] = zl[u];
+#pragma unroll
+      for (int u = 0; u < CF::DQ; ++u) st[CF::S + q * CF::DQ + u] = zu[u];
     }
   }
 

@@ -1,0 +1,408 @@
+// Backward of one spline-coupling layer for the NLL training step (SURVEY.md §8a a10 over a3;
+// naz train_flows.py:194-213 differentiating NormalizingFlow.log_prob).  Included by
+// coupling.hip after coupling_r16.h (CfgR16, the packed forward image, split8_f16, ...).
+//
+// The training forward (coupling_r16_kernel<.., VAR = 1>) stores every layer's input state
+// P[l + 1] (P[L] = data, P[0] = z; layer l maps P[l + 1] -> P[l] in the log_prob direction).
+// One launch of coupling_bwd_r16_kernel per layer l, in the order l = 0 .. L-1, takes
+// g(P[l]) = dLoss/dP[l] and the per-row weight of the log-det terms g_lp = dLoss/dlog p, and
+//   1. recomputes the layer's conditioner forward from P[l + 1] exactly as the training forward
+//      did (same packed f16x3 image, same libm-grade tanh and spline), keeping H1, H2
+//      (natural tanh values) and the raw spline parameters in registers;
+//   2. runs the upper spline's VJP per (row, dim) in registers (rqs_vjp: implicit-function rule
+//      for the inverse) -> dRaw (= dPre3, GEMM3 has no activation) and g(y2);
+//   3. backpropagates through the MLP with EXACT fp32 MFMA (v_mfma_f32_16x16x4_f32; gradients
+//      have no fixed range, so no fp16 split): dH2 = dPre3·W2, dPre2 = dH2 ⊙ (1 − H2²),
+//      dH1 = dPre2·W1, dPre1 = dH1 ⊙ (1 − H1²), dx1 = dPre1·W0[:, C:];
+//   4. runs the lower spline's VJP (shared parameters: per-workgroup sums in LDS, one atomic
+//      per parameter per workgroup) and writes g(P[l + 1]);
+//   5. writes the weight-gradient operands dPre3, H2, dPre2, H1, dPre1 and X0 = [ctx | x1] (the
+//      batch reductions dW = dPreᵀ·X run as separate GEMMs).
+// Layout: the forward kernel's 16-row waves — lane l owns row l & 15 and quarter q = l >> 4,
+// accumulator register i of block b on quarter q = feature 16b + 4q + i.  The transposed GEMMs
+// keep that layout: in step 3 a k-step feeds each quarter's OWN values (its 48 GEMM3 slots, or
+// its 32 hidden features) as the B operand, and the backward images order the weight columns to
+// match, so the results land in the forward's activation layout with no shuffles.
+#pragma once
+#include "spline_bwd.h"
+
+namespace naz {
+
+template <class CF>
+struct BwdR16 {
+  static constexpr int NS3 = 4 * CF::NO;  // GEMM3 slots per quarter = dH2 k-steps
+  static constexpr int HB = CF::HB;
+  static constexpr int U3ALL = NS3 / 4, U2ALL = CF::H / 16 * 4 / 4;  // 4-k-step units: dH2, dH1 (= H/4)
+  static constexpr int pick_u(int nb, int units) {
+    int best = 1;
+    for (int u = 1; u <= units; ++u)
+      if (units % u == 0 && nb * u * 256 <= kX6Slot) best = u;
+    return best;
+  }
+  static constexpr int U3 = pick_u(HB, U3ALL), NB3 = U3ALL / U3;   // dH2 stages
+  static constexpr int U2 = pick_u(HB, CF::H / 4), NB2 = (CF::H / 4) / U2;  // dH1 stages
+  static constexpr int S3 = HB * U3 * 256, S2 = HB * U2 * 256, SA = (CF::H / 4) * 256;
+  static constexpr int OFF2 = NB3 * S3, OFFA = OFF2 + NB2 * S2;
+  static constexpr int LAYER = OFFA + SA;
+  static constexpr int NSTG = NB3 + NB2 + 1;
+  static_assert(CF::SQ <= 4, "dx1 block holds at most 4 lower dims per quarter");
+  static constexpr __host__ __device__ int stage_off(int j) { return j < NB3 ? j * S3 : (j < NB3 + NB2 ? OFF2 + (j - NB3) * S2 : OFFA); }
+  static constexpr __host__ __device__ int stage_size(int j) { return j < NB3 ? S3 : (j < NB3 + NB2 ? S2 : SA); }
+  // DenseNN output row of quarter q's GEMM3 slot s (-1 = pad)
+  static constexpr __host__ __device__ int slot_row(int q, int s) { return r16_out_row<CF>(s >> 2, 4 * q + (s & 3)); }
+  // hidden feature fed by quarter q at k-step s of a hidden-layer backward GEMM
+  static constexpr __host__ __device__ int hid_feat(int q, int s) { return 16 * (s >> 2) + 4 * q + (s & 3); }
+};
+
+// Backward images (fp32) of every layer from the natural flat weights: [L][BwdR16::LAYER].
+template <class CF>
+__global__ void coupling_pack_bwd_r16_kernel(const float* __restrict__ flat, float* __restrict__ packed, int L) {
+  using BW = BwdR16<CF>;
+  const int64_t n = (int64_t)L * BW::LAYER;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(e / BW::LAYER);
+    const int off = (int)(e - (int64_t)l * BW::LAYER);
+    const float* W0 = flat + (int64_t)l * CF::FLAT;
+    const float* W1 = W0 + CF::N_W0 + CF::N_B0;
+    const float* W2 = W1 + CF::N_W1 + CF::N_B1;
+    float v = 0.f;
+    if (off < BW::OFF2) {  // dH2 stages: [b][u][lane][e], k-step s = 4(j U3 + u) + e
+      const int j = off / BW::S3, r = off - j * BW::S3;
+      const int b = r / (BW::U3 * 256), r2 = r - b * BW::U3 * 256;
+      const int u = r2 >> 8, lane = (r2 >> 2) & 63, ee = r2 & 3;
+      const int s = 4 * (j * BW::U3 + u) + ee, q = lane >> 4, m = lane & 15;
+      const int orow = BW::slot_row(q, s);
+      if (orow >= 0) v = W2[orow * CF::H + 16 * b + m];
+    } else if (off < BW::OFFA) {  // dH1 stages
+      const int o2 = off - BW::OFF2;
+      const int j = o2 / BW::S2, r = o2 - j * BW::S2;
+      const int b = r / (BW::U2 * 256), r2 = r - b * BW::U2 * 256;
+      const int u = r2 >> 8, lane = (r2 >> 2) & 63, ee = r2 & 3;
+      const int s = 4 * (j * BW::U2 + u) + ee, q = lane >> 4, m = lane & 15;
+      v = W1[BW::hid_feat(q, s) * CF::H + 16 * b + m];
+    } else {  // dx1: [u][lane][e]; output row m = 4q' + i -> lower dim q' SQ + i (i < SQ)
+      const int r = off - BW::OFFA;
+      const int u = r >> 8, lane = (r >> 2) & 63, ee = r & 3;
+      const int s = 4 * u + ee, q = lane >> 4, m = lane & 15;
+      const int qq = m >> 2, i = m & 3;
+      if (i < CF::SQ) v = W0[BW::hid_feat(q, s) * (CF::C + CF::S) + CF::C + qq * CF::SQ + i];
+    }
+    packed[e] = v;
+  }
+}
+
+// acc[b] += Σ_k A_b(k) B(k) over the stage's units [U0, U0 + NU) of 4 k-steps; A from the
+// stage image [b][u][lane][4], B = the lane's own values bv[s].
+template <int NBLK, int NU, int U0, int NV>
+NAZ_DEV void bwd_gemm_stage(floatx4 (&acc)[NBLK], const float* __restrict__ stage, int lane, const floatx4 (&bv)[NV]) {
+  // block-interleaved: consecutive MFMAs hit different accumulators (the f32 16x16x4 form's
+  // dependent-accumulator latency, 40 cycles, exceeds its 32-cycle issue)
+  const float4* p4 = reinterpret_cast<const float4*>(stage);
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    float4 a[NBLK];
+#pragma unroll
+    for (int b = 0; b < NBLK; ++b) a[b] = p4[(b * NU + u) * 64 + lane];
+#pragma unroll
+    for (int b = 0; b < NBLK; ++b) acc[b] = mfma16_f32(a[b].x, bv[U0 + u][0], acc[b]);
+#pragma unroll
+    for (int b = 0; b < NBLK; ++b) acc[b] = mfma16_f32(a[b].y, bv[U0 + u][1], acc[b]);
+#pragma unroll
+    for (int b = 0; b < NBLK; ++b) acc[b] = mfma16_f32(a[b].z, bv[U0 + u][2], acc[b]);
+#pragma unroll
+    for (int b = 0; b < NBLK; ++b) acc[b] = mfma16_f32(a[b].w, bv[U0 + u][3], acc[b]);
+  }
+}
+
+struct BwdOut {
+  float* h1;   // [B, H]   H1 (natural tanh)
+  float* h2;   // [B, H]   H2
+  float* dp1;  // [B, H]   dL/dpre1
+  float* dp2;  // [B, H]   dL/dpre2
+  float* dp3;  // [B, 4 NS3] dL/draw in lane-slot order (column q NS3 + s)
+  float* x0;   // [B, C + S] [ctx | x1]
+  float* g_out;       // [B, D]  dL/dP[l + 1]
+  float* g_low;       // [S (3K - 1)] lower-spline parameter gradients (atomically accumulated)
+};
+
+template <class CF>
+__global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
+    const float* __restrict__ packed, const float* __restrict__ bwd, const float* __restrict__ flat, int l,
+    const float* __restrict__ state, const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ g_in,
+    const float* __restrict__ g_lp, BwdOut o, int64_t B, float bound) {
+  using BW = BwdR16<CF>;
+  constexpr int K = CF::K, P = CF::P, H = CF::H, D = CF::D, C = CF::C, S = CF::S;
+  constexpr int NLOW = S * (3 * K - 1);
+  extern __shared__ float4 lds4[];
+  float* const slot0 = reinterpret_cast<float*>(lds4);
+  float* const slot1 = slot0 + kX6Slot;
+  float* const glow = slot1 + kX6Slot;  // [NLOW] per-workgroup lower-spline gradient sums
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane >> 4;
+  for (int i = threadIdx.x; i < NLOW; i += blockDim.x) glow[i] = 0.f;
+
+  const float* lp = packed + (int64_t)l * CF::LAYER;
+  const float* lb = bwd + (int64_t)l * BW::LAYER;
+  const float* low = flat + (int64_t)l * CF::FLAT + CF::N_W0 + CF::N_B0 + CF::N_W1 + CF::N_B1 + CF::N_W2 + CF::N_B2;
+  const int64_t ntiles = (B + kR16Rows - 1) / kR16Rows;
+  constexpr int NSTG_F = CF::NSTG, NSTG = NSTG_F + BW::NSTG;
+  auto stage_src = [&](int j) -> const float* { return j < NSTG_F ? lp + CF::stage_off(j) : lb + BW::stage_off(j - NSTG_F); };
+
+  int g = 0;  // global stage counter: stage g lives in slot (g & 1)
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) stage_issue<CF::A_SIZE, kR16Waves>(slot0, lp);  // A32 image never used: f16x3 path only
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int64_t row = tile * kR16Rows + wave * 16 + (lane & 15);
+    const bool valid = row < B;
+    const int64_t crow = valid ? row : 0;
+    float y1[CF::SQ], y2[CF::DQ], x1[CF::SQ];
+#pragma unroll
+    for (int u = 0; u < CF::SQ; ++u) y1[u] = valid ? state[crow * D + q * CF::SQ + u] : 0.f;
+#pragma unroll
+    for (int u = 0; u < CF::DQ; ++u) y2[u] = valid ? state[crow * D + S + q * CF::DQ + u] : 0.f;
+    const float gl = valid ? g_lp[crow] : 0.f;
+
+    floatx4 h1[CF::HB], h2[CF::HB], a3[CF::NO];
+    float in[CF::KS1 * 8];
+    floatx4 dp2[CF::HB];  // dPre2, then dPre1
+    floatx4 dacc[CF::HB];
+    floatx4 dx1;
+    float gy2[CF::DQ];
+    const bool has_next = tile + gridDim.x < ntiles;
+
+    static_for<0, NSTG>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      __syncthreads();  // stage j has landed in slot (g&1); every wave is done with the other slot
+      const float* cur = (g & 1) ? slot1 : slot0;
+      float* nxt = (g & 1) ? slot0 : slot1;
+      if constexpr (j + 1 < NSTG_F) {
+        stage_issue<CF::stage_size(j + 1), kR16Waves>(nxt, stage_src(j + 1));
+      } else if constexpr (j + 1 < NSTG) {
+        stage_issue<BW::stage_size(j + 1 - NSTG_F), kR16Waves>(nxt, stage_src(j + 1));
+      } else {
+        if (has_next) stage_issue<CF::A_SIZE, kR16Waves>(nxt, lp);
+      }
+      ++g;
+
+      if constexpr (j == 0) {
+        // lower spline inverse (libm-grade, as the training forward), GEMM1 over [ctx | x1]
+#pragma unroll
+        for (int u = 0; u < CF::SQ; ++u) {
+          x1[u] = y1[u];
+          if constexpr (CF::LOWER) {
+            SplineTables<K> tb;
+            const float* tp = cur + CF::A_TBL + (q * CF::SQ + u) * CF::TBL;
+#pragma unroll
+            for (int k = 0; k <= K; ++k) {
+              tb.cw[k] = tp[k];
+              tb.ch[k] = tp[K + 1 + k];
+              tb.dv[k] = tp[2 * (K + 1) + k];
+            }
+            float ld;
+            x1[u] = rqs_apply<K, true, kTrainFast>(tb, y1[u], bound, ld);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < CF::KS1; ++t)
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            const int col = r16_in_col<CF>(t, q, jj);
+            float v = 0.f;
+            if (col >= C) {
+              const int di = col - C - q * CF::SQ;  // this quarter's own x1 dims (static select)
+#pragma unroll
+              for (int u = 0; u < CF::SQ; ++u) v = di == u ? x1[u] : v;
+            } else if (col >= 0) {
+              v = ctx[crow * ldc + col];
+            }
+            in[8 * t + jj] = v;
+            if (valid && col >= 0) o.x0[row * (C + S) + col] = v;
+          }
+        const float4* b4 = reinterpret_cast<const float4*>(cur + CF::A_BIAS);
+#pragma unroll
+        for (int b = 0; b < CF::HB; ++b) {
+          const float4 bv = b4[4 * b + q];
+          h1[b] = floatx4{bv.x, bv.y, bv.z, bv.w};
+        }
+        {  // f16x3 GEMM1: the caller guarantees |x|, |ctx| < 2^15 (so the training forward took
+           // the same path; states stay within max(|x|, bound))
+          Frag2 bf[CF::KS1];
+#pragma unroll
+          for (int t = 0; t < CF::KS1; ++t) {
+            float v[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) v[jj] = in[8 * t + jj];
+            bf[t] = split8_f16(v);
+          }
+          gemm_r16_stage<CF::HB, CF::KS1>(h1, cur, lane, bf);
+        }
+        // activation -> natural tanh (stored) ; the next GEMM consumes -tanh/2 (the fold)
+#pragma unroll
+        for (int b = 0; b < CF::HB; ++b) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h1[b][r] = tanh_f<kTrainFast>(h1[b][r] * kInvSigScale);
+          if (valid) *reinterpret_cast<float4*>(o.h1 + row * H + 16 * b + 4 * q) = float4{h1[b][0], h1[b][1], h1[b][2], h1[b][3]};
+          h1[b] = h1[b] * -0.5f;  // GEMM2's operand: -tanh/2 (the packed fold), exact
+        }
+      } else if constexpr (j <= CF::NB2) {
+        constexpr int s = j - 1, T0 = s * CF::KB2;
+        if constexpr (s == 0) {
+          const float4* b4 = reinterpret_cast<const float4*>(cur + CF::B_BIAS);
+#pragma unroll
+          for (int b = 0; b < CF::HB; ++b) {
+            const float4 bv = b4[4 * b + q];
+            h2[b] = floatx4{bv.x, bv.y, bv.z, bv.w};
+          }
+        }
+        gemm_r16_lazy<CF::HB, CF::KB2, T0, false>(h2, cur, lane, h1);
+        if constexpr (s == CF::NB2 - 1) {
+#pragma unroll
+          for (int b = 0; b < CF::HB; ++b) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h2[b][r] = tanh_f<kTrainFast>(h2[b][r] * kInvSigScale);
+            if (valid)
+              *reinterpret_cast<float4*>(o.h2 + row * H + 16 * b + 4 * q) = float4{h2[b][0], h2[b][1], h2[b][2], h2[b][3]};
+            h2[b] = h2[b] * -0.5f;
+          }
+        }
+      } else if constexpr (j < NSTG_F) {
+        constexpr int s = j - 1 - CF::NB2, T0 = s * CF::KB3;
+        if constexpr (s == 0) {
+          const float4* b4 = reinterpret_cast<const float4*>(cur + CF::C_BIAS);
+#pragma unroll
+          for (int b = 0; b < CF::NO; ++b) {
+            const float4 bv = b4[4 * b + q];
+            a3[b] = floatx4{bv.x, bv.y, bv.z, bv.w};
+          }
+        }
+        gemm_r16_lazy<CF::NO, CF::KB3, T0, false>(a3, cur, lane, h2);
+        if constexpr (s == CF::NB3 - 1) {
+          // ---- upper spline VJP (inverse map, libm-grade) -> dPre3 slots (in place of the raw
+          // parameters: dim u's slots are read, then overwritten), g(y2)
+#pragma unroll
+          for (int u = 0; u < CF::DQ; ++u) {
+            __builtin_amdgcn_sched_barrier(0);
+            float uw[K], uh[K], ud[K - 1], gw[K], gh[K], gd[K - 1];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              uw[k] = a3[(u * P + k) >> 2][(u * P + k) & 3];
+              uh[k] = a3[(u * P + K + k) >> 2][(u * P + K + k) & 3];
+            }
+#pragma unroll
+            for (int k = 0; k < K - 1; ++k) ud[k] = a3[(u * P + 2 * K + k) >> 2][(u * P + 2 * K + k) & 3];
+            const float go = valid ? g_in[crow * D + S + q * CF::DQ + u] : 0.f;
+            gy2[u] = rqs_vjp<K, true, kTrainFast>(uw, uh, ud, bound, y2[u], go, gl, gw, gh, gd);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              a3[(u * P + k) >> 2][(u * P + k) & 3] = gw[k];
+              a3[(u * P + K + k) >> 2][(u * P + K + k) & 3] = gh[k];
+            }
+#pragma unroll
+            for (int k = 0; k < K - 1; ++k) a3[(u * P + 2 * K + k) >> 2][(u * P + 2 * K + k) & 3] = gd[k];
+          }
+#pragma unroll
+          for (int sl = CF::DQ * P; sl < BW::NS3; ++sl) a3[sl >> 2][sl & 3] = 0.f;  // pad slots
+          if (valid) {
+            float* dst = o.dp3 + row * (4 * BW::NS3) + q * BW::NS3;
+#pragma unroll
+            for (int b = 0; b < CF::NO; ++b)
+              *reinterpret_cast<float4*>(dst + 4 * b) = float4{a3[b][0], a3[b][1], a3[b][2], a3[b][3]};
+          }
+#pragma unroll
+          for (int b = 0; b < CF::HB; ++b) dacc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+      } else if constexpr (j < NSTG_F + BW::NB3) {
+        // ---- dH2 = dPre3 · W2 (exact fp32), k-step units [U0, U0 + U3)
+        constexpr int sb = j - NSTG_F;
+        bwd_gemm_stage<CF::HB, BW::U3, sb * BW::U3>(dacc, cur, lane, a3);
+        if constexpr (sb == BW::NB3 - 1) {
+#pragma unroll
+          for (int b = 0; b < CF::HB; ++b) {
+            // H2 re-read from this lane's own store (frees 32 VGPRs across the dH2 GEMM)
+            const float4 hv = valid ? *reinterpret_cast<const float4*>(o.h2 + row * H + 16 * b + 4 * q)
+                                    : float4{0.f, 0.f, 0.f, 0.f};
+            const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dp2[b][r] = dacc[b][r] * (1.f - hh[r] * hh[r]);
+            if (valid)
+              *reinterpret_cast<float4*>(o.dp2 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
+            dacc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      } else if constexpr (j < NSTG_F + BW::NB3 + BW::NB2) {
+        // ---- dH1 = dPre2 · W1
+        constexpr int sb = j - NSTG_F - BW::NB3;
+        bwd_gemm_stage<CF::HB, BW::U2, sb * BW::U2>(dacc, cur, lane, dp2);
+        if constexpr (sb == BW::NB2 - 1) {
+#pragma unroll
+          for (int b = 0; b < CF::HB; ++b) {
+            const float4 hv = valid ? *reinterpret_cast<const float4*>(o.h1 + row * H + 16 * b + 4 * q)
+                                    : float4{0.f, 0.f, 0.f, 0.f};
+            const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dp2[b][r] = dacc[b][r] * (1.f - hh[r] * hh[r]);  // now dPre1
+            if (valid)
+              *reinterpret_cast<float4*>(o.dp1 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
+          }
+        }
+      } else {
+        // ---- dx1 = dPre1 · W0[:, C:], lower spline VJP, g(P[l + 1])
+        floatx4 a1[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
+        bwd_gemm_stage<1, H / 4, 0>(a1, cur, lane, dp2);
+        dx1 = a1[0];
+        float gy1[CF::SQ];
+#pragma unroll
+        for (int u = 0; u < CF::SQ; ++u) {
+          __builtin_amdgcn_sched_barrier(0);  // one dim's VJP at a time (its temporaries are large)
+          const int dim = q * CF::SQ + u;
+          const float go = (valid ? g_in[crow * D + dim] : 0.f) + dx1[u];
+          gy1[u] = go;
+          if constexpr (CF::LOWER) {
+            float uw[K], uh[K], ud[K - 1], gw[K], gh[K], gd[K - 1];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              uw[k] = low[dim * K + k];
+              uh[k] = low[S * K + dim * K + k];
+            }
+#pragma unroll
+            for (int k = 0; k < K - 1; ++k) ud[k] = low[2 * S * K + dim * (K - 1) + k];
+            gy1[u] = rqs_vjp<K, true, kTrainFast>(uw, uh, ud, bound, y1[u], go, gl, gw, gh, gd);
+            // sum over the wave's 16 rows (lanes of this quarter), then one LDS add per value
+            auto red = [&](float v) {
+              v += __shfl_xor(v, 1);
+              v += __shfl_xor(v, 2);
+              v += __shfl_xor(v, 4);
+              v += __shfl_xor(v, 8);
+              return v;
+            };
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              const float a = red(gw[k]), b = red(gh[k]);
+              if ((lane & 15) == 0) {
+                atomicAdd(&glow[dim * K + k], a);
+                atomicAdd(&glow[S * K + dim * K + k], b);
+              }
+            }
+#pragma unroll
+            for (int k = 0; k < K - 1; ++k) {
+              const float a = red(gd[k]);
+              if ((lane & 15) == 0) atomicAdd(&glow[2 * S * K + dim * (K - 1) + k], a);
+            }
+          }
+        }
+        if (valid) {
+#pragma unroll
+          for (int u = 0; u < CF::SQ; ++u) o.g_out[row * D + q * CF::SQ + u] = gy1[u];
+#pragma unroll
+          for (int u = 0; u < CF::DQ; ++u) o.g_out[row * D + S + q * CF::DQ + u] = gy2[u];
+        }
+      }
+    });
+  }
+  __syncthreads();
+  if constexpr (CF::LOWER)
+    for (int i = threadIdx.x; i < NLOW; i += blockDim.x) atomicAdd(&o.g_low[i], glow[i]);
+}
+
+}  // namespace naz

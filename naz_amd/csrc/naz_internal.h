@@ -71,6 +71,16 @@ int coupling_log_prob(const naz_coupling_desc* d, const void* packed, const floa
 int coupling_sample(const naz_coupling_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx,
                     int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B,
                     hipStream_t s);
+int64_t coupling_bwd_packed_bytes(const naz_coupling_desc* d);
+int coupling_pack_bwd(const naz_coupling_desc* d, const float* flat, void* packed, hipStream_t s);
+int coupling_log_prob_train(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx,
+                            const float* ctx, int64_t ldc, const float* low, const float* high, float* out_lp,
+                            float* states, int64_t B, hipStream_t s);
+int coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const void* packed_bwd, const float* flat,
+                       int layer, const float* state, const float* ctx, int64_t ldc, const float* g_in,
+                       const float* g_lp, float* h1, float* h2, float* dp1, float* dp2, float* dp3, float* x0,
+                       float* g_out, float* g_low, int64_t B, hipStream_t s);
+int coupling_dp3_columns(const naz_coupling_desc* d, int* rows);
 
 int cnf_supported(const naz_cnf_desc* d);
 int64_t cnf_param_count(const naz_cnf_desc* d);

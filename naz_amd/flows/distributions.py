@@ -85,6 +85,9 @@ class TransformedDistribution:
     def log_prob(self, value: torch.Tensor, bounds=None) -> torch.Tensor:
         y, lead = _rows2d(value)
         if self._needs_graph(y):
+            if self._fused_ok() and self._fused.train_ready(y, self._context):
+                # the NLL step of an nsc flow: one fused forward + per-layer fused backward
+                return self._fused.train_log_prob(y, self._context, bounds).reshape(lead)
             return self._log_prob_graph(y, bounds).reshape(lead)
         lp = torch.zeros(y.shape[0], device=y.device, dtype=torch.float32)
         return self._log_prob_into(y, lp, bounds).reshape(lead)

@@ -96,8 +96,112 @@ class _FusedCoupling:
             self.desc = ops.coupling_desc(D, C, S, K, len(self.layers), H, act, lower, bound, self.mode)
             flat = torch.cat([p.detach().reshape(-1) for p in ps])
             self._packed = ops.coupling_pack(self.desc, flat, self._packed)
+            self._flat, self._packed_bwd = flat, None
             self._sig = sig
         return self._packed
+
+    # ---- the fused NLL training step (a10; coupling_train.h)
+    F16_DATA_LIMIT = 32768.0
+
+    def train_ready(self, x, context) -> bool:
+        """The fused training path applies: the 16-row f16x3 image, data and context inside
+        fp16's range (the kernels' GEMM1 split; one small device reduction + host read), and no
+        gradient wanted for x or the context (train's data).  NAZ_TRAIN_FUSED=0 disables it."""
+        if _TRAIN_FUSED == "0" or x.dim() != 2 or x.requires_grad or (context is not None and context.requires_grad):
+            return False
+        self.packed()
+        if self.mode != "f16x3r16":
+            return False
+        m = x.detach().abs().amax()
+        if context is not None and context.numel():
+            m = torch.maximum(m, context.detach().abs().amax())
+        return float(m) < self.F16_DATA_LIMIT
+
+    def packed_bwd(self) -> torch.Tensor:
+        packed = self.packed()
+        if getattr(self, "_packed_bwd", None) is None:
+            self._packed_bwd = ops.coupling_pack_bwd(self.desc, self._flat)
+        return packed, self._packed_bwd, self._flat
+
+    def train_log_prob(self, x, context=None, bounds=None):
+        """log p(x | ctx) recorded as ONE autograd node whose backward is the fused per-layer
+        HIP backward (naz_coupling_bwd_layer) + weight-gradient GEMMs (naz_gemm)."""
+        return _CouplingTrainFn.apply(x, context, bounds, self, *self.params())
+
+
+_TRAIN_FUSED = __import__("os").environ.get("NAZ_TRAIN_FUSED", "1")
+
+
+class _CouplingTrainFn(torch.autograd.Function):
+    """NormalizingFlow.log_prob of an nsc flow under autograd (naz train's loss, train_flows.py:
+    195, 208).  forward: naz_coupling_log_prob_train (all layers, one launch, layer inputs
+    saved); backward: for l = 0 .. L-1 one naz_coupling_bwd_layer launch (recomputes the layer's
+    conditioner, spline VJPs, exact-fp32 MFMA dX chain, lower-spline gradients) and three
+    batch-reduction GEMMs for dW / db."""
+
+    @staticmethod
+    def forward(ctx, x, context, bounds, plan, *params):
+        packed, pbwd, flat = plan.packed_bwd()
+        d = plan.desc
+        B = x.shape[0]
+        low = high = None
+        if bounds is not None:
+            low = bounds["low"].to(x.device, torch.float32).contiguous()
+            high = bounds["high"].to(x.device, torch.float32).contiguous()
+        states = torch.empty((d.L + 1, B, d.D), device=x.device, dtype=torch.float32)
+        lp = ops.coupling_log_prob_train(d, packed, x.detach(), None if context is None else context.detach(),
+                                         low, high, states)
+        ctx.plan, ctx.packed, ctx.pbwd, ctx.flat = plan, packed, pbwd, flat
+        ctx.save_for_backward(states, context)
+        ctx.n_params = len(params)
+        return lp
+
+    @staticmethod
+    def backward(ctx, g_lp):
+        states, context = ctx.saved_tensors
+        plan = ctx.plan
+        d = plan.desc
+        D, C, S, K, H, act, lower, bound = plan.shape
+        L, B = d.L, states.shape[1]
+        dev = states.device
+        g_lp = g_lp.contiguous().float()
+        g = (-states[0]) * g_lp[:, None]  # d/dz of the Normal(0, I) base log-density
+        g = g.contiguous()
+        g_next = torch.empty_like(g)
+        rows = plan.__dict__.get("_dp3_rows")
+        if rows is None or rows.device != dev:
+            rows = ops.coupling_dp3_columns(d).to(dev)
+            plan._dp3_rows = rows
+        valid = rows >= 0
+        cols, orow = torch.nonzero(valid).flatten(), rows[valid]
+        f32 = dict(device=dev, dtype=torch.float32)
+        bufs = {"h1": torch.empty((B, H), **f32), "h2": torch.empty((B, H), **f32),
+                "dp1": torch.empty((B, H), **f32), "dp2": torch.empty((B, H), **f32),
+                "dp3": torch.empty((B, rows.numel()), **f32), "x0": torch.empty((B, C + S), **f32)}
+        n_low = S * (3 * K - 1) if lower else 0
+        g_low = torch.zeros((L, max(n_low, 1)), **f32)
+        P = 3 * K - 1
+        per = 9 if lower else 6
+        grads = [None] * ctx.n_params
+        gw2p = torch.empty((rows.numel(), H), **f32)
+        gb2p = torch.empty((rows.numel(),), **f32)
+        for l in range(L):
+            ops.coupling_bwd_layer(d, ctx.packed, ctx.pbwd, ctx.flat, l, states[l + 1], context, g, g_lp, bufs, g_next,
+                                   g_low[l] if lower else None)
+            gW0, gb0 = torch.empty((H, C + S), **f32), torch.empty((H,), **f32)
+            gW1, gb1 = torch.empty((H, H), **f32), torch.empty((H,), **f32)
+            ops.gemm(bufs["dp1"].t(), bufs["x0"], out=gW0, rowsum=gb0)
+            ops.gemm(bufs["dp2"].t(), bufs["h1"], out=gW1, rowsum=gb1)
+            ops.gemm(bufs["dp3"].t(), bufs["h2"], out=gw2p, rowsum=gb2p)
+            gW2 = torch.zeros(((D - S) * P, H), **f32).index_copy_(0, orow, gw2p.index_select(0, cols))
+            gb2 = torch.zeros(((D - S) * P,), **f32).index_copy_(0, orow, gb2p.index_select(0, cols))
+            out = [gW0, gb0, gW1, gb1, gW2, gb2]
+            if lower:
+                gl = g_low[l]
+                out += [gl[:S * K].view(S, K), gl[S * K:2 * S * K].view(S, K), gl[2 * S * K:].view(S, K - 1)]
+            grads[l * per:(l + 1) * per] = out
+            g, g_next = g_next, g
+        return (None, None, None, None, *grads)
 
     def log_prob(self, x, context=None, bounds=None, out=None):
         low = high = None

@@ -7,6 +7,7 @@ without copies.
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import Optional, Tuple
 
 import torch
@@ -520,6 +521,64 @@ def coupling_log_prob(d: CouplingDesc, packed: Tensor, x: Tensor, context: Optio
     check(lib().naz_coupling_log_prob(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out), B,
                                       _stream(dev)), "coupling_log_prob")
     return out
+
+
+# ----------------------------------------------------------------------------- a10: fused NLL step
+def coupling_pack_bwd(d: CouplingDesc, flat: Tensor, out: Optional[Tensor] = None) -> Tensor:
+    """Per-layer fp32 backward images (naz_coupling_pack_bwd) of the flat natural parameters."""
+    n = int(lib().naz_coupling_bwd_packed_bytes(d))
+    if n < 0:
+        raise RuntimeError(f"coupling_pack_bwd: {lib().naz_last_error().decode()}")
+    dev = _dev(flat, out)
+    if out is None or out.numel() * 4 != n:
+        out = torch.empty(n // 4, device=dev, dtype=torch.float32)
+    check(lib().naz_coupling_pack_bwd(d, _p(flat.contiguous()), _p(out), _stream(dev)), "coupling_pack_bwd")
+    return out
+
+
+def coupling_log_prob_train(d: CouplingDesc, packed: Tensor, x: Tensor, context: Optional[Tensor],
+                            low: Optional[Tensor], high: Optional[Tensor], states: Tensor,
+                            out: Optional[Tensor] = None) -> Tensor:
+    """log p with the reference walk's libm-grade math; states [L+1, B, D] receives every
+    layer's input (states[0] = z) for the backward (naz_coupling_log_prob_train)."""
+    dev = _dev(packed, x, context, low, high, out, states)
+    x, ldx = _rows(x)
+    B = x.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    if states.shape != (d.L + 1, B, d.D) or not states.is_contiguous():
+        raise ValueError(f"coupling_log_prob_train: states must be contiguous {(d.L + 1, B, d.D)}")
+    if out is None:
+        out = torch.empty((B,), device=dev, dtype=torch.float32)
+    check(lib().naz_coupling_log_prob_train(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out),
+                                            _p(states), B, _stream(dev)), "coupling_log_prob_train")
+    return out
+
+
+def coupling_dp3_columns(d: CouplingDesc) -> Tensor:
+    """DenseNN output row of every dp3 column of naz_coupling_bwd_layer (-1 = padding)."""
+    n = int(lib().naz_coupling_dp3_columns(d, None))
+    if n < 0:
+        raise RuntimeError(f"coupling_dp3_columns: {lib().naz_last_error().decode()}")
+    rows = (C.c_int * n)()
+    lib().naz_coupling_dp3_columns(d, rows)
+    return torch.tensor(list(rows), dtype=torch.int64)
+
+
+def coupling_bwd_layer(d: CouplingDesc, packed: Tensor, packed_bwd: Tensor, flat: Tensor, layer: int, state: Tensor,
+                       context: Optional[Tensor], g_in: Tensor, g_lp: Tensor, bufs: dict, g_out: Tensor,
+                       g_low: Optional[Tensor]) -> None:
+    """One layer of the fused NLL backward (naz_coupling_bwd_layer); ``bufs`` holds the
+    contiguous h1, h2, dp1, dp2 [B, H], dp3 [B, ncol], x0 [B, C+S] outputs."""
+    dev = _dev(packed, packed_bwd, flat, state, context, g_in, g_lp, g_out, g_low)
+    B = state.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    for t in (state, g_in, g_lp, g_out) + tuple(bufs[k] for k in ("h1", "h2", "dp1", "dp2", "dp3", "x0")):
+        if not t.is_contiguous():
+            raise ValueError("coupling_bwd_layer: buffers must be contiguous")
+    check(lib().naz_coupling_bwd_layer(d, _p(packed), _p(packed_bwd), _p(flat), int(layer), _p(state), _p(context), ldc,
+                                       _p(g_in), _p(g_lp), _p(bufs["h1"]), _p(bufs["h2"]), _p(bufs["dp1"]),
+                                       _p(bufs["dp2"]), _p(bufs["dp3"]), _p(bufs["x0"]), _p(g_out), _p(g_low), B,
+                                       _stream(dev)), "coupling_bwd_layer")
 
 
 def coupling_sample(d: CouplingDesc, packed: Tensor, z: Tensor, context: Optional[Tensor] = None,

@@ -1282,10 +1282,10 @@ struct CouplingOps {
                        float bound, hipStream_t s) {
     if constexpr (R16OK) {
       if (B == 0) return 0;
-      const int64_t ntiles = (B + kR16Rows - 1) / kR16Rows;
-      const int64_t grid = std::min<int64_t>(ntiles, 1024);
-      const size_t lds = (size_t)(2 * kX6Slot + CR::S * (3 * CR::K - 1) + kR16Waves) * 4;
-      hipLaunchKernelGGL((coupling_bwd_r16_kernel<CR>), dim3((unsigned)grid), dim3(kR16Rows * 4), lds, s,
+      const int64_t ntiles = (B + 16 * kBwdWaves - 1) / (16 * kBwdWaves);
+      const int64_t grid = std::min<int64_t>(ntiles, 2048);
+      const size_t lds = (size_t)(2 * BwdSlot<CR>::v + CR::S * (3 * CR::K - 1)) * 4;
+      hipLaunchKernelGGL((coupling_bwd_r16_kernel<CR>), dim3((unsigned)grid), dim3(kBwdWaves * 64), lds, s,
                          reinterpret_cast<const float*>(packed), reinterpret_cast<const float*>(bwd), flat, l, state,
                          ctx, ldc, g_in, g_lp, o, B, bound);
       return check_launch("coupling_bwd_r16_kernel");

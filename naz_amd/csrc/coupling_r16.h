@@ -266,11 +266,13 @@ NAZ_DEV void gemm_r16_lazy(floatx4 (&acc)[NB], const float* __restrict__ stage, 
 // The GEMMs keep the f16x3 split.  Activated values are -tanh/2 (the fold's convention), so the
 // packed image is the same.
 constexpr float kInvSigScale = 0.34657359027997264f;  // 1 / kSigScale = ln 2 / 2
-// NAZ_TRAIN_FAST: hardware transcendentals in the training kernels' activations and splines
-#ifdef NAZ_TRAIN_FAST
-constexpr bool kTrainFast = true;
-#else
+// Training kernels' math: by default the fused inference kernel's own (sigmoid-fold activation,
+// select-first spline on hardware transcendentals, table lower spline), so the NLL step's loss is
+// the log_prob the metric kernel computes.  NAZ_TRAIN_ACCURATE: libm-grade tanh and spline.
+#ifdef NAZ_TRAIN_ACCURATE
 constexpr bool kTrainFast = false;
+#else
+constexpr bool kTrainFast = true;
 #endif
 NAZ_DEV float acc_fold(float v) { return -0.5f * tanh_f<kTrainFast>(v * kInvSigScale); }
 
@@ -376,7 +378,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
         for (int u = 0; u < CF::SQ; ++u) {
           if constexpr (DIR_INV && CF::LOWER) {
             float ld;
-            if constexpr (VAR == 1) {
+            if constexpr (VAR == 1 && !kTrainFast) {
               SplineTables<CF::K> tb;
               const float* tp = cur + CF::A_TBL + (q * CF::SQ + u) * CF::TBL;
 #pragma unroll
@@ -460,8 +462,8 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
           for (int r = 0; r < 4; ++r) acc1[b][r] = sig_fold(acc1[b][r]);
         constexpr bool kLazyAct = false;
 #else
-        constexpr bool kLazyAct = VAR == 0;  // activated per k-step inside gemm_r16_lazy
-        if constexpr (VAR == 1) {
+        constexpr bool kLazyAct = VAR == 0 || kTrainFast;  // activated per k-step inside gemm_r16_lazy
+        if constexpr (!kLazyAct) {
 #pragma unroll
           for (int b = 2 * T0; b < 2 * (T0 + CF::KB2); ++b)
 #pragma unroll
@@ -489,8 +491,8 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
           for (int r = 0; r < 4; ++r) acc2[b][r] = sig_fold(acc2[b][r]);
         constexpr bool kLazyAct = false;
 #else
-        constexpr bool kLazyAct = VAR == 0;
-        if constexpr (VAR == 1) {
+        constexpr bool kLazyAct = VAR == 0 || kTrainFast;
+        if constexpr (!kLazyAct) {
 #pragma unroll
           for (int b = 2 * T0; b < 2 * (T0 + CF::KB3); ++b)
 #pragma unroll
@@ -527,7 +529,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
         ud[k] = acc3[sd >> 2][sd & 3];
       }
       float ld;
-      if constexpr (VAR == 1) {
+      if constexpr (VAR == 1 && !kTrainFast) {
         SplineTables<CF::K> tb;
         build_tables<CF::K, kTrainFast>(uw, uh, ud, bound, tb);
         zu[u] = rqs_apply<CF::K, DIR_INV, kTrainFast>(tb, zu[u], bound, ld);

@@ -32,7 +32,9 @@ template <class CF>
 struct BwdR16 {
   static constexpr int NS3 = 4 * CF::NO;  // GEMM3 slots per quarter = dH2 k-steps
   static constexpr int HB = CF::HB;
-  static constexpr int U3ALL = NS3 / 4, U2ALL = CF::H / 16 * 4 / 4;  // 4-k-step units: dH2, dH1 (= H/4)
+  // units of 4 MFMA k-steps (one 16x16x4 k-step takes one value from each quarter): dH2 has NS3
+  // k-steps, dH1 and dx1 H/4 (each quarter feeds its H/4 own hidden features)
+  static constexpr int U3ALL = NS3 / 4, UH = CF::H / 16;
   static constexpr int pick_u(int nb, int units) {
     int best = 1;
     for (int u = 1; u <= units; ++u)
@@ -40,12 +42,13 @@ struct BwdR16 {
     return best;
   }
   static constexpr int U3 = pick_u(HB, U3ALL), NB3 = U3ALL / U3;   // dH2 stages
-  static constexpr int U2 = pick_u(HB, CF::H / 4), NB2 = (CF::H / 4) / U2;  // dH1 stages
-  static constexpr int S3 = HB * U3 * 256, S2 = HB * U2 * 256, SA = (CF::H / 4) * 256;
+  static constexpr int U2 = pick_u(HB, UH), NB2 = UH / U2;  // dH1 stages
+  static constexpr int S3 = HB * U3 * 256, S2 = HB * U2 * 256, SA = UH * 256;
   static constexpr int OFF2 = NB3 * S3, OFFA = OFF2 + NB2 * S2;
   static constexpr int LAYER = OFFA + SA;
   static constexpr int NSTG = NB3 + NB2 + 1;
   static_assert(CF::SQ <= 4, "dx1 block holds at most 4 lower dims per quarter");
+  static_assert(NS3 % 4 == 0 && CF::H % 16 == 0, "k-step units");
   static constexpr __host__ __device__ int stage_off(int j) { return j < NB3 ? j * S3 : (j < NB3 + NB2 ? OFF2 + (j - NB3) * S2 : OFFA); }
   static constexpr __host__ __device__ int stage_size(int j) { return j < NB3 ? S3 : (j < NB3 + NB2 ? S2 : SA); }
   // DenseNN output row of quarter q's GEMM3 slot s (-1 = pad)
@@ -114,6 +117,19 @@ NAZ_DEV void bwd_gemm_stage(floatx4 (&acc)[NBLK], const float* __restrict__ stag
   }
 }
 
+// the training forward's activation of a packed (sigmoid-folded) accumulator: -tanh(a)/2
+NAZ_DEV float train_fold(float v) {
+  if constexpr (kTrainFast) return sig_fold(v);
+  else return acc_fold(v);
+}
+
+template <int K>
+NAZ_DEV float train_vjp_inv(const float* uw, const float* uh, const float* ud, float bound, float y, float g_x,
+                            float g_ld, const RqsConsts<K, true>& rc, float* gw, float* gh, float* gd) {
+  if constexpr (kTrainFast) return rqs_vjp_select_inv<K>(uw, uh, ud, y, g_x, g_ld, bound, rc, gw, gh, gd);
+  else return rqs_vjp<K, true, false>(uw, uh, ud, bound, y, g_x, g_ld, gw, gh, gd);
+}
+
 struct BwdOut {
   float* h1;   // [B, H]   H1 (natural tanh)
   float* h2;   // [B, H]   H2
@@ -125,18 +141,33 @@ struct BwdOut {
   float* g_low;       // [S (3K - 1)] lower-spline parameter gradients (atomically accumulated)
 };
 
+// Workgroups of NW waves (16 rows each).  NW = 4: two independent workgroups per CU, so one's
+// VALU phases (activations, spline VJPs) overlap the other's MFMA phases; the waves of ONE
+// workgroup run the same phase between stage barriers.
+#ifndef NAZ_BWD_WAVES
+#define NAZ_BWD_WAVES 4
+#endif
+constexpr int kBwdWaves = NAZ_BWD_WAVES;
+
 template <class CF>
-__global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
+struct BwdSlot {  // LDS ring slot: the largest forward or backward stage
+  static constexpr int v = std::max({CF::A_SIZE, CF::B_SIZE, CF::C_SIZE, BwdR16<CF>::S3, BwdR16<CF>::S2,
+                                     BwdR16<CF>::SA});
+};
+
+template <class CF>
+__global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
     const float* __restrict__ packed, const float* __restrict__ bwd, const float* __restrict__ flat, int l,
     const float* __restrict__ state, const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ g_in,
     const float* __restrict__ g_lp, BwdOut o, int64_t B, float bound) {
   using BW = BwdR16<CF>;
   constexpr int K = CF::K, P = CF::P, H = CF::H, D = CF::D, C = CF::C, S = CF::S;
   constexpr int NLOW = S * (3 * K - 1);
+  constexpr int SLOT = BwdSlot<CF>::v, ROWS = 16 * kBwdWaves;
   extern __shared__ float4 lds4[];
   float* const slot0 = reinterpret_cast<float*>(lds4);
-  float* const slot1 = slot0 + kX6Slot;
-  float* const glow = slot1 + kX6Slot;  // [NLOW] per-workgroup lower-spline gradient sums
+  float* const slot1 = slot0 + SLOT;
+  float* const glow = slot1 + SLOT;  // [NLOW] per-workgroup lower-spline gradient sums
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int q = lane >> 4;
@@ -145,15 +176,16 @@ __global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
   const float* lp = packed + (int64_t)l * CF::LAYER;
   const float* lb = bwd + (int64_t)l * BW::LAYER;
   const float* low = flat + (int64_t)l * CF::FLAT + CF::N_W0 + CF::N_B0 + CF::N_W1 + CF::N_B1 + CF::N_W2 + CF::N_B2;
-  const int64_t ntiles = (B + kR16Rows - 1) / kR16Rows;
+  const int64_t ntiles = (B + ROWS - 1) / ROWS;
+  const RqsConsts<K, true> rc(bound);
   constexpr int NSTG_F = CF::NSTG, NSTG = NSTG_F + BW::NSTG;
   auto stage_src = [&](int j) -> const float* { return j < NSTG_F ? lp + CF::stage_off(j) : lb + BW::stage_off(j - NSTG_F); };
 
   int g = 0;  // global stage counter: stage g lives in slot (g & 1)
   int64_t tile = blockIdx.x;
-  if (tile < ntiles) stage_issue<CF::A_SIZE, kR16Waves>(slot0, lp);  // A32 image never used: f16x3 path only
+  if (tile < ntiles) stage_issue<CF::A_SIZE, kBwdWaves>(slot0, lp);  // A32 image never used: f16x3 path only
   for (; tile < ntiles; tile += gridDim.x) {
-    const int64_t row = tile * kR16Rows + wave * 16 + (lane & 15);
+    const int64_t row = tile * ROWS + wave * 16 + (lane & 15);
     const bool valid = row < B;
     const int64_t crow = valid ? row : 0;
     float y1[CF::SQ], y2[CF::DQ], x1[CF::SQ];
@@ -177,11 +209,11 @@ __global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
       const float* cur = (g & 1) ? slot1 : slot0;
       float* nxt = (g & 1) ? slot0 : slot1;
       if constexpr (j + 1 < NSTG_F) {
-        stage_issue<CF::stage_size(j + 1), kR16Waves>(nxt, stage_src(j + 1));
+        stage_issue<CF::stage_size(j + 1), kBwdWaves>(nxt, stage_src(j + 1));
       } else if constexpr (j + 1 < NSTG) {
-        stage_issue<BW::stage_size(j + 1 - NSTG_F), kR16Waves>(nxt, stage_src(j + 1));
+        stage_issue<BW::stage_size(j + 1 - NSTG_F), kBwdWaves>(nxt, stage_src(j + 1));
       } else {
-        if (has_next) stage_issue<CF::A_SIZE, kR16Waves>(nxt, lp);
+        if (has_next) stage_issue<CF::A_SIZE, kBwdWaves>(nxt, lp);
       }
       ++g;
 
@@ -191,16 +223,20 @@ __global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
         for (int u = 0; u < CF::SQ; ++u) {
           x1[u] = y1[u];
           if constexpr (CF::LOWER) {
-            SplineTables<K> tb;
             const float* tp = cur + CF::A_TBL + (q * CF::SQ + u) * CF::TBL;
-#pragma unroll
-            for (int k = 0; k <= K; ++k) {
-              tb.cw[k] = tp[k];
-              tb.ch[k] = tp[K + 1 + k];
-              tb.dv[k] = tp[2 * (K + 1) + k];
-            }
             float ld;
-            x1[u] = rqs_apply<K, true, kTrainFast>(tb, y1[u], bound, ld);
+            if constexpr (kTrainFast) {
+              x1[u] = rqs_table<K, true>(tp, y1[u], bound, ld);
+            } else {
+              SplineTables<K> tb;
+#pragma unroll
+              for (int k = 0; k <= K; ++k) {
+                tb.cw[k] = tp[k];
+                tb.ch[k] = tp[K + 1 + k];
+                tb.dv[k] = tp[2 * (K + 1) + k];
+              }
+              x1[u] = rqs_apply<K, true, false>(tb, y1[u], bound, ld);
+            }
           }
         }
 #pragma unroll
@@ -241,9 +277,10 @@ __global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
 #pragma unroll
         for (int b = 0; b < CF::HB; ++b) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) h1[b][r] = tanh_f<kTrainFast>(h1[b][r] * kInvSigScale);
-          if (valid) *reinterpret_cast<float4*>(o.h1 + row * H + 16 * b + 4 * q) = float4{h1[b][0], h1[b][1], h1[b][2], h1[b][3]};
-          h1[b] = h1[b] * -0.5f;  // GEMM2's operand: -tanh/2 (the packed fold), exact
+          for (int r = 0; r < 4; ++r) h1[b][r] = train_fold(h1[b][r]);  // -tanh/2: GEMM2's operand
+          if (valid)
+            *reinterpret_cast<float4*>(o.h1 + row * H + 16 * b + 4 * q) =
+                float4{-2.f * h1[b][0], -2.f * h1[b][1], -2.f * h1[b][2], -2.f * h1[b][3]};
         }
       } else if constexpr (j <= CF::NB2) {
         constexpr int s = j - 1, T0 = s * CF::KB2;
@@ -260,10 +297,10 @@ __global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
 #pragma unroll
           for (int b = 0; b < CF::HB; ++b) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) h2[b][r] = tanh_f<kTrainFast>(h2[b][r] * kInvSigScale);
+            for (int r = 0; r < 4; ++r) h2[b][r] = train_fold(h2[b][r]);
             if (valid)
-              *reinterpret_cast<float4*>(o.h2 + row * H + 16 * b + 4 * q) = float4{h2[b][0], h2[b][1], h2[b][2], h2[b][3]};
-            h2[b] = h2[b] * -0.5f;
+              *reinterpret_cast<float4*>(o.h2 + row * H + 16 * b + 4 * q) =
+                  float4{-2.f * h2[b][0], -2.f * h2[b][1], -2.f * h2[b][2], -2.f * h2[b][3]};
           }
         }
       } else if constexpr (j < NSTG_F) {
@@ -292,7 +329,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
 #pragma unroll
             for (int k = 0; k < K - 1; ++k) ud[k] = a3[(u * P + 2 * K + k) >> 2][(u * P + 2 * K + k) & 3];
             const float go = valid ? g_in[crow * D + S + q * CF::DQ + u] : 0.f;
-            gy2[u] = rqs_vjp<K, true, kTrainFast>(uw, uh, ud, bound, y2[u], go, gl, gw, gh, gd);
+            gy2[u] = train_vjp_inv<K>(uw, uh, ud, bound, y2[u], go, gl, rc, gw, gh, gd);
 #pragma unroll
             for (int k = 0; k < K; ++k) {
               a3[(u * P + k) >> 2][(u * P + k) & 3] = gw[k];
@@ -349,7 +386,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
       } else {
         // ---- dx1 = dPre1 · W0[:, C:], lower spline VJP, g(P[l + 1])
         floatx4 a1[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
-        bwd_gemm_stage<1, H / 4, 0>(a1, cur, lane, dp2);
+        bwd_gemm_stage<1, BW::UH, 0>(a1, cur, lane, dp2);
         dx1 = a1[0];
         float gy1[CF::SQ];
 #pragma unroll
@@ -367,7 +404,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, 2) coupling_bwd_r16_kernel(
             }
 #pragma unroll
             for (int k = 0; k < K - 1; ++k) ud[k] = low[2 * S * K + dim * (K - 1) + k];
-            gy1[u] = rqs_vjp<K, true, kTrainFast>(uw, uh, ud, bound, y1[u], go, gl, gw, gh, gd);
+            gy1[u] = train_vjp_inv<K>(uw, uh, ud, bound, y1[u], go, gl, rc, gw, gh, gd);
             // sum over the wave's 16 rows (lanes of this quarter), then one LDS add per value
             auto red = [&](float v) {
               v += __shfl_xor(v, 1);

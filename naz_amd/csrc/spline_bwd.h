@@ -174,3 +174,124 @@ NAZ_DEV float rqs_vjp(const float* uw, const float* uh, const float* ud, float b
 }
 
 }  // namespace naz
+
+namespace naz {
+
+// Lean VJP of the INVERSE map in the select-first parameterisation (rqs_select<K, true>, the
+// fused kernels' evaluator): knot k of either table is −B + 2B(k·m + s·E_k/E_K) from the prefix
+// sums E of the softmax numerators.  Only the selected bin's two knots per table and two slopes
+// carry gradient, so the knot -> fraction -> softmax chain collapses to closed forms:
+//   g_u_i = f_i · 2Bs · (A·[i < idx] + Bv·[i ≤ idx] − A·F_idx − Bv·F_{idx+1}),
+// A / Bv = the gradients on the bin's left / right knot (0 for the pinned end knots), F_k = E_k/E_K,
+// and only ud[idx−1], ud[idx] (the bin's interior slopes) get gradient.  Hardware
+// transcendentals throughout.  Returns dL/dy; writes the unnormalised-parameter gradients.
+template <int K>
+NAZ_DEV float rqs_vjp_select_inv(const float* uw, const float* uh, const float* ud, float y, float g_x, float g_ld,
+                                 float bound, const RqsConsts<K, true>& rc, float* gw, float* gh, float* gd) {
+  using M = Math<true>;
+  constexpr float kL2E = 1.44269504088896341f;
+  float ew[K], eh[K], Ew[K + 1], Eh[K + 1];
+  {
+    float mw = uw[0], mh = uh[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) {
+      mw = fmaxf(mw, uw[k]);
+      mh = fmaxf(mh, uh[k]);
+    }
+    const float mwl = mw * kL2E, mhl = mh * kL2E;
+    Ew[0] = 0.f;
+    Eh[0] = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      ew[k] = __builtin_amdgcn_exp2f(__builtin_fmaf(uw[k], kL2E, -mwl));
+      eh[k] = __builtin_amdgcn_exp2f(__builtin_fmaf(uh[k], kL2E, -mhl));
+      Ew[k + 1] = Ew[k] + ew[k];
+      Eh[k + 1] = Eh[k] + eh[k];
+    }
+  }
+  const float rw = M::rcp(Ew[K]), rh = M::rcp(Eh[K]);
+  const float Aw = rc.cA * rw, Ah = rc.cA * rh;
+  // search on the height knots (inverse map), select the bin's prefix sums and slopes
+  float s0 = 0.f, s1 = Eh[1], o0 = 0.f, o1 = Ew[1], udl = ud[0], udh = ud[0];
+  int idx = 0;
+#pragma unroll
+  for (int k = 1; k < K; ++k) {
+    const bool s = y >= __builtin_fmaf(Ah, Eh[k], rc.key[k]);
+    s0 = s ? Eh[k] : s0;
+    s1 = s ? Eh[k + 1] : s1;
+    o0 = s ? Ew[k] : o0;
+    o1 = s ? Ew[k + 1] : o1;
+    udl = s ? ud[k - 1] : udl;
+    if (k < K - 1) udh = s ? ud[k] : udh;
+    idx += s ? 1 : 0;
+  }
+  const bool first = idx == 0, last = idx == K - 1;
+  const float fi = (float)idx;
+  const float ch0 = __builtin_fmaf(Ah, s0, __builtin_fmaf(rc.ms, fi, rc.nb));
+  const float ch1 = last ? bound : __builtin_fmaf(Ah, s1, __builtin_fmaf(rc.ms, fi + 1.f, rc.nb));
+  const float cw0 = __builtin_fmaf(Aw, o0, __builtin_fmaf(rc.mo, fi, rc.nb));
+  const float cw1 = last ? bound : __builtin_fmaf(Aw, o1, __builtin_fmaf(rc.mo, fi + 1.f, rc.nb));
+  // slopes: softplus and its derivative (sigmoid) from one exp
+  auto sp = [](float u, float& sig) {
+    const float e = M::exp(-fabsf(u));
+    const float r = M::rcp(1.f + e);
+    sig = u >= 0.f ? r : e * r;
+    return u > 20.f ? u : fmaxf(u, 0.f) + M::log1p(e);
+  };
+  float sgl, sgh;
+  const float spl = sp(udl, sgl), sph = sp(udh, sgh);
+  const float d0 = first ? 1.f - kMinDerivative : kMinDerivative + spl;
+  const float d1 = last ? 1.f - kMinDerivative : kMinDerivative + sph;
+  const float W = cw1 - cw0, H = ch1 - ch0, iW = M::rcp(W), delta = H * iW;
+  const float T1 = (d0 + d1) - 2.f * delta;
+  const float dy = y - ch0;
+  const float a = dy * T1 + H * (delta - d0);
+  const float b = H * d0 - dy * T1;
+  const float c = -delta * dy;
+  const float th = (2.f * c) * M::rcp(-b - M::sqrt(fmaxf(b * b - 4.f * a * c, 0.f)));
+  const float om = 1.f - th, tt = th * om;
+  const float N = delta * th * th + d0 * tt;
+  const float Dn = delta + T1 * tt;
+  const float G = d1 * th * th + 2.f * delta * tt + d0 * om * om;
+  const float iDn = M::rcp(Dn), iG = M::rcp(G), iDn2 = iDn * iDn;
+  const float Np = 2.f * delta * th + d0 * (1.f - 2.f * th);
+  const float Dp = T1 * (1.f - 2.f * th);
+  const float F_th = H * (Np * Dn - N * Dp) * iDn2;
+  const float F_H = N * iDn;
+  const float F_dl = H * (th * th * Dn - N * (1.f - 2.f * tt)) * iDn2;
+  const float F_d0 = H * tt * (Dn - N) * iDn2;
+  const float F_d1 = -H * N * tt * iDn2;
+  const float Gp = 2.f * d1 * th + 2.f * delta * (1.f - 2.f * th) - 2.f * d0 * om;
+  const float L_th = Gp * iG - 2.f * Dp * iDn;
+  const float L_dl = 2.f * M::rcp(delta) + 2.f * tt * iG - 2.f * (1.f - 2.f * tt) * iDn;
+  const float L_d0 = om * om * iG - 2.f * tt * iDn;
+  const float L_d1 = th * th * iG - 2.f * tt * iDn;
+  const float gth = g_x * W - g_ld * L_th;
+  const float r = gth * M::rcp(F_th);
+  float gW = g_x * th, gH = -r * F_H;
+  const float gdl = -g_ld * L_dl - r * F_dl;
+  const float gd0 = -g_ld * L_d0 - r * F_d0;
+  const float gd1 = -g_ld * L_d1 - r * F_d1;
+  const float gcw0 = g_x, gch0 = -r;
+  gH += gdl * iW;
+  gW += -gdl * delta * iW;
+  // left / right knot gradients (pinned end knots carry none)
+  const float Aw_ = first ? 0.f : gcw0 - gW, Bw_ = last ? 0.f : gW;
+  const float Ah_ = first ? 0.f : gch0 - gH, Bh_ = last ? 0.f : gH;
+  const float Tw = (Aw_ * o0 + Bw_ * o1) * rw, Th = (Ah_ * s0 + Bh_ * s1) * rh;
+  const float inside = (y >= -bound && y <= bound) ? 1.f : 0.f;  // identity tails: no parameter gradient
+  const float cwk = rc.cA * rw * inside, chk = rc.cA * rh * inside;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const float sw_ = (i < idx ? Aw_ : 0.f) + (i <= idx ? Bw_ : 0.f) - Tw;
+    const float sh_ = (i < idx ? Ah_ : 0.f) + (i <= idx ? Bh_ : 0.f) - Th;
+    gw[i] = ew[i] * cwk * sw_;
+    gh[i] = eh[i] * chk * sh_;
+  }
+#pragma unroll
+  for (int k = 0; k < K - 1; ++k)
+    gd[k] = inside * ((k == idx - 1 ? gd0 * sgl : 0.f) + (k == idx ? gd1 * sgh : 0.f));
+  return inside != 0.f ? r : g_x;
+}
+
+}  // namespace naz

@@ -129,6 +129,21 @@ class _FusedCoupling:
         return _CouplingTrainFn.apply(x, context, bounds, self, *self.params())
 
 
+    def log_prob(self, x, context=None, bounds=None, out=None):
+        low = high = None
+        if bounds is not None:
+            low, high = bounds["low"].to(x.device, torch.float32), bounds["high"].to(x.device, torch.float32)
+        packed = self.packed()  # may re-resolve the mode: read self.desc only after it
+        return ops.coupling_log_prob(self.desc, packed, x, context, low, high, out=out)
+
+    def sample(self, z, context=None, bounds=None, with_logdet=False):
+        low = high = None
+        if bounds is not None:
+            low, high = bounds["low"].to(z.device, torch.float32), bounds["high"].to(z.device, torch.float32)
+        packed = self.packed()
+        return ops.coupling_sample(self.desc, packed, z, context, low, high, with_logdet=with_logdet)
+
+
 _TRAIN_FUSED = __import__("os").environ.get("NAZ_TRAIN_FUSED", "1")
 
 
@@ -202,20 +217,6 @@ class _CouplingTrainFn(torch.autograd.Function):
             grads[l * per:(l + 1) * per] = out
             g, g_next = g_next, g
         return (None, None, None, None, *grads)
-
-    def log_prob(self, x, context=None, bounds=None, out=None):
-        low = high = None
-        if bounds is not None:
-            low, high = bounds["low"].to(x.device, torch.float32), bounds["high"].to(x.device, torch.float32)
-        packed = self.packed()  # may re-resolve the mode: read self.desc only after it
-        return ops.coupling_log_prob(self.desc, packed, x, context, low, high, out=out)
-
-    def sample(self, z, context=None, bounds=None, with_logdet=False):
-        low = high = None
-        if bounds is not None:
-            low, high = bounds["low"].to(z.device, torch.float32), bounds["high"].to(z.device, torch.float32)
-        packed = self.packed()
-        return ops.coupling_sample(self.desc, packed, z, context, low, high, with_logdet=with_logdet)
 
 
 def _fused_plan(flow_type, flow_args, flow_kwargs, transforms) -> Optional[_FusedCoupling]:

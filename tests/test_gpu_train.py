@@ -219,17 +219,21 @@ def test_predict_batched_matches_oracle_per_draw():
 
 
 @pytest.mark.parametrize("shape", [(16, 32, 8, 8), (8, 0, 4, 6)])
-def test_fused_train_path_matches_walk(monkeypatch, shape):
-    """The fused NLL step (naz_coupling_log_prob_train + naz_coupling_bwd_layer + dW GEMMs) and
-    the per-node autograd walk give the same loss and gradients (ragged batch, bounds off)."""
+def test_fused_train_path_vs_oracle_and_walk(monkeypatch, shape):
+    """The fused NLL step (naz_coupling_log_prob_train + naz_coupling_bwd_layer + dW GEMMs, the
+    inference kernel's math) against the oracle's float64 autograd with the gradient criterion
+    of tests/parity.py, on a ragged batch; and within 5e-3 (norm-wise) of the per-node walk,
+    which uses libm-grade math (two valid fp32 evaluations of the same gradient)."""
     from naz_amd.flows import NormalizingFlow
     from naz_amd.flows import flow as flow_mod
     from naz_amd.flows import io as fio
     D, C, S, L = shape
     spec = dict(flow_type="nsc", D=D, C=C, hidden=[128, 128], L=L, K=8, split=S)
     state = {k: v.numpy() for k, v in O.random_state(spec, seed=21).items()}
-    x = torch.as_tensor(O.gaussian_mixture(3001, D, seed=2), device=DEV)
-    c = torch.as_tensor(O.context_normal(3001, C, seed=3), device=DEV) if C else None
+    xh = O.gaussian_mixture(3001, D, seed=2)
+    ch = O.context_normal(3001, C, seed=3) if C else None
+    x = torch.as_tensor(xh, device=DEV)
+    c = torch.as_tensor(ch, device=DEV) if C else None
     res = {}
     for fused in ("1", "0"):
         monkeypatch.setattr(flow_mod, "_TRAIN_FUSED", fused)
@@ -239,8 +243,20 @@ def test_fused_train_path_matches_walk(monkeypatch, shape):
         lp = f.log_prob(x, condition=c)
         (-lp.mean()).backward()
         res[fused] = (lp.detach(), {k: p.grad.detach().clone() for k, p in fio.named_state_params(f).items()})
-    torch.testing.assert_close(res["1"][0], res["0"][0], rtol=1e-4, atol=1e-4)
+    st = {k: (torch.as_tensor(np.asarray(v)) if np.asarray(v).dtype.kind in "iu" else
+              torch.as_tensor(np.asarray(v))) for k, v in state.items()}
+    g64, g32 = {}, {}
+    for dt, out in ((torch.float64, g64), (torch.float32, g32)):
+        sd = {k: (v if v.dtype == torch.int64 else v.to(dt).requires_grad_(True)) for k, v in st.items()}
+        of = O.build_flow(spec, sd, dt)
+        lpo = of.log_prob(torch.as_tensor(xh).to(dt), None if ch is None else torch.as_tensor(ch).to(dt))
+        keys = [k for k in sd if sd[k].requires_grad]
+        out.update(zip(keys, torch.autograd.grad(-lpo.mean(), [sd[k] for k in keys])))
+        out["lp"] = lpo.detach()
+    assert_parity(_np(res["1"][0]), _np(g64["lp"]), _np(g32["lp"]), what=f"{shape} fused train log_prob")
     for k, g in res["0"][1].items():
         a = res["1"][1][k]
+        ref = _np(g64[k])
+        assert_parity(_np(a), ref, _np(g32[k]), what=f"{shape} fused d/d{k}", floor=grad_floor(ref), count_factor=None)
         rel = float((a - g).norm() / g.norm().clamp_min(1e-30))
-        assert rel < 1e-3, f"{k}: fused vs walk {rel:.2e}"
+        assert rel < 5e-3, f"{k}: fused vs walk {rel:.2e}"

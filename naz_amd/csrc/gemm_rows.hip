@@ -516,11 +516,212 @@ __global__ void __launch_bounds__(256, MAXB <= 1 ? 4 : (MAXB <= 2 ? 3 : 2)) wgra
   if (p.ones && tid < N1) atomicAdd(p.rowsum + tid, dbs);
 }
 
+// wgrad_t16: the same reduction C += Gᵀ X (+ rowsum += Σ_r G[r]) on v_mfma_f32_16x16x4_f32.
+// A chunk of R rows of G and X is copied to LDS as it lies in memory (row-major, 16-byte
+// pieces, all of a thread's loads issued before its stores).  Wave w owns output row-blocks
+// w, w + 4, ... (NOW of them) x all NB2 column blocks; a 16x16x4 step takes A = G[r][o] and
+// B = X[r][j] from lane (m, kq) for ONE batch row r = base + 4 kq + t (t = step within the
+// group of four), so each operand block costs one ds_read_b32 per step and feeds NB2 (or NOW)
+// MFMAs — against one ds_read_b32 per operand per 32x32x2 MFMA in wgrad_flat.  The k order
+// inside the sum is free; it only has to be the same for A and B.
+typedef float floatx4w __attribute__((ext_vector_type(4)));
+// rows per chunk: a multiple of 16 with both operand pieces whole 1 KB DMA pieces and the
+// two-slot ring within `cap` bytes; 0 = no such R
+static int wgrad_t16_rows(int n1, int n2, int cap) {
+  int best = 0;
+  for (int R = 16; R <= 128; R += 16)
+    if ((R * n1) % 256 == 0 && (R * n2) % 256 == 0 && 2 * R * (n1 + n2) * 4 <= cap) best = R;
+  return best;
+}
+
+// JS = 2: eight waves, the column blocks split in halves between waves w and w + 4 (keeps a
+// wave's accumulators <= 12 blocks)
+template <int NOW, int NB2, int JS>
+__global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_t16_kernel(WGradArgs p, int R) {
+  extern __shared__ float tl[];
+  constexpr int N1P = 64 * NOW, N2P = 16 * NB2, NT = 256 * JS, NBW = NB2 / JS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, jh = tid >> 8, m = lane & 15,
+            kq = lane >> 4;
+  const int N1 = p.N1, N2 = p.N2;
+  const int64_t mb = (int64_t)blockIdx.x * p.rows_per_wg;
+  const int64_t me = (mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M;
+  floatx4w acc[NOW][NBW];
+#pragma unroll
+  for (int i = 0; i < NOW; ++i)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) acc[i][j] = floatx4w{0.f, 0.f, 0.f, 0.f};
+  float dsum[NOW];
+#pragma unroll
+  for (int i = 0; i < NOW; ++i) dsum[i] = 0.f;
+  // operand columns are NOT masked: a lane of a past-the-end block (o >= N1 or j >= N2) reads
+  // whatever lies there in LDS (the next row / the ring slack) and only feeds accumulator rows
+  // or columns the write-back drops, because an MFMA never mixes C rows or C columns.
+  // chunks stream through a two-slot LDS ring by LDS-DMA (global_load_lds_dwordx4, 1 KB per
+  // wave-instruction): chunk c + 1 lands while chunk c computes.  A partial last chunk is copied
+  // with bounds-checked loads instead (the DMA would read past the arrays).
+  const int CH = R * (N1 + N2);  // floats per chunk = per ring slot
+  const int nw = NT / 64, wv = tid >> 6;
+  auto issue = [&](int64_t m0, float* dst) {
+    const float* src[2] = {p.g + m0 * N1, p.x + m0 * N2};
+    const int cnt[2] = {R * N1 / 256, R * N2 / 256};
+    float* d = dst;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      for (int c = wv; c < cnt[h]; c += nw)
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src[h] + c * 256 + lane * 4),
+                                         (void __attribute__((address_space(3)))*)(d + c * 256), 16, 0, 0);
+      d += R * (h == 0 ? N1 : N2);
+    }
+  };
+  auto copy_tail = [&](int64_t m0, float* dst) {
+    const int64_t rows = me - m0;
+    const int lg = (int)(rows * N1 / 4), lx = (int)(rows * N2 / 4), fg = R * N1 / 4;
+    const float4* gp = reinterpret_cast<const float4*>(p.g + m0 * N1);
+    const float4* xp = reinterpret_cast<const float4*>(p.x + m0 * N2);
+    float4* l4 = reinterpret_cast<float4*>(dst);
+    for (int q = tid; q < CH / 4; q += NT) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < fg) {
+        if (q < lg) v = gp[q];
+      } else if (q - fg < lx) {
+        v = xp[q - fg];
+      }
+      l4[q] = v;
+    }
+  };
+  auto fill = [&](int64_t m0, float* dst) {
+    if (m0 + R <= me) issue(m0, dst);
+    else copy_tail(m0, dst);
+  };
+  int slot = 0;
+  if (mb < me) fill(mb, tl);
+  for (int64_t m0 = mb; m0 < me; m0 += R, slot ^= 1) {
+    __syncthreads();  // chunk m0 has landed (vmcnt drained); every wave is done with the other slot
+    float* const Gs = tl + slot * CH;
+    float* const Xs = Gs + R * N1;
+    if (m0 + R < me) fill(m0 + R, tl + (slot ^ 1) * CH);
+    // step s reads batch row 4 s + kq; lane bases advance 4 rows per step and the block offsets
+    // (64 i for A, 16 j for B) are immediate ds_read offsets.  Operands of step s + 1 are read
+    // before the MFMAs of step s (ping-pong registers, two steps per trip), so LDS latency hides
+    // under 12 MFMAs.  The read one step past the chunk lands in the next operand / the slack.
+    const float* pa = Gs + kq * N1 + wave * 16 + m;
+    const float* pb = Xs + kq * N2 + jh * NBW * 16 + m;
+    const int sa = 4 * N1, sb = 4 * N2;
+    float a0[NOW], b0[NBW], a1[NOW], b1[NBW];
+    auto rd = [&](float (&a)[NOW], float (&b)[NBW]) {
+#pragma unroll
+      for (int i = 0; i < NOW; ++i) a[i] = pa[64 * i];
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) b[j] = pb[16 * j];
+      pa += sa;
+      pb += sb;
+    };
+    auto step = [&](const float (&a)[NOW], const float (&b)[NBW]) {
+#pragma unroll
+      for (int i = 0; i < NOW; ++i) dsum[i] += a[i];
+#pragma unroll
+      for (int i = 0; i < NOW; ++i)
+#pragma unroll
+        for (int j = 0; j < NBW; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    };
+    rd(a0, b0);
+    for (int s = 0; s < R / 4; s += 2) {  // sched_barrier: keep the reads ahead of the MFMAs
+      rd(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      step(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      rd(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      step(a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // C[o][j]: lane holds rows o = ob 16 + 4 kq + r, column j = jb 16 + m
+#pragma unroll
+  for (int i = 0; i < NOW; ++i) {
+    const int ob = wave + 4 * i;
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const int n2 = 16 * (jh * NBW + j) + m;
+      if (n2 >= N2) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n1 = 16 * ob + 4 * kq + r;
+        if (n1 >= N1) continue;
+        float v = acc[i][j][r];
+        if (p.mask != nullptr) v *= p.mask[(int64_t)n1 * p.smm + (int64_t)n2 * p.smn];
+        atomicAdd(p.c + (int64_t)n1 * p.scm + (int64_t)n2 * p.scn, v);
+      }
+    }
+    if (p.ones && jh == 0) {  // db: column sums of G, partial per quarter -> reduce over kq
+      float v = dsum[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      const int o = 16 * ob + m;
+      if (kq == 0 && o < N1) atomicAdd(p.rowsum + o, v);
+    }
+  }
+}
+
+template <int NOW, int NB2>
+static void wgrad_t16_go(const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s) {
+  constexpr int JS = (NOW * NB2 > 12 && NB2 % 2 == 0) ? 2 : 1;
+  hipLaunchKernelGGL((wgrad_t16_kernel<NOW, NB2, JS>), dim3(gx), dim3(256 * JS), lds, s, q, R);
+}
+
+template <int NOW>
+static bool wgrad_t16_launch(int nb2, const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s) {
+  switch (nb2) {
+    case 1: wgrad_t16_go<NOW, 1>(q, R, lds, gx, s); return true;
+    case 2: wgrad_t16_go<NOW, 2>(q, R, lds, gx, s); return true;
+    case 3: wgrad_t16_go<NOW, 3>(q, R, lds, gx, s); return true;
+    case 4: wgrad_t16_go<NOW, 4>(q, R, lds, gx, s); return true;
+    case 6: wgrad_t16_go<NOW, 6>(q, R, lds, gx, s); return true;
+    case 8: wgrad_t16_go<NOW, 8>(q, R, lds, gx, s); return true;
+    default: return false;
+  }
+}
+
+// wgrad on the 16x16x4 transposed-tile kernel when the shape has an instantiation (N1 <= 256,
+// N2 <= 128, both multiples of 4); false = not taken
+static bool wgrad_t16(WGradArgs p, hipStream_t s) {
+  const int nb1 = (p.N1 + 15) / 16, now = (nb1 + 3) / 4;
+  int nb2 = (p.N2 + 15) / 16;
+  nb2 = nb2 <= 4 ? nb2 : (nb2 <= 6 ? 6 : (nb2 <= 8 ? 8 : 0));
+  if (now < 1 || now > 4 || nb2 == 0) return false;
+  // 8-wave workgroups (JS = 2) run one per CU: give them most of the LDS; 4-wave ones three
+  const bool js2 = now * nb2 > 12 && nb2 % 2 == 0;
+  const int R = wgrad_t16_rows(p.N1, p.N2, js2 ? 147456 : 49152);
+  if (R == 0) return false;
+  // + slack for the unmasked past-the-end reads (the prefetch one step past slot 1's chunk and
+  // the padding columns of its last rows)
+  const size_t lds = ((size_t)2 * R * (p.N1 + p.N2) + 4 * p.N2 + 16 * nb2 + 64) * 4;
+  int64_t rpw = (p.M + (js2 ? 511 : 767)) / (js2 ? 512 : 768);
+  rpw = (rpw + R - 1) / R * R;
+  if (rpw < 4 * R) rpw = 4 * R;
+  p.rows_per_wg = rpw;
+  const unsigned gx = (unsigned)((p.M + rpw - 1) / rpw);
+  switch (now) {
+    case 1: return wgrad_t16_launch<1>(nb2, p, R, lds, gx, s);
+    case 2: return wgrad_t16_launch<2>(nb2, p, R, lds, gx, s);
+    case 3: return wgrad_t16_launch<3>(nb2, p, R, lds, gx, s);
+    default: return wgrad_t16_launch<4>(nb2, p, R, lds, gx, s);
+  }
+}
+
 __global__ void zero2d_kernel(float* c, int64_t scm, int64_t scn, int M, int N) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)M * N) return;
   const int m = (int)(e / N), n = (int)(e - (int64_t)m * N);
   c[m * scm + n * scn] = 0.f;
+}
+
+static bool wgrad_t16_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("NAZ_WGRAD_T16");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
 }
 
 int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
@@ -537,6 +738,7 @@ int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
   const bool flat = p.sgm == p.N1 && p.sxm == p.N2 && p.N1 % 4 == 0 && p.N2 % 4 == 0 && p.N2 > 0 &&
                     (reinterpret_cast<uintptr_t>(p.g) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.x) & 15) == 0 &&
                     p.N1 <= 256 && p.N2 <= 256;
+  if (flat && p.N2 <= 128 && wgrad_t16_enabled() && wgrad_t16(p, s)) return check_launch("wgrad_t16_kernel");
   if (flat) {
     // rows per chunk: ~8192 floats of G + X (a multiple of 16, <= 128); ~1024 workgroups
     int R = 1024 * WF_Q / (p.N1 + p.N2);

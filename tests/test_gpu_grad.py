@@ -184,6 +184,21 @@ def test_gemm_strided_split_k(M, N, K, split):
     _check(rs, a.double().sum(0), a.sum(0), f"gemm {M}x{N}x{K} fused row sums (bias gradient)")
 
 
+@pytest.mark.parametrize("N1,N2,M", [(192, 128, 70001), (128, 128, 4096), (128, 40, 33333), (184, 128, 517),
+                                     (60, 20, 1000), (256, 96, 20000), (100, 52, 16), (4, 4, 9), (128, 8, 1 << 18)])
+def test_wgrad_t16_shapes(N1, N2, M):
+    """dW = G^T X (+ column sums of G) on contiguous row-major operands: the 16x16x4 LDS-ring kernel
+    (unmasked padding blocks, one-step-ahead prefetch, partial tail chunk) vs fp64."""
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(N1 * 131 + N2 + M)
+    a = torch.randn(M, N1, generator=g)
+    b = torch.randn(M, N2, generator=g)
+    rs = torch.empty(N1, device=DEV)
+    out = ops.gemm(_cuda(a).t(), _cuda(b), rowsum=rs)
+    _check(out, a.double().t() @ b.double(), a.t() @ b, f"wgrad {N1}x{N2} M={M}")
+    _check(rs, a.double().sum(0), a.sum(0), f"wgrad {N1}x{N2} M={M} row sums")
+
+
 # ------------------------------------------------------------------ a5 affine step VJP
 @pytest.mark.parametrize("inverse", [False, True])
 def test_affine_ar_grad(inverse):

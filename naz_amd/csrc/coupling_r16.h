@@ -246,7 +246,8 @@ NAZ_DEV void gemm_r16_lazy(floatx4 (&acc)[NB], const float* __restrict__ stage, 
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      v[j] = x[2 * (T0 + t) + (j >> 2)][j & 3];
+      const int blk = 2 * (T0 + t) + (j >> 2);  // past the last block (odd NX): zero k-slots
+      v[j] = blk < NX ? x[blk < NX ? blk : 0][j & 3] : 0.f;
       if constexpr (ACT) v[j] = sig_fold(v[j]);
     }
     const Frag2 b = split8_f16(v);

@@ -28,12 +28,23 @@
 
 namespace naz {
 
+// Backward GEMM precision.  Default: f16x3 (v_mfma_f32_16x16x32_f16, three products as the
+// forward) with a per-row power-of-2 scale of the gradient operand (its row maximum maps into
+// [2^13, 2^14), so the lo pieces stay clear of the f16 subnormals) and weight images held at 2^6 W;
+// 5.3x the matrix rate of the exact-fp32 form.  NAZ_BWD_EXACT_F32: v_mfma_f32_16x16x4_f32.
+#ifdef NAZ_BWD_EXACT_F32
+constexpr bool kBwdF16 = false;
+#else
+constexpr bool kBwdF16 = true;
+#endif
+constexpr float kBwdWScale = 64.f;
+
 template <class CF>
 struct BwdR16 {
   static constexpr int NS3 = 4 * CF::NO;  // GEMM3 slots per quarter = dH2 k-steps
   static constexpr int HB = CF::HB;
-  // units of 4 MFMA k-steps (one 16x16x4 k-step takes one value from each quarter): dH2 has NS3
-  // k-steps, dH1 and dx1 H/4 (each quarter feeds its H/4 own hidden features)
+  // exact fp32 — units of 4 MFMA k-steps (one 16x16x4 k-step takes one value from each
+  // quarter): dH2 has NS3 k-steps, dH1 and dx1 H/4 (each quarter feeds its H/4 own features)
   static constexpr int U3ALL = NS3 / 4, UH = CF::H / 16;
   static constexpr int pick_u(int nb, int units) {
     int best = 1;
@@ -41,9 +52,22 @@ struct BwdR16 {
       if (units % u == 0 && nb * u * 256 <= kX6Slot) best = u;
     return best;
   }
-  static constexpr int U3 = pick_u(HB, U3ALL), NB3 = U3ALL / U3;   // dH2 stages
-  static constexpr int U2 = pick_u(HB, UH), NB2 = UH / U2;  // dH1 stages
-  static constexpr int S3 = HB * U3 * 256, S2 = HB * U2 * 256, SA = UH * 256;
+  static constexpr int U3 = pick_u(HB, U3ALL), U2 = pick_u(HB, UH);
+  // f16x3 — 32-k steps of 8 own values per quarter (slot s = 8 t + j), images laid out as the
+  // forward's [block][k-step][hi | lo][lane][8 x f16]
+  static constexpr int KS3 = (NS3 + 7) / 8, KSH = CF::H / 32;
+  static constexpr int pick_kb(int nb, int ks) {
+    int best = 1;
+    for (int kb = 1; kb <= ks; ++kb)
+      if (ks % kb == 0 && nb * kb * CF::OT <= kX6Slot) best = kb;
+    return best;
+  }
+  static constexpr int KB3 = pick_kb(HB, KS3), KB2 = pick_kb(HB, KSH);
+  static constexpr int NB3 = kBwdF16 ? KS3 / KB3 : U3ALL / U3;  // dH2 stages
+  static constexpr int NB2 = kBwdF16 ? KSH / KB2 : UH / U2;     // dH1 stages
+  static constexpr int S3 = kBwdF16 ? HB * KB3 * CF::OT : HB * U3 * 256;
+  static constexpr int S2 = kBwdF16 ? HB * KB2 * CF::OT : HB * U2 * 256;
+  static constexpr int SA = kBwdF16 ? KSH * CF::OT : UH * 256;
   static constexpr int OFF2 = NB3 * S3, OFFA = OFF2 + NB2 * S2;
   static constexpr int LAYER = OFFA + SA;
   static constexpr int NSTG = NB3 + NB2 + 1;
@@ -68,6 +92,38 @@ __global__ void coupling_pack_bwd_r16_kernel(const float* __restrict__ flat, flo
     const float* W0 = flat + (int64_t)l * CF::FLAT;
     const float* W1 = W0 + CF::N_W0 + CF::N_B0;
     const float* W2 = W1 + CF::N_W1 + CF::N_B1;
+    if constexpr (kBwdF16) {
+      // word (b, tl, piece, lane, pair) of a stage: two f16 pieces of 2^6 W at k-slots
+      // j = 2 pair + e of 32-k step t = stage k-step base + tl, fed by quarter kg = lane >> 4
+      const int gsel = off < BW::OFF2 ? 0 : (off < BW::OFFA ? 1 : 2);
+      const int kb = gsel == 0 ? BW::KB3 : (gsel == 1 ? BW::KB2 : BW::KSH);
+      const int so = gsel == 0 ? off : (gsel == 1 ? off - BW::OFF2 : off - BW::OFFA);
+      const int ssz = gsel == 0 ? BW::S3 : (gsel == 1 ? BW::S2 : BW::SA);
+      const int js = so / ssz, r = so - js * ssz;
+      const int b = r / (kb * CF::OT), r1 = r - b * kb * CF::OT;
+      const int tl = r1 / CF::OT, r2 = r1 - tl * CF::OT;
+      const int piece = r2 / kChunk, u = r2 - piece * kChunk;
+      const int lane = u >> 2, pair = u & 3, m = lane & 15, kg = lane >> 4;
+      const int t = js * kb + tl;
+      unsigned word = 0;
+      for (int e2 = 0; e2 < 2; ++e2) {
+        const int jj = 2 * pair + e2;
+        float v = 0.f;
+        if (gsel == 0) {
+          const int s = 8 * t + jj;
+          const int orow = s < BW::NS3 ? BW::slot_row(kg, s) : -1;
+          if (orow >= 0) v = W2[orow * CF::H + 16 * b + m];
+        } else if (gsel == 1) {
+          v = W1[r16_feat(t, kg, jj) * CF::H + 16 * b + m];
+        } else {
+          const int qq = m >> 2, i = m & 3;
+          if (i < CF::SQ) v = W0[r16_feat(t, kg, jj) * (CF::C + CF::S) + CF::C + qq * CF::SQ + i];
+        }
+        word |= f16_piece_bits(kBwdWScale * v, piece) << (16 * e2);
+      }
+      reinterpret_cast<unsigned*>(packed)[e] = word;
+      continue;
+    }
     float v = 0.f;
     if (off < BW::OFF2) {  // dH2 stages: [b][u][lane][e], k-step s = 4(j U3 + u) + e
       const int j = off / BW::S3, r = off - j * BW::S3;
@@ -116,6 +172,29 @@ NAZ_DEV void bwd_gemm_stage(floatx4 (&acc)[NBLK], const float* __restrict__ stag
     for (int b = 0; b < NBLK; ++b) acc[b] = mfma16_f32(a[b].w, bv[U0 + u][3], acc[b]);
   }
 }
+
+// f16x3 backward operand scale: multiplies the row's values (this lane's NB blocks; the row
+// spans the four quarters, lanes n, n + 16, n + 32, n + 48) by 2^k so the row maximum lies in
+// [2^13, 2^14); returns 2^-k / kBwdWScale, which turns the GEMM result back into natural units.
+template <int NB>
+NAZ_DEV float bwd_row_scale(floatx4 (&x)[NB]) {
+  float mx = 0.f;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mx = fmaxf(mx, fabsf(x[b][r]));
+  mx = fmaxf(mx, __shfl_xor(mx, 16));
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  int k = 140 - (int)((__float_as_uint(mx) >> 23) & 255u);  // 13 - unbiased exponent
+  k = k < -100 ? -100 : (k > 110 ? 110 : k);
+  const float s = __uint_as_float((unsigned)(k + 127) << 23);
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[b][r] *= s;
+  return __uint_as_float((unsigned)(127 - k - 6) << 23);  // 2^-k / 2^6
+}
+static_assert(kBwdWScale == 64.f, "bwd_row_scale folds 2^-6");
 
 // the training forward's activation of a packed (sigmoid-folded) accumulator: -tanh(a)/2
 NAZ_DEV float train_fold(float v) {
@@ -200,6 +279,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
     floatx4 dp2[CF::HB];  // dPre2, then dPre1
     floatx4 dacc[CF::HB];
     floatx4 dx1;
+    float gscale = 1.f;  // f16x3: natural units of the current backward GEMM's accumulator
     float gy2[CF::DQ];
     const bool has_next = tile + gridDim.x < ntiles;
 
@@ -350,9 +430,14 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
           for (int b = 0; b < CF::HB; ++b) dacc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
       } else if constexpr (j < NSTG_F + BW::NB3) {
-        // ---- dH2 = dPre3 · W2 (exact fp32), k-step units [U0, U0 + U3)
+        // ---- dH2 = dPre3 · W2, k-steps of stage sb
         constexpr int sb = j - NSTG_F;
-        bwd_gemm_stage<CF::HB, BW::U3, sb * BW::U3>(dacc, cur, lane, a3);
+        if constexpr (kBwdF16) {
+          if constexpr (sb == 0) gscale = bwd_row_scale(a3);  // dPre3 already stored unscaled
+          gemm_r16_lazy<CF::HB, BW::KB3, sb * BW::KB3, false>(dacc, cur, lane, a3);
+        } else {
+          bwd_gemm_stage<CF::HB, BW::U3, sb * BW::U3>(dacc, cur, lane, a3);
+        }
         if constexpr (sb == BW::NB3 - 1) {
 #pragma unroll
           for (int b = 0; b < CF::HB; ++b) {
@@ -361,16 +446,18 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
                                     : float4{0.f, 0.f, 0.f, 0.f};
             const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dp2[b][r] = dacc[b][r] * (1.f - hh[r] * hh[r]);
+            for (int r = 0; r < 4; ++r) dp2[b][r] = (dacc[b][r] * gscale) * (1.f - hh[r] * hh[r]);
             if (valid)
               *reinterpret_cast<float4*>(o.dp2 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
             dacc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
           }
+          if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         }
       } else if constexpr (j < NSTG_F + BW::NB3 + BW::NB2) {
         // ---- dH1 = dPre2 · W1
         constexpr int sb = j - NSTG_F - BW::NB3;
-        bwd_gemm_stage<CF::HB, BW::U2, sb * BW::U2>(dacc, cur, lane, dp2);
+        if constexpr (kBwdF16) gemm_r16_lazy<CF::HB, BW::KB2, sb * BW::KB2, false>(dacc, cur, lane, dp2);
+        else bwd_gemm_stage<CF::HB, BW::U2, sb * BW::U2>(dacc, cur, lane, dp2);
         if constexpr (sb == BW::NB2 - 1) {
 #pragma unroll
           for (int b = 0; b < CF::HB; ++b) {
@@ -378,15 +465,22 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
                                     : float4{0.f, 0.f, 0.f, 0.f};
             const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dp2[b][r] = dacc[b][r] * (1.f - hh[r] * hh[r]);  // now dPre1
+            for (int r = 0; r < 4; ++r) dp2[b][r] = (dacc[b][r] * gscale) * (1.f - hh[r] * hh[r]);  // now dPre1
             if (valid)
               *reinterpret_cast<float4*>(o.dp1 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
           }
+          if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         }
       } else {
         // ---- dx1 = dPre1 · W0[:, C:], lower spline VJP, g(P[l + 1])
         floatx4 a1[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
-        bwd_gemm_stage<1, BW::UH, 0>(a1, cur, lane, dp2);
+        if constexpr (kBwdF16) {
+          gemm_r16_lazy<1, BW::KSH, 0, false>(a1, cur, lane, dp2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a1[0][r] *= gscale;
+        } else {
+          bwd_gemm_stage<1, BW::UH, 0>(a1, cur, lane, dp2);
+        }
         dx1 = a1[0];
         float gy1[CF::SQ];
 #pragma unroll

@@ -539,7 +539,7 @@ static int wgrad_t16_rows(int n1, int n2, int cap) {
 template <int NOW, int NB2, int JS>
 __global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_t16_kernel(WGradArgs p, int R) {
   extern __shared__ float tl[];
-  constexpr int N1P = 64 * NOW, N2P = 16 * NB2, NT = 256 * JS, NBW = NB2 / JS;
+  constexpr int NT = 256 * JS, NBW = NB2 / JS;
   const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, jh = tid >> 8, m = lane & 15,
             kq = lane >> 4;
   const int N1 = p.N1, N2 = p.N2;

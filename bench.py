@@ -482,6 +482,9 @@ FLOW_CASES = {
     # naz nsa (ConditionalSplineAutoregressive, D-pass inverse), pinned: D=4, C=2, H=[128,128], K=8, L=8
     "nsa": ("nsa", 4, 2, [128, 128], 8, (8,), 1 << 18,
             "naz nsa (SURVEY.md §8a a4/a6): D=4, C=2, K=8, L=8, H=[128,128], D-pass inverse per layer"),
+    # SURVEY.md §8d's config-3 autoregressive variant: the config-3 flow with nsa layers
+    "nsa16": ("nsa", 16, 32, [128, 128], 8, (8,), 1 << 18,
+              "naz nsa at SURVEY §8d's config-3 AR variant: D=16 | C=32, K=8, L=8, H=[128,128], D-pass inverse"),
     # the density-grid use (plot.py:126-127): one context vector for every row
     "maf_grid": ("maf", 2, 2, [150, 150, 150], 16, (), 1 << 18,
                  "naz maf at the paper shape with ONE context vector (density grid, plot.py:126-127): "
@@ -512,7 +515,10 @@ def run_flow_case(args, dev, rank, world, dist):
         passes = Dd
     fl_ref = 2 * passes * Ld * sum(a * b for a, b in zip(dims[:-1], dims[1:]))  # the reference's work
     fl_row = fl_ref
-    if ftype != "nsc":  # executed work of the degree-scheduled inverse (padded blocks included)
+    ar_fused = ftype == "nsa" and getattr(f, "_plan", None) is not None and hasattr(f._plan, "executed_flop_per_row")
+    if ar_fused:  # the fused autoregressive kernel's executed work (made_ar_r16.h)
+        fl_row = f._plan.executed_flop_per_row()
+    elif ftype != "nsc":  # executed work of the degree-scheduled inverse (padded blocks included)
         fl_row = 0
         for net in f.nets:
             plan = net.inverse_plan().plan()
@@ -556,7 +562,8 @@ def run_flow_case(args, dev, rank, world, dist):
             "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
             "config": {"workload": desc, "batch_per_gpu": B, "global_batch": G,
                        "parallelism": f"dp{world} (independent row shards, no collective)",
-                       "path": "fused kernel" if fused else "per-layer HIP kernels (rowgemm + spline/affine)"},
+                       "path": ("fused autoregressive-inverse kernel (naz_spline_ar_log_prob, one launch)" if ar_fused
+                                else "fused kernel" if fused else "per-layer HIP kernels (rowgemm + spline/affine)")},
             "roofline": {"bound": "mfma", "achieved": achieved,
                          "peak": FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3, "unit": "TFLOP/s",
                          "frac": achieved / (FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3),
@@ -569,11 +576,13 @@ def run_flow_case(args, dev, rank, world, dist):
                 spec.update(K=extra[0], split=extra[1])
             elif ftype == "nsa":
                 spec.update(K=extra[0])
-            xh = x[:1 << 17].cpu().numpy()
+            # ~10-30 s of host work: the D-pass reference at the 16-dim AR shape is 17.8 MFLOP/row
+            nb = 1 << 17 if fl_ref < 4e6 else 1 << 14
+            xh = x[:nb].cpu().numpy()
             ch = None
             if c is not None:
-                ch = (c.reshape(1, -1).expand(1 << 17, -1) if grid else c[:1 << 17]).cpu().numpy()
-            rec["cpu_baseline"], rec["parity_spot_check"] = cpu_baseline(f, xh, ch, budget_rows=1 << 17, spec=spec)
+                ch = (c.reshape(1, -1).expand(nb, -1) if grid else c[:nb]).cpu().numpy()
+            rec["cpu_baseline"], rec["parity_spot_check"] = cpu_baseline(f, xh, ch, budget_rows=nb, spec=spec)
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.barrier()

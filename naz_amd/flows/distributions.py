@@ -72,7 +72,7 @@ class TransformedDistribution:
         return self._fused is not None and self._fused.usable()
 
     def _log_prob_into(self, y: torch.Tensor, lp: torch.Tensor, bounds=None) -> torch.Tensor:
-        if self._fused_ok():
+        if self._fused_ok() and getattr(self._fused, "log_prob_ready", lambda *a: True)(y, self._context):
             return self._fused.log_prob(y, self._context, bounds=bounds, out=lp)
         if bounds is not None:
             y, lj = ops.bounding_fwd(y, bounds["low"], bounds["high"])
@@ -93,7 +93,7 @@ class TransformedDistribution:
         return self._log_prob_into(y, lp, bounds).reshape(lead)
 
     def _transform_z(self, z: torch.Tensor, bounds=None) -> torch.Tensor:
-        if self._fused_ok():
+        if self._fused_ok() and getattr(self._fused, "can_sample", True):
             y, _ = self._fused.sample(z, self._context, bounds=bounds)
             return y
         ld = torch.zeros(z.shape[0], device=z.device, dtype=torch.float32)

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 from torch import nn
 from torch.distributions import Normal
@@ -144,7 +145,105 @@ class _FusedCoupling:
         return ops.coupling_sample(self.desc, packed, z, context, low, high, with_logdet=with_logdet)
 
 
+class _FusedAR:
+    """All L nsa layers' log_prob as ONE HIP launch (naz_spline_ar_log_prob, csrc/made_ar_r16.h):
+    every layer's D-pass MADE inverse (pyro ConditionedSplineAutoregressive._inverse, naz
+    transforms.py:165-198) with each hidden unit computed once, in registers, on the f16x3 MFMA
+    path.  sample() and the autograd walk keep the per-layer kernels.  The kernel is compiled for
+    pyro's hidden mask indices; the masks are checked against them once per parameter change."""
+
+    can_sample = False
+    F16_DATA_LIMIT = 32768.0  # the kernel's f16x3 input split (|x|, |ctx| < 2^15)
+
+    def __init__(self, layers: List[nn.Module], D: int, C: int, H: int, K: int, act: str, bound: float):
+        self.layers = layers
+        self.shape = (D, C, H, K)
+        self.desc = ops.spline_ar_desc(D, C, H, K, len(layers), act, bound)
+        self._sig = None
+        self._packed = None
+        self._masks = None
+
+    def _nets(self):
+        return [t.nn for t in self.layers]
+
+    def masks_ok(self) -> bool:
+        """The ARN masks are pyro's create_mask for the kernel's compiled hidden indices
+        (re-checked whenever a mask or permutation tensor changes: load_state rewrites them)."""
+        sig = tuple((t.data_ptr(), t._version) for n in self._nets()
+                    for t in [n.permutation] + [l.mask for l in n.layers])
+        if self._masks is None or self._masks[0] != sig:
+            D, C, H, K = self.shape
+            P = 3 * K - 1
+            deg = ops.spline_ar_degrees(self.desc).astype(np.int64)
+            ok = True
+            for arn in self._nets():
+                m = [l.mask.detach().cpu().numpy() != 0 for l in arn.layers]
+                perm = arn.permutation.detach().cpu().numpy().astype(np.int64)
+                order = np.empty(D, dtype=np.int64)
+                order[perm] = np.arange(D)
+                in_idx = np.concatenate([np.zeros(C, dtype=np.int64), order + 1])
+                out_idx = np.tile(order + 1, P)
+                ok = ok and len(m) == 3 and m[0].shape == (H, C + D) and m[1].shape == (H, H)
+                ok = ok and bool((m[0] == (deg[:, None] >= in_idx[None, :])).all())
+                ok = ok and bool((m[1] == (deg[:, None] >= deg[None, :])).all())
+                ok = ok and bool((m[2] == (out_idx[:, None] > deg[None, :])).all())
+            self._masks = (sig, ok)
+        return self._masks[1]
+
+    def usable(self) -> bool:
+        return self.masks_ok() and not any(n.dropout_active() for n in self._nets())
+
+    def log_prob_ready(self, x, context) -> bool:
+        if x.dim() != 2:
+            return False
+        m = x.detach().abs().amax() if x.numel() else torch.zeros((), device=x.device)
+        if context is not None and context.numel():
+            m = torch.maximum(m, context.detach().abs().amax())
+        return float(m) < self.F16_DATA_LIMIT
+
+    def train_ready(self, x, context) -> bool:
+        return False
+
+    def packed(self) -> torch.Tensor:
+        ps = [p for n in self._nets() for l in n.layers for p in (l.weight, l.bias, l.mask)]
+        sig = tuple((p.data_ptr(), p._version) for p in ps) + (cache_epoch(),)
+        if sig != self._sig or self._packed is None:
+            flats, perms = [], []
+            for n in self._nets():
+                for l in n.layers:
+                    flats += [(l.weight.detach() * l.mask).float().cpu().numpy().ravel(),
+                              l.bias.detach().float().cpu().numpy()]
+                perms.append(n.permutation.detach().cpu().numpy())
+            dev = self._nets()[0].layers[0].weight.device
+            self._packed = ops.spline_ar_pack(self.desc, np.concatenate(flats), np.stack(perms), dev)
+            self._sig = sig
+        return self._packed
+
+    def log_prob(self, x, context=None, bounds=None, out=None):
+        low = high = None
+        if bounds is not None:
+            low, high = bounds["low"].to(x.device, torch.float32), bounds["high"].to(x.device, torch.float32)
+        return ops.spline_ar_log_prob(self.desc, self.packed(), x, context, low, high, out=out)
+
+    def executed_flop_per_row(self) -> int:
+        """FP32-equivalent FLOPs the kernel executes per row (an f16x3 product counted once; the
+        16-unit block recomputations and zero-padded k-slots included): per pass, hidden-layer
+        blocks over [ctx | x] and over the hidden units of degree <= p, and the output blocks."""
+        D, C, H, K = self.shape
+        deg = ops.spline_ar_degrees(self.desc)
+        E = [int((deg <= p).sum()) for p in range(D)]
+        KI, NOB = (C + 31) // 32 + 1, (3 * K - 1 + 15) // 16
+        per_layer = 0
+        for p in range(D):
+            e0 = E[p - 1] if p else 0
+            nb = ((E[p] - 1) >> 4) - (e0 >> 4) + 1 if E[p] > e0 else 0
+            kt = (E[p] + 31) // 32
+            per_layer += (nb * (KI + kt) + NOB * kt) * 16 * 32 * 2  # 16 outputs x 32 k per block-step
+        return per_layer * len(self.layers)
+
+
 _TRAIN_FUSED = __import__("os").environ.get("NAZ_TRAIN_FUSED", "1")
+_AR_FUSED = __import__("os").environ.get("NAZ_AR_FUSED", "1")
 
 
 class _CouplingTrainFn(torch.autograd.Function):
@@ -219,8 +318,21 @@ class _CouplingTrainFn(torch.autograd.Function):
         return (None, None, None, None, *grads)
 
 
-def _fused_plan(flow_type, flow_args, flow_kwargs, transforms) -> Optional[_FusedCoupling]:
-    if flow_type != "nsc" or any(isinstance(t, Permute) for t in transforms):
+def _fused_plan(flow_type, flow_args, flow_kwargs, transforms):
+    if any(isinstance(t, Permute) for t in transforms):
+        return None
+    if flow_type == "nsa" and _AR_FUSED != "0":
+        D, C, hidden, L, K = flow_args[:5]
+        hidden = list(hidden) if isinstance(hidden, (list, tuple)) else [hidden]
+        act = activation_name(flow_kwargs.get("activation", nn.Tanh()))
+        if len(hidden) != 2 or hidden[0] != hidden[1]:
+            return None
+        try:
+            plan = _FusedAR(list(transforms), D, C, hidden[0], K, act, transforms[0].bound)
+            return plan if ops.spline_ar_supported(plan.desc) and plan.masks_ok() else None
+        except Exception:
+            return None
+    if flow_type != "nsc":
         return None
     D, C, hidden, L, K, S = flow_args[:6]
     hidden = list(hidden) if isinstance(hidden, (list, tuple)) else [hidden]
@@ -278,17 +390,18 @@ class NormalizingFlow(nn.Module):
 
     def set_fused(self, enabled: bool) -> None:
         """Switch between the single fused launch and the per-layer kernels (testing aid)."""
-        if enabled and self._plan is None:
-            raise RuntimeError("no fused instantiation for this flow")
         if not enabled:
-            self._plan_saved, self._plan = self._plan, None
-        elif getattr(self, "_plan_saved", None) is not None:
+            if self._plan is not None:
+                self._plan_saved, self._plan = self._plan, None
+        elif self._plan is None:
+            if getattr(self, "_plan_saved", None) is None:
+                raise RuntimeError("no fused instantiation for this flow")
             self._plan = self._plan_saved
         self._make_dist()
 
     @property
     def fused(self) -> bool:
-        """True when log_prob/sample run as the single fused coupling launch."""
+        """True when log_prob (and, for nsc, sample) run as one fused launch."""
         return self._plan is not None
 
     def _bounds_dev(self, ref):

@@ -22,6 +22,8 @@ CASES = [
     dict(flow_type="maf", D=6, C=3, hidden=[64, 50], L=2),
     dict(flow_type="nsa", D=4, C=2, hidden=[128, 128], L=2, K=8),
     dict(flow_type="nsa", D=3, C=0, hidden=[33, 20], L=2, K=5),
+    # SURVEY §8d's config-3 AR variant (bench.py --flow nsa16): D=16 | C=32, K=8, H=[128,128], L=8
+    dict(flow_type="nsa", D=16, C=32, hidden=[128, 128], L=8, K=8, n=512),
 ]
 
 
@@ -53,7 +55,7 @@ def _id(spec):
 @pytest.mark.parametrize("spec", CASES, ids=_id)
 def test_scheduled_inverse_vs_oracle(spec):
     f, state = _flow(spec)
-    n = 2048
+    n = spec.get("n", 2048)
     x = torch.as_tensor(O.gaussian_mixture(n, spec["D"], seed=5))
     c = torch.as_tensor(O.context_normal(n, spec["C"], seed=6)) if spec["C"] else None
     with torch.no_grad():
@@ -96,7 +98,7 @@ def test_broadcast_context_folding(spec):
     schedule and the oracle."""
     from naz_amd.nn import ARInversePlan
     f, state = _flow(spec)
-    n = 2048
+    n = spec.get("n", 2048)
     x = torch.as_tensor(O.gaussian_mixture(n, spec["D"], seed=5))
     c1 = torch.as_tensor(O.context_normal(1, spec["C"], seed=6))[0]
     with torch.no_grad():

@@ -487,6 +487,21 @@ def dopri5_augmented(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor, t
     return torch.cat(xs), torch.cat(as_), nfes
 
 
+def dopri5_global(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor, t0: float, t1: float,
+                  atol: float = 1e-4, rtol: float = 1e-4, max_steps: int = 1000):
+    """torchdyn's controller as naz configures it (FFJORDTransform solver='dopri5', atol = rtol =
+    1e-4, continuous_transforms.py:73-81; torchdyn.numerics odeint with an adaptive solver): ONE
+    step size for the whole batch.  The error ratio is torchdyn's ``hairer_norm`` — the RMS over
+    every element of the augmented state tensor [B, D + 1] — of err / (atol + rtol max(|y0|, |y1|)),
+    with the same accept rule, step factor (0.9 r^(-1/5) clamped to [0.2 (1 on accept), 10]) and
+    Hairer initial step as ``dopri5_augmented``, which this is with one group spanning the batch.
+    torchdyn is absent here (parity unpinned); the last step is clipped to t1 as the kernel does
+    (torchdyn instead interpolates its dense output at t1 — the same solution within tolerance).
+    Returns x(t1), a(t1) and the batch's number of RHS evaluations."""
+    y, a, nfe = dopri5_augmented(net, x, ctx, eps, t0, t1, atol, rtol, group=x.shape[0], max_steps=max_steps)
+    return y, a, nfe[0]
+
+
 class FFJORD:
     """a11: naz ``FFJORDTransform`` (continuous_transforms.py:70-106).  ``inverse`` = its
     ``_inverse`` (integrate t 0 -> 1, the log_prob direction), ``forward`` = ``_call``

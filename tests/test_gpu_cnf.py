@@ -225,6 +225,16 @@ def _oracle_dopri5(D, C, hidden, act, x, c, eps, t0, t1, atol, rtol, seed=3):
     return y.numpy(), a.numpy(), nfe, yr.numpy(), ar.numpy()
 
 
+def _oracle_dopri5_global(D, C, hidden, act, x, c, eps, t0, t1, atol, rtol, seed=3):
+    """torchdyn's batch-global step control (oracle.dopri5_global), fp64."""
+    spec = dict(flow_type="cnf", D=D, C=C, hidden=hidden, L=1, activation=act)
+    st = {k: v.float() for k, v in O.random_state(spec, seed=seed, last_layer_scale=1.0).items()}
+    net = O.build_flow(spec, st, torch.float64).layers[0].nn
+    ct = None if c is None else torch.as_tensor(c).double()
+    y, a, nfe = O.dopri5_global(net, torch.as_tensor(x).double(), ct, torch.as_tensor(eps).double(), t0, t1, atol, rtol)
+    return y.numpy(), a.numpy(), nfe
+
+
 @pytest.mark.parametrize("D,C,hidden,act", [(4, 2, [32, 32], "softplus"), (2, 2, [128, 64, 64], "softplus"),
                                             (16, 0, [128, 128, 128], "softplus")])
 @pytest.mark.parametrize("direction", [(0.0, 1.0), (1.0, 0.0)])
@@ -260,6 +270,11 @@ def test_cnf_dopri5_vs_oracle(D, C, hidden, act, direction, mfma):
     # vs the oracle's same-controller solve where the step sequence matched
     same = np.repeat(nfe == np.asarray(nfe64), 16)[:B]
     assert np.abs(y - y64)[same].max() <= 2e-4 and np.abs(a - a64)[same].max() <= 2e-4
+    # vs torchdyn's semantics (one step size for the whole batch, hairer_norm over [B, D + 1]):
+    # a different step sequence, the same solution within the solver's promised tolerance
+    yg, ag, _ = _oracle_dopri5_global(D, C, hidden, act, x, c, eps, t0, t1, atol, rtol)
+    assert np.all(np.abs(y - yg) <= 20 * (atol + rtol * np.abs(yg))), np.abs(y - yg).max()
+    assert np.all(np.abs(a - ag) <= 20 * (atol + rtol * np.abs(ag))), np.abs(a - ag).max()
 
 
 def test_cnf_dopri5_flow_api_and_ragged():

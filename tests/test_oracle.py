@@ -222,6 +222,27 @@ def test_cnf_rk4_converges_and_inverts():
     assert (xb - x).abs().max() < 1e-10 and (ab + a128).abs().max() < 1e-10
 
 
+def test_cnf_dopri5_global_controller_meets_tolerance():
+    """torchdyn's controller (one step size for the batch, hairer_norm over [B, D + 1];
+    oracle.dopri5_global): its solution is within the promised tolerance of the converged one, and
+    of the kernel's per-16-row controller (oracle.dopri5_augmented), in both directions."""
+    spec = dict(flow_type="cnf", D=4, C=2, hidden=[32, 32], L=1)
+    blk = _cnf_flow(spec).layers[0]
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(96, 4, generator=g, dtype=torch.float64) * 0.8
+    c = torch.randn(96, 2, generator=g, dtype=torch.float64)
+    eps = torch.randn(96, 4, generator=g, dtype=torch.float64)
+    atol = rtol = 1e-4
+    for t0, t1 in ((0.0, 1.0), (1.0, 0.0)):
+        yg, ag, nfe = O.dopri5_global(blk.nn, x, c, eps, t0, t1, atol, rtol)
+        yr, ar = O.rk4_augmented(blk.nn, x, c, eps, t0, t1, 256)
+        yl, al, nfes = O.dopri5_augmented(blk.nn, x, c, eps, t0, t1, atol, rtol)
+        assert nfe >= max(nfes)  # the batch-global step is set by the hardest rows
+        assert ((yg - yr).abs() <= 20 * (atol + rtol * yr.abs())).all()
+        assert ((ag - ar).abs() <= 20 * (atol + rtol * ar.abs())).all()
+        assert ((yg - yl).abs() <= 20 * (atol + rtol * yg.abs())).all()
+
+
 @pytest.mark.parametrize("name", ["cnf_d4c2.npz", "cnf_d16c0.npz"])
 def test_golden_cnf_fixture(name):
     fx = load_golden(name)

@@ -402,3 +402,26 @@ def test_lp_layer_batched_constants():
         ol = _oracle_layers(layers, d)
         assert_parity(a[p].cpu().numpy(), J.log_prob(x, ol, ctx),
                       J.log_prob(x, J.cast_layers(ol, np.float32), ctx, np.float32), what=f"layer-batched lp {p}")
+
+
+@pytest.mark.gpu
+def test_lp_layer_batched_many_draws_few_rows():
+    """L x P beyond the batched launches' grid-z limit (65535) with few rows: the
+    layer-batched constants path caps its draw chunks at 65535 // L and budgets the per-draw
+    packs; the result equals the per-layer path draw for draw."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    spec = dict(flow_type="maf", D=2, C=2, hidden=[32, 32], L=4, P=1, B=8, ctx="vec")
+    layers, draws, x, ctx = _setup(spec)
+    base = _batched_params(draws, "cuda")
+    P = 16500  # L * P = 66000 > 65535
+    g = torch.Generator(device="cuda").manual_seed(0)
+
+    def jitter(t):
+        return t.expand(P, *t.shape[1:]) * (1 + 0.1 * (2 * torch.rand((P,) + tuple(t.shape[1:]), device="cuda",
+                                                                      generator=g) - 1))
+    params = [[(jitter(W), jitter(b)) for (W, b) in lay] for lay in base]
+    a = _flow(spec, layers, x, ctx, "cuda")["lp_batched"](params)
+    b = _flow(spec, layers, x, ctx, "cuda", batch_layers=False)["lp_batched"](params)
+    assert a.shape == (P, spec["B"]) and bool(torch.isfinite(a).all())
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-5), (a - b).abs().max()

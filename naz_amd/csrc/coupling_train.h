@@ -358,13 +358,18 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         for (int b = 0; b < CF::HB; ++b) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) h1[b][r] = train_fold(h1[b][r]);  // -tanh/2: GEMM2's operand
-          if (valid)
-            *reinterpret_cast<float4*>(o.h1 + row * H + 16 * b + 4 * q) =
-                float4{-2.f * h1[b][0], -2.f * h1[b][1], -2.f * h1[b][2], -2.f * h1[b][3]};
         }
       } else if constexpr (j <= CF::NB2) {
         constexpr int s = j - 1, T0 = s * CF::KB2;
         if constexpr (s == 0) {
+          // weight-gradient operand stores go out at the HEAD of the stage after the one that
+          // produced them: the next barrier's vmcnt(0) then waits on stores that drained under a
+          // whole stage of compute, not on stores issued just before it
+          if (valid)
+#pragma unroll
+            for (int b = 0; b < CF::HB; ++b)
+              *reinterpret_cast<float4*>(o.h1 + row * H + 16 * b + 4 * q) =
+                  float4{-2.f * h1[b][0], -2.f * h1[b][1], -2.f * h1[b][2], -2.f * h1[b][3]};
           const float4* b4 = reinterpret_cast<const float4*>(cur + CF::B_BIAS);
 #pragma unroll
           for (int b = 0; b < CF::HB; ++b) {
@@ -378,14 +383,16 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
           for (int b = 0; b < CF::HB; ++b) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) h2[b][r] = train_fold(h2[b][r]);
-            if (valid)
-              *reinterpret_cast<float4*>(o.h2 + row * H + 16 * b + 4 * q) =
-                  float4{-2.f * h2[b][0], -2.f * h2[b][1], -2.f * h2[b][2], -2.f * h2[b][3]};
           }
         }
       } else if constexpr (j < NSTG_F) {
         constexpr int s = j - 1 - CF::NB2, T0 = s * CF::KB3;
         if constexpr (s == 0) {
+          if (valid)
+#pragma unroll
+            for (int b = 0; b < CF::HB; ++b)
+              *reinterpret_cast<float4*>(o.h2 + row * H + 16 * b + 4 * q) =
+                  float4{-2.f * h2[b][0], -2.f * h2[b][1], -2.f * h2[b][2], -2.f * h2[b][3]};
           const float4* b4 = reinterpret_cast<const float4*>(cur + CF::C_BIAS);
 #pragma unroll
           for (int b = 0; b < CF::NO; ++b) {
@@ -420,18 +427,20 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
           }
 #pragma unroll
           for (int sl = CF::DQ * P; sl < BW::NS3; ++sl) a3[sl >> 2][sl & 3] = 0.f;  // pad slots
-          if (valid) {
-            float* dst = o.dp3 + row * (4 * BW::NS3) + q * BW::NS3;
-#pragma unroll
-            for (int b = 0; b < CF::NO; ++b)
-              *reinterpret_cast<float4*>(dst + 4 * b) = float4{a3[b][0], a3[b][1], a3[b][2], a3[b][3]};
-          }
 #pragma unroll
           for (int b = 0; b < CF::HB; ++b) dacc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
       } else if constexpr (j < NSTG_F + BW::NB3) {
         // ---- dH2 = dPre3 · W2, k-steps of stage sb
         constexpr int sb = j - NSTG_F;
+        if constexpr (sb == 0) {
+          if (valid) {
+            float* dst = o.dp3 + row * (4 * BW::NS3) + q * BW::NS3;
+#pragma unroll
+            for (int b = 0; b < CF::NO; ++b)
+              *reinterpret_cast<float4*>(dst + 4 * b) = float4{a3[b][0], a3[b][1], a3[b][2], a3[b][3]};
+          }
+        }
         if constexpr (kBwdF16) {
           if constexpr (sb == 0) gscale = bwd_row_scale(a3);  // dPre3 already stored unscaled
           gemm_r16_lazy<CF::HB, BW::KB3, sb * BW::KB3, false>(dacc, cur, lane, a3);
@@ -447,15 +456,19 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
             const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) dp2[b][r] = (dacc[b][r] * gscale) * (1.f - hh[r] * hh[r]);
-            if (valid)
-              *reinterpret_cast<float4*>(o.dp2 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
             dacc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
           }
-          if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         }
       } else if constexpr (j < NSTG_F + BW::NB3 + BW::NB2) {
         // ---- dH1 = dPre2 · W1
         constexpr int sb = j - NSTG_F - BW::NB3;
+        if constexpr (sb == 0) {
+          if (valid)
+#pragma unroll
+            for (int b = 0; b < CF::HB; ++b)
+              *reinterpret_cast<float4*>(o.dp2 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
+          if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
+        }
         if constexpr (kBwdF16) gemm_r16_lazy<CF::HB, BW::KB2, sb * BW::KB2, false>(dacc, cur, lane, dp2);
         else bwd_gemm_stage<CF::HB, BW::U2, sb * BW::U2>(dacc, cur, lane, dp2);
         if constexpr (sb == BW::NB2 - 1) {
@@ -466,13 +479,15 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
             const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) dp2[b][r] = (dacc[b][r] * gscale) * (1.f - hh[r] * hh[r]);  // now dPre1
-            if (valid)
-              *reinterpret_cast<float4*>(o.dp1 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
           }
-          if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         }
       } else {
         // ---- dx1 = dPre1 · W0[:, C:], lower spline VJP, g(P[l + 1])
+        if (valid)
+#pragma unroll
+          for (int b = 0; b < CF::HB; ++b)
+            *reinterpret_cast<float4*>(o.dp1 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
+        if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         floatx4 a1[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
         if constexpr (kBwdF16) {
           gemm_r16_lazy<1, BW::KSH, 0, false>(a1, cur, lane, dp2);

@@ -73,7 +73,16 @@ struct CfgR16 {
     return best;
   }
   static constexpr int KB2 = pick_kb(HB, H), NB2 = KS2 / KB2;
-  static constexpr int KB3 = pick_kb(NO, 16 * NO), NB3 = KS2 / KB3;
+  // GEMM3 in two halves of NO/2 output blocks (SPLIT3, two upper dims per quarter): half 0 holds
+  // every parameter of dim 0, so dim 0's spline can run beside half 1's MFMAs, and half 1 reuses
+  // half 0's B fragments instead of the GEMM2 accumulators
+#ifdef NAZ_R16_NOSPLIT3
+  static constexpr bool SPLIT3 = false;
+#else
+  static constexpr bool SPLIT3 = DQ == 2 && NO % 2 == 0 && (P + 3) / 4 <= NO / 2;
+#endif
+  static constexpr int NOC = SPLIT3 ? NO / 2 : NO;     // output blocks per GEMM3 stage
+  static constexpr int KB3 = pick_kb(NOC, 16 * NO), NB3H = KS2 / KB3, NB3 = (SPLIT3 ? 2 : 1) * NB3H;
   // stage A (fp16 image; the fp32 image A32 has the same size and bias/table offsets):
   //   [HB][KS1][2][256] | bias [H] | tables [S][TBL]
   static constexpr int A_BIAS = HB * KS1 * OT;
@@ -83,7 +92,7 @@ struct CfgR16 {
   static constexpr int B_BIAS = HB * KB2 * OT;
   static constexpr int B_SIZE = pad(B_BIAS + H);
   static constexpr int C_OFF = B_OFF + NB2 * B_SIZE;
-  static constexpr int C_BIAS = NO * KB3 * OT;
+  static constexpr int C_BIAS = NOC * KB3 * OT;
   static constexpr int C_SIZE = pad(C_BIAS + 16 * NO);
   static constexpr int A32_OFF = C_OFF + NB3 * C_SIZE;
   static constexpr int LAYER = A32_OFF + A_SIZE;
@@ -141,7 +150,7 @@ __global__ void coupling_pack_r16_kernel(const float* __restrict__ flat, float* 
     const float* b2 = W2 + CF::N_W2;
     const float* low = b2 + CF::N_B2;
     // f16 chunk word: (o, t, piece, lane, pair) -> two fp16 pieces of the scaled weight
-    auto chunk_word = [&](int q, int nt, int t0, int which) -> unsigned {
+    auto chunk_word = [&](int q, int nt, int t0, int which, int obase = 0) -> unsigned {
       const int o = q / (nt * CF::OT), r1 = q - o * nt * CF::OT;
       const int tl = r1 / CF::OT, r2 = r1 - tl * CF::OT;
       const int piece = r2 / kChunk, u = r2 - piece * kChunk;
@@ -157,7 +166,7 @@ __global__ void coupling_pack_r16_kernel(const float* __restrict__ flat, float* 
         } else if (which == 1) {
           v = -2.f * kSigScale * W1[(16 * o + i) * CF::H + r16_feat(t, qq, j)];
         } else {
-          const int orow = r16_out_row<CF>(o, i);
+          const int orow = r16_out_row<CF>(obase + o, i);
           v = orow >= 0 ? -2.f * W2[orow * CF::H + r16_feat(t, qq, j)] : 0.f;
         }
         out |= f16_piece_bits(v, piece) << (16 * e2);
@@ -209,7 +218,8 @@ __global__ void coupling_pack_r16_kernel(const float* __restrict__ flat, float* 
     } else {
       const int sq = (off - CF::C_OFF) / CF::C_SIZE, q = off - CF::C_OFF - sq * CF::C_SIZE;
       if (q < CF::C_BIAS) {
-        word = chunk_word(q, CF::KB3, sq * CF::KB3, 2);
+        const int hh = sq / CF::NB3H, s2 = sq - hh * CF::NB3H;
+        word = chunk_word(q, CF::KB3, s2 * CF::KB3, 2, hh * CF::NOC);
         is_word = true;
       } else if (q < CF::C_BIAS + 16 * CF::NO) {
         const int r = q - CF::C_BIAS, orow = r16_out_row<CF>(r >> 4, r & 15);
@@ -264,6 +274,47 @@ NAZ_DEV void gemm_r16_lazy(floatx4 (&acc)[NB], const float* __restrict__ stage, 
       const int base = ((o * KB + t) * 2) * 64 + lane;
       const Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
       acc[o] = mfma3_16(a, b, acc[o]);
+    }
+  }
+}
+
+// GEMM3 stage s: k-steps [T0, T0 + KB3) of output blocks [OB, OB + NOC) (OB = half · NOC).
+// Half 0 forms each k-step's B fragment from the GEMM2 accumulators (ACT: activated here) and
+// keeps it in f3; half 1 reads f3.  Bias from the stage's bias block at the half's first stage.
+template <class CF, int s, bool ACT, int NX>
+NAZ_DEV void gemm3_stage(floatx4 (&acc)[CF::NO], const float* __restrict__ cur, int lane, int q, floatx4 (&x)[NX],
+                         Frag2 (&f3)[CF::KS2]) {
+  constexpr int h = s / CF::NB3H, s2 = s % CF::NB3H, T0 = s2 * CF::KB3, OB = h * CF::NOC;
+  if constexpr (s2 == 0) {
+    const float4* b4 = reinterpret_cast<const float4*>(cur + CF::C_BIAS);
+#pragma unroll
+    for (int o = 0; o < CF::NOC; ++o) {
+      const float4 bv = b4[4 * (OB + o) + q];
+      acc[OB + o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+    }
+  }
+  const u32x4* c4 = reinterpret_cast<const u32x4*>(cur);
+#pragma unroll
+  for (int t = 0; t < CF::KB3; ++t) {
+    if constexpr (h == 0) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int blk = 2 * (T0 + t) + (j >> 2);
+        v[j] = blk < NX ? x[blk < NX ? blk : 0][j & 3] : 0.f;
+        if constexpr (ACT) v[j] = sig_fold(v[j]);
+      }
+      f3[T0 + t] = split8_f16(v);
+    }
+#ifdef NAZ_ABL_NOGEMM
+    for (int o = 0; o < CF::NOC; ++o) acc[OB + o][0] += (float)f3[T0 + t].h[0] * 1e-30f;
+    continue;
+#endif
+#pragma unroll
+    for (int o = 0; o < CF::NOC; ++o) {
+      const int base = ((o * CF::KB3 + t) * 2) * 64 + lane;
+      const Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+      acc[OB + o] = mfma3_16(a, f3[T0 + t], acc[OB + o]);
     }
   }
 }
@@ -368,6 +419,42 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
     const float* lp = packed + (int64_t)l * CF::LAYER;
     const float* lnext = packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER;
     floatx4 acc1[CF::HB], acc2[CF::HB], acc3[CF::NO];
+    Frag2 f3[CF::KS2];  // GEMM3's B fragments (half 0 forms them, half 1 reuses them)
+    // upper spline on this quarter's dim u (parameters in acc3 slots u P .. u P + P - 1)
+    auto upper = [&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      float uw[CF::K], uh[CF::K], ud[CF::K - 1];
+#pragma unroll
+      for (int k = 0; k < CF::K; ++k) {
+        constexpr int b0 = u * CF::P;
+        uw[k] = acc3[(b0 + k) >> 2][(b0 + k) & 3];
+        uh[k] = acc3[(b0 + CF::K + k) >> 2][(b0 + CF::K + k) & 3];
+      }
+#pragma unroll
+      for (int k = 0; k < CF::K - 1; ++k) {
+        constexpr int b0 = u * CF::P + 2 * CF::K;
+        ud[k] = acc3[(b0 + k) >> 2][(b0 + k) & 3];
+      }
+      float ld;
+#ifdef NAZ_ABL_NOSPLINE
+      if constexpr (VAR == 0) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int k = 0; k < CF::K; ++k) sacc += uw[k] + uh[k];
+        zu[u] += 1e-30f * sacc;
+        return;
+      }
+#endif
+      if constexpr (VAR == 1 && !kTrainFast) {
+        SplineTables<CF::K> tb;
+        build_tables<CF::K, kTrainFast>(uw, uh, ud, bound, tb);
+        zu[u] = rqs_apply<CF::K, DIR_INV, kTrainFast>(tb, zu[u], bound, ld);
+        ldsum += DIR_INV ? -ld : ld;
+      } else {
+        zu[u] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[u], bound, rc, ld);
+        ldsum += DIR_INV ? -ld : ld;
+      }
+    };
 
     static_for<0, CF::NSTG>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
@@ -501,76 +588,31 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
         gemm_r16_lazy<CF::HB, CF::KB2, T0, kLazyAct>(acc2, cur, lane, acc1);
         R16_PRIO(0);
       } else {
-        // ---------------- stage C_s: GEMM3 k-steps [T0, T0 + KB3) -> raw spline params
-        constexpr int s = j - 1 - CF::NB2, T0 = s * CF::KB3;
-#ifdef NAZ_R16_EAGER_ACT
-#pragma unroll
-        for (int b = 2 * T0; b < 2 * (T0 + CF::KB3); ++b)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc2[b][r] = sig_fold(acc2[b][r]);
-        constexpr bool kLazyAct = false;
-#else
+        // ---------------- stage C_s: GEMM3 (two halves of output blocks when SPLIT3)
+        constexpr int s = j - 1 - CF::NB2, T0s = (s % CF::NB3H) * CF::KB3;
 #ifdef NAZ_ABL_NOTANH
         constexpr bool kLazyAct = false, kNoAct = true;
 #else
         constexpr bool kLazyAct = VAR == 0 || kTrainFast, kNoAct = false;
 #endif
-        if constexpr (!kLazyAct && !kNoAct) {
+        if constexpr (!kLazyAct && !kNoAct && s < CF::NB3H) {  // accurate training forward: eager
 #pragma unroll
-          for (int b = 2 * T0; b < 2 * (T0 + CF::KB3); ++b)
+          for (int b = 2 * T0s; b < 2 * (T0s + CF::KB3); ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc2[b][r] = acc_fold(acc2[b][r]);
         }
-#endif
-        if constexpr (s == 0) {
-          const float4* b4 = reinterpret_cast<const float4*>(cur + CF::C_BIAS);
-#pragma unroll
-          for (int o = 0; o < CF::NO; ++o) {
-            const float4 bv = b4[4 * o + q];
-            acc3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
-          }
-        }
-        R16_PRIO(1);
-        gemm_r16_lazy<CF::NO, CF::KB3, T0, kLazyAct>(acc3, cur, lane, acc2);
-        R16_PRIO(0);
+        constexpr bool kHost = CF::SPLIT3 && s == CF::NB3H;  // first stage of half 1: dim 0's spline
+        if constexpr (!kHost) R16_PRIO(1);
+        gemm3_stage<CF, s, kLazyAct>(acc3, cur, lane, q, acc2, f3);
+        if constexpr (!kHost) R16_PRIO(0);
+        // dim 0's spline in the stage that issues half 1's MFMAs (the compiler still issues the
+        // MFMAs first: measured the same as NAZ_R16_NOSPLIT3, also with sched_group_barrier pins)
+        if constexpr (kHost) upper(std::integral_constant<int, 0>{});
       }
     });
 
-    // ---------------- upper spline on this quarter's DQ dims (next layer's stage A in flight)
-#pragma unroll
-    for (int u = 0; u < CF::DQ; ++u) {
-      float uw[CF::K], uh[CF::K], ud[CF::K - 1];
-#pragma unroll
-      for (int k = 0; k < CF::K; ++k) {
-        const int sw = u * CF::P + k, sh = u * CF::P + CF::K + k;
-        uw[k] = acc3[sw >> 2][sw & 3];
-        uh[k] = acc3[sh >> 2][sh & 3];
-      }
-#pragma unroll
-      for (int k = 0; k < CF::K - 1; ++k) {
-        const int sd = u * CF::P + 2 * CF::K + k;
-        ud[k] = acc3[sd >> 2][sd & 3];
-      }
-      float ld;
-#ifdef NAZ_ABL_NOSPLINE
-      if constexpr (VAR == 0) {
-        float sacc = 0.f;
-#pragma unroll
-        for (int k = 0; k < CF::K; ++k) sacc += uw[k] + uh[k];
-        zu[u] += 1e-30f * sacc;
-        continue;
-      }
-#endif
-      if constexpr (VAR == 1 && !kTrainFast) {
-        SplineTables<CF::K> tb;
-        build_tables<CF::K, kTrainFast>(uw, uh, ud, bound, tb);
-        zu[u] = rqs_apply<CF::K, DIR_INV, kTrainFast>(tb, zu[u], bound, ld);
-        ldsum += DIR_INV ? -ld : ld;
-      } else {
-        zu[u] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[u], bound, rc, ld);
-        ldsum += DIR_INV ? -ld : ld;
-      }
-    }
+    // ---------------- upper spline on this quarter's remaining dims (next layer's stage A in flight)
+    static_for<CF::SPLIT3 ? 1 : 0, CF::DQ>([&](auto uc) { upper(uc); });
   }
   if constexpr (VAR == 1) {  // P[0] = z
     if (valid) {

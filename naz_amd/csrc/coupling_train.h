@@ -278,6 +278,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
     float in[CF::KS1 * 8];
     floatx4 dp2[CF::HB];  // dPre2, then dPre1
     floatx4 dacc[CF::HB];
+    Frag2 f3[CF::KS2];  // GEMM3's B fragments (gemm3_stage)
     floatx4 dx1;
     float gscale = 1.f;  // f16x3: natural units of the current backward GEMM's accumulator
     float gy2[CF::DQ];
@@ -386,21 +387,15 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
           }
         }
       } else if constexpr (j < NSTG_F) {
-        constexpr int s = j - 1 - CF::NB2, T0 = s * CF::KB3;
+        constexpr int s = j - 1 - CF::NB2;
         if constexpr (s == 0) {
           if (valid)
 #pragma unroll
             for (int b = 0; b < CF::HB; ++b)
               *reinterpret_cast<float4*>(o.h2 + row * H + 16 * b + 4 * q) =
                   float4{-2.f * h2[b][0], -2.f * h2[b][1], -2.f * h2[b][2], -2.f * h2[b][3]};
-          const float4* b4 = reinterpret_cast<const float4*>(cur + CF::C_BIAS);
-#pragma unroll
-          for (int b = 0; b < CF::NO; ++b) {
-            const float4 bv = b4[4 * b + q];
-            a3[b] = floatx4{bv.x, bv.y, bv.z, bv.w};
-          }
         }
-        gemm_r16_lazy<CF::NO, CF::KB3, T0, false>(a3, cur, lane, h2);
+        gemm3_stage<CF, s, false>(a3, cur, lane, q, h2, f3);
         if constexpr (s == CF::NB3 - 1) {
           // ---- upper spline VJP (inverse map, libm-grade) -> dPre3 slots (in place of the raw
           // parameters: dim u's slots are read, then overwritten), g(y2)

@@ -1506,6 +1506,7 @@ static int ar_dispatch(const naz_ar_desc* d, F&& f) {
   if (d->D == 16 && d->C == 32) return f(AROps<CfgAR<16, 32, 128, 8>>{});
   if (d->D == 16 && d->C == 0) return f(AROps<CfgAR<16, 0, 128, 8>>{});
   if (d->D == 8 && d->C == 0) return f(AROps<CfgAR<8, 0, 128, 8>>{});
+  if (d->D == 4 && d->C == 2) return f(AROps<CfgAR<4, 2, 128, 8>>{});  // naz nsa bench shape
   return -2;
 }
 

@@ -9,7 +9,7 @@ import torch
 from naz_amd import ops
 
 
-@pytest.mark.parametrize("D,C", [(16, 32), (16, 0), (8, 0)])
+@pytest.mark.parametrize("D,C", [(16, 32), (16, 0), (8, 0), (4, 2)])
 def test_compiled_degrees_match_pyro_create_mask(D, C):
     d = ops.spline_ar_desc(D, C, 128, 8, 1)
     assert ops.spline_ar_supported(d)

@@ -21,6 +21,7 @@ CASES = [
     dict(flow_type="nsa", D=16, C=32, hidden=[128, 128], L=8, K=8, n=512),  # SURVEY §8d AR variant
     dict(flow_type="nsa", D=16, C=0, hidden=[128, 128], L=3, K=8, n=1000),
     dict(flow_type="nsa", D=8, C=0, hidden=[128, 128], L=2, K=8, n=1500),
+    dict(flow_type="nsa", D=4, C=2, hidden=[128, 128], L=3, K=8, n=1200),  # bench --flow nsa
 ]
 
 

@@ -521,7 +521,7 @@ def run_flow_case(args, dev, rank, world, dist):
         passes = Dd
     fl_ref = 2 * passes * Ld * sum(a * b for a, b in zip(dims[:-1], dims[1:]))  # the reference's work
     fl_row = fl_ref
-    ar_fused = ftype == "nsa" and getattr(f, "_plan", None) is not None and hasattr(f._plan, "executed_flop_per_row")
+    ar_fused = ftype in ("nsa", "maf") and getattr(f, "_plan", None) is not None and hasattr(f._plan, "executed_flop_per_row")
     if ar_fused:  # the fused autoregressive kernel's executed work (made_ar_r16.h)
         fl_row = f._plan.executed_flop_per_row()
     elif ftype != "nsc":  # executed work of the degree-scheduled inverse (padded blocks included)
@@ -568,7 +568,7 @@ def run_flow_case(args, dev, rank, world, dist):
             "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
             "config": {"workload": desc, "batch_per_gpu": B, "global_batch": G,
                        "parallelism": f"dp{world} (independent row shards, no collective)",
-                       "path": ("fused autoregressive-inverse kernel (naz_spline_ar_log_prob, one launch)" if ar_fused
+                       "path": ("fused autoregressive-inverse kernel (naz_ar_flow_log_prob, one launch)" if ar_fused
                                 else "fused kernel" if fused else "per-layer HIP kernels (rowgemm + spline/affine)")},
             "roofline": {"bound": "mfma", "achieved": achieved,
                          "peak": FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3, "unit": "TFLOP/s",

@@ -298,31 +298,38 @@ int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const fl
                              float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
                              int* nfe, int64_t B, void* stream);
 
-/* ---- §8b naz_spline_ar_inv: fused log_prob of a whole naz "nsa" flow ----------------------
+/* ---- §8b naz_spline_ar_inv / naz_affine_ar_inv: fused log_prob of a whole naz "nsa" or "maf" flow
  * Replaces the D-pass loop of pyro ConditionedSplineAutoregressive._inverse (naz
- * flows/transforms.py:165-198, NormalizingFlow.log_prob flow.py:45-79) over L layers of
- * ConditionalAutoRegressiveNN(C + D -> H -> H -> D (3K-1), tanh) conditioners: ONE launch, every
- * MADE hidden unit computed once (in the pass of its mask degree), f16x3 MFMA, the select-first
- * inverse spline per pass.  The hidden-unit degrees the kernel assumes are pyro's
- * (naz_spline_ar_degrees); the caller checks its masks against them. */
+ * flows/transforms.py:165-198) and ConditionedAffineAutoregressive._inverse (transforms.py:133-160),
+ * driven by NormalizingFlow.log_prob (flow.py:45-79), over L layers of
+ * ConditionalAutoRegressiveNN(C + D -> H x n_hidden -> D P, tanh) conditioners: ONE launch, every MADE
+ * hidden unit computed once (in the pass of its mask degree), f16x3 MFMA, the select-first inverse
+ * spline (P = 3K - 1) or the clamped affine inverse (P = 2: mean, log_scale in [-5, 3]) per pass.
+ * The hidden-unit degrees the kernel assumes are pyro's (naz_ar_flow_degrees); the caller checks
+ * its masks against them. */
+#define NAZ_AR_SPLINE 0 /* ConditionalSplineAutoregressive, quadratic RQ spline (naz nsa) */
+#define NAZ_AR_AFFINE 1 /* ConditionalAffineAutoregressive, stable=False (naz maf) */
 typedef struct naz_ar_desc {
-  int D, C, H, K, L; /* data dim, context dim, hidden width (two hidden layers), bins, layers */
+  int D, C, H, K, L; /* data dim, context dim, hidden width, bins (spline only), layers */
   int act;           /* NAZ_ACT_TANH */
-  float bound;       /* spline box half-width */
-  int reserved[8];
+  float bound;       /* spline box half-width (spline only) */
+  int n_hidden;      /* hidden layers, all of width H */
+  int kind;          /* NAZ_AR_SPLINE | NAZ_AR_AFFINE */
+  int reserved[6];
 } naz_ar_desc;
-int naz_spline_ar_supported(const naz_ar_desc* d);
-int64_t naz_spline_ar_packed_bytes(const naz_ar_desc* d);
-/* deg[u] (u < H) = mask index of hidden unit u in both hidden layers (pyro create_mask) */
-int naz_spline_ar_degrees(const naz_ar_desc* d, int* deg);
-/* HOST memory in and out.  flat: per layer W0 (x) mask0 [H][C + D] | b0 [H] | W1 (x) mask1 [H][H] | b1 [H] |
- * W2 (x) mask2 [D (3K-1)][H] (ARN rows p D + i) | b2 [D (3K-1)]; perm [L][D]: dim of order p (the ARN's
- * permutation).  packed: naz_spline_ar_packed_bytes bytes, to be copied to the device. */
-int naz_spline_ar_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed);
+int naz_ar_flow_supported(const naz_ar_desc* d);
+int64_t naz_ar_flow_packed_bytes(const naz_ar_desc* d);
+/* deg[u] (u < H) = mask index of hidden unit u in every hidden layer (pyro create_mask) */
+int naz_ar_flow_degrees(const naz_ar_desc* d, int* deg);
+/* HOST memory in and out.  flat: per layer W0 (x) mask0 [H][C + D] | b0 [H] | {Wi (x) maski [H][H] | bi [H]}
+ * for hidden layers 2 .. n_hidden | Wout (x) maskout [D P][H] (ARN rows p D + i) | bout [D P]; perm [L][D]:
+ * dim of order p (the ARN's permutation).  packed: naz_ar_flow_packed_bytes bytes, to be copied to the
+ * device. */
+int naz_ar_flow_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed);
 /* out_lp[r] = log p(x_r | ctx_r) (+ naz bounding map when low/high are set); ldc = 0 broadcasts one
  * context row.  |x|, |ctx| must stay below 2^15 (the f16x3 input split); the caller checks. */
-int naz_spline_ar_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                           int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream);
+int naz_ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                         int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,7 @@ class CouplingDesc(C.Structure):
 
 class ArDesc(C.Structure):
     _fields_ = [("D", C.c_int), ("C", C.c_int), ("H", C.c_int), ("K", C.c_int), ("L", C.c_int), ("act", C.c_int),
-                ("bound", C.c_float), ("reserved", C.c_int * 8)]
+                ("bound", C.c_float), ("n_hidden", C.c_int), ("kind", C.c_int), ("reserved", C.c_int * 6)]
 
 
 class CnfDesc(C.Structure):
@@ -81,11 +81,11 @@ SIGNATURES = {
                                     _i, _vp, _i64, _vp, _i, _i64, _vp]),
     "naz_cnf_integrate_dopri5": (C.c_int, [C.POINTER(CnfDesc), _vp, _vp, _i64, _vp, _i64, _vp, _i64, C.c_float,
                                            C.c_float, C.c_float, C.c_float, _i, _vp, _i64, _vp, _i, _vp, _i64, _vp]),
-    "naz_spline_ar_supported": (C.c_int, [C.POINTER(ArDesc)]),
-    "naz_spline_ar_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),
-    "naz_spline_ar_degrees": (C.c_int, [C.POINTER(ArDesc), _vp]),
-    "naz_spline_ar_pack_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _vp]),
-    "naz_spline_ar_log_prob": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
+    "naz_ar_flow_supported": (C.c_int, [C.POINTER(ArDesc)]),
+    "naz_ar_flow_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),
+    "naz_ar_flow_degrees": (C.c_int, [C.POINTER(ArDesc), _vp]),
+    "naz_ar_flow_pack_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _vp]),
+    "naz_ar_flow_log_prob": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
     "naz_coupling_supported": (C.c_int, [C.POINTER(CouplingDesc)]),
     "naz_coupling_param_count": (C.c_int64, [C.POINTER(CouplingDesc)]),
     "naz_coupling_packed_bytes": (C.c_int64, [C.POINTER(CouplingDesc)]),

@@ -263,20 +263,20 @@ int naz_coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const
 
 int naz_coupling_dp3_columns(const naz_coupling_desc* d, int* rows) { return coupling_dp3_columns(d, rows); }
 
-int naz_spline_ar_supported(const naz_ar_desc* d) { return spline_ar_supported(d); }
-int64_t naz_spline_ar_packed_bytes(const naz_ar_desc* d) { return spline_ar_packed_bytes(d); }
-int naz_spline_ar_degrees(const naz_ar_desc* d, int* deg) { return spline_ar_degrees(d, deg); }
-int naz_spline_ar_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed) {
-  return spline_ar_pack_host(d, flat, perm, packed);
+int naz_ar_flow_supported(const naz_ar_desc* d) { return ar_flow_supported(d); }
+int64_t naz_ar_flow_packed_bytes(const naz_ar_desc* d) { return ar_flow_packed_bytes(d); }
+int naz_ar_flow_degrees(const naz_ar_desc* d, int* deg) { return ar_flow_degrees(d, deg); }
+int naz_ar_flow_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed) {
+  return ar_flow_pack_host(d, flat, perm, packed);
 }
-int naz_spline_ar_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+int naz_ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
                            int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream) {
-  if (B < 0) return set_error("naz_spline_ar_log_prob: negative batch");
+  if (B < 0) return set_error("naz_ar_flow_log_prob: negative batch");
   if (B > 0 && (packed == nullptr || x == nullptr || out_lp == nullptr))
-    return set_error("naz_spline_ar_log_prob: null pointer");
+    return set_error("naz_ar_flow_log_prob: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
-    return set_error("naz_spline_ar_log_prob: conditional flow needs ctx");
-  return spline_ar_log_prob(d, packed, x, ldx, ctx, ldc, low, high, out_lp, B, as_stream(stream));
+    return set_error("naz_ar_flow_log_prob: conditional flow needs ctx");
+  return ar_flow_log_prob(d, packed, x, ldx, ctx, ldc, low, high, out_lp, B, as_stream(stream));
 }
 
 }  // extern "C"

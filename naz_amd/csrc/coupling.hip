@@ -1463,7 +1463,7 @@ int coupling_dp3_columns(const naz_coupling_desc* d, int* rows) {
   return rc == -2 ? unsupported(d) : rc;
 }
 
-// ---- fused autoregressive inverse (made_ar_r16.h): naz nsa log_prob ---------------------
+// ---- fused autoregressive inverse (made_ar_r16.h): naz nsa / maf log_prob -------------
 template <class CF>
 struct AROps {
   static int64_t layer_floats() { return CF::LAYER; }
@@ -1471,30 +1471,28 @@ struct AROps {
     for (int u = 0; u < CF::H; ++u) deg[u] = CF::deg(u);
     return 0;
   }
-  // flat per layer: W0m [H][C + D] | b0 [H] | W1m [H][H] | b1 [H] | W2m [D P][H] | b2 [D P]
+  // flat per layer: W0m [H][C + D] | b0 [H] | {Wim [H][H] | bi [H]} x (NHID - 1) | Woutm [D P][H] | bout [D P]
   static int pack_host(const float* flat, const int* perm, int L, float* out) {
     constexpr int H = CF::H, D = CF::D, C = CF::C, P = CF::P;
-    constexpr int64_t per = (int64_t)H * (C + D) + H + H * H + H + (int64_t)D * P * H + D * P;
+    constexpr int64_t per = (int64_t)H * (C + D) + H + (int64_t)(CF::NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
     for (int l = 0; l < L; ++l) {
-      const float* W0 = flat + l * per;
-      const float* b0 = W0 + H * (C + D);
-      const float* W1 = b0 + H;
-      const float* b1 = W1 + H * H;
-      const float* W2 = b1 + H;
-      const float* b2 = W2 + D * P * H;
-      for (int p = 0; p < D; ++p)
-        if (perm[l * D + p] < 0 || perm[l * D + p] >= D) return set_error("naz_spline_ar_pack: bad permutation");
-      made_ar_pack_layer<CF>(W0, b0, W1, b1, W2, b2, perm + l * D, out + (int64_t)l * CF::LAYER);
+      bool seen[32] = {};
+      for (int p = 0; p < D; ++p) {
+        const int v = perm[l * D + p];
+        if (v < 0 || v >= D || seen[v]) return set_error("naz_ar_flow_pack: layer %d: bad permutation", l);
+        seen[v] = true;
+      }
+      made_ar_pack_layer<CF>(flat + l * per, perm + l * D, out + (int64_t)l * CF::LAYER);
     }
     return 0;
   }
   static int log_prob(const float* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
                       const float* low, const float* high, float* out_lp, int64_t B, float bound, hipStream_t s) {
-    static_assert(2 * CF::STG * 4 <= 160 * 1024, "two pass stages exceed the LDS");
+    static_assert(2 * CF::STG * 4 <= 160 * 1024, "two weight stages exceed the LDS");
     if (B == 0 || L == 0) return 0;
-    const int64_t rows = 16 * kARWaves, grid = (B + rows - 1) / rows;
+    const int64_t rows = 16 * CF::NW, grid = (B + rows - 1) / rows;
     const size_t lds = (size_t)2 * CF::STG * 4;
-    hipLaunchKernelGGL((made_ar_r16_kernel<CF>), dim3((unsigned)grid), dim3(64 * kARWaves), lds, s, packed, L, x,
+    hipLaunchKernelGGL((made_ar_r16_kernel<CF>), dim3((unsigned)grid), dim3(64 * CF::NW), lds, s, packed, L, x,
                        ldx, ctx, ldc, low, high, out_lp, B, bound);
     return check_launch("made_ar_r16_kernel");
   }
@@ -1502,19 +1500,30 @@ struct AROps {
 
 template <class F>
 static int ar_dispatch(const naz_ar_desc* d, F&& f) {
-  if (d == nullptr || d->act != NAZ_ACT_TANH || d->K != 8 || d->H != 128 || !(d->bound > 0.f) || d->L < 0) return -2;
-  if (d->D == 16 && d->C == 32) return f(AROps<CfgAR<16, 32, 128, 8>>{});
-  if (d->D == 16 && d->C == 0) return f(AROps<CfgAR<16, 0, 128, 8>>{});
-  if (d->D == 8 && d->C == 0) return f(AROps<CfgAR<8, 0, 128, 8>>{});
-  if (d->D == 4 && d->C == 2) return f(AROps<CfgAR<4, 2, 128, 8>>{});  // naz nsa bench shape
+  if (d == nullptr || d->act != NAZ_ACT_TANH || d->L < 0) return -2;
+  if (d->kind == NAZ_AR_SPLINE) {
+    if (d->K != 8 || d->H != 128 || d->n_hidden != 2 || !(d->bound > 0.f)) return -2;
+    if (d->D == 16 && d->C == 32) return f(AROps<CfgAR<16, 32, 128, 8>>{});
+    if (d->D == 16 && d->C == 0) return f(AROps<CfgAR<16, 0, 128, 8>>{});
+    if (d->D == 8 && d->C == 0) return f(AROps<CfgAR<8, 0, 128, 8>>{});
+    if (d->D == 4 && d->C == 2) return f(AROps<CfgAR<4, 2, 128, 8>>{});  // naz nsa bench shape
+    return -2;
+  }
+  if (d->kind == NAZ_AR_AFFINE) {
+    // K is unused (the instances carry 8); the maf paper shape (train_mle_all_data.py:62-70) and
+    // SURVEY §8d's config-3 AR variant
+    if (d->D == 2 && d->C == 2 && d->H == 150 && d->n_hidden == 3) return f(AROps<CfgAR<2, 2, 150, 8, 3, true>>{});
+    if (d->D == 16 && d->C == 32 && d->H == 128 && d->n_hidden == 2) return f(AROps<CfgAR<16, 32, 128, 8, 2, true>>{});
+    return -2;
+  }
   return -2;
 }
 
-int spline_ar_supported(const naz_ar_desc* d) {
+int ar_flow_supported(const naz_ar_desc* d) {
   return ar_dispatch(d, [](auto) { return 1; }) == 1 ? 1 : 0;
 }
 
-int64_t spline_ar_packed_bytes(const naz_ar_desc* d) {
+int64_t ar_flow_packed_bytes(const naz_ar_desc* d) {
   int64_t v = -1;
   ar_dispatch(d, [&](auto ops) {
     v = decltype(ops)::layer_floats() * d->L * 4;
@@ -1524,28 +1533,28 @@ int64_t spline_ar_packed_bytes(const naz_ar_desc* d) {
 }
 
 static int ar_unsupported(const naz_ar_desc* d) {
-  if (d == nullptr) return set_error("naz_spline_ar: null descriptor");
-  return set_error("naz_spline_ar: no fused instantiation for D=%d C=%d H=%d K=%d act=%d", d->D, d->C, d->H, d->K,
-                   d->act);
+  if (d == nullptr) return set_error("naz_ar_flow: null descriptor");
+  return set_error("naz_ar_flow: no fused instantiation for kind=%d D=%d C=%d H=%d x %d K=%d act=%d", d->kind, d->D,
+                   d->C, d->H, d->n_hidden, d->K, d->act);
 }
 
-int spline_ar_degrees(const naz_ar_desc* d, int* deg) {
-  if (deg == nullptr) return set_error("naz_spline_ar_degrees: null output");
+int ar_flow_degrees(const naz_ar_desc* d, int* deg) {
+  if (deg == nullptr) return set_error("naz_ar_flow_degrees: null output");
   const int rc = ar_dispatch(d, [&](auto ops) { return decltype(ops)::degrees(deg); });
   return rc == -2 ? ar_unsupported(d) : rc;
 }
 
-int spline_ar_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed) {
-  if (flat == nullptr || perm == nullptr || packed == nullptr) return set_error("naz_spline_ar_pack_host: null pointer");
+int ar_flow_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed) {
+  if (flat == nullptr || perm == nullptr || packed == nullptr) return set_error("naz_ar_flow_pack_host: null pointer");
   const int rc = ar_dispatch(d, [&](auto ops) {
     return decltype(ops)::pack_host(flat, perm, d->L, static_cast<float*>(packed));
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }
 
-int spline_ar_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                       int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s) {
-  if ((low == nullptr) != (high == nullptr)) return set_error("naz_spline_ar_log_prob: low/high must both be set");
+int ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                     int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s) {
+  if ((low == nullptr) != (high == nullptr)) return set_error("naz_ar_flow_log_prob: low/high must both be set");
   const int rc = ar_dispatch(d, [&](auto ops) {
     return decltype(ops)::log_prob(static_cast<const float*>(packed), d->L, x, ldx, ctx, ldc, low, high, out_lp, B,
                                    d->bound, s);

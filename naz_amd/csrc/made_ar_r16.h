@@ -1,8 +1,10 @@
-// Fused autoregressive-inverse flow: log_prob of a whole naz "nsa" flow (L layers of pyro
-// ConditionalSplineAutoregressive over a ConditionalAutoRegressiveNN with two tanh hidden layers)
-// in ONE launch.  SURVEY.md §8a rows a4/a6/a8 (naz/flows/transforms.py:165-198, pyro
-// SplineAutoregressive._inverse); the §8b `naz_spline_ar_inv` entry.  Included by coupling.hip
-// after coupling_r16.h (Frag2, split8_f16, sig_fold, kSigScale, stage_issue, r16_feat, ...).
+// Fused autoregressive-inverse flow: log_prob of a whole naz "nsa" or "maf" flow (L layers of
+// pyro ConditionalSplineAutoregressive / ConditionalAffineAutoregressive over a
+// ConditionalAutoRegressiveNN with NHID tanh hidden layers) in ONE launch.  SURVEY.md §8a rows
+// a4/a5/a6/a8 (naz/flows/transforms.py:133-198, pyro SplineAutoregressive._inverse /
+// AffineAutoregressive._inverse); the §8b `naz_spline_ar_inv` / `naz_affine_ar_inv` entries.
+// Included by coupling.hip after coupling_r16.h (Frag2, split8_f16, sig_fold, kSigScale,
+// stage_issue, r16_feat, ...).
 //
 // The reference inverts a layer with D sequential passes of the WHOLE MADE network (pass k makes
 // the dim of order k final).  A hidden unit with mask index m ("degree": it reads the context and
@@ -12,18 +14,21 @@
 // wave (lane = batch row l & 15, quarter q = l >> 4, the r16 layout):
 //   pass p (order p, dim d_p = perm[p]):
 //     * recompute the 16-unit blocks of hidden layer 1 that hold units of degree p (f16x3 MFMA
-//       over [ctx | x]; dims of order >= p are still 0 or garbage-free zeros, and units of
-//       higher degree in the same block are recomputed in their own pass), activate, and keep
-//       them as f16 hi/lo B fragments in registers (the whole layer: H/32 fragments);
-//     * the same for hidden layer 2 from layer 1's fragments (k-steps up to unit E[p]);
-//     * the 3K-1 spline parameters of dim d_p from layer 2's fragments (2 output blocks);
-//     * gather the parameters of the row into every lane of the row (ds_bpermute) and run the
-//       select-first inverse spline on x[d_p] (every quarter redundantly: no broadcast after).
+//       over [ctx | x]; dims of order >= p only reach units of higher degree, which are
+//       recomputed in their own pass), activate, and keep them as f16 hi/lo B fragments in
+//       registers (the whole layer: ceil(H/32) fragments);
+//     * the same for every further hidden layer from the previous one's fragments (k-steps up to
+//       unit E[p]);
+//     * the output rows of dim d_p (3K-1 spline parameters, or (mean, log_scale));
+//     * spline: gather the row's parameters into every lane of the row (ds_bpermute) and run the
+//       select-first inverse spline on x[d_p]; affine: x[d_p] = (y - mean) exp(-clamp(ls, -5, 3))
+//       (every quarter redundantly: no broadcast after).
 //   Masked-out products are exact zeros of the packed image (W ⊙ mask), so the values equal
 //   pyro's D full passes; the conditioner work is one triangular network per layer instead of D.
-// Weights stream per pass through the coupling kernels' two-slot LDS-DMA ring (one <= 40 KB
-// stage per pass, packed on the host by made_ar_pack); x stays in registers in natural dim order
-// (the uniform dim index d_p addresses it through M0-relative moves).
+// Weights stream through the coupling kernels' two-slot LDS-DMA ring: the per-pass sub-layers
+// (hidden layer 1, 2, ..., output) are grouped greedily into stages of at most kARCap floats
+// (nsa at H = 128: one stage per pass).  x stays in registers in natural dim order (the uniform
+// dim index d_p addresses it through M0-relative moves).
 #pragma once
 
 namespace naz {
@@ -37,53 +42,98 @@ constexpr int ar_round_half_even(double v) {
   return static_cast<int>(i);
 }
 
-template <int D_, int C_, int H_, int K_>
+constexpr int kARCap = 20480;  // floats per ring slot at most (2 slots = 160 KB, one workgroup per CU)
+
+template <int D_, int C_, int H_, int K_, int NHID_ = 2, bool AFFINE_ = false>
 struct CfgAR {
-  static constexpr int D = D_, C = C_, H = H_, K = K_, P = 3 * K - 1;
-  static constexpr int HB = H / 16, KSH = H / 32;      // hidden 16-unit blocks, 32-k steps over them
-  static constexpr int KC = (C + 31) / 32;             // context k-steps of hidden layer 1
-  static constexpr int KI = KC + 1;                    // + one k-step over x (D <= 32)
-  static constexpr int NOB = (P + 15) / 16;            // output blocks (params of one dim)
-  static constexpr int OT = 2 * kChunk;                // floats per (block, k-step): hi + lo
+  static constexpr int D = D_, C = C_, H = H_, K = K_, NHID = NHID_;
+  static constexpr bool AFFINE = AFFINE_;
+  static constexpr int P = AFFINE ? 2 : 3 * K - 1;      // ARN outputs per dim
+  static constexpr int HP = (H + 31) / 32 * 32;         // padded hidden width
+  static constexpr int HB = HP / 16, KSH = HP / 32;     // hidden 16-unit blocks, 32-k steps over them
+  static constexpr int KC = (C + 31) / 32;              // context k-steps of hidden layer 1
+  static constexpr int KI = KC + 1;                     // + one k-step over x (D <= 32)
+  static constexpr int NOB = (P + 15) / 16;             // output blocks (params of one dim)
+  static constexpr int OT = 2 * kChunk;                 // floats per (block, k-step): hi + lo
   static constexpr int deg(int u) {
     if (C > 0) return ar_round_half_even(1.0 + (double)u * (double)(D - 1) / (double)(H - 1)) - 1;
     return ar_round_half_even(1.0 + (double)u * (double)(D - 2) / (double)(H - 1));
   }
-  // E(p) = number of hidden units of degree <= p (a prefix: degrees are non-decreasing)
-  static constexpr int E(int p) {
-    int n = 0;
-    for (int u = 0; u < H; ++u) n += deg(u) <= p ? 1 : 0;
-    return n;
-  }
-  static constexpr int Ep(int p) { return p < 0 ? 0 : E(p); }
-  // blocks (re)computed in pass p: those holding units of degree p; blo > bhi = none
-  static constexpr int blo(int p) { return Ep(p - 1) >> 4; }
-  static constexpr int bhi(int p) { return Ep(p) > Ep(p - 1) ? (Ep(p) - 1) >> 4 : blo(p) - 1; }
-  static constexpr int nb(int p) { return bhi(p) - blo(p) + 1; }
-  static constexpr int kt(int p) { return (Ep(p) + 31) / 32; }  // k-steps over units of degree <= p
   static constexpr int pad(int n) { return (n + 255) / 256 * 256; }
-  // stage of pass p: [L1 blocks nb x KI x OT] [L2 blocks nb x kt x OT] [out NOB x kt x OT]
-  //                  [bias: L1 blocks nb x 16 | L2 blocks nb x 16 | out NOB x 16]
-  static constexpr int off_l2(int p) { return nb(p) * KI * OT; }
-  static constexpr int off_out(int p) { return off_l2(p) + nb(p) * kt(p) * OT; }
-  static constexpr int off_bias(int p) { return off_out(p) + NOB * kt(p) * OT; }
-  static constexpr int stage_floats(int p) { return pad(off_bias(p) + 32 * nb(p) + 16 * NOB); }
-  static constexpr int max_stage() {
-    int m = 0;
-    for (int p = 0; p < D; ++p) m = stage_floats(p) > m ? stage_floats(p) : m;
-    return m;
+  // the per-layer plan, computed once per instantiation (a table: the nested constexpr calls of a
+  // direct formulation exceed the compiler's constant-evaluation step limit)
+  struct Layout {
+    int E[32];         // E[p] = number of hidden units of degree <= p (a prefix: degrees are non-decreasing)
+    int sid[32][4];    // stage holding sub-layer i of pass p
+    int off[32][4];    // its offset in the stage (floats)
+    int sfl[128];      // floats of stage s (padded)
+    int nstg, stg;
+  };
+  static constexpr int E_of(const Layout& y, int p) { return p < 0 ? 0 : y.E[p]; }
+  static constexpr int blo_of(const Layout& y, int p) { return E_of(y, p - 1) >> 4; }
+  static constexpr int bhi_of(const Layout& y, int p) {
+    return E_of(y, p) > E_of(y, p - 1) ? (E_of(y, p) - 1) >> 4 : blo_of(y, p) - 1;
   }
-  static constexpr int STG = max_stage();              // stage stride = LDS ring slot (floats)
-  // per layer: D stages | perm (D ints)
-  static constexpr int PERM_OFF = D * STG;
+  static constexpr int nb_of(const Layout& y, int p) { return bhi_of(y, p) - blo_of(y, p) + 1; }
+  static constexpr int kt_of(const Layout& y, int p) { return (E_of(y, p) + 31) / 32; }
+  // sub-layer i of pass p: 0 = hidden layer 1 over [ctx | x], 1 .. NHID-1 = hidden layer i + 1,
+  // NHID = output rows; image: [fragments (block, k-step)] [bias: 16 per block]
+  static constexpr int frags_of(const Layout& y, int p, int i) {
+    return i == 0 ? nb_of(y, p) * KI : (i < NHID ? nb_of(y, p) * kt_of(y, p) : NOB * kt_of(y, p));
+  }
+  static constexpr int sub_floats_of(const Layout& y, int p, int i) {
+    return frags_of(y, p, i) * OT + 16 * (i < NHID ? nb_of(y, p) : NOB);
+  }
+  static constexpr Layout make_layout() {
+    Layout y{};
+    int cnt[32] = {};
+    for (int u = 0; u < H; ++u) ++cnt[deg(u) < 0 ? 0 : deg(u)];
+    for (int p = 0, run = 0; p < D; ++p) y.E[p] = run += cnt[p];
+    // greedy grouping of each pass's sub-layers into stages of <= kARCap floats
+    int s = -1;
+    for (int p = 0; p < D; ++p) {
+      int run = 0;
+      for (int i = 0; i <= NHID; ++i) {
+        const int sz = sub_floats_of(y, p, i);
+        if (i == 0 || run + sz > kARCap) {
+          ++s;
+          run = 0;
+        }
+        y.sid[p][i] = s;
+        y.off[p][i] = run;
+        run += sz;
+        y.sfl[s] = pad(run);
+      }
+    }
+    y.nstg = s + 1;
+    for (int t = 0; t < y.nstg; ++t) y.stg = y.sfl[t] > y.stg ? y.sfl[t] : y.stg;
+    return y;
+  }
+  static constexpr Layout LY = make_layout();
+  static constexpr int E(int p) { return E_of(LY, p); }
+  static constexpr int blo(int p) { return blo_of(LY, p); }  // blocks (re)computed in pass p: those
+  static constexpr int bhi(int p) { return bhi_of(LY, p); }  // holding units of degree p; none if blo > bhi
+  static constexpr int nb(int p) { return nb_of(LY, p); }
+  static constexpr int kt(int p) { return kt_of(LY, p); }    // k-steps over units of degree <= p
+  static constexpr int frags(int p, int i) { return frags_of(LY, p, i); }
+  static constexpr int stage_id(int p, int i) { return LY.sid[p][i]; }
+  static constexpr int sub_off(int p, int i) { return LY.off[p][i]; }
+  static constexpr int stage_floats(int s) { return LY.sfl[s]; }
+  static constexpr int NSTG = LY.nstg;
+  static constexpr int STG = LY.stg;                  // stage stride = LDS ring slot (floats)
+  // per layer: NSTG stages | perm (D ints)
+  static constexpr int PERM_OFF = NSTG * STG;
   static constexpr int LAYER = pad(PERM_OFF + D);
-  static_assert(H % 32 == 0 && H <= 256 && D <= 32 && D >= 2, "unsupported fused autoregressive shape");
-  static_assert(P <= 16 * NOB && NOB <= 2, "output blocks");
+  // waves per workgroup (one workgroup per CU): 12 (3 per SIMD) when the live set fits 168 VGPRs
+  static constexpr int NW = NHID * KSH <= 8 ? 12 : 8;
+  static_assert(H <= 256 && D <= 32 && D >= 2 && NHID >= 1 && NHID <= 3, "unsupported fused autoregressive shape");
+  static_assert(NOB <= 2 && NSTG <= 128, "output blocks / stages");
 };
 
-// ---------------------------------------------------------------- host packer (made_ar_pack)
-// flat per layer (natural layouts, masks already applied): W0m [H][C + D], b0 [H], W1m [H][H],
-// b1 [H], W2m [D P][H] (ARN rows p D + i), b2 [D P]; perm[l][p] = dim of order p.
+// ---------------------------------------------------------------- host packer (ar_flow_pack)
+// flat per layer (natural layouts, masks already applied): W0m [H][C + D], b0 [H],
+// {Wim [H][H], bi [H]} for hidden layers 2 .. NHID, Woutm [D P][H] (ARN rows p D + i), bout [D P];
+// perm[l][p] = dim of order p.
 static unsigned short ar_f16_bits(float v) {
   const _Float16 h = (_Float16)v;
   return __builtin_bit_cast(unsigned short, h);
@@ -95,9 +145,19 @@ static unsigned ar_piece(float v, int piece) {
 }
 
 template <class CF>
-static void made_ar_pack_layer(const float* W0, const float* b0, const float* W1, const float* b1, const float* W2,
-                               const float* b2, const int* perm, float* out) {
+static void made_ar_pack_layer(const float* flat, const int* perm, float* out) {
   constexpr int D = CF::D, C = CF::C, H = CF::H, P = CF::P;
+  const float* Wl[CF::NHID + 1];
+  const float* bl[CF::NHID + 1];
+  {
+    const float* f = flat;
+    for (int i = 0; i <= CF::NHID; ++i) {
+      const int rows = i < CF::NHID ? H : D * P, cols = i == 0 ? C + D : H;
+      Wl[i] = f;
+      bl[i] = f + rows * cols;
+      f += rows * cols + rows;
+    }
+  }
   unsigned* ou = reinterpret_cast<unsigned*>(out);
   for (int i = 0; i < CF::LAYER; ++i) out[i] = 0.f;
   // one (block, k-step) fragment image: word (piece, lane, pair) holds slots j = 2 pair, 2 pair + 1
@@ -111,39 +171,45 @@ static void made_ar_pack_layer(const float* W0, const float* b0, const float* W1
         }
   };
   for (int p = 0; p < D; ++p) {
-    unsigned* st = ou + p * CF::STG;
     const int dp = perm[p];
-    for (int bi = 0; bi < CF::nb(p); ++bi) {
-      const int b = CF::blo(p) + bi;
-      for (int t = 0; t < CF::KI; ++t)  // hidden layer 1 over [ctx | x]
-        frag(st + (bi * CF::KI + t) * CF::OT, [&](int m, int kg, int j) -> float {
-          const int u = 16 * b + m;
-          if (u >= H) return 0.f;
-          const int col = t < CF::KC ? 32 * t + 8 * kg + j : -1;
-          if (t < CF::KC) return col < C ? kSigScale * W0[u * (C + D) + col] : 0.f;
-          const int d = 8 * kg + j;
-          return d < D ? kSigScale * W0[u * (C + D) + C + d] : 0.f;
-        });
-      for (int t = 0; t < CF::kt(p); ++t)  // hidden layer 2 over layer 1's fragments
-        frag(st + CF::off_l2(p) + (bi * CF::kt(p) + t) * CF::OT, [&](int m, int kg, int j) -> float {
-          const int u = 16 * b + m, v = r16_feat(t, kg, j);
-          return (u < H && v < H) ? -2.f * kSigScale * W1[u * H + v] : 0.f;
-        });
-    }
-    for (int o = 0; o < CF::NOB; ++o)
-      for (int t = 0; t < CF::kt(p); ++t)  // the 3K-1 parameters of dim d_p
-        frag(st + CF::off_out(p) + (o * CF::kt(p) + t) * CF::OT, [&](int m, int kg, int j) -> float {
-          const int pi = 16 * o + m, v = r16_feat(t, kg, j);
-          return (pi < P && v < H) ? -2.f * W2[(pi * D + dp) * H + v] : 0.f;
-        });
-    float* bias = out + p * CF::STG + CF::off_bias(p);
-    for (int bi = 0; bi < CF::nb(p); ++bi)
-      for (int r = 0; r < 16; ++r) {
-        const int u = 16 * (CF::blo(p) + bi) + r;
-        bias[16 * bi + r] = u < H ? kSigScale * b0[u] : 0.f;
-        bias[16 * (CF::nb(p) + bi) + r] = u < H ? kSigScale * b1[u] : 0.f;
+    for (int i = 0; i <= CF::NHID; ++i) {
+      const int base = CF::stage_id(p, i) * CF::STG + CF::sub_off(p, i);
+      unsigned* st = ou + base;
+      float* bias = out + base + CF::frags(p, i) * CF::OT;
+      if (i < CF::NHID) {
+        const int kts = i == 0 ? CF::KI : CF::kt(p);
+        for (int bi = 0; bi < CF::nb(p); ++bi) {
+          const int b = CF::blo(p) + bi;
+          for (int t = 0; t < kts; ++t)
+            frag(st + (bi * kts + t) * CF::OT, [&](int m, int kg, int j) -> float {
+              const int u = 16 * b + m;
+              if (u >= H) return 0.f;
+              if (i > 0) {  // over the previous hidden layer's fragments
+                const int v = r16_feat(t, kg, j);
+                return v < H ? -2.f * kSigScale * Wl[i][u * H + v] : 0.f;
+              }
+              if (t < CF::KC) {
+                const int col = 32 * t + 8 * kg + j;
+                return col < C ? kSigScale * Wl[0][u * (C + D) + col] : 0.f;
+              }
+              const int d = 8 * kg + j;
+              return d < D ? kSigScale * Wl[0][u * (C + D) + C + d] : 0.f;
+            });
+          for (int r = 0; r < 16; ++r) {
+            const int u = 16 * b + r;
+            bias[16 * bi + r] = u < H ? kSigScale * bl[i][u] : 0.f;
+          }
+        }
+      } else {
+        for (int o = 0; o < CF::NOB; ++o)
+          for (int t = 0; t < CF::kt(p); ++t)  // the output rows of dim d_p
+            frag(st + (o * CF::kt(p) + t) * CF::OT, [&](int m, int kg, int j) -> float {
+              const int pi = 16 * o + m, v = r16_feat(t, kg, j);
+              return (pi < P && v < H) ? -2.f * Wl[CF::NHID][(pi * D + dp) * H + v] : 0.f;
+            });
+        for (int r = 0; r < 16 * CF::NOB; ++r) bias[r] = r < P ? bl[CF::NHID][r * D + dp] : 0.f;
       }
-    for (int r = 0; r < 16 * CF::NOB; ++r) bias[32 * CF::nb(p) + r] = r < P ? b2[r * D + dp] : 0.f;
+    }
   }
   for (int p = 0; p < D; ++p) reinterpret_cast<int*>(out)[CF::PERM_OFF + p] = perm[p];
 }
@@ -164,31 +230,19 @@ NAZ_DEV void ar_split4(Frag2& f, const floatx4& a) {
   f.l = __builtin_bit_cast(half8, Lo);
 }
 
-#ifndef NAZ_AR_WAVES
-#define NAZ_AR_WAVES 12
-#endif
-// waves (16 rows each) per workgroup; one workgroup per CU (the two pass stages take ~84 KB of
-// LDS), NAZ_AR_WAVES / 4 waves per SIMD
-constexpr int kARWaves = NAZ_AR_WAVES;
-#ifndef NAZ_AR_STAGGER
-constexpr bool kARStagger = false;
-#else
-constexpr bool kARStagger = true;
-#endif
-
 template <class CF>
-__global__ void __launch_bounds__(64 * kARWaves, kARWaves / 4) made_ar_r16_kernel(
+__global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, int64_t B, float bound) {
-  constexpr int D = CF::D, K = CF::K, P = CF::P;
+  constexpr int D = CF::D, K = CF::K, P = CF::P, NW = CF::NW, NHID = CF::NHID;
   extern __shared__ float4 lds4[];
   float* const slot0 = reinterpret_cast<float*>(lds4);
   float* const slot1 = slot0 + CF::STG;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int q = lane >> 4;
-  const int64_t row = (int64_t)blockIdx.x * (16 * kARWaves) + wave * 16 + (lane & 15);
+  const int64_t row = (int64_t)blockIdx.x * (16 * NW) + wave * 16 + (lane & 15);
   const bool valid = row < B;
   const int64_t crow = valid ? row : 0;
 
@@ -219,31 +273,8 @@ __global__ void __launch_bounds__(64 * kARWaves, kARWaves / 4) made_ar_r16_kerne
   }
 
   const RqsConsts<K, true> rc(bound);
-  float ldsum = 0.f;
-  // Stagger (NAZ_AR_STAGGER, off: measured 8.60 vs 8.24 ms per 2^20 rows): the late half of the
-  // workgroup (waves >= NW/2, which share SIMDs with the early half) runs each pass's spline at
-  // the head of the NEXT pass interval, before that pass's MFMAs, so that inside an interval one
-  // half would be on the matrix pipe while the other is on the vector pipe.  The pending
-  // parameters (o3) and dim stay in registers across the barrier.
-  const bool late = kARStagger && __builtin_amdgcn_readfirstlane(wave) >= kARWaves / 2;
-  floatx4 o3[CF::NOB];
-  int pend = -1;  // dim whose parameters o3 holds, not yet applied (late waves)
-  auto spline = [&](int dp) {
-    // parameter pi sits in block pi >> 4, register pi & 3 of quarter (pi & 15) >> 2
-    float uw[K], uh[K], ud[K - 1];
-#pragma unroll
-    for (int pi = 0; pi < P; ++pi) {
-      const float val = __shfl(o3[pi >> 4][pi & 3], (lane & 15) + 16 * ((pi & 15) >> 2));
-      if (pi < K) uw[pi] = val;
-      else if (pi < 2 * K) uh[pi - K] = val;
-      else ud[pi - 2 * K] = val;
-    }
-    float ld;
-    const float y = v[dp];
-    v[dp] = rqs_select<K, true>(uw, uh, ud, y, bound, rc, ld);
-    ldsum -= ld;
-  };
-  stage_issue<CF::stage_floats(0), kARWaves>(slot0, packed + (int64_t)(L - 1) * CF::LAYER);
+  float ldsum = 0.f;  // the layers' forward log-dets (log p = base - ldsum + logjac)
+  stage_issue<CF::stage_floats(0), NW>(slot0, packed + (int64_t)(L - 1) * CF::LAYER);
   int g = 0;
   for (int li = 0; li < L; ++li) {
     const int l = L - 1 - li;
@@ -253,40 +284,43 @@ __global__ void __launch_bounds__(64 * kARWaves, kARWaves / 4) made_ar_r16_kerne
     int dps[D];  // dim of order p, wave-uniform (SGPRs)
 #pragma unroll
     for (int p = 0; p < D; ++p) dps[p] = __builtin_amdgcn_readfirstlane(perm[p]);
-    Frag2 h1[CF::KSH], h2[CF::KSH];  // hidden layers as B fragments; zero = nothing computed yet
+    Frag2 hf[NHID][CF::KSH];  // hidden layers as B fragments; zero = nothing computed yet
 #pragma unroll
-    for (int t = 0; t < CF::KSH; ++t) {
-      h1[t] = Frag2{half8{}, half8{}};
-      h2[t] = Frag2{half8{}, half8{}};
-    }
+    for (int i = 0; i < NHID; ++i)
+#pragma unroll
+      for (int t = 0; t < CF::KSH; ++t) hf[i][t] = Frag2{half8{}, half8{}};
+    const float* cur = slot0;
     static_for<0, D>([&](auto pc) {
       constexpr int p = decltype(pc)::value;
       // pass constants bound to constexpr locals (a constexpr function in a loop bound or argument
       // is not folded reliably: the loops then stay rolled and the fragments go to scratch)
       constexpr int NBP = CF::nb(p), BLO = CF::blo(p), KT = CF::kt(p);
-      constexpr int OFF_L2 = CF::off_l2(p), OFF_OUT = CF::off_out(p), OFF_BIAS = CF::off_bias(p);
-      constexpr int SF_NEXT = p + 1 < D ? CF::stage_floats(p + 1) : CF::stage_floats(0);
-      __syncthreads();  // stage p has landed in slot (g & 1); every wave is done with the other slot
-      const float* cur = (g & 1) ? slot1 : slot0;
-      float* nxt = (g & 1) ? slot0 : slot1;
-      if constexpr (p + 1 < D) {
-        stage_issue<SF_NEXT, kARWaves>(nxt, lp + (p + 1) * CF::STG);
-      } else {
-        if (li + 1 < L) stage_issue<SF_NEXT, kARWaves>(nxt, lnext);
-      }
-      ++g;
-      const u32x4* c4 = reinterpret_cast<const u32x4*>(cur);
-      auto afrag = [&](int off_floats, int idx) {  // A fragment idx of the region at off_floats
-        const int base = (off_floats >> 2) + idx * 128 + lane;
-        return Frag2{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
-      };
       const int dp = dps[p];
-      if (late && pend >= 0) spline(pend);  // the previous pass's spline (previous layer's at p = 0)
-      const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF_BIAS);
-      // ---- hidden layer 1: blocks holding degree-p units, over [ctx | x]
-      if constexpr (NBP > 0) {
-        Frag2 xf;
-        {
+      floatx4 o3[CF::NOB];
+      static_for<0, NHID + 1>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int SID = CF::stage_id(p, i), OFF = CF::sub_off(p, i);
+        constexpr int OFF_BIAS = OFF + CF::frags(p, i) * CF::OT;
+        if constexpr (OFF == 0) {  // a new stage: it has landed in slot (g & 1)
+          constexpr int SF_NEXT = SID + 1 < CF::NSTG ? CF::stage_floats(SID + 1) : CF::stage_floats(0);
+          __syncthreads();  // ... and every wave is done with the other slot
+          cur = (g & 1) ? slot1 : slot0;
+          float* nxt = (g & 1) ? slot0 : slot1;
+          if constexpr (SID + 1 < CF::NSTG) {
+            stage_issue<SF_NEXT, NW>(nxt, lp + (SID + 1) * CF::STG);
+          } else {
+            if (li + 1 < L) stage_issue<SF_NEXT, NW>(nxt, lnext);
+          }
+          ++g;
+        }
+        const u32x4* c4 = reinterpret_cast<const u32x4*>(cur);
+        auto afrag = [&](int idx) {  // A fragment idx of this sub-layer
+          const int base = (OFF >> 2) + idx * 128 + lane;
+          return Frag2{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+        };
+        const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF_BIAS);
+        if constexpr (i == 0 && NBP > 0) {
+          // ---- hidden layer 1: blocks holding degree-p units, over [ctx | x]
           float x8[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -296,42 +330,63 @@ __global__ void __launch_bounds__(64 * kARWaves, kARWaves / 4) made_ar_r16_kerne
               if (8 * qq + j < D) s = q == qq ? v[8 * qq + j] : s;
             x8[j] = s;
           }
-          xf = split8_f16(x8);
+          const Frag2 xf = split8_f16(x8);
+          static_for<0, NBP>([&](auto bc) {
+            constexpr int bi = decltype(bc)::value, b = BLO + bi;
+            const float4 bv = bias4[4 * bi + q];
+            floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+            for (int t = 0; t < CF::KC; ++t) acc = mfma3_16(afrag(bi * CF::KI + t), cf[t], acc);
+            acc = mfma3_16(afrag(bi * CF::KI + CF::KC), xf, acc);
+            ar_split4<b & 1>(hf[0][b >> 1], acc);
+          });
+        } else if constexpr (i > 0 && i < NHID && NBP > 0) {
+          // ---- hidden layer i + 1: the same blocks, over layer i's units of degree <= p
+          static_for<0, NBP>([&](auto bc) {
+            constexpr int bi = decltype(bc)::value, b = BLO + bi;
+            const float4 bv = bias4[4 * bi + q];
+            floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+            for (int t = 0; t < KT; ++t) acc = mfma3_16(afrag(bi * KT + t), hf[i - 1][t], acc);
+            ar_split4<b & 1>(hf[i][b >> 1], acc);
+          });
+        } else if constexpr (i == NHID) {
+          // ---- the output rows of dim d_p, then the elementwise inverse on x[d_p]
+#pragma unroll
+          for (int o = 0; o < CF::NOB; ++o) {
+            const float4 bv = bias4[4 * o + q];
+            o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+          }
+#pragma unroll
+          for (int t = 0; t < KT; ++t)
+#pragma unroll
+            for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KT + t), hf[NHID - 1][t], o3[o]);
+          const float y = v[dp];
+          if constexpr (CF::AFFINE) {
+            // pyro AffineAutoregressive._inverse: rows 0, 1 = (mean, log_scale) of dim d_p, held by
+            // quarter 0 registers 0, 1; log_scale clamped to [-5, 3]; log|det| = the clamped ls
+            const float mean = __shfl(o3[0][0], lane & 15);
+            const float ls = fminf(fmaxf(__shfl(o3[0][1], lane & 15), -5.f), 3.f);
+            v[dp] = (y - mean) * __expf(-ls);
+            ldsum += ls;
+          } else {
+            // parameter pi sits in block pi >> 4, register pi & 3 of quarter (pi & 15) >> 2
+            float uw[K], uh[K], ud[K - 1];
+#pragma unroll
+            for (int pi = 0; pi < P; ++pi) {
+              const float val = __shfl(o3[pi >> 4][pi & 3], (lane & 15) + 16 * ((pi & 15) >> 2));
+              if (pi < K) uw[pi] = val;
+              else if (pi < 2 * K) uh[pi - K] = val;
+              else ud[pi - 2 * K] = val;
+            }
+            float ld;
+            v[dp] = rqs_select<K, true>(uw, uh, ud, y, bound, rc, ld);
+            ldsum -= ld;
+          }
         }
-        static_for<0, NBP>([&](auto bc) {
-          constexpr int bi = decltype(bc)::value, b = BLO + bi;
-          const float4 bv = bias4[4 * bi + q];
-          floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-          for (int t = 0; t < CF::KC; ++t) acc = mfma3_16(afrag(0, bi * CF::KI + t), cf[t], acc);
-          acc = mfma3_16(afrag(0, bi * CF::KI + CF::KC), xf, acc);
-          ar_split4<b & 1>(h1[b >> 1], acc);
-        });
-        // ---- hidden layer 2: the same blocks, over layer 1's units of degree <= p
-        static_for<0, NBP>([&](auto bc) {
-          constexpr int bi = decltype(bc)::value, b = BLO + bi;
-          const float4 bv = bias4[4 * (NBP + bi) + q];
-          floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-          for (int t = 0; t < KT; ++t) acc = mfma3_16(afrag(OFF_L2, bi * KT + t), h1[t], acc);
-          ar_split4<b & 1>(h2[b >> 1], acc);
-        });
-      }
-      // ---- the 3K-1 raw spline parameters of dim d_p
-#pragma unroll
-      for (int o = 0; o < CF::NOB; ++o) {
-        const float4 bv = bias4[4 * (2 * NBP + o) + q];
-        o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
-      }
-#pragma unroll
-      for (int t = 0; t < KT; ++t)
-#pragma unroll
-        for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(OFF_OUT, o * KT + t), h2[t], o3[o]);
-      if (late) pend = dp;
-      else spline(dp);
+      });
     });
   }
-  if (late && pend >= 0) spline(pend);
   constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
   float base = 0.f;
 #pragma unroll

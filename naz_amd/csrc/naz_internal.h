@@ -82,11 +82,11 @@ int coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const voi
                        float* g_out, float* g_low, int64_t B, hipStream_t s);
 int coupling_dp3_columns(const naz_coupling_desc* d, int* rows);
 
-int spline_ar_supported(const naz_ar_desc* d);
-int64_t spline_ar_packed_bytes(const naz_ar_desc* d);
-int spline_ar_degrees(const naz_ar_desc* d, int* deg);
-int spline_ar_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed);
-int spline_ar_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+int ar_flow_supported(const naz_ar_desc* d);
+int64_t ar_flow_packed_bytes(const naz_ar_desc* d);
+int ar_flow_degrees(const naz_ar_desc* d, int* deg);
+int ar_flow_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed);
+int ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
                        int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s);
 
 int cnf_supported(const naz_cnf_desc* d);

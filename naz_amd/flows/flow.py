@@ -146,19 +146,23 @@ class _FusedCoupling:
 
 
 class _FusedAR:
-    """All L nsa layers' log_prob as ONE HIP launch (naz_spline_ar_log_prob, csrc/made_ar_r16.h):
-    every layer's D-pass MADE inverse (pyro ConditionedSplineAutoregressive._inverse, naz
-    transforms.py:165-198) with each hidden unit computed once, in registers, on the f16x3 MFMA
-    path.  sample() and the autograd walk keep the per-layer kernels.  The kernel is compiled for
-    pyro's hidden mask indices; the masks are checked against them once per parameter change."""
+    """All L nsa / maf layers' log_prob as ONE HIP launch (naz_ar_flow_log_prob,
+    csrc/made_ar_r16.h): every layer's D-pass MADE inverse (pyro ConditionedSplineAutoregressive /
+    ConditionedAffineAutoregressive._inverse, naz transforms.py:133-198) with each hidden unit
+    computed once, in registers, on the f16x3 MFMA path.  sample() and the autograd walk keep the
+    per-layer kernels.  The kernel is compiled for pyro's hidden mask indices; the masks are checked
+    against them once per parameter change."""
 
     can_sample = False
     F16_DATA_LIMIT = 32768.0  # the kernel's f16x3 input split (|x|, |ctx| < 2^15)
 
-    def __init__(self, layers: List[nn.Module], D: int, C: int, H: int, K: int, act: str, bound: float):
+    def __init__(self, layers: List[nn.Module], kind: str, D: int, C: int, H: int, n_hidden: int, K: int, act: str,
+                 bound: float):
         self.layers = layers
-        self.shape = (D, C, H, K)
-        self.desc = ops.spline_ar_desc(D, C, H, K, len(layers), act, bound)
+        self.kind = kind
+        self.shape = (D, C, H, n_hidden, K)
+        self.P = 2 if kind == "maf" else 3 * K - 1
+        self.desc = ops.ar_flow_desc(kind, D, C, H, len(layers), n_hidden, K, act, bound)
         self._sig = None
         self._packed = None
         self._masks = None
@@ -172,9 +176,8 @@ class _FusedAR:
         sig = tuple((t.data_ptr(), t._version) for n in self._nets()
                     for t in [n.permutation] + [l.mask for l in n.layers])
         if self._masks is None or self._masks[0] != sig:
-            D, C, H, K = self.shape
-            P = 3 * K - 1
-            deg = ops.spline_ar_degrees(self.desc).astype(np.int64)
+            D, C, H, NH, K = self.shape
+            deg = ops.ar_flow_degrees(self.desc).astype(np.int64)
             ok = True
             for arn in self._nets():
                 m = [l.mask.detach().cpu().numpy() != 0 for l in arn.layers]
@@ -182,11 +185,12 @@ class _FusedAR:
                 order = np.empty(D, dtype=np.int64)
                 order[perm] = np.arange(D)
                 in_idx = np.concatenate([np.zeros(C, dtype=np.int64), order + 1])
-                out_idx = np.tile(order + 1, P)
-                ok = ok and len(m) == 3 and m[0].shape == (H, C + D) and m[1].shape == (H, H)
+                out_idx = np.tile(order + 1, self.P)
+                ok = ok and len(m) == NH + 1 and m[0].shape == (H, C + D) and m[-1].shape == (D * self.P, H)
                 ok = ok and bool((m[0] == (deg[:, None] >= in_idx[None, :])).all())
-                ok = ok and bool((m[1] == (deg[:, None] >= deg[None, :])).all())
-                ok = ok and bool((m[2] == (out_idx[:, None] > deg[None, :])).all())
+                for i in range(1, NH):
+                    ok = ok and m[i].shape == (H, H) and bool((m[i] == (deg[:, None] >= deg[None, :])).all())
+                ok = ok and bool((m[-1] == (out_idx[:, None] > deg[None, :])).all())
             self._masks = (sig, ok)
         return self._masks[1]
 
@@ -215,7 +219,7 @@ class _FusedAR:
                               l.bias.detach().float().cpu().numpy()]
                 perms.append(n.permutation.detach().cpu().numpy())
             dev = self._nets()[0].layers[0].weight.device
-            self._packed = ops.spline_ar_pack(self.desc, np.concatenate(flats), np.stack(perms), dev)
+            self._packed = ops.ar_flow_pack(self.desc, np.concatenate(flats), np.stack(perms), dev)
             self._sig = sig
         return self._packed
 
@@ -223,22 +227,23 @@ class _FusedAR:
         low = high = None
         if bounds is not None:
             low, high = bounds["low"].to(x.device, torch.float32), bounds["high"].to(x.device, torch.float32)
-        return ops.spline_ar_log_prob(self.desc, self.packed(), x, context, low, high, out=out)
+        return ops.ar_flow_log_prob(self.desc, self.packed(), x, context, low, high, out=out)
 
     def executed_flop_per_row(self) -> int:
         """FP32-equivalent FLOPs the kernel executes per row (an f16x3 product counted once; the
-        16-unit block recomputations and zero-padded k-slots included): per pass, hidden-layer
-        blocks over [ctx | x] and over the hidden units of degree <= p, and the output blocks."""
-        D, C, H, K = self.shape
-        deg = ops.spline_ar_degrees(self.desc)
+        16-unit block recomputations and zero-padded k-slots included): per pass, the first hidden
+        layer's blocks over [ctx | x], the further hidden layers' blocks over the units of degree
+        <= p, and the output blocks."""
+        D, C, H, NH, K = self.shape
+        deg = ops.ar_flow_degrees(self.desc)
         E = [int((deg <= p).sum()) for p in range(D)]
-        KI, NOB = (C + 31) // 32 + 1, (3 * K - 1 + 15) // 16
+        KI, NOB = (C + 31) // 32 + 1, (self.P + 15) // 16
         per_layer = 0
         for p in range(D):
             e0 = E[p - 1] if p else 0
             nb = ((E[p] - 1) >> 4) - (e0 >> 4) + 1 if E[p] > e0 else 0
             kt = (E[p] + 31) // 32
-            per_layer += (nb * (KI + kt) + NOB * kt) * 16 * 32 * 2  # 16 outputs x 32 k per block-step
+            per_layer += (nb * (KI + (NH - 1) * kt) + NOB * kt) * 16 * 32 * 2  # 16 outputs x 32 k per block-step
         return per_layer * len(self.layers)
 
 
@@ -321,15 +326,17 @@ class _CouplingTrainFn(torch.autograd.Function):
 def _fused_plan(flow_type, flow_args, flow_kwargs, transforms):
     if any(isinstance(t, Permute) for t in transforms):
         return None
-    if flow_type == "nsa" and _AR_FUSED != "0":
-        D, C, hidden, L, K = flow_args[:5]
+    if flow_type in ("nsa", "maf") and _AR_FUSED != "0":
+        D, C, hidden, L = flow_args[:4]
+        K = flow_args[4] if flow_type == "nsa" else 8
         hidden = list(hidden) if isinstance(hidden, (list, tuple)) else [hidden]
         act = activation_name(flow_kwargs.get("activation", nn.Tanh()))
-        if len(hidden) != 2 or hidden[0] != hidden[1]:
+        if any(h != hidden[0] for h in hidden):
             return None
         try:
-            plan = _FusedAR(list(transforms), D, C, hidden[0], K, act, transforms[0].bound)
-            return plan if ops.spline_ar_supported(plan.desc) and plan.masks_ok() else None
+            bound = transforms[0].bound if flow_type == "nsa" else 3.0
+            plan = _FusedAR(list(transforms), flow_type, D, C, hidden[0], len(hidden), K, act, bound)
+            return plan if ops.ar_flow_supported(plan.desc) and plan.masks_ok() else None
         except Exception:
             return None
     if flow_type != "nsc":

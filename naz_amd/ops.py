@@ -524,49 +524,55 @@ def coupling_log_prob(d: CouplingDesc, packed: Tensor, x: Tensor, context: Optio
     return out
 
 
-# ----------------------------------------------------------------------------- §8b naz_spline_ar_inv
-def spline_ar_desc(D: int, C: int, H: int, K: int, L: int, act: str = "tanh", bound: float = 3.0) -> ArDesc:
+# ----------------------------------------------------------------------------- §8b naz_{spline,affine}_ar_inv
+AR_KIND = {"nsa": 0, "maf": 1}  # NAZ_AR_SPLINE, NAZ_AR_AFFINE
+
+
+def ar_flow_desc(kind: str, D: int, C: int, H: int, L: int, n_hidden: int = 2, K: int = 8, act: str = "tanh",
+                 bound: float = 3.0) -> ArDesc:
+    """naz_ar_desc of an L-layer nsa / maf flow with n_hidden tanh hidden layers of width H."""
     d = ArDesc()
     d.D, d.C, d.H, d.K, d.L = D, C, H, K, L
     d.act, d.bound = ACT.get(act, -1), float(bound)
+    d.n_hidden, d.kind = n_hidden, AR_KIND.get(kind, -1)
     return d
 
 
-def spline_ar_supported(d: ArDesc) -> bool:
-    return bool(lib().naz_spline_ar_supported(d))
+def ar_flow_supported(d: ArDesc) -> bool:
+    return bool(lib().naz_ar_flow_supported(d))
 
 
-def spline_ar_degrees(d: ArDesc) -> np.ndarray:
+def ar_flow_degrees(d: ArDesc) -> np.ndarray:
     """The hidden-unit mask indices the fused kernel is compiled for (pyro create_mask's)."""
     out = np.zeros(d.H, dtype=np.int32)
-    check(lib().naz_spline_ar_degrees(d, out.ctypes.data), "spline_ar_degrees")
+    check(lib().naz_ar_flow_degrees(d, out.ctypes.data), "ar_flow_degrees")
     return out
 
 
-def spline_ar_pack(d: ArDesc, flat: np.ndarray, perm: np.ndarray, device) -> Tensor:
-    """Host-side pack (naz_spline_ar_pack_host) of the masked per-layer weights, then one copy to
-    the device.  flat: fp32 per layer W0m|b0|W1m|b1|W2m|b2; perm: int32 [L, D]."""
+def ar_flow_pack(d: ArDesc, flat: np.ndarray, perm: np.ndarray, device) -> Tensor:
+    """Host-side pack (naz_ar_flow_pack_host) of the masked per-layer weights, then one copy to
+    the device.  flat: fp32 per layer W0m|b0|{Wim|bi}|Woutm|bout; perm: int32 [L, D]."""
     flat = np.ascontiguousarray(flat, dtype=np.float32)
     perm = np.ascontiguousarray(perm, dtype=np.int32)
-    nbytes = int(lib().naz_spline_ar_packed_bytes(d))
+    nbytes = int(lib().naz_ar_flow_packed_bytes(d))
     if nbytes <= 0:
-        raise RuntimeError("naz_amd spline_ar_pack: unsupported descriptor")
+        raise RuntimeError("naz_amd ar_flow_pack: unsupported descriptor")
     host = np.empty(nbytes // 4, dtype=np.float32)
-    check(lib().naz_spline_ar_pack_host(d, flat.ctypes.data, perm.ctypes.data, host.ctypes.data), "spline_ar_pack")
+    check(lib().naz_ar_flow_pack_host(d, flat.ctypes.data, perm.ctypes.data, host.ctypes.data), "ar_flow_pack")
     return torch.from_numpy(host).to(device)
 
 
-def spline_ar_log_prob(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,
-                       low: Optional[Tensor] = None, high: Optional[Tensor] = None,
-                       out: Optional[Tensor] = None) -> Tensor:
+def ar_flow_log_prob(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,
+                     low: Optional[Tensor] = None, high: Optional[Tensor] = None,
+                     out: Optional[Tensor] = None) -> Tensor:
     dev = _dev(packed, x, context, low, high, out)
     x, ldx = _rows(x)
     B = x.shape[0]
     context, ldc = _ctx_arg(context, B)
     if out is None:
         out = torch.empty((B,), device=dev, dtype=torch.float32)
-    check(lib().naz_spline_ar_log_prob(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out), B,
-                                       _stream(dev)), "spline_ar_log_prob")
+    check(lib().naz_ar_flow_log_prob(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out), B,
+                                     _stream(dev)), "ar_flow_log_prob")
     return out
 
 

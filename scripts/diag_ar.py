@@ -26,7 +26,7 @@ with torch.no_grad():
     out = torch.empty(B, device="cuda")
     e0.record()
     for _ in range(3):
-        ops.spline_ar_log_prob(plan.desc, packed, x, c, out=out)
+        ops.ar_flow_log_prob(plan.desc, packed, x, c, out=out)
     e1.record(); torch.cuda.synchronize()
     print("kernel ms", e0.elapsed_time(e1) / 3, flush=True)
     pr = cProfile.Profile(); pr.enable()

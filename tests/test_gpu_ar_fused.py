@@ -1,4 +1,4 @@
-"""GPU: the fused autoregressive-inverse flow kernel (naz_spline_ar_log_prob, csrc/made_ar_r16.h) —
+"""GPU: the fused autoregressive-inverse flow kernel (naz_ar_flow_log_prob, csrc/made_ar_r16.h) —
 naz nsa NormalizingFlow.log_prob (pyro ConditionedSplineAutoregressive._inverse, the D-pass loop
 of naz/flows/transforms.py:165-198, over L layers) as one launch.
 
@@ -22,6 +22,8 @@ CASES = [
     dict(flow_type="nsa", D=16, C=0, hidden=[128, 128], L=3, K=8, n=1000),
     dict(flow_type="nsa", D=8, C=0, hidden=[128, 128], L=2, K=8, n=1500),
     dict(flow_type="nsa", D=4, C=2, hidden=[128, 128], L=3, K=8, n=1200),  # bench --flow nsa
+    dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=16, n=3000),  # the maf paper shape
+    dict(flow_type="maf", D=16, C=32, hidden=[128, 128], L=4, n=700),
 ]
 
 
@@ -32,14 +34,15 @@ def _gpu():
 
 
 def _id(spec):
-    return f"D{spec['D']}C{spec['C']}L{spec['L']}"
+    return f"{spec['flow_type']}D{spec['D']}C{spec['C']}L{spec['L']}"
 
 
 def _flow(spec, bounds=None):
     from naz_amd.flows import NormalizingFlow
     from naz_amd.flows import io as fio
     state = {k: v.float() for k, v in O.random_state(spec, seed=11).items()}
-    f = NormalizingFlow("nsa", bounds, spec["D"], spec["C"], spec["hidden"], spec["L"], spec["K"])
+    extra = (spec["K"],) if spec["flow_type"] == "nsa" else ()
+    f = NormalizingFlow(spec["flow_type"], bounds, spec["D"], spec["C"], spec["hidden"], spec["L"], *extra)
     fio.load_state(f, {k: v.numpy() for k, v in state.items()})
     return f.to(DEV), state
 
@@ -59,19 +62,21 @@ def test_fused_ar_vs_oracle_and_per_layer(spec):
         f.set_fused(True)
     lp64 = O.build_flow(spec, state, torch.float64).log_prob(x.double(), None if c is None else c.double()).numpy()
     lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, c).numpy()
-    st = assert_parity(lp, lp64, lp32, what=f"fused nsa {_id(spec)}")
-    assert_parity(lp_walk, lp64, lp32, what=f"per-layer nsa {_id(spec)}")
+    st = assert_parity(lp, lp64, lp32, what=f"fused {_id(spec)}")
+    assert_parity(lp_walk, lp64, lp32, what=f"per-layer {_id(spec)}")
     print(_id(spec), st, "max |fused - walk|", float(np.abs(lp - lp_walk).max()))
 
 
-def test_fused_ar_broadcast_context_bounds_ragged_empty():
-    spec = dict(flow_type="nsa", D=16, C=32, hidden=[128, 128], L=2, K=8)
-    lo, hi = np.full(16, -9.0, np.float32), np.full(16, 9.5, np.float32)
+@pytest.mark.parametrize("spec", [dict(flow_type="nsa", D=16, C=32, hidden=[128, 128], L=2, K=8),
+                                  dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=5)], ids=_id)
+def test_fused_ar_broadcast_context_bounds_ragged_empty(spec):
+    D, C = spec["D"], spec["C"]
+    lo, hi = np.full(D, -9.0, np.float32), np.full(D, 9.5, np.float32)
     f, _ = _flow(spec, bounds={"low": lo, "high": hi})
     assert f.fused
     g = torch.Generator().manual_seed(3)
-    x = (torch.rand(777, 16, generator=g) * 17.0 - 8.0).to(DEV)
-    c1 = torch.randn(32, generator=g).to(DEV)
+    x = (torch.rand(777, D, generator=g) * 17.0 - 8.0).to(DEV)
+    c1 = torch.randn(C, generator=g).to(DEV)
     with torch.no_grad():
         lp = f.log_prob(x, condition=c1)
         f.set_fused(False)

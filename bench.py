@@ -475,6 +475,107 @@ def run_cnf(args, dev, rank, world, dist):
         dist.destroy_process_group()
 
 
+def run_cnf_train(args, dev, rank, world, dist):
+    """§8f rank 3: the NLL training step of naz's CNF (train_flows.py:194-213 over the configs[4]
+    FFJORD block): fused RK4 forward with per-step checkpoints, discrete-adjoint backward on the HIP
+    walk (flows/cnf_adjoint.py), gradient all-reduce (one flat bucket), clip, Adam."""
+    from naz_amd.trainers import DataParallel, nll_step
+    from naz_amd.trainers.train_flows import _flow_parameters
+    from naz_amd.flows import NormalizingFlow
+    torch.manual_seed(1234)
+    f = NormalizingFlow("cnf", None, CNF_D, 0, CNF_H, 1, steps=CNF_STEPS)
+    lo, hi, G = shard(args, rank, world, 1 << 18)
+    B = hi - lo
+    x = torch.as_tensor(mixture_rows(lo, hi, CNF_D, seed=0), device=dev) * 0.5
+    dp = DataParallel()
+    params = _flow_parameters(f)
+    dp.broadcast_params(params)
+    opt = torch.optim.Adam(params, lr=1e-4)
+
+    def step():
+        return nll_step(f, x, None, opt, params, dp, G, clip_val=1.0, micro_batch=args.micro_batch)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    if rank == 0:
+        step_s = elapsed / args.steps
+        # per RHS evaluation: forward value + JVP (2 MLP passes, fused kernel), backward recompute (2),
+        # dX of the stacked rows (2), dW over the stacked rows (2): 8 MLP-forward equivalents
+        flop_row = cnf_flops_per_row() // 2 * 8
+        achieved = flop_row * B / step_s / 1e12
+        rec = {
+            "metric": "samples/sec through the CNF NLL training step (FFJORD log_prob fwd + adjoint backward + "
+                      "grad all-reduce + clip + Adam), 16-dim CNF",
+            "value": G / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": args.scaling,
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: x ~ 0.5 x 8-component Gaussian mixture; random-init weights; eps redrawn per step",
+            "config": {"workload": "SURVEY §8f rank 3 on BASELINE configs[4]: FFJORD block D=16, H=[128]*3, "
+                                   "softplus, RK4 x 8, NLL step with the discrete adjoint",
+                       "batch_per_gpu": B, "global_batch": G, "micro_batch": args.micro_batch,
+                       "parallelism": f"dp{world} (RCCL all-reduce, one flat bucket)"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "whole step",
+                         "flop_per_row": flop_row,
+                         "peak_note": "exact-FP32 MFMA peak (the backward walk's GEMMs; the fused forward, "
+                                      "1/4 of the FLOPs, runs on the f16x3 pipe)"},
+            "final_loss": float(loss),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import naz_oracle as O  # baseline only
+            cores = host_cores()
+            torch.set_num_threads(cores["threads"])
+            lins = f.transforms[0].net.linears()
+            Ws = [l.weight.detach().cpu().clone().requires_grad_(True) for l in lins]
+            bs = [l.bias.detach().cpu().clone().requires_grad_(True) for l in lins]
+            net = O.FCNN(Ws, bs)
+            nrow = 1 << 12
+            xs = x[:nrow].cpu()
+            copt = torch.optim.Adam(Ws + bs, lr=1e-4)
+
+            def cstep():
+                copt.zero_grad()
+                eps = torch.randn(nrow, CNF_D)
+                z, a = O.rk4_augmented(net, xs, None, eps, 0.0, 1.0, CNF_STEPS)
+                loss_c = -(O.base_log_prob(z) - a).mean()
+                loss_c.backward()
+                torch.nn.utils.clip_grad_norm_(Ws + bs, 1.0)
+                copt.step()
+
+            cstep()
+            runs = []
+            for _ in range(5):
+                c0 = time.perf_counter()
+                cstep()
+                runs.append(time.perf_counter() - c0)
+            med = statistics.median(runs)
+            rec["cpu_baseline"] = {"value": nrow / med, "unit": "samples/s", "cores": cores["threads"],
+                                   "kind": "port", "host": cores,
+                                   "sample": f"{nrow} rows, oracle FFJORD (torch fp32, create_graph VJP trace as "
+                                             f"torchdyn's hutch_trace) RK4 x 8, autograd backward + clip + Adam, "
+                                             f"median of 5 after 1 warm-up ({med:.2f} s)"}
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 # --flow: the other §8 rows at the reference's own shapes, through the naz_amd NormalizingFlow API
 # (torch.no_grad, one log_prob call = one step).  (flow_type, D, C, hidden, L, extra args, batch)
 FLOW_CASES = {
@@ -787,6 +888,9 @@ def main():
     ap.add_argument("--cnf", action="store_true",
                     help="BASELINE configs[4]: 16-dim FFJORD CNF (H=[128]*3, softplus, Hutchinson trace, RK4 x 8 "
                          "steps) log_prob at 2^18 rows")
+    ap.add_argument("--cnf-train", action="store_true",
+                    help="§8f rank 3: the CNF NLL training step (configs[4] block, RK4 x 8, discrete-adjoint "
+                         "backward on the HIP walk) over 2^18 rows")
     ap.add_argument("--cnf-solver", choices=["rk4", "dopri5"], default="rk4",
                     help="--cnf: pinned fixed-step RK4 x 8 (default) or adaptive dopri5 (atol = rtol = 1e-4)")
     ap.add_argument("--flow", choices=sorted(FLOW_CASES), default=None,
@@ -820,6 +924,8 @@ def main():
 
     if args.train:
         return run_train(args, dev, rank, world, dist)
+    if args.cnf_train:
+        return run_cnf_train(args, dev, rank, world, dist)
     if args.cnf:
         return run_cnf(args, dev, rank, world, dist)
     if args.flow:

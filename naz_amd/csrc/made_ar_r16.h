@@ -301,7 +301,11 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
         constexpr int i = decltype(ic)::value;
         constexpr int SID = CF::stage_id(p, i), OFF = CF::sub_off(p, i);
         constexpr int OFF_BIAS = OFF + CF::frags(p, i) * CF::OT;
-        if constexpr (OFF == 0) {  // a new stage: it has landed in slot (g & 1)
+        // a stage starts at sub-layer 0 of every pass and wherever the grouping opened a new one
+        // (not at OFF == 0: empty sub-layers — no units of degree p, e.g. pass 0 without a
+        // context — also sit at offset 0 of their pass's stage)
+        constexpr bool NEW_STAGE = i == 0 || SID != CF::stage_id(p, i > 0 ? i - 1 : 0);
+        if constexpr (NEW_STAGE) {  // it has landed in slot (g & 1)
           constexpr int SF_NEXT = SID + 1 < CF::NSTG ? CF::stage_floats(SID + 1) : CF::stage_floats(0);
           __syncthreads();  // ... and every wave is done with the other slot
           cur = (g & 1) ? slot1 : slot0;

@@ -1,0 +1,198 @@
+"""Gradients through a FFJORD block solve: the CNF training step.
+
+naz trains its continuous flows with torchdyn ``NeuralODE(..., sensitivity='adjoint')``
+(naz/flows/continuous_transforms.py:73-82) through ``train`` / ``train_lightning``
+(naz/trainers/train_flows.py:194-213, :244-278): the loss is -log_prob, whose CNF part is the
+augmented solve d[x, a]/dt = [f(x, ctx), -eps^T (df/dx) eps] (hutch_trace, :85-89).
+
+``CnfSolveFn`` is that solve as one autograd node.
+
+* Forward: the fused solve kernels (csrc/cnf.hip).  For ``solver='rk4'`` one ``naz_cnf_integrate``
+  launch per step, so the step-start states x_n are kept as checkpoints (B x D floats each);
+  for ``'dopri5'`` the adaptive kernel, keeping only x(t1).
+* Backward, rk4 (``sensitivity`` 'adjoint' or 'autograd'): the discrete adjoint of the pinned RK4
+  solve, i.e. exactly the gradient of what the forward computed.  Per step, last to first: the
+  four stages are recomputed from the checkpoint, then the step's adjoint recursion runs in
+  reverse (g_k4 = h/6 lam, g_k3 = h/3 lam + h g_z4, g_k2 = h/3 lam + h/2 g_z3,
+  g_k1 = h/6 lam + h/2 g_z2; lam <- lam + sum g_z; the log-det's adjoint mu = dL/da is constant
+  because the RHS does not read a).  Memory is one step's activations, as with an adjoint solve.
+* Backward, dopri5: torchdyn's continuous adjoint — the system [x, lam, theta_bar] integrated from
+  t1 back to t0 (dx/dt = f, dlam/dt = -(lam^T df/dx + mu d(-tr)/dx), dtheta_bar/dt = -(lam^T df/dtheta +
+  mu d(-tr)/dtheta)) with ``adjoint_steps`` fixed RK4 steps (x reconstructed backwards in time, as
+  torchdyn does).  Its gradient approximates the continuous one, not the forward's step sequence.
+
+Every RHS evaluation and VJP is HIP (``CnfWalk``): the vector field under the Hutchinson JVP is a
+chain of batch-row GEMMs over the stacked rows [h; dh] (2B rows: value and tangent share each
+weight read, ``naz_linear_act``), the activation pair ``naz_act_jvp``; the VJP is ``naz_act_jvp_bwd``
+(value rows need act'' because the tangent reads pre through act') and ``naz_gemm`` for dX and the
+2B-row dW reductions.  Torch only forms the [B, D]-sized RK4 combinations.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+from torch.autograd import Function
+
+from .. import ops
+
+
+class CnfWalk:
+    """The FFJORD vector field (ConditionalFCNN, naz continuous_transforms.py:38-60, input
+    cat([x, ctx]), x first) with its Hutchinson JVP, evaluated layer by layer on HIP kernels."""
+
+    def __init__(self, net):
+        lins = net.linears()
+        self.W = [lin.weight.detach() for lin in lins]
+        self.b = [lin.bias.detach() for lin in lins]
+        self.act = net.act
+        self.D, self.C = net.input_dim, net.context_dim
+
+    def rhs(self, z: torch.Tensor, ctx: Optional[torch.Tensor], eps: torch.Tensor):
+        """(f(z), -eps^T J eps, saved activations) for z [B, D]."""
+        B, D, C = z.shape[0], self.D, self.C
+        S = torch.zeros((2 * B, D + C), device=z.device, dtype=z.dtype)
+        S[:B, :D] = z
+        S[B:, :D] = eps
+        if C:
+            S[:B, D:] = ctx.reshape(-1, C).expand(B, C) if ctx.numel() == C else ctx
+        saved = [S]
+        for W, b in zip(self.W[:-1], self.b[:-1]):
+            P = ops.linear_act(S, W, None)
+            S = ops.act_jvp(P, b, self.act)
+            saved += [P, S]
+        O = ops.linear_act(S, self.W[-1], None)
+        k = O[:B] + self.b[-1]
+        t = -(eps * O[B:]).sum(1)
+        return k, t, saved
+
+    def vjp(self, saved: List[torch.Tensor], eps: torch.Tensor, g_k: torch.Tensor, g_t: torch.Tensor,
+            gW: List[torch.Tensor], gb: List[torch.Tensor], g_ctx: Optional[torch.Tensor]) -> torch.Tensor:
+        """Adjoints (g_k, g_t) of (f, -tr) at the point ``rhs`` saved -> returns g_z [B, D];
+        accumulates the weight / bias gradients into gW / gb and the context's into g_ctx."""
+        B, D, C = g_k.shape[0], self.D, self.C
+        G = torch.empty((2 * B, D), device=g_k.device, dtype=g_k.dtype)
+        G[:B] = g_k
+        G[B:] = -g_t[:, None] * eps
+        n = len(self.W)
+        ops.gemm(G.t(), saved[-1], out=gW[-1], accumulate=True)
+        ops.colsum(g_k, out=gb[-1])
+        GS = ops.gemm(G, self.W[-1])
+        for i in reversed(range(n - 1)):
+            P, S_in = saved[2 * i + 1], saved[2 * i]
+            GP = ops.act_jvp_bwd(P, self.b[i], GS, self.act, g_bias=gb[i])
+            ops.gemm(GP.t(), S_in, out=gW[i], accumulate=True)
+            if i > 0:
+                GS = ops.gemm(GP, self.W[i])
+            else:
+                GP = GP[:B]  # the tangent rows' input is eps (no gradient)
+                g_z = ops.gemm(GP, self.W[0][:, :D])
+                if C and g_ctx is not None:
+                    Wc = self.W[0][:, D:]
+                    if g_ctx.shape[0] == B and g_ctx.dim() == 2:
+                        ops.gemm(GP, Wc, out=g_ctx, accumulate=True)
+                    else:
+                        ops.gemm(ops.colsum(GP).reshape(1, -1), Wc, out=g_ctx.view(1, C), accumulate=True)
+        return g_z
+
+
+def _rk4_step_adjoint(walk, x, ctx, eps, h, lam, mu, gW, gb, g_ctx):
+    """Discrete adjoint of one classical RK4 step from checkpoint x (naz odeint.py:46-52)."""
+    k1, _, s1 = walk.rhs(x, ctx, eps)
+    k2, _, s2 = walk.rhs(x + 0.5 * h * k1, ctx, eps)
+    k3, _, s3 = walk.rhs(x + 0.5 * h * k2, ctx, eps)
+    _, _, s4 = walk.rhs(x + h * k3, ctx, eps)
+    del k1, k2, k3
+    w1, w2 = h / 6.0, h / 3.0
+    gz4 = walk.vjp(s4, eps, w1 * lam, w1 * mu, gW, gb, g_ctx)
+    del s4
+    gz3 = walk.vjp(s3, eps, w2 * lam + h * gz4, w2 * mu, gW, gb, g_ctx)
+    del s3
+    gz2 = walk.vjp(s2, eps, w2 * lam + 0.5 * h * gz3, w2 * mu, gW, gb, g_ctx)
+    del s2
+    gz1 = walk.vjp(s1, eps, w1 * lam + 0.5 * h * gz2, w1 * mu, gW, gb, g_ctx)
+    return lam + gz1 + gz2 + gz3 + gz4
+
+
+def _continuous_adjoint(walk, y1, ctx, eps, t0, t1, steps, lam, mu, gW, gb, g_ctx):
+    """torchdyn-style adjoint: RK4 on [x, lam, theta_bar] from t1 back to t0."""
+    h = (t0 - t1) / steps
+    x = y1
+
+    def stage(xs, ls, c):
+        # derivative of [x, lam, theta_bar]: (f, -g_z, -g_theta); the parameter / context part is
+        # accumulated directly with its RK4 weight c (the VJP is linear in its adjoint inputs)
+        k, _, sv = walk.rhs(xs, ctx, eps)
+        gz = walk.vjp(sv, eps, -c * ls, -c * mu, gW, gb, g_ctx)
+        return k, gz / c
+
+    for _ in range(steps):
+        k1, d1 = stage(x, lam, h / 6.0)
+        k2, d2 = stage(x + 0.5 * h * k1, lam + 0.5 * h * d1, h / 3.0)
+        k3, d3 = stage(x + 0.5 * h * k2, lam + 0.5 * h * d2, h / 3.0)
+        k4, d4 = stage(x + h * k3, lam + h * d3, h / 6.0)
+        x = x + h / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
+        lam = lam + h / 6.0 * (d1 + 2 * d2 + 2 * d3 + d4)
+    return lam
+
+
+class CnfSolveFn(Function):
+    """(y, ld) = FFJORD block solve of v from t0 to t1 (ld = int -eps^T J eps dt), differentiable
+    in v, the context and the vector field's parameters (see the module docstring)."""
+
+    @staticmethod
+    def forward(ctx, v, context, eps, core, t0: float, t1: float, *params):
+        plan = core._plan
+        packed = plan.packed()
+        desc = plan.desc
+        v = v.detach().contiguous()
+        if core.solver == "dopri5":
+            y, ld = core._dopri5(desc, packed, v, eps, t0, t1, None, ops.LD_ROWSUM)
+            ctx.checkpoints = None
+            ctx.save_for_backward(y, eps, context)
+        else:
+            steps = core.steps
+            ld = torch.zeros(v.shape[0], device=v.device, dtype=torch.float32)
+            xs = [v]
+            dt = (t1 - t0) / steps
+            for n in range(steps):
+                y, _ = ops.cnf_integrate(desc, packed, xs[-1], eps, t0 + n * dt, t0 + (n + 1) * dt, 1,
+                                         context=context, ld_out=ld, ld_mode=ops.LD_ROWSUM_ADD)
+                xs.append(y)
+            ctx.checkpoints = len(xs) - 1
+            ctx.save_for_backward(eps, context, *xs[:-1])
+        ctx.core, ctx.t0, ctx.t1 = core, t0, t1
+        return y, ld
+
+    @staticmethod
+    def backward(ctx, g_y, g_ld):
+        core, t0, t1 = ctx.core, ctx.t0, ctx.t1
+        saved = ctx.saved_tensors
+        walk = CnfWalk(core._net)
+        if ctx.checkpoints is None:
+            y1, eps, context = saved
+            B = y1.shape[0]
+        else:
+            eps, context = saved[0], saved[1]
+            xs = saved[2:]
+            B = xs[0].shape[0]
+        dev = eps.device
+        lam = torch.zeros((B, walk.D), device=dev) if g_y is None else g_y.contiguous().clone()
+        mu = torch.zeros(B, device=dev) if g_ld is None else g_ld.contiguous()
+        gW = [torch.zeros_like(W) for W in walk.W]
+        gb = [torch.zeros_like(b) for b in walk.b]
+        need_c = context is not None and ctx.needs_input_grad[1]
+        g_ctx = torch.zeros(context.shape, device=dev) if need_c else None
+        if g_ctx is not None and g_ctx.dim() == 1:
+            g_ctx = g_ctx.reshape(1, -1)
+        if B:
+            if ctx.checkpoints is None:
+                lam = _continuous_adjoint(walk, y1, context, eps, t0, t1, core.adjoint_steps, lam, mu, gW, gb, g_ctx)
+            else:
+                h = (t1 - t0) / ctx.checkpoints
+                for n in reversed(range(ctx.checkpoints)):
+                    lam = _rk4_step_adjoint(walk, xs[n], context, eps, h, lam, mu, gW, gb, g_ctx)
+        if g_ctx is not None:
+            g_ctx = g_ctx.reshape(context.shape)
+        grads = [t for pair in zip(gW, gb) for t in pair]
+        return (lam if ctx.needs_input_grad[0] else None, g_ctx, None, None, None, None, *grads)

@@ -10,8 +10,10 @@ registers, the MLP resident in LDS (csrc/cnf.hip).
 Solver: naz constructs torchdyn ``NeuralODE(solver='dopri5', atol=rtol=1e-4, sensitivity=
 'adjoint')`` (:73-81).  SURVEY.md §8d pins config 5 to fixed-step classical RK4 with 8 steps
 (NFE 32) — the default here (``solver='rk4', steps=8``); ``solver='dopri5'`` runs the adaptive
-Dormand-Prince solve (naz_cnf_integrate_dopri5, one step size per 16-row group); the adjoint
-backward is §8f rank 3 and raises NotImplementedError.  The Hutchinson probe eps ~ N(0, I)
+Dormand-Prince solve (naz_cnf_integrate_dopri5, one step size per 16-row group).  Under autograd
+the solve is one ``CnfSolveFn`` node (flows/cnf_adjoint.py, §8f rank 3): rk4 backpropagates by the
+discrete adjoint of the pinned solve from per-step checkpoints, dopri5 by the continuous adjoint
+(``adjoint_steps`` RK4 steps back from t1), every RHS and VJP on HIP kernels.  The Hutchinson probe eps ~ N(0, I)
 is drawn per solve on the device, as torchdyn does; assign ``transform.noise`` to fix it.
 """
 from __future__ import annotations
@@ -114,28 +116,40 @@ class _CnfPlan:
 class _FFJORDCore:
     """Shared solve logic of the conditional and unconditional transforms."""
 
-    def _solve(self, v, t0, t1, ld_buf, ld_mode):
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self._net.parameters()):
-            raise NotImplementedError("naz_amd CNF: differentiating through the ODE solve (adjoint) is SURVEY.md "
-                                      "§8f rank 3; evaluate under torch.no_grad()")
-        noise = self.noise if self.noise is not None else torch.randn(v.shape, device=v.device, dtype=torch.float32)
-        packed = self._plan.packed()  # may re-resolve the mode: read desc only after it
-        if self.solver == "dopri5":  # §8f rank 3: adaptive Dormand-Prince, per-16-row step control
-            nfe = self._nfe_buffer(v)
-            y, ld = ops.cnf_integrate_dopri5(self._plan.desc, packed, v, noise, t0, t1, self.atol, self.rtol,
-                                             self.max_steps, context=self._context, ld_out=ld_buf, ld_mode=ld_mode,
-                                             nfe=nfe)
-            # a group that hit max_steps before t1 writes a negative count (cnf.hip): its state and
-            # log-det are from partway through the interval, so fail loudly (strict, the default)
-            if self.strict and nfe.numel() and bool((nfe < 0).any()):
-                bad = int((nfe < 0).sum())
-                raise RuntimeError(f"naz_amd CNF dopri5: {bad} of {nfe.numel()} 16-row groups reached max_steps="
-                                   f"{self.max_steps} before t1 (step size collapsed or non-finite state); "
-                                   "raise max_steps, loosen atol/rtol, or set strict=False to accept partial solves")
-        else:
-            y, ld = ops.cnf_integrate(self._plan.desc, packed, v, noise, t0, t1, self.steps,
-                                      context=self._context, ld_out=ld_buf, ld_mode=ld_mode)
+    def _needs_graph(self, v) -> bool:
+        return torch.is_grad_enabled() and (v.requires_grad or any(p.requires_grad for p in self._net.parameters())
+                                            or (self._context is not None and self._context.requires_grad))
+
+    def _noise(self, v):
+        return self.noise if self.noise is not None else torch.randn(v.shape, device=v.device, dtype=torch.float32)
+
+    def _dopri5(self, desc, packed, v, noise, t0, t1, ld_buf, ld_mode):
+        """§8f rank 3: adaptive Dormand-Prince, per-16-row step control."""
+        nfe = self._nfe_buffer(v)
+        y, ld = ops.cnf_integrate_dopri5(desc, packed, v, noise, t0, t1, self.atol, self.rtol, self.max_steps,
+                                         context=self._context, ld_out=ld_buf, ld_mode=ld_mode, nfe=nfe)
+        # a group that hit max_steps before t1 writes a negative count (cnf.hip): its state and
+        # log-det are from partway through the interval, so fail loudly (strict, the default)
+        if self.strict and nfe.numel() and bool((nfe < 0).any()):
+            bad = int((nfe < 0).sum())
+            raise RuntimeError(f"naz_amd CNF dopri5: {bad} of {nfe.numel()} 16-row groups reached max_steps="
+                               f"{self.max_steps} before t1 (step size collapsed or non-finite state); "
+                               "raise max_steps, loosen atol/rtol, or set strict=False to accept partial solves")
         return y, ld
+
+    def _solve(self, v, t0, t1, ld_buf, ld_mode):
+        if ld_buf is None and self._needs_graph(v):
+            # (the in-place accumulating forms, _inverse_acc / _call_acc, serve the no-grad walk and
+            # sample; their outputs are not differentiable)
+            from .cnf_adjoint import CnfSolveFn
+            ps = [t for lin in self._net.linears() for t in (lin.weight, lin.bias)]
+            return CnfSolveFn.apply(v, self._context, self._noise(v), self, float(t0), float(t1), *ps)
+        noise = self._noise(v)
+        packed = self._plan.packed()  # may re-resolve the mode: read desc only after it
+        if self.solver == "dopri5":
+            return self._dopri5(self._plan.desc, packed, v, noise, t0, t1, ld_buf, ld_mode)
+        return ops.cnf_integrate(self._plan.desc, packed, v, noise, t0, t1, self.steps,
+                                 context=self._context, ld_out=ld_buf, ld_mode=ld_mode)
 
     def _nfe_buffer(self, v):
         """RHS evaluations per 16-row group of the last dopri5 solve (``last_nfe``)."""
@@ -165,8 +179,9 @@ class _FFJORDCore:
         return y
 
     def _inv_ld(self, y):
-        raise NotImplementedError("naz_amd CNF: differentiating through the ODE solve (adjoint) is SURVEY.md §8f "
-                                  "rank 3; evaluate under torch.no_grad()")
+        """The autograd walk's step (flows/distributions.py): x and the forward log-det, both
+        differentiable through the solve (flows/cnf_adjoint.py)."""
+        return self._solve(y, 0.0, 1.0, None, ops.LD_ROWSUM)
 
 
 def _check_solver(solver, steps):
@@ -185,13 +200,14 @@ class FFJORDTransform(_FFJORDCore, TransformModule):
     bijective = True
 
     def __init__(self, net, input_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4, steps=8,
-                 max_steps=1000, strict=True):
+                 max_steps=1000, strict=True, adjoint_steps=16):
         super().__init__()
         _check_solver(solver, steps)
         self.net, self.input_dim, self.steps = net, input_dim, int(steps)
         self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
         self.max_steps = int(max_steps)
         self.strict = bool(strict)
+        self.adjoint_steps = int(adjoint_steps)
         self.last_nfe = None
         self._plan = _CnfPlan(net)
         self._cached_logdet = None
@@ -233,7 +249,7 @@ class _ConditionedFFJORD(_FFJORDCore, Transform):
         return self.module.noise
 
     def __getattr__(self, name):  # solver settings live on the module
-        if name in ("solver", "atol", "rtol", "max_steps", "strict"):
+        if name in ("solver", "atol", "rtol", "max_steps", "strict", "adjoint_steps"):
             return getattr(self.module, name)
         raise AttributeError(name)
 
@@ -243,13 +259,14 @@ class ConditionalFFJORDTransform(ConditionalTransformModule):
     monkey-patch of the vector field's ``forward``."""
 
     def __init__(self, net, input_dim, context_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4,
-                 steps=8, max_steps=1000, strict=True):
+                 steps=8, max_steps=1000, strict=True, adjoint_steps=16):
         super().__init__()
         _check_solver(solver, steps)
         self.net, self.input_dim, self.context_dim, self.steps = net, input_dim, context_dim, int(steps)
         self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
         self.max_steps = int(max_steps)
         self.strict = bool(strict)
+        self.adjoint_steps = int(adjoint_steps)
         self._plan = _CnfPlan(net)
         self.noise: Optional[torch.Tensor] = None
 

@@ -378,7 +378,17 @@ class FCNN:
 def hutchinson_rhs(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor) -> Tuple[Tensor, Tensor]:
     """torchdyn ``CNF.forward`` with naz's ``hutch_trace`` (continuous_transforms.py:78,85-89):
     d[a, x]/dt = [-eps^T (df/dx) eps, f(x)], the VJP eps^T J taken by reverse-mode autograd
-    exactly as the reference does; eps is fixed for one solve."""
+    exactly as the reference does; eps is fixed for one solve.
+
+    Under grad mode with a trainable input or weight (the CNF training step), the VJP is taken
+    with ``create_graph=True`` and nothing is detached, as torchdyn's hutch_trace must for the
+    trace to carry a gradient: autograd through this RHS is the gradient oracle of the adjoint."""
+    if torch.is_grad_enabled() and (x.requires_grad or any(w.requires_grad for w in net.weights + net.biases)
+                                    or (ctx is not None and ctx.requires_grad)):
+        x_in = x if x.requires_grad else x.detach().requires_grad_(True)
+        f = net(x_in, ctx)
+        vjp = torch.autograd.grad(f, x_in, eps, create_graph=True)[0]
+        return f, -torch.einsum("bi,bi->b", vjp, eps)
     with torch.enable_grad():
         x_in = x.detach().requires_grad_(True)
         f = net(x_in, ctx)

@@ -185,9 +185,11 @@ def test_cnf_flow_api():
     assert not torch.equal(lp1, lp2)  # Hutchinson probes are redrawn per solve, as torchdyn does
     s = f.sample([64], condition=c[0])
     assert s.shape == (64, 4) and bool(torch.isfinite(s).all())
-    with torch.enable_grad():
-        with pytest.raises(NotImplementedError):
-            f.log_prob(x, condition=c)
+    with torch.enable_grad():  # the training path: differentiable through the solve (test_gpu_cnf_grad.py)
+        lp = f.log_prob(x, condition=c)
+        assert lp.requires_grad
+        lp.mean().backward()
+        assert all(p.grad is not None and bool(torch.isfinite(p.grad).all()) for p in f.parameters())
 
 
 @pytest.mark.parametrize("scale", [1.0, 3000.0])

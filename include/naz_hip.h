@@ -298,17 +298,15 @@ int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const fl
                              float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
                              int* nfe, int64_t B, void* stream);
 /* CNF training (§8f rank 3; replaces the autograd graph torchdyn's adjoint builds through naz's
- * hutch_trace, continuous_transforms.py:75-89): the activation of one vector-field layer under the
- * Hutchinson JVP on stacked rows.  P [2B, N] (ldp): rows 0..B-1 the value pre-activations W h,
- * rows B..2B-1 the tangents W dh, both without bias; bias [N] nullable.  S [2B, N] (lds):
- *   S[m] = act(P[m] + b),   S[B + m] = act'(P[m] + b) * P[B + m]. */
-int naz_act_jvp(const float* P, int64_t ldp, const float* bias, float* S, int64_t lds, int64_t B, int N, int act,
-                void* stream);
-/* Its VJP: G [2B, N] (ldg) = adjoints of S; GP [2B, N] (ldgp), with pre = P[m] + b:
- *   GP[m] = G[m] act'(pre) + G[B + m] act''(pre) P[B + m],   GP[B + m] = G[B + m] act'(pre);
+ * hutch_trace, continuous_transforms.py:75-89): the VJP of one vector-field activation under the
+ * Hutchinson JVP, on stacked rows.  The forward maps [h_in; dh_in] to S = [h; dh] =
+ * [act(W h_in + b); act'(W h_in + b) (W dh_in)] (naz_linear_act with its activation epilogue +
+ * naz_gemm_dact).  S [2B, N] (lds); G [2B, N] (ldg) = adjoints of S; GP [2B, N] (ldgp) = adjoints
+ * of the pre-activations [W h_in + b; W dh_in], with act', act''/act' recovered from h:
+ *   GP[m] = G[m] act' + G[B + m] (act''/act') dh[m],   GP[B + m] = G[B + m] act';
  * g_bias [N] (nullable) += sum_m GP[m]. */
-int naz_act_jvp_bwd(const float* P, int64_t ldp, const float* bias, const float* G, int64_t ldg, float* GP,
-                    int64_t ldgp, float* g_bias, int64_t B, int N, int act, void* stream);
+int naz_act_jvp_bwd(const float* S, int64_t lds, const float* G, int64_t ldg, float* GP, int64_t ldgp,
+                    float* g_bias, int64_t B, int N, int act, void* stream);
 
 /* ---- §8b naz_spline_ar_inv / naz_affine_ar_inv: fused log_prob of a whole naz "nsa" or "maf" flow
  * Replaces the D-pass loop of pyro ConditionedSplineAutoregressive._inverse (naz

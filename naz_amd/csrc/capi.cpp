@@ -217,19 +217,12 @@ int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const fl
                               ld_mode, nfe, B, as_stream(stream));
 }
 
-int naz_act_jvp(const float* P, int64_t ldp, const float* bias, float* S, int64_t lds, int64_t B, int N, int act,
-                void* stream) {
-  if (B < 0 || N < 0) return set_error("naz_act_jvp: negative size");
-  if (act < 0 || act > NAZ_ACT_SIGMOID) return set_error("naz_act_jvp: unknown activation %d", act);
-  if (B > 0 && N > 0 && (P == nullptr || S == nullptr)) return set_error("naz_act_jvp: null pointer");
-  return act_jvp(P, ldp, bias, S, lds, B, N, act, as_stream(stream));
-}
-int naz_act_jvp_bwd(const float* P, int64_t ldp, const float* bias, const float* G, int64_t ldg, float* GP,
-                    int64_t ldgp, float* g_bias, int64_t B, int N, int act, void* stream) {
+int naz_act_jvp_bwd(const float* S, int64_t lds, const float* G, int64_t ldg, float* GP, int64_t ldgp, float* g_bias,
+                    int64_t B, int N, int act, void* stream) {
   if (B < 0 || N < 0) return set_error("naz_act_jvp_bwd: negative size");
   if (act < 0 || act > NAZ_ACT_SIGMOID) return set_error("naz_act_jvp_bwd: unknown activation %d", act);
-  if (B > 0 && N > 0 && (P == nullptr || G == nullptr || GP == nullptr)) return set_error("naz_act_jvp_bwd: null pointer");
-  return act_jvp_bwd(P, ldp, bias, G, ldg, GP, ldgp, g_bias, B, N, act, as_stream(stream));
+  if (B > 0 && N > 0 && (S == nullptr || G == nullptr || GP == nullptr)) return set_error("naz_act_jvp_bwd: null pointer");
+  return act_jvp_bwd(S, lds, G, ldg, GP, ldgp, g_bias, B, N, act, as_stream(stream));
 }
 
 int naz_coupling_supported(const naz_coupling_desc* d) { return coupling_supported(d); }

@@ -908,93 +908,89 @@ int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int
 }
 
 // ---- the CNF backward walk (§8f rank 3: FFJORD training; flows/cnf_adjoint.py) -----------------
-// A vector-field layer under the Hutchinson JVP maps the stacked rows [h; dh] (value rows 0..B-1,
-// tangent rows B..2B-1) to [act(W h + b); act'(W h + b) ⊙ (W dh)].  The GEMM W·[h; dh] is one
-// batch-row GEMM over 2B rows (naz_linear_act); these two kernels are the activation between them
-// and its VJP, which needs act'' because the tangent depends on pre through act'.
+// A vector-field layer under the Hutchinson JVP maps [h; dh] to [act(W h + b); act'(W h + b) ⊙ (W dh)]
+// (forward: naz_linear_act with the activation epilogue and naz_gemm_dact).  Its VJP needs act'
+// and, because the tangent reads pre through act', act'' — both recovered from the stored
+// post-activation value h (act''·dpre = (act''/act')·dh), so the walk keeps only [h; dh]:
+//   GP[m] = G[m] act'(pre) + G[B + m] (act''/act')(pre) dh,   GP[B + m] = G[B + m] act'(pre).
 
-// value, first and second derivative of the activation at pre (torch's forms: softplus with
-// beta = 1 / threshold = 20 is the identity above 20, derivative z / (z + 1), z = e^pre)
-NAZ_DEV void act_d012(int act, float pre, float& v, float& d1, float& d2) {
+// act'(pre) and act''(pre) / act'(pre) from h = act(pre) (torch's forms: softplus with beta = 1,
+// threshold 20 — above it the identity, act' = 1 - e^-h -> 1 and act''/act' = e^-h -> 0 in fp32)
+NAZ_DEV void act_d1_ratio(int act, float h, float& d1, float& r) {
   switch (act) {
-    case ACT_SOFTPLUS: {
-      if (pre > 20.f) {
-        v = pre, d1 = 1.f, d2 = 0.f;
-      } else {
-        const float z = expf(pre);
-        v = log1pf(z);
-        d1 = z / (z + 1.f);
-        d2 = d1 * (1.f - d1);
-      }
-      break;
-    }
-    case ACT_TANH: v = tanh_f(pre), d1 = 1.f - v * v, d2 = -2.f * v * d1; break;
-    case ACT_RELU: v = fmaxf(pre, 0.f), d1 = pre > 0.f ? 1.f : 0.f, d2 = 0.f; break;
-    case ACT_SIGMOID: v = 1.f / (1.f + expf(-pre)), d1 = v * (1.f - v), d2 = d1 * (1.f - 2.f * v); break;
-    default: v = pre, d1 = 1.f, d2 = 0.f;
+    case ACT_SOFTPLUS: d1 = -expm1f(-h), r = 1.f - d1; break;  // sigmoid(pre), 1 - sigmoid(pre)
+    case ACT_TANH: d1 = 1.f - h * h, r = -2.f * h; break;
+    case ACT_RELU: d1 = h > 0.f ? 1.f : 0.f, r = 0.f; break;
+    case ACT_SIGMOID: d1 = h * (1.f - h), r = 1.f - 2.f * h; break;
+    default: d1 = 1.f, r = 0.f;
   }
 }
 
-__global__ void act_jvp_kernel(const float* __restrict__ P, int64_t ldp, const float* __restrict__ bias,
-                               float* __restrict__ S, int64_t lds, int64_t B, int N, int act) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= B * N) return;
-  const int64_t m = e / N;
-  const int n = (int)(e - m * N);
-  float v, d1, d2;
-  act_d012(act, P[m * ldp + n] + (bias != nullptr ? bias[n] : 0.f), v, d1, d2);
-  S[m * lds + n] = v;
-  S[(B + m) * lds + n] = d1 * P[(B + m) * ldp + n];
-}
-
-// 64 columns x 4 row lanes per block; each block walks `rpb` rows and adds its share of the bias
-// gradient (the value half's column sums) with one atomic per column.
-constexpr int kJvpCols = 64, kJvpRowLanes = 4;
-
-__global__ void act_jvp_bwd_kernel(const float* __restrict__ P, int64_t ldp, const float* __restrict__ bias,
-                                   const float* __restrict__ G, int64_t ldg, float* __restrict__ GP, int64_t ldgp,
-                                   float* __restrict__ g_bias, int64_t B, int N, int act, int64_t rpb) {
-  __shared__ float red[kJvpRowLanes][kJvpCols];
-  const int tx = threadIdx.x % kJvpCols, ty = threadIdx.x / kJvpCols;
-  const int n = blockIdx.x * kJvpCols + tx;
+// 32 column groups of V adjacent columns x 8 row lanes per block (V = 4: 16-byte accesses, a wave
+// covers two 512-byte row pieces); each block walks `rpb` rows and adds its share of the bias
+// gradient (the value rows' column sums) with one atomic per column.
+template <int V>
+__global__ void act_jvp_bwd_kernel(const float* __restrict__ S, int64_t lds, const float* __restrict__ G, int64_t ldg,
+                                   float* __restrict__ GP, int64_t ldgp, float* __restrict__ g_bias, int64_t B, int N,
+                                   int act, int64_t rpb) {
+  __shared__ float red[8][32 * V];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int n0 = (blockIdx.x * 32 + tx) * V;
   const int64_t m0 = (int64_t)blockIdx.y * rpb;
   const int64_t m1 = m0 + rpb < B ? m0 + rpb : B;
-  float acc = 0.f;
-  if (n < N) {
-    const float b = bias != nullptr ? bias[n] : 0.f;
-    for (int64_t m = m0 + ty; m < m1; m += kJvpRowLanes) {
-      float v, d1, d2;
-      act_d012(act, P[m * ldp + n] + b, v, d1, d2);
-      const float gv = G[m * ldg + n], gt = G[(B + m) * ldg + n];
-      const float gp = gv * d1 + gt * d2 * P[(B + m) * ldp + n];
-      GP[m * ldgp + n] = gp;
-      GP[(B + m) * ldgp + n] = gt * d1;
-      acc += gp;
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  if (n0 < N) {
+    for (int64_t m = m0 + ty; m < m1; m += 8) {
+      float h[V], dh[V], gv[V], gt[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        h[j] = S[m * lds + n0 + j], dh[j] = S[(B + m) * lds + n0 + j];
+        gv[j] = G[m * ldg + n0 + j], gt[j] = G[(B + m) * ldg + n0 + j];
+      }
+      float pv[V], pt[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float d1, r;
+        act_d1_ratio(act, h[j], d1, r);
+        pv[j] = gv[j] * d1 + gt[j] * dh[j] * r;
+        pt[j] = gt[j] * d1;
+        acc[j] += pv[j];
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) GP[m * ldgp + n0 + j] = pv[j], GP[(B + m) * ldgp + n0 + j] = pt[j];
     }
   }
   if (g_bias == nullptr) return;
-  red[ty][tx] = acc;
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[ty][tx * V + j] = acc[j];
   __syncthreads();
-  if (ty == 0 && n < N) atomicAdd(g_bias + n, red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx]);
+  if (ty == 0 && n0 < N) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) t += red[r][tx * V + j];
+      atomicAdd(g_bias + n0 + j, t);
+    }
+  }
 }
 
-int act_jvp(const float* P, int64_t ldp, const float* bias, float* S, int64_t lds, int64_t B, int N, int act,
-            hipStream_t s) {
+int act_jvp_bwd(const float* S, int64_t lds, const float* G, int64_t ldg, float* GP, int64_t ldgp, float* g_bias,
+                int64_t B, int N, int act, hipStream_t s) {
   if (B <= 0 || N <= 0) return 0;
-  const int64_t n = B * N;
-  hipLaunchKernelGGL(act_jvp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, ldp, bias, S, lds, B, N,
-                     act);
-  return check_launch("act_jvp_kernel");
-}
-
-int act_jvp_bwd(const float* P, int64_t ldp, const float* bias, const float* G, int64_t ldg, float* GP, int64_t ldgp,
-                float* g_bias, int64_t B, int N, int act, hipStream_t s) {
-  if (B <= 0 || N <= 0) return 0;
-  int64_t rpb = 256;  // rows per block, grown so grid.y stays within 65535
+  const bool vec = N % 4 == 0 && lds % 4 == 0 && ldg % 4 == 0 && ldgp % 4 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(S) | reinterpret_cast<uintptr_t>(G) |
+                     reinterpret_cast<uintptr_t>(GP)) & 15) == 0;
+  const int cols = vec ? 128 : 32;
+  int64_t rpb = 64;  // rows per block (4 thousand blocks at 2^18 rows), grown so grid.y stays within 65535
   if ((B + rpb - 1) / rpb > 65535) rpb = (B + 65534) / 65535;
-  const dim3 grid((unsigned)((N + kJvpCols - 1) / kJvpCols), (unsigned)((B + rpb - 1) / rpb));
-  hipLaunchKernelGGL(act_jvp_bwd_kernel, grid, dim3(kJvpCols * kJvpRowLanes), 0, s, P, ldp, bias, G, ldg, GP, ldgp,
-                     g_bias, B, N, act, rpb);
+  const dim3 grid((unsigned)((N + cols - 1) / cols), (unsigned)((B + rpb - 1) / rpb));
+  if (vec)
+    hipLaunchKernelGGL(act_jvp_bwd_kernel<4>, grid, dim3(256), 0, s, S, lds, G, ldg, GP, ldgp, g_bias, B, N, act, rpb);
+  else
+    hipLaunchKernelGGL(act_jvp_bwd_kernel<1>, grid, dim3(256), 0, s, S, lds, G, ldg, GP, ldgp, g_bias, B, N, act, rpb);
   return check_launch("act_jvp_bwd_kernel");
 }
 

@@ -77,16 +77,26 @@ __global__ void __launch_bounds__(256) gemm_kernel(int M, int N, int64_t K, cons
   }
 }
 
-// out[n] (+)= Σ_m A[m, n]   (A row-major with row stride lda); 256 columns x 64-row chunks per block
+// out[n] (+)= Σ_m A[m, n]   (A row-major with row stride lda).  A block is `cw` adjacent columns
+// (a power of two <= 64, >= N when N is narrow) x 256 / cw row lanes, so a wave reads whole
+// 256-byte row pieces (the [B, 16] bias gradients of the CNF walk: 16 x 16), walking
+// `rows_per_block` rows; the row lanes reduce through LDS, one atomic per column per block.
 __global__ void colsum_kernel(const float* __restrict__ A, int64_t lda, int64_t M, int N, float* __restrict__ out,
-                              int64_t rows_per_block) {
-  const int n = blockIdx.y * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+                              int64_t rows_per_block, int cw) {
+  __shared__ float red[256];
+  const int tx = threadIdx.x & (cw - 1), ty = threadIdx.x / cw, lanes = 256 / cw;
+  const int n = blockIdx.y * cw + tx;
   const int64_t m0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t m1 = (m0 + rows_per_block) < M ? (m0 + rows_per_block) : M;
   float s = 0.f;
-  for (int64_t m = m0; m < m1; ++m) s += A[m * lda + n];
-  atomicAdd(out + n, s);
+  if (n < N)
+    for (int64_t m = m0 + ty; m < m1; m += lanes) s += A[m * lda + n];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (ty == 0 && n < N) {
+    for (int r = 1; r < lanes; ++r) s += red[r * cw + tx];
+    atomicAdd(out + n, s);
+  }
 }
 
 // dPre = dY ⊙ act'(Y), both [M, N] with row strides
@@ -128,9 +138,12 @@ int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, cons
 
 int colsum(const float* A, int64_t lda, int64_t M, int N, float* out, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
-  const int64_t rpb = 1024;
-  dim3 grid((unsigned)((M + rpb - 1) / rpb), (unsigned)((N + 255) / 256));
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, A, lda, M, N, out, rpb);
+  int cw = 1;
+  while (cw < N && cw < 64) cw *= 2;
+  int64_t rpb = 1024;  // rows per block, grown so grid.x stays within 65535 * 16
+  if ((M + rpb - 1) / rpb > 65535 * 16) rpb = (M + 65535 * 16 - 1) / (65535 * 16);
+  dim3 grid((unsigned)((M + rpb - 1) / rpb), (unsigned)((N + cw - 1) / cw));
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, A, lda, M, N, out, rpb, cw);
   return check_launch("colsum_kernel");
 }
 

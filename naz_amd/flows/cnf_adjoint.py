@@ -21,11 +21,12 @@ augmented solve d[x, a]/dt = [f(x, ctx), -eps^T (df/dx) eps] (hutch_trace, :85-8
   mu d(-tr)/dtheta)) with ``adjoint_steps`` fixed RK4 steps (x reconstructed backwards in time, as
   torchdyn does).  Its gradient approximates the continuous one, not the forward's step sequence.
 
-Every RHS evaluation and VJP is HIP (``CnfWalk``): the vector field under the Hutchinson JVP is a
-chain of batch-row GEMMs over the stacked rows [h; dh] (2B rows: value and tangent share each
-weight read, ``naz_linear_act``), the activation pair ``naz_act_jvp``; the VJP is ``naz_act_jvp_bwd``
-(value rows need act'' because the tangent reads pre through act') and ``naz_gemm`` for dX and the
-2B-row dW reductions.  Torch only forms the [B, D]-sized RK4 combinations.
+Every RHS evaluation and VJP is HIP (``CnfWalk``): per hidden layer the value GEMM with its
+bias + activation epilogue (``naz_linear_act``) and the tangent GEMM with the act' epilogue
+(``naz_gemm_dact``), kept as stacked rows [h; dh] (2B rows); the VJP is ``naz_act_jvp_bwd`` (value
+rows need act'' because the tangent reads pre through act'; both derivatives come from h) and
+``naz_gemm`` for dX and the 2B-row dW reductions.  Torch only forms the [B, D]-sized RK4
+combinations.
 """
 from __future__ import annotations
 
@@ -37,62 +38,83 @@ from torch.autograd import Function
 from .. import ops
 
 
+def _stacked(B: int, N: int, like: torch.Tensor) -> torch.Tensor:
+    """[2B, N] value/tangent rows, rows padded to 16 bytes (the batch-row kernels' fast path)."""
+    npad = (N + 3) // 4 * 4
+    t = torch.empty((2 * B, npad), device=like.device, dtype=like.dtype)
+    return t[:, :N] if npad != N else t
+
+
 class CnfWalk:
     """The FFJORD vector field (ConditionalFCNN, naz continuous_transforms.py:38-60, input
-    cat([x, ctx]), x first) with its Hutchinson JVP, evaluated layer by layer on HIP kernels."""
+    cat([x, ctx]), x first) with its Hutchinson JVP, evaluated layer by layer on HIP kernels.
+
+    Hidden layer i keeps S_i = [h_i; dh_i] (2B rows): h_i = act(W_i h + b_i) by naz_linear_act
+    (activation epilogue), dh_i = act'(pre) ⊙ (W_i dh) by naz_gemm_dact (act' from h_i in the
+    epilogue).  The VJP needs nothing else: act' and act''/act' are functions of h_i."""
 
     def __init__(self, net):
         lins = net.linears()
         self.W = [lin.weight.detach() for lin in lins]
         self.b = [lin.bias.detach() for lin in lins]
         self.act = net.act
-        self.D, self.C = net.input_dim, net.context_dim
+        self.D, self.C = D, C = net.input_dim, net.context_dim
+        W0 = self.W[0]
+        # naz_linear_act concatenates [ctx | x]; the CNF input is [x | ctx]: reorder W0's columns
+        self.W0_cx = torch.cat([W0[:, D:], W0[:, :D]], 1).contiguous() if C else W0.contiguous()
+        self.WT = [W0[:, :D].t().contiguous()] + [W.t().contiguous() for W in self.W[1:]]  # tangent GEMMs
 
     def rhs(self, z: torch.Tensor, ctx: Optional[torch.Tensor], eps: torch.Tensor):
         """(f(z), -eps^T J eps, saved activations) for z [B, D]."""
-        B, D, C = z.shape[0], self.D, self.C
-        S = torch.zeros((2 * B, D + C), device=z.device, dtype=z.dtype)
-        S[:B, :D] = z
-        S[B:, :D] = eps
-        if C:
-            S[:B, D:] = ctx.reshape(-1, C).expand(B, C) if ctx.numel() == C else ctx
-        saved = [S]
-        for W, b in zip(self.W[:-1], self.b[:-1]):
-            P = ops.linear_act(S, W, None)
-            S = ops.act_jvp(P, b, self.act)
-            saved += [P, S]
-        O = ops.linear_act(S, self.W[-1], None)
-        k = O[:B] + self.b[-1]
-        t = -(eps * O[B:]).sum(1)
+        B, n = z.shape[0], len(self.W)
+        saved = [z]
+        h, dh = None, eps
+        for i in range(n - 1):
+            S = _stacked(B, self.W[i].shape[0], z)
+            if i == 0:
+                ops.linear_act(z, self.W0_cx, self.b[0], self.act, context=ctx if self.C else None, out=S[:B])
+            else:
+                ops.linear_act(h, self.W[i], self.b[i], self.act, out=S[:B])
+            ops.gemm_dact(dh, self.WT[i], S[:B], self.act, out=S[B:])
+            h, dh = S[:B], S[B:]
+            saved.append(S)
+        k = ops.linear_act(h, self.W[-1], self.b[-1])
+        jv = ops.gemm(dh, self.WT[-1])
+        t = -(eps * jv).sum(1)
         return k, t, saved
 
-    def vjp(self, saved: List[torch.Tensor], eps: torch.Tensor, g_k: torch.Tensor, g_t: torch.Tensor,
-            gW: List[torch.Tensor], gb: List[torch.Tensor], g_ctx: Optional[torch.Tensor]) -> torch.Tensor:
+    def vjp(self, saved: List[torch.Tensor], ctx: Optional[torch.Tensor], eps: torch.Tensor, g_k: torch.Tensor,
+            g_t: torch.Tensor, gW: List[torch.Tensor], gb: List[torch.Tensor], g_ctx: Optional[torch.Tensor]):
         """Adjoints (g_k, g_t) of (f, -tr) at the point ``rhs`` saved -> returns g_z [B, D];
         accumulates the weight / bias gradients into gW / gb and the context's into g_ctx."""
-        B, D, C = g_k.shape[0], self.D, self.C
+        B, D, C, n = g_k.shape[0], self.D, self.C, len(self.W)
+        z = saved[0]
         G = torch.empty((2 * B, D), device=g_k.device, dtype=g_k.dtype)
         G[:B] = g_k
         G[B:] = -g_t[:, None] * eps
-        n = len(self.W)
         ops.gemm(G.t(), saved[-1], out=gW[-1], accumulate=True)
         ops.colsum(g_k, out=gb[-1])
         GS = ops.gemm(G, self.W[-1])
         for i in reversed(range(n - 1)):
-            P, S_in = saved[2 * i + 1], saved[2 * i]
-            GP = ops.act_jvp_bwd(P, self.b[i], GS, self.act, g_bias=gb[i])
-            ops.gemm(GP.t(), S_in, out=gW[i], accumulate=True)
+            GP = ops.act_jvp_bwd(saved[i + 1], GS, self.act, g_bias=gb[i])
             if i > 0:
+                ops.gemm(GP.t(), saved[i], out=gW[i], accumulate=True)
                 GS = ops.gemm(GP, self.W[i])
-            else:
-                GP = GP[:B]  # the tangent rows' input is eps (no gradient)
-                g_z = ops.gemm(GP, self.W[0][:, :D])
-                if C and g_ctx is not None:
-                    Wc = self.W[0][:, D:]
-                    if g_ctx.shape[0] == B and g_ctx.dim() == 2:
-                        ops.gemm(GP, Wc, out=g_ctx, accumulate=True)
-                    else:
-                        ops.gemm(ops.colsum(GP).reshape(1, -1), Wc, out=g_ctx.view(1, C), accumulate=True)
+                continue
+            S0 = torch.zeros((2 * B, D + C), device=z.device, dtype=z.dtype)  # [[z, ctx]; [eps, 0]]
+            S0[:B, :D] = z
+            S0[B:, :D] = eps
+            if C:
+                S0[:B, D:] = ctx.reshape(-1, C).expand(B, C) if ctx.numel() == C else ctx
+            ops.gemm(GP.t(), S0, out=gW[0], accumulate=True)
+            GP = GP[:B]  # the tangent rows' input is eps (no gradient)
+            g_z = ops.gemm(GP, self.W[0][:, :D])
+            if C and g_ctx is not None:
+                Wc = self.W[0][:, D:]
+                if g_ctx.shape[0] == B and g_ctx.dim() == 2:
+                    ops.gemm(GP, Wc, out=g_ctx, accumulate=True)
+                else:
+                    ops.gemm(ops.colsum(GP).reshape(1, -1), Wc, out=g_ctx.view(1, C), accumulate=True)
         return g_z
 
 
@@ -104,13 +126,13 @@ def _rk4_step_adjoint(walk, x, ctx, eps, h, lam, mu, gW, gb, g_ctx):
     _, _, s4 = walk.rhs(x + h * k3, ctx, eps)
     del k1, k2, k3
     w1, w2 = h / 6.0, h / 3.0
-    gz4 = walk.vjp(s4, eps, w1 * lam, w1 * mu, gW, gb, g_ctx)
+    gz4 = walk.vjp(s4, ctx, eps, w1 * lam, w1 * mu, gW, gb, g_ctx)
     del s4
-    gz3 = walk.vjp(s3, eps, w2 * lam + h * gz4, w2 * mu, gW, gb, g_ctx)
+    gz3 = walk.vjp(s3, ctx, eps, w2 * lam + h * gz4, w2 * mu, gW, gb, g_ctx)
     del s3
-    gz2 = walk.vjp(s2, eps, w2 * lam + 0.5 * h * gz3, w2 * mu, gW, gb, g_ctx)
+    gz2 = walk.vjp(s2, ctx, eps, w2 * lam + 0.5 * h * gz3, w2 * mu, gW, gb, g_ctx)
     del s2
-    gz1 = walk.vjp(s1, eps, w1 * lam + 0.5 * h * gz2, w1 * mu, gW, gb, g_ctx)
+    gz1 = walk.vjp(s1, ctx, eps, w1 * lam + 0.5 * h * gz2, w1 * mu, gW, gb, g_ctx)
     return lam + gz1 + gz2 + gz3 + gz4
 
 
@@ -123,7 +145,7 @@ def _continuous_adjoint(walk, y1, ctx, eps, t0, t1, steps, lam, mu, gW, gb, g_ct
         # derivative of [x, lam, theta_bar]: (f, -g_z, -g_theta); the parameter / context part is
         # accumulated directly with its RK4 weight c (the VJP is linear in its adjoint inputs)
         k, _, sv = walk.rhs(xs, ctx, eps)
-        gz = walk.vjp(sv, eps, -c * ls, -c * mu, gW, gb, g_ctx)
+        gz = walk.vjp(sv, ctx, eps, -c * ls, -c * mu, gW, gb, g_ctx)
         return k, gz / c
 
     for _ in range(steps):

@@ -21,7 +21,7 @@ Tensor = torch.Tensor
 __all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "made_affine_inv1", "gemm_dact", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
-           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5", "act_jvp", "act_jvp_bwd",
+           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5", "act_jvp_bwd",
            "LAYOUT_ARN", "LAYOUT_DENSE", "LD_PERDIM", "LD_ROWSUM", "LD_ROWSUM_ADD",
            "LD_ROWSUM_SUB"]
 
@@ -445,35 +445,21 @@ def act_bwd(g_y: Tensor, y: Tensor, act: str) -> Tensor:
     return gp
 
 
-def act_jvp(P: Tensor, bias: Optional[Tensor], act: str) -> Tensor:
-    """Stacked value/tangent activation of a CNF vector-field layer (naz_act_jvp): P [2B, N] =
-    [W h; W dh] without bias -> [act(W h + b); act'(W h + b) * (W dh)]."""
-    dev = _dev(P, bias)
-    P, ldp = _rows(P)
-    M, N = P.shape
-    if M % 2:
-        raise ValueError("act_jvp: P must stack value and tangent rows ([2B, N])")
-    if bias is not None and (bias.shape != (N,) or not bias.is_contiguous()):
-        raise ValueError(f"act_jvp: bias must be a contiguous [{N}] tensor")
-    S = torch.empty((M, N), device=dev, dtype=torch.float32)
-    check(lib().naz_act_jvp(_p(P), ldp, _p(bias), _p(S), N, M // 2, N, ACT[act], _stream(dev)), "act_jvp")
-    return S
-
-
-def act_jvp_bwd(P: Tensor, bias: Optional[Tensor], G: Tensor, act: str, g_bias: Optional[Tensor] = None) -> Tensor:
-    """VJP of ``act_jvp`` (naz_act_jvp_bwd): adjoints G [2B, N] of its output -> adjoints of P
-    (value rows: G_v act' + G_t act'' (W dh); tangent rows: G_t act'); ``g_bias`` [N] += the value
-    rows' column sums."""
-    dev = _dev(P, bias, G, g_bias)
-    P, ldp = _rows(P)
+def act_jvp_bwd(S: Tensor, G: Tensor, act: str, g_bias: Optional[Tensor] = None) -> Tensor:
+    """VJP of a CNF vector-field activation under the Hutchinson JVP (naz_act_jvp_bwd): S = [h; dh]
+    [2B, N] (post-activation values and tangents), G [2B, N] their adjoints -> the adjoints of
+    the pre-activations [W h + b; W dh]; ``g_bias`` [N] += the value rows' column sums."""
+    dev = _dev(S, G, g_bias)
+    S, lds = _rows(S)
     G, ldg = _rows(G)
-    M, N = P.shape
+    M, N = S.shape
     if M % 2 or G.shape != (M, N):
-        raise ValueError("act_jvp_bwd: P and G must both be [2B, N]")
+        raise ValueError("act_jvp_bwd: S and G must both be [2B, N]")
     if g_bias is not None and (g_bias.shape != (N,) or not g_bias.is_contiguous()):
         raise ValueError(f"act_jvp_bwd: g_bias must be a contiguous [{N}] tensor")
-    GP = torch.empty((M, N), device=dev, dtype=torch.float32)
-    check(lib().naz_act_jvp_bwd(_p(P), ldp, _p(bias), _p(G), ldg, _p(GP), N, _p(g_bias), M // 2, N, ACT[act],
+    npad = (N + 3) // 4 * 4
+    GP = torch.empty((M, npad), device=dev, dtype=torch.float32)[:, :N]
+    check(lib().naz_act_jvp_bwd(_p(S), lds, _p(G), ldg, _p(GP), GP.stride(0), _p(g_bias), M // 2, N, ACT[act],
                                 _stream(dev)), "act_jvp_bwd")
     return GP
 

@@ -1,7 +1,7 @@
 """CPU: the host logic of the CNF backward (naz_amd/flows/cnf_adjoint.py) — the stacked
 value/tangent walk, the discrete RK4 adjoint recursion and the continuous adjoint — with every HIP
 launch replaced by a float64 torch statement of the kernel's documented semantics
-(include/naz_hip.h: naz_linear_act, naz_act_jvp, naz_act_jvp_bwd, naz_gemm, naz_colsum).  Checked
+(include/naz_hip.h: naz_linear_act, naz_gemm_dact, naz_act_jvp_bwd, naz_gemm, naz_colsum).  Checked
 against the oracle's float64 autograd through the same RK4 solve (oracle hutchinson_rhs with
 create_graph).  The kernels themselves are covered on the GPU by tests/test_gpu_cnf_grad.py."""
 import types
@@ -13,32 +13,35 @@ from torch import nn
 from oracle import naz_oracle as O
 
 
-def _act(act, pre):
+def _d1_ratio(act, h):
     if act == "softplus":
-        v = torch.where(pre > 20, pre, torch.log1p(torch.exp(pre)))
-        d1 = torch.where(pre > 20, torch.ones_like(pre), torch.sigmoid(pre))
-        d2 = torch.where(pre > 20, torch.zeros_like(pre), d1 * (1 - d1))
-    else:
-        v = torch.tanh(pre)
-        d1 = 1 - v * v
-        d2 = -2 * v * d1
-    return v, d1, d2
+        d1 = -torch.expm1(-h)
+        return d1, 1 - d1
+    return 1 - h * h, -2 * h
 
 
 def _fake_ops():
+    acts = {"identity": lambda v: v, "softplus": lambda v: torch.where(v > 20, v, torch.log1p(torch.exp(v))),
+            "tanh": torch.tanh}
+
+    def _put(out, r):
+        if out is None:
+            return r
+        out.copy_(r)
+        return out
+
     def linear_act(x, W, b, act="identity", context=None, mask=None, out=None):
-        assert b is None and act == "identity" and context is None
-        return x @ W.t()
+        inp = x if context is None else torch.cat([context.reshape(-1, context.shape[-1]).expand(x.shape[0], -1), x], 1)
+        pre = inp @ W.t() + (0 if b is None else b)
+        return _put(out, acts[act](pre))
 
-    def act_jvp(P, b, act):
-        B = P.shape[0] // 2
-        v, d1, _ = _act(act, P[:B] + b)
-        return torch.cat([v, d1 * P[B:]])
+    def gemm_dact(a, W, y, act, mask=None, out=None):
+        return _put(out, (a @ W) * _d1_ratio(act, y)[0])
 
-    def act_jvp_bwd(P, b, G, act, g_bias=None):
-        B = P.shape[0] // 2
-        _, d1, d2 = _act(act, P[:B] + b)
-        gp = G[:B] * d1 + G[B:] * d2 * P[B:]
+    def act_jvp_bwd(S, G, act, g_bias=None):
+        B = S.shape[0] // 2
+        d1, r = _d1_ratio(act, S[:B])
+        gp = G[:B] * d1 + G[B:] * S[B:] * r
         if g_bias is not None:
             g_bias += gp.sum(0)
         return torch.cat([gp, G[B:] * d1])
@@ -59,7 +62,7 @@ def _fake_ops():
         out += a.sum(0)
         return out
 
-    return types.SimpleNamespace(linear_act=linear_act, act_jvp=act_jvp, act_jvp_bwd=act_jvp_bwd, gemm=gemm,
+    return types.SimpleNamespace(linear_act=linear_act, gemm_dact=gemm_dact, act_jvp_bwd=act_jvp_bwd, gemm=gemm,
                                  colsum=colsum)
 
 

@@ -42,10 +42,13 @@ NAZ_DEV floatx4 mfma3_16(const Frag2& a, const Frag2& b, floatx4 acc) {
 
 // GEMM stages run at wave priority 1, the splines at 0: a SIMD's matrix pipe is fed first
 // and the spline VALU of the other waves fills the MFMA issue gaps (+0.5 %, same-box A/B).
-#ifndef NAZ_R16_NO_PRIO
-#define R16_PRIO(p) __builtin_amdgcn_s_setprio(p)
-#else
+// NAZ_R16_STATIC_PRIO (experiment): no per-stage flips; the second-dispatched half of the workgroup
+// (waves 4-7, the arbitration losers) runs at priority 1 for the whole kernel (MI355X_MICROARCH.md,
+// "two waves per SIMD" item 4).
+#if defined(NAZ_R16_NO_PRIO) || defined(NAZ_R16_STATIC_PRIO)
 #define R16_PRIO(p) ((void)0)
+#else
+#define R16_PRIO(p) __builtin_amdgcn_s_setprio(p)
 #endif
 
 constexpr int kR16Waves = 8;                 // 8 waves x 16 rows = 128 rows per workgroup
@@ -351,6 +354,9 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
   const int64_t row = (int64_t)blockIdx.x * kR16Rows + wave * 16 + (lane & 15);
   const bool valid = row < B;
   const int64_t crow = valid ? row : 0;
+#ifdef NAZ_R16_STATIC_PRIO
+  if (wave >= kR16Waves / 2) __builtin_amdgcn_s_setprio(1);
+#endif
 
   float zl[CF::SQ], zu[CF::DQ];
   float ldsum = 0.f, logjac = 0.f;

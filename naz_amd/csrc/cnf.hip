@@ -918,7 +918,7 @@ int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int
 // threshold 20 — above it the identity, act' = 1 - e^-h -> 1 and act''/act' = e^-h -> 0 in fp32)
 NAZ_DEV void act_d1_ratio(int act, float h, float& d1, float& r) {
   switch (act) {
-    case ACT_SOFTPLUS: d1 = -expm1f(-h), r = 1.f - d1; break;  // sigmoid(pre), 1 - sigmoid(pre)
+    case ACT_SOFTPLUS: d1 = -Math<true>::expm1(-h), r = 1.f - d1; break;  // sigmoid(pre), 1 - sigmoid(pre)
     case ACT_TANH: d1 = 1.f - h * h, r = -2.f * h; break;
     case ACT_RELU: d1 = h > 0.f ? 1.f : 0.f, r = 0.f; break;
     case ACT_SIGMOID: d1 = h * (1.f - h), r = 1.f - 2.f * h; break;

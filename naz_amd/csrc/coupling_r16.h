@@ -51,7 +51,10 @@ NAZ_DEV floatx4 mfma3_16(const Frag2& a, const Frag2& b, floatx4 acc) {
 #define R16_PRIO(p) __builtin_amdgcn_s_setprio(p)
 #endif
 
-constexpr int kR16Waves = 8;                 // 8 waves x 16 rows = 128 rows per workgroup
+#ifndef NAZ_R16_WAVES
+#define NAZ_R16_WAVES 8
+#endif
+constexpr int kR16Waves = NAZ_R16_WAVES;     // 8 waves x 16 rows = 128 rows per workgroup
 constexpr int kR16Rows = 16 * kR16Waves;
 
 // feature carried by k-slot 8q + j of 32-k step t (GEMM2/3 inputs)

@@ -68,6 +68,7 @@ struct RowGemmArgs {
   const float* dy;
   int64_t lddy;
   int dact;
+  int dyvec;  // dy rows allow 16-byte loads (set by rowgemm())
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -211,10 +212,18 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
         float4 v = *reinterpret_cast<const float4*>(E + row * EP + 4 * c4);
         if (p.dy != nullptr) {  // chained act' (naz_gemm_dact), applied on the 16-byte row piece
           const float* dyr = p.dy + m * p.lddy + col;
-          v.x *= activate_grad_from_out(p.dact, dyr[0]);
-          if (col + 1 < p.N) v.y *= activate_grad_from_out(p.dact, dyr[1]);
-          if (col + 2 < p.N) v.z *= activate_grad_from_out(p.dact, dyr[2]);
-          if (col + 3 < p.N) v.w *= activate_grad_from_out(p.dact, dyr[3]);
+          if (p.dyvec && col + 4 <= p.N) {  // one 16-byte load of the row piece
+            const float4 d4 = *reinterpret_cast<const float4*>(dyr);
+            v.x *= activate_grad_from_out(p.dact, d4.x);
+            v.y *= activate_grad_from_out(p.dact, d4.y);
+            v.z *= activate_grad_from_out(p.dact, d4.z);
+            v.w *= activate_grad_from_out(p.dact, d4.w);
+          } else {
+            v.x *= activate_grad_from_out(p.dact, dyr[0]);
+            if (col + 1 < p.N) v.y *= activate_grad_from_out(p.dact, dyr[1]);
+            if (col + 2 < p.N) v.z *= activate_grad_from_out(p.dact, dyr[2]);
+            if (col + 3 < p.N) v.w *= activate_grad_from_out(p.dact, dyr[3]);
+          }
         }
         if (col + 4 <= p.N) {
           float4* dst = reinterpret_cast<float4*>(p.c + m * p.ldc + col);
@@ -268,6 +277,7 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   p.vec = (p.ka0 % 8 == 0) && (p.ka0 == 0 || (al16(p.a0) && p.lda0 % 4 == 0)) &&
           (p.ka1 == 0 || (al16(p.a1) && p.lda1 % 4 == 0));
   p.vst = p.ldc % 4 == 0 && al16(p.c);  // 16-byte row pieces; a ragged row tail is stored per column
+  p.dyvec = p.dy != nullptr && p.lddy % 4 == 0 && al16(p.dy);
   if (nz > 1) {  // every problem's base keeps the alignment
     p.vec = p.vec && p.za0 % 4 == 0 && p.za1 % 4 == 0;
     p.vst = p.vst && p.zc % 4 == 0;

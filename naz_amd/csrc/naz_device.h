@@ -53,6 +53,13 @@ struct Math<true> {
     const float d = u - 1.f;
     return d == 0.f ? x : log(u) * div(x, d);
   }
+  // expm1 with full relative precision for small x (Kahan: (u - 1) x / log(u), u = e^x)
+  static NAZ_DEV float expm1(float x) {
+    const float u = exp(x);
+    if (u == 1.f) return x;
+    const float um1 = u - 1.f;
+    return um1 == -1.f ? -1.f : um1 * div(x, log(u));
+  }
 };
 
 // torch.nn.functional.softplus(beta=1, threshold=20)
@@ -93,7 +100,10 @@ NAZ_DEV float activate_rt(int act, float x) {
   switch (act) {
     case ACT_TANH: return tanh_f(x);
     case ACT_RELU: return fmaxf(x, 0.f);
-    case ACT_SOFTPLUS: return softplus(x);
+    // hardware exp/log with a Kahan log1p (~10 VALU, fp32-grade; the libm form cost the CNF walk's
+    // 128-wide layer GEMMs ~55 VALU per element in the epilogue).  Softplus only appears in the
+    // CNF vector field, whose fused kernel uses the same forms (cnf.hip act_jvp).
+    case ACT_SOFTPLUS: return softplus<true>(x);
     case ACT_SIGMOID: return 1.f / (1.f + expf(-x));
     default: return x;
   }
@@ -104,7 +114,7 @@ NAZ_DEV float activate_grad_from_out(int act, float y) {
   switch (act) {
     case ACT_TANH: return 1.f - y * y;
     case ACT_RELU: return y > 0.f ? 1.f : 0.f;
-    case ACT_SOFTPLUS: return -expm1f(-y);  // sigmoid(pre) = 1 - exp(-softplus(pre))
+    case ACT_SOFTPLUS: return -Math<true>::expm1(-y);  // sigmoid(pre) = 1 - exp(-softplus(pre))
     case ACT_SIGMOID: return y * (1.f - y);
     default: return 1.f;
   }

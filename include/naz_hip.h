@@ -298,15 +298,17 @@ int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const fl
                              float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
                              int* nfe, int64_t B, void* stream);
 /* CNF training (§8f rank 3; replaces the autograd graph torchdyn's adjoint builds through naz's
- * hutch_trace, continuous_transforms.py:75-89): the VJP of one vector-field activation under the
- * Hutchinson JVP, on stacked rows.  The forward maps [h_in; dh_in] to S = [h; dh] =
- * [act(W h_in + b); act'(W h_in + b) (W dh_in)] (naz_linear_act with its activation epilogue +
- * naz_gemm_dact).  S [2B, N] (lds); G [2B, N] (ldg) = adjoints of S; GP [2B, N] (ldgp) = adjoints
- * of the pre-activations [W h_in + b; W dh_in], with act', act''/act' recovered from h:
- *   GP[m] = G[m] act' + G[B + m] (act''/act') dh[m],   GP[B + m] = G[B + m] act';
- * g_bias [N] (nullable) += sum_m GP[m]. */
-int naz_act_jvp_bwd(const float* S, int64_t lds, const float* G, int64_t ldg, float* GP, int64_t ldgp,
-                    float* g_bias, int64_t B, int N, int act, void* stream);
+ * hutch_trace, continuous_transforms.py:75-89): the input-adjoint GEMM of one vector-field layer
+ * under the Hutchinson JVP, with the VJP of the layer's activation fused into its epilogue.  The
+ * forward maps (h_in, dh_in) to (h, dh) = (act(W h_in + b), act'(W h_in + b) (W dh_in))
+ * (naz_linear_act with its activation epilogue + naz_gemm_dact), kept as row PAIRS: S [M = 2B, N]
+ * (lds) with row 2i = h and 2i + 1 = dh of batch row i.  A [M, K] (lda) = the adjoints of the next
+ * layer's pre-activations in the same pairing, W [K, N] (ldw), G = A · W, and
+ *   C[2i] = G[2i] act' + G[2i+1] (act''/act') dh_i,   C[2i+1] = G[2i+1] act'
+ * with act', act''/act' recovered from h_i (softplus: 1 - e^-h, e^-h; tanh: 1 - h², -2h) — the
+ * adjoints of this layer's pre-activations.  M even; C rows 16-byte aligned (ldc % 4 == 0). */
+int naz_gemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
+                     const float* S, int64_t lds, int act, int64_t M, int N, void* stream);
 
 /* ---- §8b naz_spline_ar_inv / naz_affine_ar_inv: fused log_prob of a whole naz "nsa" or "maf" flow
  * Replaces the D-pass loop of pyro ConditionedSplineAutoregressive._inverse (naz

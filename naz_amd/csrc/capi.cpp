@@ -217,12 +217,15 @@ int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const fl
                               ld_mode, nfe, B, as_stream(stream));
 }
 
-int naz_act_jvp_bwd(const float* S, int64_t lds, const float* G, int64_t ldg, float* GP, int64_t ldgp, float* g_bias,
-                    int64_t B, int N, int act, void* stream) {
-  if (B < 0 || N < 0) return set_error("naz_act_jvp_bwd: negative size");
-  if (act < 0 || act > NAZ_ACT_SIGMOID) return set_error("naz_act_jvp_bwd: unknown activation %d", act);
-  if (B > 0 && N > 0 && (S == nullptr || G == nullptr || GP == nullptr)) return set_error("naz_act_jvp_bwd: null pointer");
-  return act_jvp_bwd(S, lds, G, ldg, GP, ldgp, g_bias, B, N, act, as_stream(stream));
+int naz_gemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
+                     const float* S, int64_t lds, int act, int64_t M, int N, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return set_error("naz_gemm_jvp_bwd: negative shape");
+  if (M == 0 || N == 0) return 0;
+  if (A == nullptr || W == nullptr || C == nullptr || S == nullptr) return set_error("naz_gemm_jvp_bwd: null pointer");
+  if (act < 0 || act > NAZ_ACT_SIGMOID) return set_error("naz_gemm_jvp_bwd: unknown activation %d", act);
+  const int rc = rowgemm_jvp_bwd(A, lda, K, W, ldw, C, ldc, S, lds, act, M, N, as_stream(stream));
+  if (rc == 1) return set_error("naz_gemm_jvp_bwd: weights too large for the batch-row kernel");
+  return rc;
 }
 
 int naz_coupling_supported(const naz_coupling_desc* d) { return coupling_supported(d); }

@@ -907,96 +907,6 @@ int cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int
   });
 }
 
-// ---- the CNF backward walk (§8f rank 3: FFJORD training; flows/cnf_adjoint.py) -----------------
-// A vector-field layer under the Hutchinson JVP maps [h; dh] to [act(W h + b); act'(W h + b) ⊙ (W dh)]
-// (forward: naz_linear_act with the activation epilogue and naz_gemm_dact).  Its VJP needs act'
-// and, because the tangent reads pre through act', act'' — both recovered from the stored
-// post-activation value h (act''·dpre = (act''/act')·dh), so the walk keeps only [h; dh]:
-//   GP[m] = G[m] act'(pre) + G[B + m] (act''/act')(pre) dh,   GP[B + m] = G[B + m] act'(pre).
-
-// act'(pre) and act''(pre) / act'(pre) from h = act(pre) (torch's forms: softplus with beta = 1,
-// threshold 20 — above it the identity, act' = 1 - e^-h -> 1 and act''/act' = e^-h -> 0 in fp32)
-NAZ_DEV void act_d1_ratio(int act, float h, float& d1, float& r) {
-  switch (act) {
-    case ACT_SOFTPLUS: d1 = -Math<true>::expm1(-h), r = 1.f - d1; break;  // sigmoid(pre), 1 - sigmoid(pre)
-    case ACT_TANH: d1 = 1.f - h * h, r = -2.f * h; break;
-    case ACT_RELU: d1 = h > 0.f ? 1.f : 0.f, r = 0.f; break;
-    case ACT_SIGMOID: d1 = h * (1.f - h), r = 1.f - 2.f * h; break;
-    default: d1 = 1.f, r = 0.f;
-  }
-}
-
-// 32 column groups of V adjacent columns x 8 row lanes per block (V = 4: 16-byte accesses, a wave
-// covers two 512-byte row pieces); each block walks `rpb` rows and adds its share of the bias
-// gradient (the value rows' column sums) with one atomic per column.
-template <int V>
-__global__ void act_jvp_bwd_kernel(const float* __restrict__ S, int64_t lds, const float* __restrict__ G, int64_t ldg,
-                                   float* __restrict__ GP, int64_t ldgp, float* __restrict__ g_bias, int64_t B, int N,
-                                   int act, int64_t rpb) {
-  __shared__ float red[8][32 * V];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int n0 = (blockIdx.x * 32 + tx) * V;
-  const int64_t m0 = (int64_t)blockIdx.y * rpb;
-  const int64_t m1 = m0 + rpb < B ? m0 + rpb : B;
-  float acc[V];
-#pragma unroll
-  for (int j = 0; j < V; ++j) acc[j] = 0.f;
-  if (n0 < N) {
-#pragma unroll 4
-    for (int64_t m = m0 + ty; m < m1; m += 8) {  // (unrolled: 16 loads in flight per thread)
-      float h[V], dh[V], gv[V], gt[V];
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        h[j] = S[m * lds + n0 + j], dh[j] = S[(B + m) * lds + n0 + j];
-        gv[j] = G[m * ldg + n0 + j], gt[j] = G[(B + m) * ldg + n0 + j];
-      }
-      float pv[V], pt[V];
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float d1, r;
-        act_d1_ratio(act, h[j], d1, r);
-        pv[j] = gv[j] * d1 + gt[j] * dh[j] * r;
-        pt[j] = gt[j] * d1;
-        acc[j] += pv[j];
-      }
-#pragma unroll
-      for (int j = 0; j < V; ++j) GP[m * ldgp + n0 + j] = pv[j], GP[(B + m) * ldgp + n0 + j] = pt[j];
-    }
-  }
-  if (g_bias == nullptr) return;
-#pragma unroll
-  for (int j = 0; j < V; ++j) red[ty][tx * V + j] = acc[j];
-  __syncthreads();
-  if (ty == 0 && n0 < N) {
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) t += red[r][tx * V + j];
-      atomicAdd(g_bias + n0 + j, t);
-    }
-  }
-}
-
-int act_jvp_bwd(const float* S, int64_t lds, const float* G, int64_t ldg, float* GP, int64_t ldgp, float* g_bias,
-                int64_t B, int N, int act, hipStream_t s) {
-  if (B <= 0 || N <= 0) return 0;
-  const bool vec = N % 4 == 0 && lds % 4 == 0 && ldg % 4 == 0 && ldgp % 4 == 0 &&
-                   ((reinterpret_cast<uintptr_t>(S) | reinterpret_cast<uintptr_t>(G) |
-                     reinterpret_cast<uintptr_t>(GP)) & 15) == 0;
-  const int cols = vec ? 128 : 32;
-  // rows per block: 256 (1024 blocks at 2^18 rows); 64 measured 2x slower (4x the bias atomics on
-  // the same N addresses); grown so grid.y stays within 65535
-  int64_t rpb = 256;
-  if ((B + rpb - 1) / rpb > 65535) rpb = (B + 65534) / 65535;
-  const dim3 grid((unsigned)((N + cols - 1) / cols), (unsigned)((B + rpb - 1) / rpb));
-  if (vec)
-    hipLaunchKernelGGL(act_jvp_bwd_kernel<4>, grid, dim3(256), 0, s, S, lds, G, ldg, GP, ldgp, g_bias, B, N, act, rpb);
-  else
-    hipLaunchKernelGGL(act_jvp_bwd_kernel<1>, grid, dim3(256), 0, s, S, lds, G, ldg, GP, ldgp, g_bias, B, N, act, rpb);
-  return check_launch("act_jvp_bwd_kernel");
-}
-
 int cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
                          int64_t ldc, const float* eps, int64_t lde, float t0, float t1, float atol, float rtol,
                          int max_steps, float* y, int64_t ldy, float* ld, int ld_mode, int* nfe, int64_t B,

@@ -89,8 +89,10 @@ __global__ void colsum_kernel(const float* __restrict__ A, int64_t lda, int64_t 
   const int64_t m0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t m1 = (m0 + rows_per_block) < M ? (m0 + rows_per_block) : M;
   float s = 0.f;
-  if (n < N)
-    for (int64_t m = m0 + ty; m < m1; m += lanes) s += A[m * lda + n];
+  if (n < N) {
+#pragma unroll 8
+    for (int64_t m = m0 + ty; m < m1; m += lanes) s += A[m * lda + n];  // (unrolled: 8 loads in flight)
+  }
   red[threadIdx.x] = s;
   __syncthreads();
   if (ty == 0 && n < N) {
@@ -140,8 +142,10 @@ int colsum(const float* A, int64_t lda, int64_t M, int N, float* out, hipStream_
   if (M <= 0 || N <= 0) return 0;
   int cw = 1;
   while (cw < N && cw < 64) cw *= 2;
-  int64_t rpb = 1024;  // rows per block, grown so grid.x stays within 65535 * 16
-  if ((M + rpb - 1) / rpb > 65535 * 16) rpb = (M + 65535 * 16 - 1) / (65535 * 16);
+  // rows per block: about 1024 blocks over the rows (enough to fill the chip; more would pile
+  // atomics onto the same N addresses), at least 64
+  int64_t rpb = (M + 1023) / 1024;
+  rpb = rpb < 64 ? 64 : (rpb + 63) / 64 * 64;
   dim3 grid((unsigned)((M + rpb - 1) / rpb), (unsigned)((N + cw - 1) / cw));
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, A, lda, M, N, out, rpb, cw);
   return check_launch("colsum_kernel");

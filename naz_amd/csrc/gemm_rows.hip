@@ -69,6 +69,13 @@ struct RowGemmArgs {
   int64_t lddy;
   int dact;
   int dyvec;  // dy rows allow 16-byte loads (set by rowgemm())
+  // optional VJP epilogue of a CNF vector-field layer under the Hutchinson JVP (naz_gemm_jvp_bwd):
+  // rows come in (value, tangent) pairs 2i, 2i + 1 and jvp = the layer's stacked output S with the
+  // same pairing; C[2i] = G[2i] act' + G[2i+1] (act''/act') S[2i+1], C[2i+1] = G[2i+1] act',
+  // act', act''/act' from h = S[2i] (act_d1_ratio).  null = none
+  const float* jvp;
+  int64_t ldjvp;
+  int jact;
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -204,6 +211,28 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
       constexpr int F4R = 8 * EG, RPI = 64 / F4R;
       const int rr = lane / F4R, c4 = lane % F4R;
       const int col = n0 + 32 * o0 + 4 * c4;
+      if (p.jvp != nullptr) {  // naz_gemm_jvp_bwd: RPI (value, tangent) row pairs per wave-instruction
+#pragma unroll
+        for (int it = 0; it < 16 / RPI; ++it) {
+          const int pr = it * RPI + rr;
+          const int64_t m = m0 + wave * 32 + 2 * pr;  // value row; m + 1 = its tangent row (M is even)
+          if (m >= p.M || col >= p.N) continue;
+          const float* ev = E + (2 * pr) * EP + 4 * c4;
+          const float* sv = p.jvp + m * p.ldjvp + col;
+          float* cv = p.c + m * p.ldc + col;
+          const int nt = p.N - col < 4 ? p.N - col : 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (j >= nt) continue;
+            float d1, rat;
+            act_d1_ratio(p.jact, sv[j], d1, rat);
+            const float gv = ev[j], gt = ev[EP + j];
+            cv[j] = gv * d1 + gt * sv[p.ldjvp + j] * rat;
+            cv[p.ldc + j] = gt * d1;
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int it = 0; it < 32 / RPI; ++it) {
         const int row = it * RPI + rr;
@@ -883,6 +912,30 @@ int rowgemm_dact(const float* A, int64_t lda, int K, const float* W, int64_t ldw
   p.dy = dy;
   p.lddy = lddy;
   p.dact = dact;
+  return rowgemm(p, s);
+}
+
+// naz_gemm_jvp_bwd: C = (A · W) through the VJP epilogue of the CNF layer activation (see jvp above)
+int rowgemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
+                    const float* S, int64_t lds, int act, int64_t M, int N, hipStream_t s) {
+  if (M % 2 != 0) return set_error("naz_gemm_jvp_bwd: M must pair value and tangent rows (even)");
+  if (ldc % 4 != 0 || (reinterpret_cast<uintptr_t>(C) & 15) != 0)
+    return set_error("naz_gemm_jvp_bwd: C needs 16-byte aligned rows (ldc %% 4 == 0)");
+  RowGemmArgs p{};
+  p.a1 = A;
+  p.lda1 = lda;
+  p.ka1 = K;
+  p.b = W;  // B(k, n) = W[k, n]
+  p.sbk = ldw;
+  p.sbn = 1;
+  p.c = C;
+  p.ldc = ldc;
+  p.M = M;
+  p.N = N;
+  p.act = NAZ_ACT_IDENTITY;
+  p.jvp = S;
+  p.ldjvp = lds;
+  p.jact = act;
   return rowgemm(p, s);
 }
 

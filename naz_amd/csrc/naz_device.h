@@ -120,6 +120,18 @@ NAZ_DEV float activate_grad_from_out(int act, float y) {
   }
 }
 
+// act'(pre) and act''(pre) / act'(pre) from h = act(pre) (torch's forms: softplus with beta = 1,
+// threshold 20 — above it the identity, act' = 1 - e^-h -> 1 and act''/act' = e^-h -> 0 in fp32)
+NAZ_DEV void act_d1_ratio(int act, float h, float& d1, float& r) {
+  switch (act) {
+    case ACT_SOFTPLUS: d1 = -Math<true>::expm1(-h), r = 1.f - d1; break;  // sigmoid(pre), 1 - sigmoid(pre)
+    case ACT_TANH: d1 = 1.f - h * h, r = -2.f * h; break;
+    case ACT_RELU: d1 = h > 0.f ? 1.f : 0.f, r = 0.f; break;
+    case ACT_SIGMOID: d1 = h * (1.f - h), r = 1.f - 2.f * h; break;
+    default: d1 = 1.f, r = 0.f;
+  }
+}
+
 // Normalised spline tables for one dimension: K+1 knots in x and y, K+1 knot slopes.
 template <int K>
 struct SplineTables {

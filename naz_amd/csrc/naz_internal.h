@@ -100,7 +100,7 @@ int cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const float*
                          int64_t ldc, const float* eps, int64_t lde, float t0, float t1, float atol, float rtol,
                          int max_steps, float* y, int64_t ldy, float* ld, int ld_mode, int* nfe, int64_t B,
                          hipStream_t s);
-int act_jvp_bwd(const float* S, int64_t lds, const float* G, int64_t ldg, float* GP, int64_t ldgp, float* g_bias,
-                int64_t B, int N, int act, hipStream_t s);
+int rowgemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
+                    const float* S, int64_t lds, int act, int64_t M, int N, hipStream_t s);
 
 }  // namespace naz

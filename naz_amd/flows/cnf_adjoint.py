@@ -23,10 +23,11 @@ augmented solve d[x, a]/dt = [f(x, ctx), -eps^T (df/dx) eps] (hutch_trace, :85-8
 
 Every RHS evaluation and VJP is HIP (``CnfWalk``): per hidden layer the value GEMM with its
 bias + activation epilogue (``naz_linear_act``) and the tangent GEMM with the act' epilogue
-(``naz_gemm_dact``), kept as stacked rows [h; dh] (2B rows); the VJP is ``naz_act_jvp_bwd`` (value
-rows need act'' because the tangent reads pre through act'; both derivatives come from h) and
-``naz_gemm`` for dX and the 2B-row dW reductions.  Torch only forms the [B, D]-sized RK4
-combinations.
+(``naz_gemm_dact``), kept as (value, tangent) row pairs (2B rows); the VJP is the input-adjoint
+GEMM with the activation's VJP in its epilogue (``naz_gemm_jvp_bwd``: value rows need act''
+because the tangent reads pre through act'; both derivatives come from h), ``naz_gemm`` for the
+2B-row dW reductions and ``naz_colsum`` for the bias gradients.  Torch only forms the [B, D]-sized
+RK4 combinations.
 """
 from __future__ import annotations
 
@@ -38,8 +39,9 @@ from torch.autograd import Function
 from .. import ops
 
 
-def _stacked(B: int, N: int, like: torch.Tensor) -> torch.Tensor:
-    """[2B, N] value/tangent rows, rows padded to 16 bytes (the batch-row kernels' fast path)."""
+def _pairs(B: int, N: int, like: torch.Tensor) -> torch.Tensor:
+    """[B, 2 Np] storage of (value, tangent) row pairs, Np = N padded to 16 bytes, returned as its
+    [2B, N] view: row 2i = value of batch row i, row 2i + 1 = its tangent."""
     npad = (N + 3) // 4 * 4
     t = torch.empty((2 * B, npad), device=like.device, dtype=like.dtype)
     return t[:, :N] if npad != N else t
@@ -49,9 +51,11 @@ class CnfWalk:
     """The FFJORD vector field (ConditionalFCNN, naz continuous_transforms.py:38-60, input
     cat([x, ctx]), x first) with its Hutchinson JVP, evaluated layer by layer on HIP kernels.
 
-    Hidden layer i keeps S_i = [h_i; dh_i] (2B rows): h_i = act(W_i h + b_i) by naz_linear_act
-    (activation epilogue), dh_i = act'(pre) ⊙ (W_i dh) by naz_gemm_dact (act' from h_i in the
-    epilogue).  The VJP needs nothing else: act' and act''/act' are functions of h_i."""
+    Hidden layer i keeps S_i as (value, tangent) row pairs [2B, H] (row 2r = h_i, 2r + 1 = dh_i of
+    batch row r): h_i = act(W_i h + b_i) by naz_linear_act (activation epilogue) written to the
+    even rows, dh_i = act'(pre) ⊙ (W_i dh) by naz_gemm_dact (act' from h_i in the epilogue) to the
+    odd rows.  The VJP needs nothing else: act' and act''/act' are functions of h_i, applied in the
+    input-adjoint GEMM's epilogue (naz_gemm_jvp_bwd)."""
 
     def __init__(self, net):
         lins = net.linears()
@@ -70,13 +74,14 @@ class CnfWalk:
         saved = [z]
         h, dh = None, eps
         for i in range(n - 1):
-            S = _stacked(B, self.W[i].shape[0], z)
+            S = _pairs(B, self.W[i].shape[0], z)
+            hv, tv = S[0::2], S[1::2]  # [B, H] views at row stride 2 Np
             if i == 0:
-                ops.linear_act(z, self.W0_cx, self.b[0], self.act, context=ctx if self.C else None, out=S[:B])
+                ops.linear_act(z, self.W0_cx, self.b[0], self.act, context=ctx if self.C else None, out=hv)
             else:
-                ops.linear_act(h, self.W[i], self.b[i], self.act, out=S[:B])
-            ops.gemm_dact(dh, self.WT[i], S[:B], self.act, out=S[B:])
-            h, dh = S[:B], S[B:]
+                ops.linear_act(h, self.W[i], self.b[i], self.act, out=hv)
+            ops.gemm_dact(dh, self.WT[i], hv, self.act, out=tv)
+            h, dh = hv, tv
             saved.append(S)
         k = ops.linear_act(h, self.W[-1], self.b[-1])
         jv = ops.gemm(dh, self.WT[-1])
@@ -89,32 +94,33 @@ class CnfWalk:
         accumulates the weight / bias gradients into gW / gb and the context's into g_ctx."""
         B, D, C, n = g_k.shape[0], self.D, self.C, len(self.W)
         z = saved[0]
-        G = torch.empty((2 * B, D), device=g_k.device, dtype=g_k.dtype)
-        G[:B] = g_k
-        G[B:] = -g_t[:, None] * eps
+        G = _pairs(B, D, g_k)  # output adjoints in row pairs: (g_f, g_(J eps)) = (g_k, -g_t eps)
+        G[0::2] = g_k
+        G[1::2] = -g_t[:, None] * eps
         ops.gemm(G.t(), saved[-1], out=gW[-1], accumulate=True)
         ops.colsum(g_k, out=gb[-1])
-        GS = ops.gemm(G, self.W[-1])
+        W_next = self.W[-1]
         for i in reversed(range(n - 1)):
-            GP = ops.act_jvp_bwd(saved[i + 1], GS, self.act, g_bias=gb[i])
+            GP = ops.gemm_jvp_bwd(G, W_next, saved[i + 1], self.act)  # pre-activation adjoints, pairs
+            ops.colsum(GP[0::2], out=gb[i])
             if i > 0:
                 ops.gemm(GP.t(), saved[i], out=gW[i], accumulate=True)
-                GS = ops.gemm(GP, self.W[i])
+                G, W_next = GP, self.W[i]
                 continue
-            S0 = torch.zeros((2 * B, D + C), device=z.device, dtype=z.dtype)  # [[z, ctx]; [eps, 0]]
-            S0[:B, :D] = z
-            S0[B:, :D] = eps
+            S0 = torch.zeros((2 * B, D + C), device=z.device, dtype=z.dtype)  # pairs ([z, ctx], [eps, 0])
+            S0[0::2, :D] = z
+            S0[1::2, :D] = eps
             if C:
-                S0[:B, D:] = ctx.reshape(-1, C).expand(B, C) if ctx.numel() == C else ctx
+                S0[0::2, D:] = ctx.reshape(-1, C).expand(B, C) if ctx.numel() == C else ctx
             ops.gemm(GP.t(), S0, out=gW[0], accumulate=True)
-            GP = GP[:B]  # the tangent rows' input is eps (no gradient)
-            g_z = ops.gemm(GP, self.W[0][:, :D])
+            GPv = GP[0::2]  # the tangent rows' input is eps (no gradient)
+            g_z = ops.gemm(GPv, self.W[0][:, :D])
             if C and g_ctx is not None:
                 Wc = self.W[0][:, D:]
                 if g_ctx.shape[0] == B and g_ctx.dim() == 2:
-                    ops.gemm(GP, Wc, out=g_ctx, accumulate=True)
+                    ops.gemm(GPv, Wc, out=g_ctx, accumulate=True)
                 else:
-                    ops.gemm(ops.colsum(GP).reshape(1, -1), Wc, out=g_ctx.view(1, C), accumulate=True)
+                    ops.gemm(ops.colsum(GPv).reshape(1, -1), Wc, out=g_ctx.view(1, C), accumulate=True)
         return g_z
 
 

@@ -21,7 +21,7 @@ Tensor = torch.Tensor
 __all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "made_affine_inv1", "gemm_dact", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
-           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5", "act_jvp_bwd",
+           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5", "gemm_jvp_bwd",
            "LAYOUT_ARN", "LAYOUT_DENSE", "LD_PERDIM", "LD_ROWSUM", "LD_ROWSUM_ADD",
            "LD_ROWSUM_SUB"]
 
@@ -445,23 +445,26 @@ def act_bwd(g_y: Tensor, y: Tensor, act: str) -> Tensor:
     return gp
 
 
-def act_jvp_bwd(S: Tensor, G: Tensor, act: str, g_bias: Optional[Tensor] = None) -> Tensor:
-    """VJP of a CNF vector-field activation under the Hutchinson JVP (naz_act_jvp_bwd): S = [h; dh]
-    [2B, N] (post-activation values and tangents), G [2B, N] their adjoints -> the adjoints of
-    the pre-activations [W h + b; W dh]; ``g_bias`` [N] += the value rows' column sums."""
-    dev = _dev(S, G, g_bias)
+def gemm_jvp_bwd(a: Tensor, weight: Tensor, S: Tensor, act: str, out: Optional[Tensor] = None) -> Tensor:
+    """Input adjoints of a CNF vector-field layer under the Hutchinson JVP (naz_gemm_jvp_bwd): rows in
+    (value, tangent) pairs 2i, 2i + 1.  a [2B, K] = the next layer's pre-activation adjoints,
+    weight [K, N] (unit column stride), S [2B, N] = this layer's (h, dh) pairs -> the adjoints of
+    this layer's pre-activations (a @ weight through the activation's VJP), [2B, N]."""
+    dev = _dev(a, weight, S, out)
+    a, lda = _rows(a)
     S, lds = _rows(S)
-    G, ldg = _rows(G)
-    M, N = S.shape
-    if M % 2 or G.shape != (M, N):
-        raise ValueError("act_jvp_bwd: S and G must both be [2B, N]")
-    if g_bias is not None and (g_bias.shape != (N,) or not g_bias.is_contiguous()):
-        raise ValueError(f"act_jvp_bwd: g_bias must be a contiguous [{N}] tensor")
-    npad = (N + 3) // 4 * 4
-    GP = torch.empty((M, npad), device=dev, dtype=torch.float32)[:, :N]
-    check(lib().naz_act_jvp_bwd(_p(S), lds, _p(G), ldg, _p(GP), GP.stride(0), _p(g_bias), M // 2, N, ACT[act],
-                                _stream(dev)), "act_jvp_bwd")
-    return GP
+    M, K = a.shape
+    if weight.shape[0] != K or weight.stride(1) != 1:
+        raise ValueError("gemm_jvp_bwd: weight must be [K, N] with unit column stride")
+    N = weight.shape[1]
+    if M % 2 or S.shape != (M, N):
+        raise ValueError(f"gemm_jvp_bwd: S must be [{M}, {N}] with M even (value/tangent row pairs)")
+    if out is None:
+        npad = (N + 3) // 4 * 4
+        out = torch.empty((M, npad), device=dev, dtype=torch.float32)[:, :N]
+    check(lib().naz_gemm_jvp_bwd(_p(a), lda, K, _p(weight), weight.stride(0), _p(out), out.stride(0), _p(S), lds,
+                                 ACT[act], M, N, _stream(dev)), "gemm_jvp_bwd")
+    return out
 
 
 def dropout(x: Tensor, p: float, seed: int, out: Optional[Tensor] = None) -> Tensor:

@@ -1,7 +1,7 @@
 """CPU: the host logic of the CNF backward (naz_amd/flows/cnf_adjoint.py) — the stacked
 value/tangent walk, the discrete RK4 adjoint recursion and the continuous adjoint — with every HIP
 launch replaced by a float64 torch statement of the kernel's documented semantics
-(include/naz_hip.h: naz_linear_act, naz_gemm_dact, naz_act_jvp_bwd, naz_gemm, naz_colsum).  Checked
+(include/naz_hip.h: naz_linear_act, naz_gemm_dact, naz_gemm_jvp_bwd, naz_gemm, naz_colsum).  Checked
 against the oracle's float64 autograd through the same RK4 solve (oracle hutchinson_rhs with
 create_graph).  The kernels themselves are covered on the GPU by tests/test_gpu_cnf_grad.py."""
 import types
@@ -38,13 +38,13 @@ def _fake_ops():
     def gemm_dact(a, W, y, act, mask=None, out=None):
         return _put(out, (a @ W) * _d1_ratio(act, y)[0])
 
-    def act_jvp_bwd(S, G, act, g_bias=None):
-        B = S.shape[0] // 2
-        d1, r = _d1_ratio(act, S[:B])
-        gp = G[:B] * d1 + G[B:] * S[B:] * r
-        if g_bias is not None:
-            g_bias += gp.sum(0)
-        return torch.cat([gp, G[B:] * d1])
+    def gemm_jvp_bwd(a, W, S, act, out=None):
+        G = a @ W
+        d1, r = _d1_ratio(act, S[0::2])
+        C = torch.empty_like(G)
+        C[0::2] = G[0::2] * d1 + G[1::2] * S[1::2] * r
+        C[1::2] = G[1::2] * d1
+        return _put(out, C)
 
     def gemm(a, b, out=None, accumulate=False, **kw):
         r = a @ b
@@ -62,7 +62,7 @@ def _fake_ops():
         out += a.sum(0)
         return out
 
-    return types.SimpleNamespace(linear_act=linear_act, gemm_dact=gemm_dact, act_jvp_bwd=act_jvp_bwd, gemm=gemm,
+    return types.SimpleNamespace(linear_act=linear_act, gemm_dact=gemm_dact, gemm_jvp_bwd=gemm_jvp_bwd, gemm=gemm,
                                  colsum=colsum)
 
 

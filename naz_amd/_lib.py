@@ -36,6 +36,12 @@ class CnfDesc(C.Structure):
                 ("mfma_mode", C.c_int), ("reserved", C.c_int * 7)]
 
 
+class FlowDesc(C.Structure):
+    _fields_ = [("kind", C.c_int), ("coupling", CouplingDesc), ("ar", ArDesc), ("reserved", C.c_int * 8)]
+
+
+FLOW_COUPLING, FLOW_AR = 1, 2
+
 # name -> (restype, argtypes); every symbol declared in include/naz_hip.h
 SIGNATURES = {
     "naz_last_error": (C.c_char_p, []),
@@ -87,6 +93,11 @@ SIGNATURES = {
     "naz_ar_flow_degrees": (C.c_int, [C.POINTER(ArDesc), _vp]),
     "naz_ar_flow_pack_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _vp]),
     "naz_ar_flow_log_prob": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
+    "naz_flow_packed_bytes": (C.c_int64, [C.POINTER(FlowDesc)]),
+    "naz_workspace_bytes": (C.c_int64, [C.POINTER(FlowDesc), _i64]),
+    "naz_flow_log_prob": (C.c_int, [C.POINTER(FlowDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
+    "naz_flow_sample": (C.c_int, [C.POINTER(FlowDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64,
+                                  _vp]),
     "naz_coupling_supported": (C.c_int, [C.POINTER(CouplingDesc)]),
     "naz_coupling_param_count": (C.c_int64, [C.POINTER(CouplingDesc)]),
     "naz_coupling_packed_bytes": (C.c_int64, [C.POINTER(CouplingDesc)]),

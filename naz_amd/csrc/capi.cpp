@@ -290,4 +290,38 @@ int naz_ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* 
   return ar_flow_log_prob(d, packed, x, ldx, ctx, ldc, low, high, out_lp, B, as_stream(stream));
 }
 
+// ---- §8b whole-flow entries over the fused kinds ----------------------------------------
+int64_t naz_flow_packed_bytes(const naz_flow_desc* d) {
+  if (d == nullptr) return -1;
+  if (d->kind == NAZ_FLOW_COUPLING) return coupling_packed_bytes(&d->coupling);
+  if (d->kind == NAZ_FLOW_AR) return ar_flow_packed_bytes(&d->ar);
+  return -1;
+}
+
+int64_t naz_workspace_bytes(const naz_flow_desc* d, int64_t B) {
+  (void)B;  // the fused kernels keep every intermediate on chip
+  return naz_flow_packed_bytes(d) < 0 ? -1 : 0;
+}
+
+int naz_flow_log_prob(const naz_flow_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                      int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream) {
+  if (d == nullptr) return set_error("naz_flow_log_prob: null descriptor");
+  if (d->kind == NAZ_FLOW_COUPLING)
+    return naz_coupling_log_prob(&d->coupling, packed, x, ldx, ctx, ldc, low, high, out_lp, B, stream);
+  if (d->kind == NAZ_FLOW_AR) return naz_ar_flow_log_prob(&d->ar, packed, x, ldx, ctx, ldc, low, high, out_lp, B, stream);
+  return set_error("naz_flow_log_prob: unknown flow kind %d", d->kind);
+}
+
+int naz_flow_sample(const naz_flow_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx,
+                    int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B,
+                    void* stream) {
+  if (d == nullptr) return set_error("naz_flow_sample: null descriptor");
+  if (d->kind == NAZ_FLOW_COUPLING)
+    return naz_coupling_sample(&d->coupling, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, stream);
+  if (d->kind == NAZ_FLOW_AR)
+    return set_error("naz_flow_sample: autoregressive flows sample layer by layer (naz_made_affine_fwd / "
+                     "naz_linear_act + naz_rqs_fwd), no fused whole-flow sampler");
+  return set_error("naz_flow_sample: unknown flow kind %d", d->kind);
+}
+
 }  // extern "C"

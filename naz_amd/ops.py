@@ -13,15 +13,15 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-from ._lib import (ACT, LAYOUT_ARN, LAYOUT_DENSE, RQS_FAST, LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD, LD_ROWSUM_SUB, ArDesc,
-                   CnfDesc, CouplingDesc, check, lib)
+from ._lib import (ACT, FLOW_AR, FLOW_COUPLING, LAYOUT_ARN, LAYOUT_DENSE, RQS_FAST, LD_PERDIM, LD_ROWSUM, LD_ROWSUM_ADD,
+                   LD_ROWSUM_SUB, ArDesc, CnfDesc, CouplingDesc, FlowDesc, check, lib)
 
 Tensor = torch.Tensor
 
 __all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "made_affine_inv1", "gemm_dact", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
-           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5", "gemm_jvp_bwd",
+           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5", "gemm_jvp_bwd", "flow_desc", "flow_log_prob", "flow_sample",
            "LAYOUT_ARN", "LAYOUT_DENSE", "LD_PERDIM", "LD_ROWSUM", "LD_ROWSUM_ADD",
            "LD_ROWSUM_SUB"]
 
@@ -599,6 +599,48 @@ def ar_flow_log_prob(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Ten
 
 
 # ----------------------------------------------------------------------------- a10: fused NLL step
+# ----------------------------------------------------------------------------- §8b whole-flow entries
+def flow_desc(part) -> FlowDesc:
+    """naz_flow_desc wrapping a coupling (nsc) or autoregressive (nsa / maf) descriptor."""
+    d = FlowDesc()
+    if isinstance(part, CouplingDesc):
+        d.kind, d.coupling = FLOW_COUPLING, part
+    elif isinstance(part, ArDesc):
+        d.kind, d.ar = FLOW_AR, part
+    else:
+        raise TypeError("flow_desc: a CouplingDesc or an ArDesc")
+    return d
+
+
+def flow_log_prob(d: FlowDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,
+                  low: Optional[Tensor] = None, high: Optional[Tensor] = None,
+                  out: Optional[Tensor] = None) -> Tensor:
+    """NormalizingFlow.log_prob of a fused-kind flow through the generic entry (naz_flow_log_prob)."""
+    dev = _dev(packed, x, context, low, high, out)
+    x, ldx = _rows(x)
+    B = x.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    if out is None:
+        out = torch.empty((B,), device=dev, dtype=torch.float32)
+    check(lib().naz_flow_log_prob(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out), B,
+                                  _stream(dev)), "flow_log_prob")
+    return out
+
+
+def flow_sample(d: FlowDesc, packed: Tensor, z: Tensor, context: Optional[Tensor] = None,
+                low: Optional[Tensor] = None, high: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """(y, sum log|det|) through the generic entry (naz_flow_sample; coupling flows)."""
+    dev = _dev(packed, z, context, low, high)
+    z, ldz = _rows(z)
+    B = z.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    y = torch.empty_like(z)
+    ld = torch.empty((B,), device=dev, dtype=torch.float32)
+    check(lib().naz_flow_sample(d, _p(packed), _p(z), ldz, _p(context), ldc, _p(low), _p(high), _p(y), y.stride(0),
+                                _p(ld), B, _stream(dev)), "flow_sample")
+    return y, ld
+
+
 def coupling_pack_bwd(d: CouplingDesc, flat: Tensor, out: Optional[Tensor] = None) -> Tensor:
     """Per-layer fp32 backward images (naz_coupling_pack_bwd) of the flat natural parameters."""
     n = int(lib().naz_coupling_bwd_packed_bytes(d))

@@ -64,3 +64,23 @@ def test_no_cpu_fallback():
     f = NormalizingFlow("nsc", None, 4, 3, [64, 64], 2, 8, 2)
     with pytest.raises(RuntimeError, match="GPU only"):
         f.log_prob(torch.zeros(3, 4), condition=torch.zeros(3, 3))
+
+
+def test_generic_flow_entries_dispatch_without_compute():
+    """naz_flow_*: packed sizes and workspace of both fused kinds (host-only calls), and the
+    documented errors (unknown kind, no fused whole-flow sampler for AR flows)."""
+    from naz_amd import _lib, ops
+    L = _lib.lib()
+    c = ops.coupling_desc(16, 32, 8, 8, 8, 128)
+    a = ops.ar_flow_desc("maf", 2, 2, 150, 16, n_hidden=3)
+    fc, fa = ops.flow_desc(c), ops.flow_desc(a)
+    assert L.naz_flow_packed_bytes(fc) == L.naz_coupling_packed_bytes(c) > 0
+    assert L.naz_flow_packed_bytes(fa) == L.naz_ar_flow_packed_bytes(a) > 0
+    assert L.naz_workspace_bytes(fc, 1 << 20) == 0 and L.naz_workspace_bytes(fa, 1 << 20) == 0
+    bad = _lib.FlowDesc()
+    bad.kind = 7
+    assert L.naz_flow_packed_bytes(bad) == -1
+    assert L.naz_flow_log_prob(bad, None, None, 0, None, 0, None, None, None, 0, None) != 0
+    assert b"unknown flow kind" in L.naz_last_error()
+    assert L.naz_flow_sample(fa, None, None, 0, None, 0, None, None, None, 0, None, 0, None) != 0
+    assert b"layer by layer" in L.naz_last_error()

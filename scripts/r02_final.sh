@@ -19,5 +19,6 @@ step bench 300 python bench.py
 step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_final -o run --output-format csv -- python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline
 step cnftrain 300 python bench.py --cnf-train --steps 5 --warmup 2
 step proftrain 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cnftrain -o run --output-format csv -- python3 bench.py --cnf-train --steps 3 --warmup 1 --no-cpu-baseline
-step nsa16 300 python bench.py --flow nsa16
+step nsa16 300 python bench.py --flow nsa16 --batch 1048576
+step maf 300 python bench.py --flow maf
 exit 0

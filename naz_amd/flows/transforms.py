@@ -393,7 +393,15 @@ class _ConditionedSplineAutoregressive(_LDCache, Transform):
         return self._map(x, False, ld, ops.LD_ROWSUM_ADD)
 
     def _inv_ld(self, y):
-        """Differentiable D-pass inverse; autograd runs back through every pass, as pyro's does."""
+        """Differentiable inverse.  Degree-scheduled (every MADE unit once, ARInversePlan.run_grad:
+        per pass the order-k dim's spline on its 3K-1 ARN rows, single-dim naz_rqs_inv + its VJP)
+        unless the conditioner's degree_schedule is off; then pyro's D full passes, autograd running
+        back through every pass as pyro's does."""
+        plan = self.arn.inverse_plan() if y.dim() == 2 else None
+        if plan is not None:
+            x, ld = plan.run_grad(y, self.context, lambda k, i, raw: ag.rqs(
+                y[:, i:i + 1], raw, self.count_bins, ops.LAYOUT_ARN, True, self.bound))
+            return x, -ld  # the steps' log-dets are the inverse's; the walk wants the forward's
         x = torch.zeros_like(y)
         ld = None
         for _ in range(y.shape[-1]):

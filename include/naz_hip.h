@@ -343,13 +343,24 @@ int naz_ar_flow_pack_host(const naz_ar_desc* d, const float* flat, const int* pe
 int naz_ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
                          int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream);
 
+/* The sampling direction of the same flows (pyro *Autoregressive._call, flow.py:94-129): one launch
+ * for all L layers in forward order, each layer ONE MADE pass over its input followed by every dim's
+ * map; y = T_L ∘ … ∘ T_1(z), out_ld (nullable) = Σ forward log-dets, low/high: inverse bounding of
+ * y.  Its own packed image (naz_ar_flow_fwd_packed_bytes; host pack from the same flat layout as
+ * naz_ar_flow_pack_host, no permutation: the masks carry the order).  |ctx| < 2^15. */
+int64_t naz_ar_flow_fwd_packed_bytes(const naz_ar_desc* d);
+int naz_ar_flow_pack_fwd_host(const naz_ar_desc* d, const float* flat, void* packed);
+int naz_ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx,
+                       int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld,
+                       int64_t B, void* stream);
+
 /* ---- §8b: whole-flow entries over the fused kinds -------------------------------------
  * One descriptor for the flows whose whole log_prob is one launch: the spline coupling flow (naz
  * "nsc": naz_coupling_*) and the autoregressive flows (naz "nsa" / "maf": naz_ar_flow_*).  The
  * packed image is the kind's own (naz_coupling_pack on the device, naz_ar_flow_pack_host on the
  * host); these entries only dispatch.  Replaces NormalizingFlow.log_prob / .sample
  * (naz/flows/flow.py:45-79, 94-129).  naz_workspace_bytes is 0: the fused kernels keep every
- * intermediate on chip.  naz_flow_sample: coupling flows only (AR flows sample layer by layer). */
+ * intermediate on chip.  naz_flow_sample of an AR flow takes its forward image (naz_ar_flow_pack_fwd_host). */
 #define NAZ_FLOW_COUPLING 1
 #define NAZ_FLOW_AR 2
 typedef struct naz_flow_desc {

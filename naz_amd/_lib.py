@@ -93,6 +93,10 @@ SIGNATURES = {
     "naz_ar_flow_degrees": (C.c_int, [C.POINTER(ArDesc), _vp]),
     "naz_ar_flow_pack_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _vp]),
     "naz_ar_flow_log_prob": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
+    "naz_ar_flow_fwd_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),
+    "naz_ar_flow_pack_fwd_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp]),
+    "naz_ar_flow_sample": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64,
+                                     _vp]),
     "naz_flow_packed_bytes": (C.c_int64, [C.POINTER(FlowDesc)]),
     "naz_workspace_bytes": (C.c_int64, [C.POINTER(FlowDesc), _i64]),
     "naz_flow_log_prob": (C.c_int, [C.POINTER(FlowDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),

@@ -290,6 +290,20 @@ int naz_ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* 
   return ar_flow_log_prob(d, packed, x, ldx, ctx, ldc, low, high, out_lp, B, as_stream(stream));
 }
 
+int64_t naz_ar_flow_fwd_packed_bytes(const naz_ar_desc* d) { return ar_flow_fwd_packed_bytes(d); }
+int naz_ar_flow_pack_fwd_host(const naz_ar_desc* d, const float* flat, void* packed) {
+  return ar_flow_pack_fwd_host(d, flat, packed);
+}
+int naz_ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx,
+                       int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld,
+                       int64_t B, void* stream) {
+  if (B < 0) return set_error("naz_ar_flow_sample: negative batch");
+  if (B > 0 && (packed == nullptr || z == nullptr || y == nullptr)) return set_error("naz_ar_flow_sample: null pointer");
+  if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
+    return set_error("naz_ar_flow_sample: conditional flow needs ctx");
+  return ar_flow_sample(d, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, as_stream(stream));
+}
+
 // ---- §8b whole-flow entries over the fused kinds ----------------------------------------
 int64_t naz_flow_packed_bytes(const naz_flow_desc* d) {
   if (d == nullptr) return -1;
@@ -318,9 +332,8 @@ int naz_flow_sample(const naz_flow_desc* d, const void* packed, const float* z, 
   if (d == nullptr) return set_error("naz_flow_sample: null descriptor");
   if (d->kind == NAZ_FLOW_COUPLING)
     return naz_coupling_sample(&d->coupling, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, stream);
-  if (d->kind == NAZ_FLOW_AR)
-    return set_error("naz_flow_sample: autoregressive flows sample layer by layer (naz_made_affine_fwd / "
-                     "naz_linear_act + naz_rqs_fwd), no fused whole-flow sampler");
+  if (d->kind == NAZ_FLOW_AR)  // packed = the forward image (naz_ar_flow_pack_fwd_host)
+    return naz_ar_flow_sample(&d->ar, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, stream);
   return set_error("naz_flow_sample: unknown flow kind %d", d->kind);
 }
 

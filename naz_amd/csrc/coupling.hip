@@ -1496,6 +1496,25 @@ struct AROps {
                        ldx, ctx, ldc, low, high, out_lp, B, bound);
     return check_launch("made_ar_r16_kernel");
   }
+  // forward (sample) direction: made_ar_fwd_kernel over CfgARF's per-layer image
+  using FW = CfgARF<CF>;
+  static int64_t fwd_layer_floats() { return FW::LAYER; }
+  static int pack_fwd_host(const float* flat, int L, float* out) {
+    constexpr int H = CF::H, D = CF::D, C = CF::C, P = CF::P;
+    constexpr int64_t per = (int64_t)H * (C + D) + H + (int64_t)(CF::NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
+    for (int l = 0; l < L; ++l) made_ar_pack_fwd_layer<FW>(flat + l * per, out + (int64_t)l * FW::LAYER);
+    return 0;
+  }
+  static int sample(const float* packed, int L, const float* z, int64_t ldz, const float* ctx, int64_t ldc,
+                    const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B, float bound,
+                    hipStream_t s) {
+    if (B == 0) return 0;
+    const int64_t rows = 16 * FW::NW, grid = (B + rows - 1) / rows;
+    const size_t lds = (size_t)2 * FW::STG * 4;
+    hipLaunchKernelGGL((made_ar_fwd_kernel<FW>), dim3((unsigned)grid), dim3(64 * FW::NW), lds, s, packed, L, z, ldz,
+                       ctx, ldc, low, high, y, ldy, out_ld, B, bound);
+    return check_launch("made_ar_fwd_kernel");
+  }
 };
 
 template <class F>
@@ -1548,6 +1567,33 @@ int ar_flow_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, 
   if (flat == nullptr || perm == nullptr || packed == nullptr) return set_error("naz_ar_flow_pack_host: null pointer");
   const int rc = ar_dispatch(d, [&](auto ops) {
     return decltype(ops)::pack_host(flat, perm, d->L, static_cast<float*>(packed));
+  });
+  return rc == -2 ? ar_unsupported(d) : rc;
+}
+
+int64_t ar_flow_fwd_packed_bytes(const naz_ar_desc* d) {
+  int64_t v = -1;
+  ar_dispatch(d, [&](auto ops) {
+    v = decltype(ops)::fwd_layer_floats() * d->L * 4;
+    return 0;
+  });
+  return v;
+}
+
+int ar_flow_pack_fwd_host(const naz_ar_desc* d, const float* flat, void* packed) {
+  if (flat == nullptr || packed == nullptr) return set_error("naz_ar_flow_pack_fwd_host: null pointer");
+  const int rc = ar_dispatch(d, [&](auto ops) {
+    return decltype(ops)::pack_fwd_host(flat, d->L, static_cast<float*>(packed));
+  });
+  return rc == -2 ? ar_unsupported(d) : rc;
+}
+
+int ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx, int64_t ldc,
+                   const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B, hipStream_t s) {
+  if ((low == nullptr) != (high == nullptr)) return set_error("naz_ar_flow_sample: low/high must both be set");
+  const int rc = ar_dispatch(d, [&](auto ops) {
+    return decltype(ops)::sample(static_cast<const float*>(packed), d->L, z, ldz, ctx, ldc, low, high, y, ldy, out_ld,
+                                 B, d->bound, s);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }

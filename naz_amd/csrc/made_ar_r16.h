@@ -398,4 +398,264 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
   if (q == 0 && valid) out_lp[row] = base - ldsum + logjac;
 }
 
+// ================================================================ forward (sample) direction
+// pyro ConditionedSplineAutoregressive._call / AffineAutoregressive._call (naz transforms.py:
+// 133-198), the sampling direction of TransformedDistribution.sample (flow.py:94-129): ONE MADE pass
+// per layer over the layer input, then every dim's map — y_d = spline(x_d) or x_d exp(ls_d) + m_d —
+// all of a layer's dims from the same hidden activations (no sequential dependence: the masks
+// already encode the order).  The whole flow is one launch: per layer, all hidden blocks (f16x3
+// MFMA, register-resident B fragments, the inverse kernel's machinery), then per dim its output
+// rows and the elementwise map.  Weights: per layer "units" — (hidden layer i, 16-unit block b)
+// with its k-steps and bias, then (dim d) with its output blocks — grouped greedily into LDS-ring
+// stages of <= kARCap floats.  Forward values can grow through the layers (affine scales up to
+// e^3 per layer), so the layer input is split into f16 pieces at a per-row power-of-two scale and
+// the x part of hidden layer 1 rescaled in fp32 (the context keeps the caller's |ctx| < 2^15).
+template <class G>
+struct CfgARF {
+  static constexpr int D = G::D, C = G::C, H = G::H, K = G::K, NHID = G::NHID, P = G::P;
+  static constexpr int HB = G::HB, KSH = G::KSH, KC = G::KC, KI = G::KI, NOB = G::NOB, OT = G::OT;
+  // the forward spline's live set at D = 16 exceeds the 168 VGPRs of 12-wave workgroups (spilled
+  // 352-468 B/lane): 8 waves (2 per SIMD) there
+  static constexpr int NW = (G::AFFINE || D <= 8) ? G::NW : 8;
+  static constexpr bool AFFINE = G::AFFINE;
+  static constexpr int NU = NHID * HB + D;  // units: hidden (i, b) row-major, then one per dim
+  static constexpr int unit_blocks(int u) { return u < NHID * HB ? 1 : NOB; }
+  static constexpr int unit_kts(int u) { return u < HB ? KI : KSH; }
+  static constexpr int unit_floats(int u) { return unit_blocks(u) * (unit_kts(u) * OT + 16); }
+  struct Layout {
+    int sid[NU], off[NU], sfl[NU];
+    int nstg, stg;
+  };
+  static constexpr Layout make_layout() {
+    Layout y{};
+    int s = -1, run = 0;
+    for (int u = 0; u < NU; ++u) {
+      const int sz = unit_floats(u);
+      if (u == 0 || run + sz > kARCap) {
+        ++s;
+        run = 0;
+      }
+      y.sid[u] = s;
+      y.off[u] = run;
+      run += sz;
+      y.sfl[s] = G::pad(run);
+    }
+    y.nstg = s + 1;
+    for (int t = 0; t < y.nstg; ++t) y.stg = y.sfl[t] > y.stg ? y.sfl[t] : y.stg;
+    return y;
+  }
+  static constexpr Layout LY = make_layout();
+  static constexpr int stage_id(int u) { return LY.sid[u]; }
+  static constexpr int unit_off(int u) { return LY.off[u]; }
+  static constexpr int stage_floats(int s) { return LY.sfl[s]; }
+  static constexpr int NSTG = LY.nstg, STG = LY.stg;
+  static constexpr int LAYER = G::pad(NSTG * STG);
+  static_assert(2 * STG * 4 <= 160 * 1024, "two forward weight stages exceed the LDS");
+};
+
+// host packer of one layer's forward image (flat as made_ar_pack_layer's, masks applied)
+template <class CF>
+static void made_ar_pack_fwd_layer(const float* flat, float* out) {
+  constexpr int D = CF::D, C = CF::C, H = CF::H, P = CF::P, HB = CF::HB, KSH = CF::KSH;
+  const float* Wl[CF::NHID + 1];
+  const float* bl[CF::NHID + 1];
+  {
+    const float* f = flat;
+    for (int i = 0; i <= CF::NHID; ++i) {
+      const int rows = i < CF::NHID ? H : D * P, cols = i == 0 ? C + D : H;
+      Wl[i] = f;
+      bl[i] = f + rows * cols;
+      f += rows * cols + rows;
+    }
+  }
+  unsigned* ou = reinterpret_cast<unsigned*>(out);
+  for (int i = 0; i < CF::LAYER; ++i) out[i] = 0.f;
+  auto frag = [&](unsigned* dst, auto&& wf) {  // as made_ar_pack_layer's
+    for (int piece = 0; piece < 2; ++piece)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int pair = 0; pair < 4; ++pair) {
+          unsigned w = 0;
+          for (int e = 0; e < 2; ++e) w |= ar_piece(wf(lane & 15, lane >> 4, 2 * pair + e), piece) << (16 * e);
+          dst[(piece * 64 + lane) * 4 + pair] = w;
+        }
+  };
+  for (int u = 0; u < CF::NU; ++u) {
+    const int base = CF::stage_id(u) * CF::STG + CF::unit_off(u);
+    unsigned* st = ou + base;
+    if (u < CF::NHID * HB) {
+      const int i = u / HB, b = u % HB, kts = CF::unit_kts(u);
+      for (int t = 0; t < kts; ++t)
+        frag(st + t * CF::OT, [&](int m, int kg, int j) -> float {
+          const int un = 16 * b + m;
+          if (un >= H) return 0.f;
+          if (i > 0) {
+            const int v = r16_feat(t, kg, j);
+            return v < H ? -2.f * kSigScale * Wl[i][un * H + v] : 0.f;
+          }
+          if (t < CF::KC) {
+            const int col = 32 * t + 8 * kg + j;
+            return col < C ? kSigScale * Wl[0][un * (C + D) + col] : 0.f;
+          }
+          const int d = 8 * kg + j;
+          return d < D ? kSigScale * Wl[0][un * (C + D) + C + d] : 0.f;
+        });
+      float* bias = out + base + kts * CF::OT;
+      for (int r = 0; r < 16; ++r) bias[r] = 16 * b + r < H ? kSigScale * bl[i][16 * b + r] : 0.f;
+    } else {
+      const int d = u - CF::NHID * HB;
+      for (int o = 0; o < CF::NOB; ++o)
+        for (int t = 0; t < KSH; ++t)
+          frag(st + (o * KSH + t) * CF::OT, [&](int m, int kg, int j) -> float {
+            const int pi = 16 * o + m, v = r16_feat(t, kg, j);
+            return (pi < P && v < H) ? -2.f * Wl[CF::NHID][(pi * D + d) * H + v] : 0.f;
+          });
+      float* bias = out + base + CF::NOB * KSH * CF::OT;
+      for (int r = 0; r < 16 * CF::NOB; ++r) bias[r] = r < P ? bl[CF::NHID][r * D + d] : 0.f;
+    }
+  }
+}
+
+template <class CF>
+__global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
+    const float* __restrict__ packed, int L, const float* __restrict__ z, int64_t ldz,
+    const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
+    float* __restrict__ y, int64_t ldy, float* __restrict__ out_ld, int64_t B, float bound) {
+  constexpr int D = CF::D, K = CF::K, P = CF::P, NW = CF::NW, NHID = CF::NHID, HB = CF::HB, KSH = CF::KSH;
+  extern __shared__ float4 lds4[];
+  float* const slot0 = reinterpret_cast<float*>(lds4);
+  float* const slot1 = slot0 + CF::STG;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int q = lane >> 4;
+  const int64_t row = (int64_t)blockIdx.x * (16 * NW) + wave * 16 + (lane & 15);
+  const bool valid = row < B;
+  const int64_t crow = valid ? row : 0;
+
+  float v[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) v[d] = valid ? z[crow * ldz + d] : 0.f;
+  Frag2 cf[CF::KC > 0 ? CF::KC : 1];
+#pragma unroll
+  for (int t = 0; t < CF::KC; ++t) {
+    float c8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 32 * t + 8 * q + j;
+      c8[j] = col < CF::C ? ctx[crow * ldc + col] : 0.f;
+    }
+    cf[t] = split8_f16(c8);
+  }
+  const RqsConsts<K, false> rc(bound);
+  float ldsum = 0.f;
+  stage_issue<CF::stage_floats(0), NW>(slot0, packed);
+  int g = 0;
+  for (int l = 0; l < L; ++l) {
+    const float* lp = packed + (int64_t)l * CF::LAYER;
+    const float* lnext = packed + (int64_t)(l + 1) * CF::LAYER;
+    Frag2 hf[NHID][KSH];
+#pragma unroll
+    for (int i = 0; i < NHID; ++i)
+#pragma unroll
+      for (int t = 0; t < KSH; ++t) hf[i][t] = Frag2{half8{}, half8{}};
+    // the layer input's f16 split at a per-row power-of-two scale (|x| sc < 2^14)
+    float xmax = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) xmax = fmaxf(xmax, fabsf(v[d]));
+    const int e = xmax >= 16384.f ? ilogbf(xmax) - 13 : 0;
+    const float sc = ldexpf(1.f, -e), us = ldexpf(1.f, e);
+    float x8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+        if (8 * qq + j < D) s = q == qq ? v[8 * qq + j] : s;
+      x8[j] = s * sc;
+    }
+    const Frag2 xf = split8_f16(x8);
+    const float* cur = slot0;
+    static_for<0, CF::NU>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      constexpr int SID = CF::stage_id(u), OFF = CF::unit_off(u);
+      constexpr bool NEW_STAGE = u == 0 || SID != CF::stage_id(u > 0 ? u - 1 : 0);
+      if constexpr (NEW_STAGE) {  // stage SID has landed in slot (g & 1)
+        __syncthreads();  // ... and every wave is done with the other slot
+        cur = (g & 1) ? slot1 : slot0;
+        float* nxt = (g & 1) ? slot0 : slot1;
+        if constexpr (SID + 1 < CF::NSTG) {
+          stage_issue<CF::stage_floats(SID + 1), NW>(nxt, lp + (SID + 1) * CF::STG);
+        } else {
+          if (l + 1 < L) stage_issue<CF::stage_floats(0), NW>(nxt, lnext);
+        }
+        ++g;
+      }
+      const u32x4* c4 = reinterpret_cast<const u32x4*>(cur);
+      auto afrag = [&](int idx) {
+        const int base = (OFF >> 2) + idx * 128 + lane;
+        return Frag2{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+      };
+      if constexpr (u < NHID * HB) {
+        constexpr int i = u / HB, b = u % HB, KT = CF::unit_kts(u);
+        const float4 bv = reinterpret_cast<const float4*>(cur + OFF + KT * CF::OT)[q];
+        floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
+        if constexpr (i == 0) {
+#pragma unroll
+          for (int t = 0; t < CF::KC; ++t) acc = mfma3_16(afrag(t), cf[t], acc);
+          const floatx4 ax = mfma3_16(afrag(CF::KC), xf, floatx4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(ax[r], us, acc[r]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < KSH; ++t) acc = mfma3_16(afrag(t), hf[i - 1][t], acc);
+        }
+        ar_split4<b & 1>(hf[i][b >> 1], acc);
+      } else {
+        constexpr int d = u - NHID * HB;
+        floatx4 o3[CF::NOB];
+        const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF + CF::NOB * KSH * CF::OT);
+#pragma unroll
+        for (int o = 0; o < CF::NOB; ++o) {
+          const float4 bv = bias4[4 * o + q];
+          o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+        }
+#pragma unroll
+        for (int t = 0; t < KSH; ++t)
+#pragma unroll
+          for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KSH + t), hf[NHID - 1][t], o3[o]);
+        if constexpr (CF::AFFINE) {
+          // pyro AffineAutoregressive._call: y = exp(clamp(ls)) x + mean, log|det| = clamp(ls)
+          const float mean = __shfl(o3[0][0], lane & 15);
+          const float ls = fminf(fmaxf(__shfl(o3[0][1], lane & 15), -5.f), 3.f);
+          v[d] = __builtin_fmaf(v[d], __expf(ls), mean);
+          ldsum += ls;
+        } else {
+          float uw[K], uh[K], ud[K - 1];
+#pragma unroll
+          for (int pi = 0; pi < P; ++pi) {
+            const float val = __shfl(o3[pi >> 4][pi & 3], (lane & 15) + 16 * ((pi & 15) >> 2));
+            if (pi < K) uw[pi] = val;
+            else if (pi < 2 * K) uh[pi - K] = val;
+            else ud[pi - 2 * K] = val;
+          }
+          float ld;
+          v[d] = rqs_select<K, false>(uw, uh, ud, v[d], bound, rc, ld);
+          ldsum += ld;
+        }
+        // the dims are independent: unpinned, the scheduler hoists later dims' output MFMAs over
+        // this dim's spline and their accumulators spill (460 B/lane at D = 16)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+  }
+  if (low != nullptr) {  // naz inverse_bounding_transform (transforms.py:24-27, flow.py:129)
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = (1.f / (1.f + expf(-v[d]))) * (high[d] - low[d]) + low[d];
+  }
+  if (q == 0 && valid) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) y[row * ldy + d] = v[d];
+    if (out_ld != nullptr) out_ld[row] = ldsum;
+  }
+}
+
 }  // namespace naz

@@ -93,7 +93,8 @@ class TransformedDistribution:
         return self._log_prob_into(y, lp, bounds).reshape(lead)
 
     def _transform_z(self, z: torch.Tensor, bounds=None) -> torch.Tensor:
-        if self._fused_ok() and getattr(self._fused, "can_sample", True):
+        if self._fused_ok() and getattr(self._fused, "can_sample", True) and \
+                getattr(self._fused, "sample_ready", lambda *a: True)(z, self._context):
             y, _ = self._fused.sample(z, self._context, bounds=bounds)
             return y
         ld = torch.zeros(z.shape[0], device=z.device, dtype=torch.float32)

@@ -149,11 +149,12 @@ class _FusedAR:
     """All L nsa / maf layers' log_prob as ONE HIP launch (naz_ar_flow_log_prob,
     csrc/made_ar_r16.h): every layer's D-pass MADE inverse (pyro ConditionedSplineAutoregressive /
     ConditionedAffineAutoregressive._inverse, naz transforms.py:133-198) with each hidden unit
-    computed once, in registers, on the f16x3 MFMA path.  sample() and the autograd walk keep the
-    per-layer kernels.  The kernel is compiled for pyro's hidden mask indices; the masks are checked
-    against them once per parameter change."""
+    computed once, in registers, on the f16x3 MFMA path.  sample() is one naz_ar_flow_sample launch
+    (the forward direction: one MADE pass per layer, then every dim's map); the autograd walk keeps
+    the per-layer kernels.  The kernel is compiled for pyro's hidden mask indices; the masks are
+    checked against them once per parameter change."""
 
-    can_sample = False
+    can_sample = True  # sample(): naz_ar_flow_sample (the forward direction, one launch)
     F16_DATA_LIMIT = 32768.0  # the kernel's f16x3 input split (|x|, |ctx| < 2^15)
 
     def __init__(self, layers: List[nn.Module], kind: str, D: int, C: int, H: int, n_hidden: int, K: int, act: str,
@@ -165,6 +166,7 @@ class _FusedAR:
         self.desc = ops.ar_flow_desc(kind, D, C, H, len(layers), n_hidden, K, act, bound)
         self._sig = None
         self._packed = None
+        self._fsig, self._fpacked = None, None
         self._masks = None
 
     def _nets(self):
@@ -222,6 +224,38 @@ class _FusedAR:
             self._packed = ops.ar_flow_pack(self.desc, np.concatenate(flats), np.stack(perms), dev)
             self._sig = sig
         return self._packed
+
+    def _flat(self):
+        flats = []
+        for n in self._nets():
+            for l in n.layers:
+                flats += [(l.weight.detach() * l.mask).float().cpu().numpy().ravel(),
+                          l.bias.detach().float().cpu().numpy()]
+        return np.concatenate(flats)
+
+    def packed_fwd(self) -> torch.Tensor:
+        """The forward (sample) image, re-packed when a weight, bias or mask changes."""
+        ps = [p for n in self._nets() for l in n.layers for p in (l.weight, l.bias, l.mask)]
+        sig = tuple((p.data_ptr(), p._version) for p in ps) + (cache_epoch(),)
+        if sig != self._fsig or self._fpacked is None:
+            dev = self._nets()[0].layers[0].weight.device
+            self._fpacked = ops.ar_flow_pack_fwd(self.desc, self._flat(), dev)
+            self._fsig = sig
+        return self._fpacked
+
+    def sample_ready(self, z, context) -> bool:
+        """The kernel splits the context into f16 pieces (|ctx| < 2^15); z is rescaled per row."""
+        if z.dim() != 2:
+            return False
+        if context is not None and context.numel():
+            return float(context.detach().abs().amax()) < self.F16_DATA_LIMIT
+        return True
+
+    def sample(self, z, context=None, bounds=None, with_logdet=False):
+        low = high = None
+        if bounds is not None:
+            low, high = bounds["low"].contiguous(), bounds["high"].contiguous()
+        return ops.ar_flow_sample(self.desc, self.packed_fwd(), z, context, low, high, with_logdet=with_logdet)
 
     def log_prob(self, x, context=None, bounds=None, out=None):
         low = high = None

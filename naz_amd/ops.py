@@ -584,6 +584,33 @@ def ar_flow_pack(d: ArDesc, flat: np.ndarray, perm: np.ndarray, device) -> Tenso
     return torch.from_numpy(host).to(device)
 
 
+def ar_flow_pack_fwd(d: ArDesc, flat: np.ndarray, device) -> Tensor:
+    """Host-side pack of the forward (sample) image (naz_ar_flow_pack_fwd_host) from the same flat
+    masked weights as ``ar_flow_pack``; one copy to the device."""
+    flat = np.ascontiguousarray(flat, dtype=np.float32)
+    nbytes = int(lib().naz_ar_flow_fwd_packed_bytes(d))
+    if nbytes <= 0:
+        raise RuntimeError("naz_amd ar_flow_pack_fwd: unsupported descriptor")
+    host = np.empty(nbytes // 4, dtype=np.float32)
+    check(lib().naz_ar_flow_pack_fwd_host(d, flat.ctypes.data, host.ctypes.data), "ar_flow_pack_fwd")
+    return torch.from_numpy(host).to(device)
+
+
+def ar_flow_sample(d: ArDesc, packed_fwd: Tensor, z: Tensor, context: Optional[Tensor] = None,
+                   low: Optional[Tensor] = None, high: Optional[Tensor] = None,
+                   with_logdet: bool = False) -> Tuple[Tensor, Optional[Tensor]]:
+    """y = T_L ∘ … ∘ T_1(z) of an nsa / maf flow in one launch (naz_ar_flow_sample)."""
+    dev = _dev(packed_fwd, z, context, low, high)
+    z, ldz = _rows(z)
+    B = z.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    y = torch.empty_like(z)
+    ld = torch.empty((B,), device=dev, dtype=torch.float32) if with_logdet else None
+    check(lib().naz_ar_flow_sample(d, _p(packed_fwd), _p(z), ldz, _p(context), ldc, _p(low), _p(high), _p(y),
+                                   y.stride(0), _p(ld), B, _stream(dev)), "ar_flow_sample")
+    return y, ld
+
+
 def ar_flow_log_prob(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,
                      low: Optional[Tensor] = None, high: Optional[Tensor] = None,
                      out: Optional[Tensor] = None) -> Tensor:

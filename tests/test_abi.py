@@ -68,7 +68,7 @@ def test_no_cpu_fallback():
 
 def test_generic_flow_entries_dispatch_without_compute():
     """naz_flow_*: packed sizes and workspace of both fused kinds (host-only calls), and the
-    documented errors (unknown kind, no fused whole-flow sampler for AR flows)."""
+    documented errors (unknown kind, missing buffers)."""
     from naz_amd import _lib, ops
     L = _lib.lib()
     c = ops.coupling_desc(16, 32, 8, 8, 8, 128)
@@ -82,5 +82,7 @@ def test_generic_flow_entries_dispatch_without_compute():
     assert L.naz_flow_packed_bytes(bad) == -1
     assert L.naz_flow_log_prob(bad, None, None, 0, None, 0, None, None, None, 0, None) != 0
     assert b"unknown flow kind" in L.naz_last_error()
-    assert L.naz_flow_sample(fa, None, None, 0, None, 0, None, None, None, 0, None, 0, None) != 0
-    assert b"layer by layer" in L.naz_last_error()
+    assert L.naz_flow_sample(fa, None, None, 0, None, 0, None, None, None, 0, None, 0, None) == 0  # B = 0
+    assert L.naz_flow_sample(fa, None, None, 0, None, 0, None, None, None, 0, None, 1, None) != 0
+    assert b"null pointer" in L.naz_last_error()
+    assert L.naz_ar_flow_fwd_packed_bytes(a) > 0

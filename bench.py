@@ -637,16 +637,30 @@ def run_flow_case(args, dev, rank, world, dist):
             else:
                 fl_row += sum(2 * blk.w.shape[0] * blk.w.shape[1] for grp in plan.hidden for _, blk in grp)
                 fl_row += sum(2 * wb.shape[0] * n for _, n, wb, _ in plan.outs)
+    if args.sample:  # the sampling direction: one conditioner pass per layer (flow.py:94-129)
+        if ftype == "nsc":
+            raise SystemExit("--sample: the coupling flow's sampler is the fused naz_coupling_sample (bench.py --flow "
+                             "config2 times log_prob); use an nsa / maf case")
+        fl_ref = fl_ref // passes  # the reference's one MADE pass per layer
+        fl_row = fl_ref
+        z = torch.as_tensor(normal_rows(lo, hi, Dd, seed=2), device=dev)
+        pdf = f._pdf(c)
+
+        def run():  # the transform of NormalizingFlow.sample (z drawn outside the timed region)
+            return pdf._transform_z(z)
+    else:
+        def run():
+            return f.log_prob(x, condition=c)
     with torch.no_grad():
         for _ in range(args.warmup):
-            f.log_prob(x, condition=c)
+            run()
         torch.cuda.synchronize(dev)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            lp = f.log_prob(x, condition=c)
+            lp = run()
         torch.cuda.synchronize(dev)
         if dist is not None:
             dist.barrier()
@@ -662,22 +676,50 @@ def run_flow_case(args, dev, rank, world, dist):
         achieved = fl_row * B / step_s / 1e12
         fused = getattr(f, "fused", False)
         rec = {
-            "metric": f"samples/sec through log_prob+log|detJ|, naz {ftype} flow (NormalizingFlow API)",
+            "metric": (f"samples/sec through sample (forward transform + log|detJ|), naz {ftype} flow (NormalizingFlow "
+                       "API)" if args.sample else
+                       f"samples/sec through log_prob+log|detJ|, naz {ftype} flow (NormalizingFlow API)"),
             "value": G / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
             "config": {"workload": desc, "batch_per_gpu": B, "global_batch": G,
                        "parallelism": f"dp{world} (independent row shards, no collective)",
-                       "path": ("fused autoregressive-inverse kernel (naz_ar_flow_log_prob, one launch)" if ar_fused
+                       "path": (("fused autoregressive sampler (naz_ar_flow_sample, one launch)" if args.sample else
+                                 "fused autoregressive-inverse kernel (naz_ar_flow_log_prob, one launch)") if ar_fused
                                 else "fused kernel" if fused else "per-layer HIP kernels (rowgemm + spline/affine)")},
             "roofline": {"bound": "mfma", "achieved": achieved,
                          "peak": FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3, "unit": "TFLOP/s",
                          "frac": achieved / (FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3),
-                         "traffic": None, "kernel": "whole log_prob call", "flop_per_row": fl_row,
+                         "traffic": None, "kernel": "whole sample call" if args.sample else "whole log_prob call",
+                         "flop_per_row": fl_row,
                          "reference_flop_per_row": fl_ref},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and args.sample:
+            from naz_amd.flows import io as fio
+            from oracle import naz_oracle as O  # baseline only
+            spec = dict(flow_type=ftype, D=Dd, C=Cd, hidden=list(hid), L=Ld)
+            if ftype == "nsa":
+                spec.update(K=extra[0])
+            of = O.build_flow(spec, fio.export_state(f), torch.float32)
+            cores = host_cores()
+            torch.set_num_threads(cores["threads"])
+            nb = 1 << 16
+            zh = z[:nb].cpu()
+            chh = None if c is None else (c.reshape(1, -1).expand(nb, -1) if grid else c[:nb]).cpu()
+            with torch.inference_mode():
+                of.forward_with_logdet(zh[:4096], None if chh is None else chh[:4096])
+                runs = []
+                for _ in range(5):
+                    t1 = time.perf_counter()
+                    of.forward_with_logdet(zh, chh)
+                    runs.append(time.perf_counter() - t1)
+            med = statistics.median(runs)
+            rec["cpu_baseline"] = {"value": nb / med, "unit": "samples/s", "cores": cores["threads"], "kind": "port",
+                                   "host": cores,
+                                   "sample": f"{nb} rows, oracle forward_with_logdet (torch fp32, pyro _call semantics), "
+                                             f"median of 5 after 1 warm-up ({med:.2f} s)"}
+        elif not args.no_cpu_baseline:
             spec = dict(flow_type=ftype, D=Dd, C=Cd, hidden=list(hid), L=Ld)
             if ftype == "nsc":
                 spec.update(K=extra[0], split=extra[1])
@@ -893,6 +935,9 @@ def main():
                          "backward on the HIP walk) over 2^18 rows")
     ap.add_argument("--cnf-solver", choices=["rk4", "dopri5"], default="rk4",
                     help="--cnf: pinned fixed-step RK4 x 8 (default) or adaptive dopri5 (atol = rtol = 1e-4)")
+    ap.add_argument("--sample", action="store_true",
+                    help="--flow nsa/maf cases: time the sampling direction (NormalizingFlow.sample's transform) "
+                         "instead of log_prob")
     ap.add_argument("--flow", choices=sorted(FLOW_CASES), default=None,
                     help="time log_prob of another §8 flow through the NormalizingFlow API (see FLOW_CASES)")
     ap.add_argument("--bayes", choices=["lp", "sample", "grad"], default=None,

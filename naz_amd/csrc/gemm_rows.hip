@@ -27,7 +27,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int RG_BM = 128;  // batch rows per workgroup (4 waves x 32)
+#ifndef NAZ_RG_BM
+#define NAZ_RG_BM 128
+#endif
+constexpr int RG_BM = NAZ_RG_BM;  // batch rows per workgroup (4 waves x 32)
+constexpr int RG_T = 2 * RG_BM;   // threads: one (row, k-half) A loader each
 #ifndef NAZ_RG_BK
 #define NAZ_RG_BK 16
 #endif
@@ -89,7 +93,7 @@ NAZ_DEV float rg_a(const RowGemmArgs& p, int64_t m, int k) {
 #endif
 // waves per SIMD: up to 4 blocks of accumulators fit 128 VGPRs (4 waves/SIMD); wider tiles 2
 template <int NB>
-__global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(RowGemmArgs p) {
+__global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(RowGemmArgs p) {
   {  // problem of this z slice (uniform: stays in SGPRs)
     const int64_t z = blockIdx.z;
     p.a0 += z * p.za0;
@@ -115,7 +119,7 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
   const int64_t am = m0 + ar;
   const bool arow = am < p.M;
   // B chunk: RG_BK k x BN n: thread -> (k = tid % RG_BK, n = tid / RG_BK + (256 / RG_BK) j)
-  constexpr int BKS = 256 / RG_BK;
+  constexpr int BKS = RG_T / RG_BK;
   const int bk = tid % RG_BK, bn0 = tid / RG_BK;
   constexpr int BPT = BN / BKS;
 
@@ -190,7 +194,7 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
   if (p.vst) {
     // staged through this wave's share of the (now free) LDS: EG blocks at a time are written
     // [32 rows][32 EG cols] and stored back as whole 16-byte row pieces
-    constexpr int SHARE = (AS_F + BS_F) / 4;
+    constexpr int SHARE = (AS_F + BS_F) / (RG_T / 64);
     constexpr int EG = SHARE >= 32 * (64 + 4) ? 2 : 1;
     constexpr int EP = 32 * EG + 4;  // pitch
     float* E = smem + wave * SHARE;
@@ -291,7 +295,7 @@ __global__ void __launch_bounds__(256, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel(
 template <int NB>
 void rowgemm_launch(const RowGemmArgs& p, int nz, hipStream_t s) {
   dim3 grid((unsigned)((p.M + RG_BM - 1) / RG_BM), (unsigned)((p.N + 32 * NB - 1) / (32 * NB)), (unsigned)nz);
-  hipLaunchKernelGGL(rowgemm_kernel<NB>, grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL(rowgemm_kernel<NB>, grid, dim3(RG_T), 0, s, p);
 }
 
 static bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }

@@ -289,6 +289,11 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
     for (int i = 0; i < NHID; ++i)
 #pragma unroll
       for (int t = 0; t < CF::KSH; ++t) hf[i][t] = Frag2{half8{}, half8{}};
+    float xmax = 0.f;
+    if constexpr (CF::AFFINE) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) xmax = fmaxf(xmax, fabsf(v[d]));
+    }
     const float* cur = slot0;
     static_for<0, D>([&](auto pc) {
       constexpr int p = decltype(pc)::value;
@@ -325,6 +330,15 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
         const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF_BIAS);
         if constexpr (i == 0 && NBP > 0) {
           // ---- hidden layer 1: blocks holding degree-p units, over [ctx | x]
+          // the row's values (inverted dims and still-pending ones alike: a masked weight times an
+          // f16 overflow would be NaN) split at a per-row power-of-two scale, |x| sc < 2^14: the
+          // inverse maps can grow values (maf: e^5 per layer) past the launch-time input check
+          // (xmax: a running bound, max |v| at the layer's start and every value written since).
+          // Affine flows only: a spline maps [-B, B] into itself and is the identity outside, so an
+          // nsa row never exceeds max(|input|, B) and the launch-time input check covers it.
+          int e = 0;
+          if constexpr (CF::AFFINE) e = xmax >= 16384.f ? __builtin_amdgcn_frexp_expf(xmax) - 14 : 0;
+          const float sc = __builtin_amdgcn_ldexpf(1.f, -e), us = __builtin_amdgcn_ldexpf(1.f, e);
           float x8[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -332,7 +346,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq)
               if (8 * qq + j < D) s = q == qq ? v[8 * qq + j] : s;
-            x8[j] = s;
+            x8[j] = s * sc;
           }
           const Frag2 xf = split8_f16(x8);
           static_for<0, NBP>([&](auto bc) {
@@ -341,7 +355,13 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
             floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
             for (int t = 0; t < CF::KC; ++t) acc = mfma3_16(afrag(bi * CF::KI + t), cf[t], acc);
-            acc = mfma3_16(afrag(bi * CF::KI + CF::KC), xf, acc);
+            if constexpr (CF::AFFINE) {
+              const floatx4 ax = mfma3_16(afrag(bi * CF::KI + CF::KC), xf, floatx4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(ax[r], us, acc[r]);
+            } else {
+              acc = mfma3_16(afrag(bi * CF::KI + CF::KC), xf, acc);
+            }
             ar_split4<b & 1>(hf[0][b >> 1], acc);
           });
         } else if constexpr (i > 0 && i < NHID && NBP > 0) {
@@ -372,6 +392,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
             const float mean = __shfl(o3[0][0], lane & 15);
             const float ls = fminf(fmaxf(__shfl(o3[0][1], lane & 15), -5.f), 3.f);
             v[dp] = (y - mean) * __expf(-ls);
+            xmax = fmaxf(xmax, fabsf(v[dp]));
             ldsum += ls;
           } else {
             // parameter pi sits in block pi >> 4, register pi & 3 of quarter (pi & 15) >> 2
@@ -558,11 +579,13 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
 #pragma unroll
       for (int t = 0; t < KSH; ++t) hf[i][t] = Frag2{half8{}, half8{}};
     // the layer input's f16 split at a per-row power-of-two scale (|x| sc < 2^14)
-    float xmax = 0.f;
+    float xmax = 0.f;  // (affine only: splines keep a row within max(|z|, B), see the inverse kernel)
+    if constexpr (CF::AFFINE) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) xmax = fmaxf(xmax, fabsf(v[d]));
-    const int e = xmax >= 16384.f ? ilogbf(xmax) - 13 : 0;
-    const float sc = ldexpf(1.f, -e), us = ldexpf(1.f, e);
+      for (int d = 0; d < D; ++d) xmax = fmaxf(xmax, fabsf(v[d]));
+    }
+    const int e = xmax >= 16384.f ? __builtin_amdgcn_frexp_expf(xmax) - 14 : 0;
+    const float sc = __builtin_amdgcn_ldexpf(1.f, -e), us = __builtin_amdgcn_ldexpf(1.f, e);
     float x8[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {

@@ -163,3 +163,27 @@ def test_fused_ar_sample_broadcast_context_bounds_ragged():
         torch.manual_seed(0)
         b = f.sample([1000], condition=c1)
     np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_fused_ar_inverse_growing_values_stay_finite():
+    """maf inverse with log-scales at the -5 clamp: every layer multiplies by e^5, so the values
+    pass the f16 range inside the launch (the input check cannot see it); the per-row scaling of
+    the hidden-layer-1 split keeps the fused result equal to the fp32 per-layer walk."""
+    spec = dict(flow_type="maf", D=16, C=32, hidden=[128, 128], L=4)
+    f, _ = _flow(spec)
+    D = spec["D"]
+    with torch.no_grad():
+        for t in f.flow_dist.transforms:
+            last = t.nn.layers[-1]
+            last.weight.mul_(1e-3)
+            last.bias[D:].fill_(-10.0)  # clamped to -5
+    g = torch.Generator().manual_seed(9)
+    x = (torch.randn(500, D, generator=g) * 3.0).to(DEV)
+    c = torch.randn(500, 32, generator=g).to(DEV)
+    with torch.no_grad():
+        assert f.fused
+        lp = f.log_prob(x, condition=c)
+        f.set_fused(False)
+        ref = f.log_prob(x, condition=c)
+    assert torch.isfinite(lp).all() and torch.isfinite(ref).all()
+    np.testing.assert_allclose(lp.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-3)

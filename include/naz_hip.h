@@ -354,6 +354,19 @@ int naz_ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z,
                        int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld,
                        int64_t B, void* stream);
 
+/* §8f ranks 1-2: the sampler batched over P weight draws of one flow (naz's Bayesian MAF,
+ * bflow_jax_maf.py:196-236 sampler per draw: calibrate.py:145-151).  naz_ar_flow_pack_fwd packs the
+ * forward images of P draws ON THE DEVICE: flat rows at flat + p sflat (the naz_ar_flow_pack_host
+ * flat layout, masks applied), images at packed + p spk (spk >= naz_ar_flow_fwd_packed_bytes / 4).
+ * naz_ar_flow_sample_batched: draw p maps z + p sz -> y + p sy (B rows each, row strides ldz /
+ * ldy), out_ld + p sld (nullable) = Σ forward log-dets; ctx shared by every draw (ldc = 0: one
+ * context vector).  P <= 65535 per call. */
+int naz_ar_flow_pack_fwd(const naz_ar_desc* d, const float* flat, int64_t sflat, void* packed, int64_t spk, int64_t P,
+                         void* stream);
+int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* z, int64_t ldz,
+                               int64_t sz, const float* ctx, int64_t ldc, float* y, int64_t ldy, int64_t sy,
+                               float* out_ld, int64_t sld, int64_t B, int64_t P, void* stream);
+
 /* ---- §8b: whole-flow entries over the fused kinds -------------------------------------
  * One descriptor for the flows whose whole log_prob is one launch: the spline coupling flow (naz
  * "nsc": naz_coupling_*) and the autoregressive flows (naz "nsa" / "maf": naz_ar_flow_*).  The

@@ -304,6 +304,22 @@ int naz_ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z,
   return ar_flow_sample(d, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, as_stream(stream));
 }
 
+int naz_ar_flow_pack_fwd(const naz_ar_desc* d, const float* flat, int64_t sflat, void* packed, int64_t spk, int64_t P,
+                         void* stream) {
+  if (P < 0) return set_error("naz_ar_flow_pack_fwd: negative draw count");
+  return ar_flow_pack_fwd(d, flat, sflat, packed, spk, P, as_stream(stream));
+}
+int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* z, int64_t ldz,
+                               int64_t sz, const float* ctx, int64_t ldc, float* y, int64_t ldy, int64_t sy,
+                               float* out_ld, int64_t sld, int64_t B, int64_t P, void* stream) {
+  if (B < 0 || P < 0) return set_error("naz_ar_flow_sample_batched: negative size");
+  if (B > 0 && P > 0 && (packed == nullptr || z == nullptr || y == nullptr))
+    return set_error("naz_ar_flow_sample_batched: null pointer");
+  if (d != nullptr && d->C > 0 && B > 0 && P > 0 && ctx == nullptr)
+    return set_error("naz_ar_flow_sample_batched: conditional flow needs ctx");
+  return ar_flow_sample_batched(d, packed, spk, z, ldz, sz, ctx, ldc, y, ldy, sy, out_ld, sld, B, P, as_stream(stream));
+}
+
 // ---- §8b whole-flow entries over the fused kinds ----------------------------------------
 int64_t naz_flow_packed_bytes(const naz_flow_desc* d) {
   if (d == nullptr) return -1;

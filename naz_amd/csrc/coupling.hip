@@ -1507,13 +1507,26 @@ struct AROps {
   }
   static int sample(const float* packed, int L, const float* z, int64_t ldz, const float* ctx, int64_t ldc,
                     const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B, float bound,
-                    hipStream_t s) {
-    if (B == 0) return 0;
+                    hipStream_t s, int64_t P = 1, int64_t spk = 0, int64_t sz = 0, int64_t sy = 0, int64_t sld = 0) {
+    if (B == 0 || P == 0) return 0;
+    if (P > 65535) return set_error("naz_ar_flow_sample_batched: at most 65535 draws per call");
     const int64_t rows = 16 * FW::NW, grid = (B + rows - 1) / rows;
     const size_t lds = (size_t)2 * FW::STG * 4;
-    hipLaunchKernelGGL((made_ar_fwd_kernel<FW>), dim3((unsigned)grid), dim3(64 * FW::NW), lds, s, packed, L, z, ldz,
-                       ctx, ldc, low, high, y, ldy, out_ld, B, bound);
+    hipLaunchKernelGGL((made_ar_fwd_kernel<FW>), dim3((unsigned)grid, (unsigned)P), dim3(64 * FW::NW), lds, s, packed,
+                       L, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, bound, spk, sz, sy, sld);
     return check_launch("made_ar_fwd_kernel");
+  }
+  static int64_t flat_floats() {
+    constexpr int H = CF::H, D = CF::D, C = CF::C, P = CF::P;
+    return (int64_t)H * (C + D) + H + (int64_t)(CF::NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
+  }
+  static int pack_fwd_device(const float* flat, int64_t sflat, float* packed, int64_t spk, int L, int64_t P,
+                             hipStream_t s) {
+    if (L == 0 || P == 0) return 0;
+    if (P > 65535 || L > 65535) return set_error("naz_ar_flow_pack_fwd: at most 65535 draws / layers per call");
+    const dim3 grid((unsigned)((FW::LAYER + 255) / 256), (unsigned)L, (unsigned)P);
+    hipLaunchKernelGGL((made_ar_pack_fwd_kernel<FW>), grid, dim3(256), 0, s, flat, sflat, packed, spk);
+    return check_launch("made_ar_pack_fwd_kernel");
   }
 };
 
@@ -1594,6 +1607,28 @@ int ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z, int
   const int rc = ar_dispatch(d, [&](auto ops) {
     return decltype(ops)::sample(static_cast<const float*>(packed), d->L, z, ldz, ctx, ldc, low, high, y, ldy, out_ld,
                                  B, d->bound, s);
+  });
+  return rc == -2 ? ar_unsupported(d) : rc;
+}
+
+int ar_flow_pack_fwd(const naz_ar_desc* d, const float* flat, int64_t sflat, void* packed, int64_t spk, int64_t P,
+                     hipStream_t s) {
+  if (flat == nullptr || packed == nullptr) return set_error("naz_ar_flow_pack_fwd: null pointer");
+  const int rc = ar_dispatch(d, [&](auto ops) {
+    using O = decltype(ops);
+    if (sflat < O::flat_floats() * d->L || spk < O::fwd_layer_floats() * d->L)
+      return set_error("naz_ar_flow_pack_fwd: draw strides shorter than one flow");
+    return O::pack_fwd_device(flat, sflat, static_cast<float*>(packed), spk, d->L, P, s);
+  });
+  return rc == -2 ? ar_unsupported(d) : rc;
+}
+
+int ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* z, int64_t ldz,
+                           int64_t sz, const float* ctx, int64_t ldc, float* y, int64_t ldy, int64_t sy, float* out_ld,
+                           int64_t sld, int64_t B, int64_t P, hipStream_t s) {
+  const int rc = ar_dispatch(d, [&](auto ops) {
+    return decltype(ops)::sample(static_cast<const float*>(packed), d->L, z, ldz, ctx, ldc, nullptr, nullptr, y, ldy,
+                                 out_ld, B, d->bound, s, P, spk, sz, sy, sld);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }

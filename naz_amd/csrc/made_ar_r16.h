@@ -536,12 +536,106 @@ static void made_ar_pack_fwd_layer(const float* flat, float* out) {
   }
 }
 
+// Device form of made_ar_pack_fwd_layer (the Bayesian sampler packs every weight draw on the GPU):
+// thread = one 32-bit word of one layer image; blockIdx.y = layer, blockIdx.z = draw.  flat rows at
+// flat + draw * sflat (L layers of the made_ar_pack_fwd_layer flat layout, masks applied), images
+// at packed + draw * spk.
+NAZ_DEV unsigned ar_piece_dev(float v, int piece) {
+  const _Float16 hi = (_Float16)v;
+  const _Float16 r = piece == 0 ? hi : (_Float16)(v - (float)hi);
+  return (unsigned)__builtin_bit_cast(unsigned short, r);
+}
+
+template <class CF>
+__global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t sflat, float* __restrict__ packed,
+                                        int64_t spk) {
+  constexpr int D = CF::D, C = CF::C, H = CF::H, P = CF::P, HB = CF::HB, KSH = CF::KSH, NHID = CF::NHID;
+  constexpr int64_t per = (int64_t)H * (C + D) + H + (int64_t)(NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
+  const int pos = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pos >= CF::LAYER) return;
+  const int l = blockIdx.y;
+  const float* f = flat + blockIdx.z * sflat + (int64_t)l * per;
+  float* out = packed + blockIdx.z * spk + (int64_t)l * CF::LAYER;
+  // per-sub-layer base pointers of the flat layout
+  auto Wl = [&](int i) {
+    int64_t o = 0;
+    for (int j = 0; j < i; ++j) o += (int64_t)H * (j == 0 ? C + D : H) + H;
+    return f + o;
+  };
+  auto bl = [&](int i) { return Wl(i) + (int64_t)(i < NHID ? H : D * P) * (i == 0 ? C + D : H); };
+  unsigned word = 0;
+  bool done = false;
+  static_for<0, CF::NU>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    constexpr int base = CF::stage_id(u) * CF::STG + CF::unit_off(u);
+    constexpr int nfr = CF::unit_blocks(u) * CF::unit_kts(u);
+    if (done || pos < base || pos >= base + CF::unit_floats(u)) return;
+    done = true;
+    const int rel = pos - base;
+    if (rel >= nfr * CF::OT) {  // bias
+      const int r = rel - nfr * CF::OT;
+      float v = 0.f;
+      if constexpr (u < NHID * HB) {
+        constexpr int i = u / HB, b = u % HB;
+        if (16 * b + r < H) v = kSigScale * bl(i)[16 * b + r];
+      } else {
+        constexpr int d = u - NHID * HB;
+        if (r < P) v = bl(NHID)[r * D + d];
+      }
+      word = __builtin_bit_cast(unsigned, v);
+      return;
+    }
+    const int fr = rel / CF::OT, w = rel % CF::OT;
+    const int piece = w / 256, lane = (w % 256) / 4, pair = w % 4;
+    const int m = lane & 15, kg = lane >> 4;
+    for (int e = 0; e < 2; ++e) {
+      const int j = 2 * pair + e;
+      float v = 0.f;
+      if constexpr (u < NHID * HB) {
+        constexpr int i = u / HB, b = u % HB;
+        const int t = fr, un = 16 * b + m;
+        if (un < H) {
+          if constexpr (i > 0) {
+            const int vv = r16_feat(t, kg, j);
+            if (vv < H) v = -2.f * kSigScale * Wl(i)[(int64_t)un * H + vv];
+          } else {
+            if (t < CF::KC) {
+              const int col = 32 * t + 8 * kg + j;
+              if (col < C) v = kSigScale * Wl(0)[(int64_t)un * (C + D) + col];
+            } else {
+              const int dd = 8 * kg + j;
+              if (dd < D) v = kSigScale * Wl(0)[(int64_t)un * (C + D) + C + dd];
+            }
+          }
+        }
+      } else {
+        constexpr int d = u - NHID * HB;
+        const int o = fr / KSH, t = fr % KSH;
+        const int pi = 16 * o + m, vv = r16_feat(t, kg, j);
+        if (pi < P && vv < H) v = -2.f * Wl(NHID)[((int64_t)pi * D + d) * H + vv];
+      }
+      word |= ar_piece_dev(v, piece) << (16 * e);
+    }
+  });
+  reinterpret_cast<unsigned*>(out)[pos] = word;  // padding words (no unit) stay 0
+}
+
+// blockIdx.y = draw (the Bayesian front end's weight draws, naz_ar_flow_sample_batched): its image at
+// packed + draw * spk, its rows at z + draw * sz, y + draw * sy, out_ld + draw * sld
 template <class CF>
 __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ z, int64_t ldz,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
-    float* __restrict__ y, int64_t ldy, float* __restrict__ out_ld, int64_t B, float bound) {
+    float* __restrict__ y, int64_t ldy, float* __restrict__ out_ld, int64_t B, float bound, int64_t spk = 0,
+    int64_t sz = 0, int64_t sy = 0, int64_t sld = 0) {
   constexpr int D = CF::D, K = CF::K, P = CF::P, NW = CF::NW, NHID = CF::NHID, HB = CF::HB, KSH = CF::KSH;
+  {
+    const int64_t dz = blockIdx.y;
+    packed += dz * spk;
+    z += dz * sz;
+    y += dz * sy;
+    if (out_ld != nullptr) out_ld += dz * sld;
+  }
   extern __shared__ float4 lds4[];
   float* const slot0 = reinterpret_cast<float*>(lds4);
   float* const slot1 = slot0 + CF::STG;

@@ -222,7 +222,7 @@ def _flat_layer(layer, P, dev):
 
 def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bounds=None, context=None,
                           rows_per_chunk: int = 1 << 23, fold_context: bool = True,
-                          fuse_pass2: bool = True, batch_layers: bool = True) -> Dict[str, object]:
+                          fuse_pass2: bool = True, batch_layers: bool = True, fused_ar: bool = True) -> Dict[str, object]:
     """naz ``make_normalizing_flow`` (bflow_jax_maf.py:196-225) on MI355X.  Returns
     ``{"lp": f(params) -> [B], "sampler": f(params, rng_key, size) -> (y, log_j),
     "lp_batched": f(params_P) -> [P, B], "sampler_batched": f(params_P, rng_key, size)}``.
@@ -261,6 +261,18 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         assert all(mp.numel() == n_packed for mp in made_maps), "made pack map out of sync with made.hip"
     act = spec.activation
     width_sum = max(sum(pl.widths) for pl in plans)
+    # the whole flow's sampling direction in ONE launch for all draws (naz_ar_flow_sample_batched,
+    # csrc/made_ar_r16.h, f16x3 MFMA) at the compiled shapes (the paper's D=2 | C=2, H=[150]*3)
+    ar_desc = None
+    hd = list(spec.hidden_dims)
+    if fused_ar and act == "tanh" and len(set(hd)) == 1:
+        d_ = ops.ar_flow_desc("maf", D, C, hd[0], len(masks), len(hd))
+        if ops.ar_flow_supported(d_):
+            ar_desc = d_
+            # per layer: F[:, 1:] * mask-vector = the flat layout naz_ar_flow_pack_fwd reads
+            ar_maskvec = [torch.cat([t for m, (ws, bs) in zip(ms, spec.param_shapes)
+                                     for t in (m.reshape(-1).to(torch.float32), torch.ones(bs[0]))]).to(dev)
+                          for ms in masks]
 
     def _chunks(P, rows, max_draws=65535):
         """Draw ranges per launch set: at most ``max_draws`` (the grid-z limit of the batched
@@ -515,6 +527,13 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         P, S = z.shape[0], z.shape[1]
         lj = lj_out.reshape(P * S)
         ops.base_log_prob(z.reshape(P * S, D), out=lj)
+        if ar_desc is not None and (ctx_s is None or float(ctx_s.abs().max()) < 32768.0):
+            flat = torch.cat([_flat_layer(params[l], P, dev)[:, 1:] * ar_maskvec[l] for l in range(len(plans))], 1)
+            packed = ops.ar_flow_pack_fwd_batched(ar_desc, flat)
+            y, ld = ops.ar_flow_sample_batched(ar_desc, packed, z, ctx_s)
+            y_out.copy_(y)
+            lj_out.add_(ld)
+            return
         cur = z
         if fused_fwd:
             for l in range(len(plans)):

@@ -611,6 +611,37 @@ def ar_flow_sample(d: ArDesc, packed_fwd: Tensor, z: Tensor, context: Optional[T
     return y, ld
 
 
+def ar_flow_pack_fwd_batched(d: ArDesc, flat: Tensor) -> Tensor:
+    """Forward images of P weight draws packed on the device (naz_ar_flow_pack_fwd): flat [P, L * per]
+    (the naz_ar_flow_pack_host flat layout, masks applied) -> [P, image floats]."""
+    dev = _dev(flat)
+    flat = flat.contiguous()
+    P = flat.shape[0]
+    n = int(lib().naz_ar_flow_fwd_packed_bytes(d)) // 4
+    if n <= 0:
+        raise RuntimeError("naz_amd ar_flow_pack_fwd: unsupported descriptor")
+    out = torch.empty((P, n), device=dev, dtype=torch.float32)
+    check(lib().naz_ar_flow_pack_fwd(d, _p(flat), flat.stride(0), _p(out), n, P, _stream(dev)), "ar_flow_pack_fwd")
+    return out
+
+
+def ar_flow_sample_batched(d: ArDesc, packed: Tensor, z: Tensor, context: Optional[Tensor] = None,
+                           with_logdet: bool = True) -> Tuple[Tensor, Optional[Tensor]]:
+    """Draw p of ``packed`` [P, image] maps z[p] ([P, S, D]) -> y[p]; one context vector for all draws
+    (naz_ar_flow_sample_batched).  Returns (y [P, S, D], Σ forward log-dets [P, S])."""
+    dev = _dev(packed, z, context)
+    z = z.contiguous()
+    P, S, D = z.shape
+    if packed.shape[0] != P or not packed.is_contiguous():
+        raise ValueError("ar_flow_sample_batched: packed must be a contiguous [P, image] tensor")
+    ctx = None if context is None else context.reshape(1, -1).contiguous()
+    y = torch.empty_like(z)
+    ld = torch.empty((P, S), device=dev, dtype=torch.float32) if with_logdet else None
+    check(lib().naz_ar_flow_sample_batched(d, _p(packed), packed.stride(0), _p(z), D, S * D, _p(ctx), 0, _p(y), D,
+                                           S * D, _p(ld), S, S, P, _stream(dev)), "ar_flow_sample_batched")
+    return y, ld
+
+
 def ar_flow_log_prob(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,
                      low: Optional[Tensor] = None, high: Optional[Tensor] = None,
                      out: Optional[Tensor] = None) -> Tensor:

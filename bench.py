@@ -842,6 +842,11 @@ def run_bayes(args, dev, rank, world, dist):
                      "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "whole batched call",
                      "flop_per_row": fl_row, "reference_flop_per_row": fl_ref},
     }
+    if lp_mode and flow["lp_fused_ar"]:  # the whole flow per draw in one naz_ar_flow_log_prob_batched launch
+        peak = BF16_PEAK_TFLOPS / 3
+        rec["roofline"].update(peak=peak, frac=achieved / peak, peak_note="split f16x3 ceiling (2.5 PF / 3 products)")
+        rec["config"]["path"] = ("device pack of every draw's inverse image (naz_ar_flow_pack) + ONE "
+                                 "naz_ar_flow_log_prob_batched launch for all layers and draws")
     if args.bayes == "sample":  # the whole flow per draw in one naz_ar_flow_sample_batched launch (f16x3 MFMA)
         peak = BF16_PEAK_TFLOPS / 3
         rec["roofline"].update(peak=peak, frac=achieved / peak, peak_note="split f16x3 ceiling (2.5 PF / 3 products)")

@@ -367,6 +367,20 @@ int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t
                                int64_t sz, const float* ctx, int64_t ldc, float* y, int64_t ldy, int64_t sy,
                                float* out_ld, int64_t sld, int64_t B, int64_t P, void* stream);
 
+/* §8f rank 1: the log-density batched over P weight draws (naz's Bayesian MAF lp over the training
+ * set per posterior draw, bflow_jax_maf.py:196-225 log_prob vmapped over draws: the NUTS potential
+ * of calibrate.py).  naz_ar_flow_pack packs the inverse images of P draws ON THE DEVICE: flat rows
+ * at flat + p sflat (the naz_ar_flow_pack_host flat layout, masks applied), perm [L][D] in device
+ * memory shared by every draw (a permutation of 0..D-1 per layer: the caller checks), images at
+ * packed + p spk (spk >= naz_ar_flow_packed_bytes / 4).  naz_ar_flow_log_prob_batched: out_lp + p slp
+ * [B] = log p(x + p sx | ctx) under draw p (sx = 0: the same rows for every draw; ldc = 0: one
+ * context vector); no bounding.  P <= 65535 per call. */
+int naz_ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
+                     int64_t P, void* stream);
+int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
+                                 int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B,
+                                 int64_t P, void* stream);
+
 /* ---- §8b: whole-flow entries over the fused kinds -------------------------------------
  * One descriptor for the flows whose whole log_prob is one launch: the spline coupling flow (naz
  * "nsc": naz_coupling_*) and the autoregressive flows (naz "nsa" / "maf": naz_ar_flow_*).  The

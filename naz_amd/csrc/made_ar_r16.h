@@ -234,8 +234,14 @@ template <class CF>
 __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
-    float* __restrict__ out_lp, int64_t B, float bound) {
+    float* __restrict__ out_lp, int64_t B, float bound, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0) {
   constexpr int D = CF::D, K = CF::K, P = CF::P, NW = CF::NW, NHID = CF::NHID;
+  {  // blockIdx.y = draw (naz_ar_flow_log_prob_batched): image packed + draw spk, rows x + draw sx
+    const int64_t dz = blockIdx.y;
+    packed += dz * spk;
+    x += dz * sx;
+    out_lp += dz * slp;
+  }
   extern __shared__ float4 lds4[];
   float* const slot0 = reinterpret_cast<float*>(lds4);
   float* const slot1 = slot0 + CF::STG;
@@ -540,10 +546,19 @@ static void made_ar_pack_fwd_layer(const float* flat, float* out) {
 // thread = one 32-bit word of one layer image; blockIdx.y = layer, blockIdx.z = draw.  flat rows at
 // flat + draw * sflat (L layers of the made_ar_pack_fwd_layer flat layout, masks applied), images
 // at packed + draw * spk.
+// f16 code of v, round-to-nearest-even also below 2^-14, where v_cvt_f16_f32 was measured to round
+// the lo pieces of f16-split weights 1 code off the host packer's conversion: there the code is
+// rint(|v| 2^24) (exact scaling, v_rndne_f32; 1024 carries into the smallest normal)
+NAZ_DEV unsigned ar_f16_rne_dev(float v) {
+  const float a = fabsf(v);
+  if (a < 6.103515625e-05f)
+    return (unsigned)__builtin_rintf(a * 16777216.f) | ((__builtin_bit_cast(unsigned, v) >> 16) & 0x8000u);
+  return (unsigned)__builtin_bit_cast(unsigned short, (_Float16)v);
+}
 NAZ_DEV unsigned ar_piece_dev(float v, int piece) {
-  const _Float16 hi = (_Float16)v;
-  const _Float16 r = piece == 0 ? hi : (_Float16)(v - (float)hi);
-  return (unsigned)__builtin_bit_cast(unsigned short, r);
+  const unsigned hi = ar_f16_rne_dev(v);
+  if (piece == 0) return hi;
+  return ar_f16_rne_dev(v - (float)__builtin_bit_cast(_Float16, (unsigned short)hi));
 }
 
 template <class CF>
@@ -618,6 +633,91 @@ __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t 
     }
   });
   reinterpret_cast<unsigned*>(out)[pos] = word;  // padding words (no unit) stay 0
+}
+
+// Device form of made_ar_pack_layer (the Bayesian log-density packs every weight draw on the GPU,
+// naz_ar_flow_pack): thread = one 32-bit word of one layer image, blockIdx.y = layer, blockIdx.z =
+// draw; flat as made_ar_pack_fwd_kernel's, perm [L][D] shared by every draw (checked on the host).
+template <class CF>
+__global__ void made_ar_pack_kernel(const float* __restrict__ flat, int64_t sflat, const int* __restrict__ perm,
+                                    float* __restrict__ packed, int64_t spk) {
+  constexpr int D = CF::D, C = CF::C, H = CF::H, P = CF::P, NHID = CF::NHID;
+  constexpr int64_t per = (int64_t)H * (C + D) + H + (int64_t)(NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
+  const int pos = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pos >= CF::LAYER) return;
+  const int l = blockIdx.y;
+  const float* f = flat + blockIdx.z * sflat + (int64_t)l * per;
+  const int* pm = perm + l * D;
+  unsigned* out = reinterpret_cast<unsigned*>(packed + blockIdx.z * spk + (int64_t)l * CF::LAYER);
+  if (pos >= CF::PERM_OFF) {
+    out[pos] = pos - CF::PERM_OFF < D ? (unsigned)pm[pos - CF::PERM_OFF] : 0u;
+    return;
+  }
+  auto Wl = [&](int i) {
+    int64_t o = 0;
+    for (int j = 0; j < i; ++j) o += (int64_t)H * (j == 0 ? C + D : H) + H;
+    return f + o;
+  };
+  auto bl = [&](int i) { return Wl(i) + (int64_t)(i < NHID ? H : D * P) * (i == 0 ? C + D : H); };
+  unsigned word = 0;
+  bool done = false;
+  static_for<0, D>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    static_for<0, NHID + 1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int base = CF::stage_id(p, i) * CF::STG + CF::sub_off(p, i);
+      constexpr int nfr = CF::frags(p, i);
+      constexpr int size = nfr * CF::OT + 16 * (i < NHID ? CF::nb(p) : CF::NOB);
+      if (done || pos < base || pos >= base + size) return;
+      done = true;
+      const int dp = pm[p];
+      const int rel = pos - base;
+      if (rel >= nfr * CF::OT) {  // bias
+        const int r = rel - nfr * CF::OT;
+        float v = 0.f;
+        if constexpr (i < NHID) {
+          const int u = 16 * (CF::blo(p) + r / 16) + r % 16;
+          if (u < H) v = kSigScale * bl(i)[u];
+        } else {
+          if (r < P) v = bl(NHID)[r * D + dp];
+        }
+        word = __builtin_bit_cast(unsigned, v);
+        return;
+      }
+      if constexpr (nfr > 0) {
+        const int fr = rel / CF::OT, w = rel % CF::OT;
+        const int piece = w / 256, lane = (w % 256) / 4, pair = w % 4;
+        const int m = lane & 15, kg = lane >> 4;
+        for (int e = 0; e < 2; ++e) {
+          const int j = 2 * pair + e;
+          float v = 0.f;
+          if constexpr (i < NHID) {
+            constexpr int kts = i == 0 ? CF::KI : CF::kt(p);
+            const int t = fr % kts, u = 16 * (CF::blo(p) + fr / kts) + m;
+            if (u < H) {
+              if constexpr (i > 0) {
+                const int vv = r16_feat(t, kg, j);
+                if (vv < H) v = -2.f * kSigScale * Wl(i)[(int64_t)u * H + vv];
+              } else if (t < CF::KC) {
+                const int col = 32 * t + 8 * kg + j;
+                if (col < C) v = kSigScale * Wl(0)[(int64_t)u * (C + D) + col];
+              } else {
+                const int dd = 8 * kg + j;
+                if (dd < D) v = kSigScale * Wl(0)[(int64_t)u * (C + D) + C + dd];
+              }
+            }
+          } else {
+            constexpr int kts = CF::kt(p);
+            const int o = fr / kts, t = fr % kts;
+            const int pi = 16 * o + m, vv = r16_feat(t, kg, j);
+            if (pi < P && vv < H) v = -2.f * Wl(NHID)[((int64_t)pi * D + dp) * H + vv];
+          }
+          word |= ar_piece_dev(v, piece) << (16 * e);
+        }
+      }
+    });
+  });
+  out[pos] = word;  // padding words (no sub-layer) stay 0
 }
 
 // blockIdx.y = draw (the Bayesian front end's weight draws, naz_ar_flow_sample_batched): its image at

@@ -273,6 +273,20 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             ar_maskvec = [torch.cat([t for m, (ws, bs) in zip(ms, spec.param_shapes)
                                      for t in (m.reshape(-1).to(torch.float32), torch.ones(bs[0]))]).to(dev)
                           for ms in masks]
+    # the whole log-density in ONE launch for all draws (naz_ar_flow_log_prob_batched): the
+    # inverse kernel's degree passes assume pyro's create_mask for each layer's permutation, one
+    # context vector (or none) and rows inside the f16x3 input split's range
+    ar_perm = None
+    if ar_desc is not None and (C == 0 or ctx.dim() == 1) and float(x.abs().max()) < 32768.0 and \
+            (C == 0 or float(ctx.abs().max()) < 32768.0):
+        pm = [torch.as_tensor(p_).cpu().to(torch.int64) for p_ in perms]
+        ok = True
+        for ms, p_ in zip(masks, pm):
+            ref, _ = create_mask(D, C, hd, p_, 2)
+            ok = ok and len(ref) == len(ms) and all(
+                torch.equal(r.to(torch.float32), m.detach().cpu().to(torch.float32)) for r, m in zip(ref, ms))
+        if ok:
+            ar_perm = torch.stack(pm).numpy()
 
     def _chunks(P, rows, max_draws=65535):
         """Draw ranges per launch set: at most ``max_draws`` (the grid-z limit of the batched
@@ -503,9 +517,24 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
                                      ops.LD_ROWSUM_SUB)
         ops.base_log_prob(z.reshape(P * B, D), out=lp, accumulate=True)
 
+    def _lp_chunk_ar(params: Params, out: Tensor):
+        """Every draw's inverse image packed on the device (naz_ar_flow_pack), then the whole flow
+        for all draws in one naz_ar_flow_log_prob_batched launch (csrc/made_ar_r16.h)."""
+        P = _draws(params)
+        flat = torch.cat([_flat_layer(params[l], P, dev)[:, 1:] * ar_maskvec[l] for l in range(len(plans))], 1)
+        packed = ops.ar_flow_pack_batched(ar_desc, flat, ar_perm)
+        out.copy_(ops.ar_flow_log_prob_batched(ar_desc, packed, x, ctx))
+
     def lp_batched(params: Params) -> Tensor:
         P = _draws(params)
         out = torch.empty((P, B), device=dev, dtype=torch.float32)
+        if ar_perm is not None:
+            # budget: the flat weights and the packed image per draw (~64-float units), plus its rows
+            img = int(ops.lib().naz_ar_flow_packed_bytes(ar_desc)) // 4
+            per_draw = (img + len(plans) * _flat_layer_size(params[0])) // 64 + B // 64 + 1
+            for p0, p1 in _chunks(P, per_draw):
+                _lp_chunk_ar([[(w[p0:p1], b[p0:p1]) for (w, b) in layer] for layer in params], out[p0:p1])
+            return out
         run = _lp_chunk_const if (const_ctx and fold_context) else _lp_chunk
         per_draw, max_draws = B * max(1, width_sum // 64), 65535
         if run is _lp_chunk_const and batch_layers and _same_structure():
@@ -665,10 +694,11 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         return y[0], lj[0]
 
     def lp_flops_per_row() -> int:
-        """Executed GEMM FLOPs per (draw, row) of lp_batched (padded blocks included)."""
+        """GEMM FLOPs per (draw, row) of lp_batched: the degree schedule's (every MADE unit once; the
+        fused AR kernel executes these plus padding), or with the context folded the per-row part."""
         tot = 0
         for plan in plans:
-            if const_ctx and fold_context:
+            if const_ctx and fold_context and ar_perm is None:
                 split, osplit = _split_maps(plan)
                 for g in range(1, D):
                     for (li, a, b, n, w, bb), (e, wc, wr) in zip(plan.hidden[g], split[g]):
@@ -681,4 +711,4 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
 
     return {"lp": lp, "sampler": sampler, "lp_batched": lp_batched, "sampler_batched": sampler_batched,
             "lp_and_grad": lp_and_grad, "grad_state": grad_flow, "lp_flops_per_row": lp_flops_per_row,
-            "plans": plans, "fused_fwd": fused_fwd}
+            "plans": plans, "fused_fwd": fused_fwd, "lp_fused_ar": ar_perm is not None}

@@ -621,7 +621,7 @@ def ar_flow_pack_fwd_batched(d: ArDesc, flat: Tensor) -> Tensor:
     if n <= 0:
         raise RuntimeError("naz_amd ar_flow_pack_fwd: unsupported descriptor")
     out = torch.empty((P, n), device=dev, dtype=torch.float32)
-    check(lib().naz_ar_flow_pack_fwd(d, _p(flat), flat.stride(0), _p(out), n, P, _stream(dev)), "ar_flow_pack_fwd")
+    check(lib().naz_ar_flow_pack_fwd(d, _p(flat), flat.shape[1], _p(out), n, P, _stream(dev)), "ar_flow_pack_fwd")
     return out
 
 
@@ -640,6 +640,52 @@ def ar_flow_sample_batched(d: ArDesc, packed: Tensor, z: Tensor, context: Option
     check(lib().naz_ar_flow_sample_batched(d, _p(packed), packed.stride(0), _p(z), D, S * D, _p(ctx), 0, _p(y), D,
                                            S * D, _p(ld), S, S, P, _stream(dev)), "ar_flow_sample_batched")
     return y, ld
+
+
+_AR_PERMS: dict = {}
+
+
+def ar_flow_pack_batched(d: ArDesc, flat: Tensor, perm) -> Tensor:
+    """Inverse (log_prob) images of P weight draws packed on the device (naz_ar_flow_pack): flat
+    [P, L * per] (the naz_ar_flow_pack_host flat layout, masks applied), perm [L, D] shared by the
+    draws (checked here: the kernel indexes its registers by it) -> [P, image floats]."""
+    dev = _dev(flat)
+    flat = flat.contiguous()
+    P = flat.shape[0]
+    pm = np.ascontiguousarray(np.asarray(perm), dtype=np.int32)
+    key = (pm.shape, pm.tobytes(), str(dev))
+    pmd = _AR_PERMS.get(key)
+    if pmd is None:  # checked and copied once per permutation set and device
+        if pm.shape != (d.L, d.D) or any(sorted(r) != list(range(d.D)) for r in pm.tolist()):
+            raise ValueError(f"ar_flow_pack_batched: perm must hold {d.L} permutations of 0..{d.D - 1}")
+        pmd = _AR_PERMS[key] = torch.from_numpy(pm).to(dev)
+    n = int(lib().naz_ar_flow_packed_bytes(d)) // 4
+    if n <= 0:
+        raise RuntimeError("naz_amd ar_flow_pack: unsupported descriptor")
+    out = torch.empty((P, n), device=dev, dtype=torch.float32)
+    check(lib().naz_ar_flow_pack(d, _p(flat), flat.shape[1], _p(pmd), _p(out), n, P, _stream(dev)), "ar_flow_pack")
+    return out
+
+
+def ar_flow_log_prob_batched(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None) -> Tensor:
+    """out[p] = log p(x | ctx) under draw p of ``packed`` [P, image] (naz_ar_flow_log_prob_batched);
+    x [B, D] (the same rows for every draw) or [P, B, D]; one context vector [C] for all rows."""
+    dev = _dev(packed, x, context)
+    P = packed.shape[0]
+    if not packed.is_contiguous():
+        raise ValueError("ar_flow_log_prob_batched: packed must be a contiguous [P, image] tensor")
+    x = x.contiguous()
+    if x.dim() == 2:
+        B, sx = x.shape[0], 0
+    elif x.dim() == 3 and x.shape[0] == P:
+        B, sx = x.shape[1], x.shape[1] * x.shape[2]
+    else:
+        raise ValueError("ar_flow_log_prob_batched: x must be [B, D] or [P, B, D]")
+    ctx = None if context is None else context.reshape(1, -1).contiguous()
+    out = torch.empty((P, B), device=dev, dtype=torch.float32)
+    check(lib().naz_ar_flow_log_prob_batched(d, _p(packed), packed.stride(0), _p(x), x.shape[-1], sx, _p(ctx), 0,
+                                             _p(out), B, B, P, _stream(dev)), "ar_flow_log_prob_batched")
+    return out
 
 
 def ar_flow_log_prob(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,

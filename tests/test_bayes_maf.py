@@ -324,8 +324,8 @@ def test_lp_context_folding(_gpu, D, C, hidden):
     spec = dict(flow_type="maf", D=D, C=C, hidden=hidden, L=2, P=4, B=600, ctx="vec")
     layers, draws, x, ctx = _setup(spec)
     params = _batched_params(draws, "cuda")
-    a = _flow(spec, layers, x, ctx, "cuda")["lp_batched"](params)
-    b = _flow(spec, layers, x, ctx, "cuda", fold_context=False)["lp_batched"](params)
+    a = _flow(spec, layers, x, ctx, "cuda", fused_ar=False)["lp_batched"](params)
+    b = _flow(spec, layers, x, ctx, "cuda", fold_context=False, fused_ar=False)["lp_batched"](params)
     assert torch.allclose(a, b, rtol=2e-5, atol=2e-5), (a - b).abs().max()
     for p, d in enumerate(draws):
         ol = _oracle_layers(layers, d)
@@ -395,8 +395,8 @@ def test_lp_layer_batched_constants():
     spec = dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=4, P=5, B=700, ctx="vec")
     layers, draws, x, ctx = _setup(spec)
     params = _batched_params(draws, "cuda")
-    a = _flow(spec, layers, x, ctx, "cuda")["lp_batched"](params)
-    b = _flow(spec, layers, x, ctx, "cuda", batch_layers=False)["lp_batched"](params)
+    a = _flow(spec, layers, x, ctx, "cuda", fused_ar=False)["lp_batched"](params)
+    b = _flow(spec, layers, x, ctx, "cuda", batch_layers=False, fused_ar=False)["lp_batched"](params)
     assert torch.allclose(a, b, rtol=1e-5, atol=1e-5), (a - b).abs().max()
     for p, d in enumerate(draws):
         ol = _oracle_layers(layers, d)
@@ -449,3 +449,37 @@ def test_sampler_batched_fused_ar_paper_shape(_gpu):
         assert_parity(y[p], y64, y32, what=f"fused-AR sampler y draw {p}")
         assert_parity(lj[p], lj64, lj32, what=f"fused-AR sampler log_j draw {p}", count_factor=3.0)
     np.testing.assert_allclose(y, y_m.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,B", [(5, 700), (3, 1)])
+def test_lp_batched_fused_ar_paper_shape(_gpu, P, B):
+    """At the paper shape the batched log-density packs every draw's inverse image on the device
+    (naz_ar_flow_pack) and runs the whole flow for all draws in ONE naz_ar_flow_log_prob_batched
+    launch; against the numpy restatement of the reference's JAX log_prob, the layer-batched
+    MADE path, and a flow whose masks are not pyro's create_mask (must not take the fused path)."""
+    from naz_amd.flows import bflow_maf as BM
+    spec = dict(D=2, C=2, hidden=[150, 150, 150], L=5, P=P, B=B, ctx="vec", flow_type="maf")
+    layers, draws, x, ctx = _setup(spec)
+    params = _batched_params(draws, "cuda")
+    calls = []
+    orig = BM.ops.ar_flow_log_prob_batched
+    BM.ops.ar_flow_log_prob_batched = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        lp = _flow(spec, layers, x, ctx, "cuda")["lp_batched"](params)
+        assert calls, "the fused batched AR log_prob was not used"
+        # a mask that is not create_mask's for the permutation: the degree passes do not apply
+        bad = [(p_, perm, [m.copy() for m in ms]) for (p_, perm, ms) in layers]
+        bad[0][2][0][0, 0] = 0.0  # a context input of a degree-0 unit
+        calls.clear()
+        _flow(spec, bad, x, ctx, "cuda")["lp_batched"](params)
+        assert not calls
+    finally:
+        BM.ops.ar_flow_log_prob_batched = orig
+    ref = _flow(spec, layers, x, ctx, "cuda", fused_ar=False)["lp_batched"](params)
+    assert torch.allclose(lp, ref, rtol=1e-4, atol=1e-4), (lp - ref).abs().max()
+    lp = lp.cpu().numpy()
+    for p, d in enumerate(draws):
+        ol = _oracle_layers(layers, d)
+        assert_parity(lp[p], J.log_prob(x, ol, ctx), J.log_prob(x, J.cast_layers(ol, np.float32), ctx, np.float32),
+                      what=f"fused-AR lp draw {p}")

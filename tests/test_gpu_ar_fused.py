@@ -187,3 +187,36 @@ def test_fused_ar_inverse_growing_values_stay_finite():
         ref = f.log_prob(x, condition=c)
     assert torch.isfinite(lp).all() and torch.isfinite(ref).all()
     np.testing.assert_allclose(lp.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("spec", [CASES[0], CASES[4]], ids=_id)
+def test_fused_ar_device_pack_and_batched_draws(spec):
+    """naz_ar_flow_pack (device pack of P weight draws) gives the host packer's image bit for bit,
+    and naz_ar_flow_log_prob_batched (grid y = draw, one context vector) gives every draw's
+    naz_ar_flow_log_prob bit for bit, for shared rows (sx = 0) and per-draw rows."""
+    from naz_amd import ops
+    f, _ = _flow(spec)
+    plan = f._plan
+    flat = plan._flat().astype(np.float32)
+    perm = np.stack([n.permutation.detach().cpu().numpy() for n in plan._nets()]).astype(np.int32)
+    flats = [flat, flat * np.float32(1.03), flat * np.float32(0.97)]
+    dev = ops.ar_flow_pack_batched(plan.desc, torch.tensor(np.stack(flats), device=DEV), perm)
+    for p, fl in enumerate(flats):
+        # bit for bit, subnormal f16 lo pieces included (the maf shape's |W| 2^-11 falls below 2^-14)
+        host = ops.ar_flow_pack(plan.desc, fl, perm, DEV)
+        nbad = int((dev[p].view(torch.int32) != host.view(torch.int32)).sum())
+        assert nbad == 0, f"draw {p} image: {nbad} words differ"
+    fwd = ops.ar_flow_pack_fwd_batched(plan.desc, torch.tensor(np.stack(flats), device=DEV))  # the sampler's
+    for p, fl in enumerate(flats):
+        assert torch.equal(fwd[p].view(torch.int32), ops.ar_flow_pack_fwd(plan.desc, fl, DEV).view(torch.int32))
+    n, D, C = 777, spec["D"], spec["C"]
+    x = torch.as_tensor(O.gaussian_mixture(n, D, seed=9)).to(DEV)
+    xs = torch.stack([x, 0.9 * x, 1.1 * x])
+    c1 = torch.as_tensor(O.context_normal(1, C, seed=3)).reshape(-1).to(DEV)
+    shared = ops.ar_flow_log_prob_batched(plan.desc, dev, x, c1)
+    per = ops.ar_flow_log_prob_batched(plan.desc, dev, xs, c1)
+    for p in range(3):
+        assert torch.equal(shared[p], ops.ar_flow_log_prob(plan.desc, dev[p], x, c1))
+        assert torch.equal(per[p], ops.ar_flow_log_prob(plan.desc, dev[p], xs[p], c1))
+    with pytest.raises(ValueError):
+        ops.ar_flow_pack_batched(plan.desc, torch.tensor(np.stack(flats), device=DEV), perm[:, ::-1] * 0)

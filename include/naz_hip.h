@@ -375,11 +375,20 @@ int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t
  * packed + p spk (spk >= naz_ar_flow_packed_bytes / 4).  naz_ar_flow_log_prob_batched: out_lp + p slp
  * [B] = log p(x + p sx | ctx) under draw p (sx = 0: the same rows for every draw; ldc = 0: one
  * context vector); no bounding.  P <= 65535 per call. */
+/* pass0 (nullable, conditional flows with ONE context vector): per draw (stride sp0 >=
+ * naz_ar_flow_pass0_floats) and layer, the per-draw constants of the first degree pass — the
+ * degree-0 hidden units see only the context — as n_hidden x ceil(E0 / 16) blocks of 16 values
+ * (2.8853900817779268 · pre-activation of units 0 .. E0 - 1, E0 = units of mask index 0 per
+ * naz_ar_flow_degrees, the block's remaining slots 0) then ceil(P / 16) blocks of 16 (the ARN outputs
+ * of the first dim in order, rows p D + perm[0], p < P); the packer writes them in place of that
+ * pass's weights, and the image must then be evaluated with pass0_const = 1 and ldc = 0: the
+ * kernel skips the first pass's MFMA work. */
+int64_t naz_ar_flow_pass0_floats(const naz_ar_desc* d);
 int naz_ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
-                     int64_t P, void* stream);
+                     int64_t P, const float* pass0, int64_t sp0, void* stream);
 int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                                  int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B,
-                                 int64_t P, void* stream);
+                                 int64_t P, int pass0_const, void* stream);
 
 /* ---- §8b: whole-flow entries over the fused kinds -------------------------------------
  * One descriptor for the flows whose whole log_prob is one launch: the spline coupling flow (naz

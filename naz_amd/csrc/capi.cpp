@@ -320,20 +320,22 @@ int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t
   return ar_flow_sample_batched(d, packed, spk, z, ldz, sz, ctx, ldc, y, ldy, sy, out_ld, sld, B, P, as_stream(stream));
 }
 
+int64_t naz_ar_flow_pass0_floats(const naz_ar_desc* d) { return ar_flow_pass0_floats(d); }
 int naz_ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
-                     int64_t P, void* stream) {
+                     int64_t P, const float* pass0, int64_t sp0, void* stream) {
   if (P < 0) return set_error("naz_ar_flow_pack: negative draw count");
-  return ar_flow_pack(d, flat, sflat, perm, packed, spk, P, as_stream(stream));
+  return ar_flow_pack(d, flat, sflat, perm, packed, spk, P, pass0, sp0, as_stream(stream));
 }
 int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                                  int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B,
-                                 int64_t P, void* stream) {
+                                 int64_t P, int pass0_const, void* stream) {
   if (B < 0 || P < 0) return set_error("naz_ar_flow_log_prob_batched: negative size");
   if (B > 0 && P > 0 && (packed == nullptr || x == nullptr || out_lp == nullptr))
     return set_error("naz_ar_flow_log_prob_batched: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && P > 0 && ctx == nullptr)
     return set_error("naz_ar_flow_log_prob_batched: conditional flow needs ctx");
-  return ar_flow_log_prob_batched(d, packed, spk, x, ldx, sx, ctx, ldc, out_lp, slp, B, P, as_stream(stream));
+  return ar_flow_log_prob_batched(d, packed, spk, x, ldx, sx, ctx, ldc, out_lp, slp, B, P, pass0_const,
+                                  as_stream(stream));
 }
 
 // ---- §8b whole-flow entries over the fused kinds ----------------------------------------

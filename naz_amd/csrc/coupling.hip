@@ -1488,22 +1488,23 @@ struct AROps {
   }
   static int log_prob(const float* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
                       const float* low, const float* high, float* out_lp, int64_t B, float bound, hipStream_t s,
-                      int64_t P = 1, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0) {
+                      int64_t P = 1, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0, int c0mode = 0) {
     static_assert(2 * CF::STG * 4 <= 160 * 1024, "two weight stages exceed the LDS");
     if (B == 0 || L == 0 || P == 0) return 0;
     if (P > 65535) return set_error("naz_ar_flow_log_prob_batched: at most 65535 draws per call");
     const int64_t rows = 16 * CF::NW, grid = (B + rows - 1) / rows;
     const size_t lds = (size_t)2 * CF::STG * 4;
     hipLaunchKernelGGL((made_ar_r16_kernel<CF>), dim3((unsigned)grid, (unsigned)P), dim3(64 * CF::NW), lds, s, packed,
-                       L, x, ldx, ctx, ldc, low, high, out_lp, B, bound, spk, sx, slp);
+                       L, x, ldx, ctx, ldc, low, high, out_lp, B, bound, spk, sx, slp, c0mode);
     return check_launch("made_ar_r16_kernel");
   }
+  static int64_t pass0_floats() { return CF::C0; }
   static int pack_device(const float* flat, int64_t sflat, const int* perm, float* packed, int64_t spk, int L,
-                         int64_t P, hipStream_t s) {
+                         int64_t P, hipStream_t s, const float* c0 = nullptr, int64_t sc0 = 0) {
     if (L == 0 || P == 0) return 0;
     if (P > 65535 || L > 65535) return set_error("naz_ar_flow_pack: at most 65535 draws / layers per call");
     const dim3 grid((unsigned)((CF::LAYER + 255) / 256), (unsigned)L, (unsigned)P);
-    hipLaunchKernelGGL((made_ar_pack_kernel<CF>), grid, dim3(256), 0, s, flat, sflat, perm, packed, spk);
+    hipLaunchKernelGGL((made_ar_pack_kernel<CF>), grid, dim3(256), 0, s, flat, sflat, perm, packed, spk, c0, sc0);
     return check_launch("made_ar_pack_kernel");
   }
   // forward (sample) direction: made_ar_fwd_kernel over CfgARF's per-layer image
@@ -1643,24 +1644,39 @@ int ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk
   return rc == -2 ? ar_unsupported(d) : rc;
 }
 
+int64_t ar_flow_pass0_floats(const naz_ar_desc* d) {
+  int64_t v = -1;
+  ar_dispatch(d, [&](auto ops) {
+    v = decltype(ops)::pass0_floats() * d->L;
+    return 0;
+  });
+  return v;
+}
+
 int ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
-                 int64_t P, hipStream_t s) {
+                 int64_t P, const float* pass0, int64_t sp0, hipStream_t s) {
   if (flat == nullptr || perm == nullptr || packed == nullptr) return set_error("naz_ar_flow_pack: null pointer");
+  if (pass0 != nullptr && (d == nullptr || d->C <= 0))
+    return set_error("naz_ar_flow_pack: pass-0 constants need a conditional flow");
   const int rc = ar_dispatch(d, [&](auto ops) {
     using O = decltype(ops);
     if (sflat < O::flat_floats() * d->L || spk < O::layer_floats() * d->L)
       return set_error("naz_ar_flow_pack: draw strides shorter than one flow");
-    return O::pack_device(flat, sflat, perm, static_cast<float*>(packed), spk, d->L, P, s);
+    if (pass0 != nullptr && sp0 < O::pass0_floats() * d->L)
+      return set_error("naz_ar_flow_pack: pass-0 stride shorter than one flow");
+    return O::pack_device(flat, sflat, perm, static_cast<float*>(packed), spk, d->L, P, s, pass0, sp0);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }
 
 int ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                              int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B, int64_t P,
-                             hipStream_t s) {
+                             int pass0_const, hipStream_t s) {
+  if (pass0_const && (d == nullptr || d->C <= 0 || ldc != 0))
+    return set_error("naz_ar_flow_log_prob_batched: pass-0 constants need one context vector (ldc = 0)");
   const int rc = ar_dispatch(d, [&](auto ops) {
     return decltype(ops)::log_prob(static_cast<const float*>(packed), d->L, x, ldx, ctx, ldc, nullptr, nullptr, out_lp,
-                                   B, d->bound, s, P, spk, sx, slp);
+                                   B, d->bound, s, P, spk, sx, slp, pass0_const ? 1 : 0);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }

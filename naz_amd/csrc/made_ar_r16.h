@@ -123,6 +123,9 @@ struct CfgAR {
   static constexpr int STG = LY.stg;                  // stage stride = LDS ring slot (floats)
   // per layer: NSTG stages | perm (D ints)
   static constexpr int PERM_OFF = NSTG * STG;
+  // pass-0 constants per layer (one context vector): NHID x nb(0) blocks of 16 kSigScale-scaled
+  // pre-activations, then NOB blocks of 16 output values of the first dim in order
+  static constexpr int C0 = 16 * (NHID * nb_of(LY, 0) + NOB);
   static constexpr int LAYER = pad(PERM_OFF + D);
   // waves per workgroup (one workgroup per CU): 12 (3 per SIMD) when the live set fits 168 VGPRs
   static constexpr int NW = NHID * KSH <= 8 ? 12 : 8;
@@ -234,7 +237,8 @@ template <class CF>
 __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
-    float* __restrict__ out_lp, int64_t B, float bound, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0) {
+    float* __restrict__ out_lp, int64_t B, float bound, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0,
+    int c0mode = 0) {
   constexpr int D = CF::D, K = CF::K, P = CF::P, NW = CF::NW, NHID = CF::NHID;
   {  // blockIdx.y = draw (naz_ar_flow_log_prob_batched): image packed + draw spk, rows x + draw sx
     const int64_t dz = blockIdx.y;
@@ -334,7 +338,31 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
           return Frag2{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
         };
         const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF_BIAS);
+        bool done0 = false;
+        if constexpr (p == 0) {
+          if (c0mode) {
+            // one context vector (naz_ar_flow_pack with pass0): the degree-0 units and the first
+            // dim's parameters are per-draw constants, written by the packer in place of this
+            // pass's fragments (kSigScale-scaled pre-activations / output values, 16 per block)
+            const float4* cv = reinterpret_cast<const float4*>(cur + OFF);
+            if constexpr (i < NHID) {
+              static_for<0, NBP>([&](auto bc) {
+                constexpr int bi = decltype(bc)::value, b = BLO + bi;
+                const float4 c = cv[4 * bi + q];
+                ar_split4<b & 1>(hf[i][b >> 1], floatx4{c.x, c.y, c.z, c.w});
+              });
+            } else {
+#pragma unroll
+              for (int o = 0; o < CF::NOB; ++o) {
+                const float4 c = cv[4 * o + q];
+                o3[o] = floatx4{c.x, c.y, c.z, c.w};
+              }
+            }
+            done0 = true;
+          }
+        }
         if constexpr (i == 0 && NBP > 0) {
+         if (!done0) {
           // ---- hidden layer 1: blocks holding degree-p units, over [ctx | x]
           // the row's values (inverted dims and still-pending ones alike: a masked weight times an
           // f16 overflow would be NaN) split at a per-row power-of-two scale, |x| sc < 2^14: the
@@ -370,9 +398,10 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
             }
             ar_split4<b & 1>(hf[0][b >> 1], acc);
           });
+         }
         } else if constexpr (i > 0 && i < NHID && NBP > 0) {
           // ---- hidden layer i + 1: the same blocks, over layer i's units of degree <= p
-          static_for<0, NBP>([&](auto bc) {
+          if (!done0) static_for<0, NBP>([&](auto bc) {
             constexpr int bi = decltype(bc)::value, b = BLO + bi;
             const float4 bv = bias4[4 * bi + q];
             floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
@@ -382,15 +411,17 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
           });
         } else if constexpr (i == NHID) {
           // ---- the output rows of dim d_p, then the elementwise inverse on x[d_p]
+          if (!done0) {
 #pragma unroll
-          for (int o = 0; o < CF::NOB; ++o) {
-            const float4 bv = bias4[4 * o + q];
-            o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+            for (int o = 0; o < CF::NOB; ++o) {
+              const float4 bv = bias4[4 * o + q];
+              o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+            }
+#pragma unroll
+            for (int t = 0; t < KT; ++t)
+#pragma unroll
+              for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KT + t), hf[NHID - 1][t], o3[o]);
           }
-#pragma unroll
-          for (int t = 0; t < KT; ++t)
-#pragma unroll
-            for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KT + t), hf[NHID - 1][t], o3[o]);
           const float y = v[dp];
           if constexpr (CF::AFFINE) {
             // pyro AffineAutoregressive._inverse: rows 0, 1 = (mean, log_scale) of dim d_p, held by
@@ -640,7 +671,8 @@ __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t 
 // draw; flat as made_ar_pack_fwd_kernel's, perm [L][D] shared by every draw (checked on the host).
 template <class CF>
 __global__ void made_ar_pack_kernel(const float* __restrict__ flat, int64_t sflat, const int* __restrict__ perm,
-                                    float* __restrict__ packed, int64_t spk) {
+                                    float* __restrict__ packed, int64_t spk, const float* __restrict__ c0,
+                                    int64_t sc0) {
   constexpr int D = CF::D, C = CF::C, H = CF::H, P = CF::P, NHID = CF::NHID;
   constexpr int64_t per = (int64_t)H * (C + D) + H + (int64_t)(NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
   const int pos = blockIdx.x * blockDim.x + threadIdx.x;
@@ -670,8 +702,15 @@ __global__ void made_ar_pack_kernel(const float* __restrict__ flat, int64_t sfla
       constexpr int size = nfr * CF::OT + 16 * (i < NHID ? CF::nb(p) : CF::NOB);
       if (done || pos < base || pos >= base + size) return;
       done = true;
-      const int dp = pm[p];
       const int rel = pos - base;
+      if constexpr (p == 0) {
+        if (c0 != nullptr) {  // pass-0 constants (CfgAR::C0 layout) in place of its fragments
+          constexpr int cnt = 16 * (i < NHID ? CF::nb(0) : CF::NOB), cb = 16 * CF::nb(0) * (i < NHID ? i : NHID);
+          if (rel < cnt) word = __builtin_bit_cast(unsigned, c0[blockIdx.z * sc0 + (int64_t)l * CF::C0 + cb + rel]);
+          return;
+        }
+      }
+      const int dp = pm[p];
       if (rel >= nfr * CF::OT) {  // bias
         const int r = rel - nfr * CF::OT;
         float v = 0.f;

@@ -645,10 +645,17 @@ def ar_flow_sample_batched(d: ArDesc, packed: Tensor, z: Tensor, context: Option
 _AR_PERMS: dict = {}
 
 
-def ar_flow_pack_batched(d: ArDesc, flat: Tensor, perm) -> Tensor:
+def ar_flow_pass0_floats(d: ArDesc) -> int:
+    """Floats per draw of naz_ar_flow_pack's pass-0 constants (all L layers)."""
+    return int(lib().naz_ar_flow_pass0_floats(d))
+
+
+def ar_flow_pack_batched(d: ArDesc, flat: Tensor, perm, pass0: Optional[Tensor] = None) -> Tensor:
     """Inverse (log_prob) images of P weight draws packed on the device (naz_ar_flow_pack): flat
     [P, L * per] (the naz_ar_flow_pack_host flat layout, masks applied), perm [L, D] shared by the
-    draws (checked here: the kernel indexes its registers by it) -> [P, image floats]."""
+    draws (checked here: the kernel indexes its registers by it) -> [P, image floats].  pass0
+    [P, ar_flow_pass0_floats]: the first degree pass's per-draw constants (one context vector;
+    include/naz_hip.h) written in place of that pass's weights."""
     dev = _dev(flat)
     flat = flat.contiguous()
     P = flat.shape[0]
@@ -662,14 +669,23 @@ def ar_flow_pack_batched(d: ArDesc, flat: Tensor, perm) -> Tensor:
     n = int(lib().naz_ar_flow_packed_bytes(d)) // 4
     if n <= 0:
         raise RuntimeError("naz_amd ar_flow_pack: unsupported descriptor")
+    sp0 = 0
+    if pass0 is not None:
+        pass0 = pass0.contiguous()
+        sp0 = ar_flow_pass0_floats(d)
+        if pass0.shape != (P, sp0):
+            raise ValueError(f"ar_flow_pack_batched: pass0 must be [{P}, {sp0}]")
     out = torch.empty((P, n), device=dev, dtype=torch.float32)
-    check(lib().naz_ar_flow_pack(d, _p(flat), flat.shape[1], _p(pmd), _p(out), n, P, _stream(dev)), "ar_flow_pack")
+    check(lib().naz_ar_flow_pack(d, _p(flat), flat.shape[1], _p(pmd), _p(out), n, P, _p(pass0), sp0, _stream(dev)),
+          "ar_flow_pack")
     return out
 
 
-def ar_flow_log_prob_batched(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None) -> Tensor:
+def ar_flow_log_prob_batched(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,
+                             pass0_const: bool = False) -> Tensor:
     """out[p] = log p(x | ctx) under draw p of ``packed`` [P, image] (naz_ar_flow_log_prob_batched);
-    x [B, D] (the same rows for every draw) or [P, B, D]; one context vector [C] for all rows."""
+    x [B, D] (the same rows for every draw) or [P, B, D]; one context vector [C] for all rows.
+    pass0_const: the images carry pass-0 constants (ar_flow_pack_batched(pass0=...))."""
     dev = _dev(packed, x, context)
     P = packed.shape[0]
     if not packed.is_contiguous():
@@ -684,7 +700,8 @@ def ar_flow_log_prob_batched(d: ArDesc, packed: Tensor, x: Tensor, context: Opti
     ctx = None if context is None else context.reshape(1, -1).contiguous()
     out = torch.empty((P, B), device=dev, dtype=torch.float32)
     check(lib().naz_ar_flow_log_prob_batched(d, _p(packed), packed.stride(0), _p(x), x.shape[-1], sx, _p(ctx), 0,
-                                             _p(out), B, B, P, _stream(dev)), "ar_flow_log_prob_batched")
+                                             _p(out), B, B, P, int(pass0_const), _stream(dev)),
+          "ar_flow_log_prob_batched")
     return out
 
 

@@ -478,6 +478,9 @@ def test_lp_batched_fused_ar_paper_shape(_gpu, P, B):
         BM.ops.ar_flow_log_prob_batched = orig
     ref = _flow(spec, layers, x, ctx, "cuda", fused_ar=False)["lp_batched"](params)
     assert torch.allclose(lp, ref, rtol=1e-4, atol=1e-4), (lp - ref).abs().max()
+    # fold_context=False: the first degree pass computed per row instead of packed as constants
+    lp_rows = _flow(spec, layers, x, ctx, "cuda", fold_context=False)["lp_batched"](params)
+    assert torch.allclose(lp, lp_rows, rtol=1e-4, atol=1e-4), (lp - lp_rows).abs().max()
     lp = lp.cpu().numpy()
     for p, d in enumerate(draws):
         ol = _oracle_layers(layers, d)

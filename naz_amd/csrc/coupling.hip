@@ -208,6 +208,25 @@ NAZ_DEV void stage_issue(float* lds, const float* __restrict__ src) {
   }
 }
 
+// stage_issue of the first nch (wave-uniform, <= NFLOATS / 256) 1 KB chunks only
+template <int NFLOATS, int NW>
+NAZ_DEV void stage_issue_lim(float* lds, const float* __restrict__ src, int nch) {
+  static_assert(NFLOATS % 256 == 0, "stage must be whole 1 KB chunks");
+  constexpr int CHUNKS = NFLOATS / 256;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  nch = nch < CHUNKS ? nch : CHUNKS;
+#pragma unroll
+  for (int c0 = 0; c0 < CHUNKS; c0 += NW) {
+    const int c = c0 + wave;
+    if (c < nch) {
+      __builtin_amdgcn_global_load_lds(
+          (const void __attribute__((address_space(1)))*)(src + c * 256 + lane * 4),
+          (void __attribute__((address_space(3)))*)(lds + c * 256), 16, 0, 0);
+    }
+  }
+}
+
 // Accumulators init from the packed bias block [o][h][16]
 template <int NB>
 NAZ_DEV void init_bias(floatx16 (&acc)[NB], const float* __restrict__ bias, int h) {

@@ -126,6 +126,22 @@ struct CfgAR {
   // pass-0 constants per layer (one context vector): NHID x nb(0) blocks of 16 kSigScale-scaled
   // pre-activations, then NOB blocks of 16 output values of the first dim in order
   static constexpr int C0 = 16 * (NHID * nb_of(LY, 0) + NOB);
+  // in a pass-0-constant image the constants of pass 0's sub-layer i sit compactly at c0_off(i) of
+  // its stage (pass 0's stages hold nothing else), so those stages stream only c0_chunks(s) KB
+  static constexpr int c0_cnt(int i) { return 16 * (i < NHID ? nb_of(LY, 0) : NOB); }
+  static constexpr int c0_off(int i) {
+    int o = 0;
+    for (int j = 0; j < i; ++j)
+      if (LY.sid[0][j] == LY.sid[0][i]) o += c0_cnt(j);
+    return o;
+  }
+  static constexpr int c0_chunks(int s) {
+    if (s > LY.sid[0][NHID]) return LY.sfl[s] / 256;
+    int e = 0;
+    for (int i = 0; i <= NHID; ++i)
+      if (LY.sid[0][i] == s && c0_off(i) + c0_cnt(i) > e) e = c0_off(i) + c0_cnt(i);
+    return (e + 255) / 256;
+  }
   static constexpr int LAYER = pad(PERM_OFF + D);
   // waves per workgroup (one workgroup per CU): 12 (3 per SIMD) when the live set fits 168 VGPRs
   static constexpr int NW = NHID * KSH <= 8 ? 12 : 8;
@@ -284,7 +300,8 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
 
   const RqsConsts<K, true> rc(bound);
   float ldsum = 0.f;  // the layers' forward log-dets (log p = base - ldsum + logjac)
-  stage_issue<CF::stage_floats(0), NW>(slot0, packed + (int64_t)(L - 1) * CF::LAYER);
+  const int ch0 = c0mode ? CF::c0_chunks(0) : CF::stage_floats(0) / 256;  // stage 0's KB to stream
+  stage_issue_lim<CF::stage_floats(0), NW>(slot0, packed + (int64_t)(L - 1) * CF::LAYER, ch0);
   int g = 0;
   for (int li = 0; li < L; ++li) {
     const int l = L - 1 - li;
@@ -326,9 +343,10 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
           cur = (g & 1) ? slot1 : slot0;
           float* nxt = (g & 1) ? slot0 : slot1;
           if constexpr (SID + 1 < CF::NSTG) {
-            stage_issue<SF_NEXT, NW>(nxt, lp + (SID + 1) * CF::STG);
+            stage_issue_lim<SF_NEXT, NW>(nxt, lp + (SID + 1) * CF::STG,
+                                         c0mode ? CF::c0_chunks(SID + 1) : SF_NEXT / 256);
           } else {
-            if (li + 1 < L) stage_issue<SF_NEXT, NW>(nxt, lnext);
+            if (li + 1 < L) stage_issue_lim<SF_NEXT, NW>(nxt, lnext, ch0);
           }
           ++g;
         }
@@ -344,7 +362,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
             // one context vector (naz_ar_flow_pack with pass0): the degree-0 units and the first
             // dim's parameters are per-draw constants, written by the packer in place of this
             // pass's fragments (kSigScale-scaled pre-activations / output values, 16 per block)
-            const float4* cv = reinterpret_cast<const float4*>(cur + OFF);
+            const float4* cv = reinterpret_cast<const float4*>(cur + CF::c0_off(i));
             if constexpr (i < NHID) {
               static_for<0, NBP>([&](auto bc) {
                 constexpr int bi = decltype(bc)::value, b = BLO + bi;
@@ -693,6 +711,15 @@ __global__ void made_ar_pack_kernel(const float* __restrict__ flat, int64_t sfla
   auto bl = [&](int i) { return Wl(i) + (int64_t)(i < NHID ? H : D * P) * (i == 0 ? C + D : H); };
   unsigned word = 0;
   bool done = false;
+  if (c0 != nullptr) {  // pass-0 stages: only the constants, compact per stage (CfgAR::c0_off)
+    static_for<0, NHID + 1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int sb = CF::stage_id(0, i) * CF::STG, co = sb + CF::c0_off(i), cnt = CF::c0_cnt(i);
+      constexpr int cb = 16 * CF::nb(0) * (i < NHID ? i : NHID);
+      if (pos >= sb && pos < sb + CF::STG) done = true;
+      if (pos >= co && pos < co + cnt) word = __builtin_bit_cast(unsigned, c0[blockIdx.z * sc0 + (int64_t)l * CF::C0 + cb + pos - co]);
+    });
+  }
   static_for<0, D>([&](auto pc) {
     constexpr int p = decltype(pc)::value;
     static_for<0, NHID + 1>([&](auto ic) {
@@ -703,13 +730,6 @@ __global__ void made_ar_pack_kernel(const float* __restrict__ flat, int64_t sfla
       if (done || pos < base || pos >= base + size) return;
       done = true;
       const int rel = pos - base;
-      if constexpr (p == 0) {
-        if (c0 != nullptr) {  // pass-0 constants (CfgAR::C0 layout) in place of its fragments
-          constexpr int cnt = 16 * (i < NHID ? CF::nb(0) : CF::NOB), cb = 16 * CF::nb(0) * (i < NHID ? i : NHID);
-          if (rel < cnt) word = __builtin_bit_cast(unsigned, c0[blockIdx.z * sc0 + (int64_t)l * CF::C0 + cb + rel]);
-          return;
-        }
-      }
       const int dp = pm[p];
       if (rel >= nfr * CF::OT) {  // bias
         const int r = rel - nfr * CF::OT;

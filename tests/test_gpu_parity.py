@@ -248,7 +248,12 @@ def test_full_size_exact_properties():
     x = torch.as_tensor(O.gaussian_mixture(B, 16, seed=0), device=DEV)
     c = torch.randn(B, 32, device=DEV, generator=g)
     lp = f.log_prob(x, condition=c)
-    assert bool(torch.isfinite(lp).all())
+    bad = torch.nonzero(~torch.isfinite(lp)).reshape(-1)
+    if bad.numel():  # name the rows (seen once, not reproduced) and whether they repeat
+        again = f.log_prob(x[bad[:8]], condition=c[bad[:8]])
+        pytest.fail(f"non-finite log_prob in {bad.numel()} rows {bad[:8].tolist()} (128-row workgroups "
+                    f"{(bad // 128).unique()[:8].tolist()}): {lp[bad[:8]].tolist()}; the same rows alone: "
+                    f"{again.tolist()}")
     assert torch.equal(lp, f.log_prob(x, condition=c))  # deterministic
     perm = torch.randperm(B, device=DEV, generator=g)
     assert torch.equal(f.log_prob(x[perm], condition=c[perm]), lp[perm])

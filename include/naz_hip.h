@@ -360,9 +360,11 @@ int naz_ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z,
  * flat layout, masks applied), images at packed + p spk (spk >= naz_ar_flow_fwd_packed_bytes / 4).
  * naz_ar_flow_sample_batched: draw p maps z + p sz -> y + p sy (B rows each, row strides ldz /
  * ldy), out_ld + p sld (nullable) = Σ forward log-dets; ctx shared by every draw (ldc = 0: one
- * context vector).  P <= 65535 per call. */
+ * context vector).  P <= 65535 per call.  mask (nullable, both device packers): the L x per masks
+ * in the flat layout (biases 1), shared by every draw; then flat rows are the UNMASKED weights
+ * (e.g. the front end's posterior draws as stored) and the packer applies the masks. */
 int naz_ar_flow_pack_fwd(const naz_ar_desc* d, const float* flat, int64_t sflat, void* packed, int64_t spk, int64_t P,
-                         void* stream);
+                         const float* mask, void* stream);
 int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* z, int64_t ldz,
                                int64_t sz, const float* ctx, int64_t ldc, float* y, int64_t ldy, int64_t sy,
                                float* out_ld, int64_t sld, int64_t B, int64_t P, void* stream);
@@ -385,7 +387,7 @@ int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t
  * kernel skips the first pass's MFMA work. */
 int64_t naz_ar_flow_pass0_floats(const naz_ar_desc* d);
 int naz_ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
-                     int64_t P, const float* pass0, int64_t sp0, void* stream);
+                     int64_t P, const float* pass0, int64_t sp0, const float* mask, void* stream);
 int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                                  int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B,
                                  int64_t P, int pass0_const, void* stream);

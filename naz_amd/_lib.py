@@ -95,10 +95,10 @@ SIGNATURES = {
     "naz_ar_flow_log_prob": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
     "naz_ar_flow_fwd_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),
     "naz_ar_flow_pass0_floats": (C.c_int64, [C.POINTER(ArDesc)]),
-    "naz_ar_flow_pack": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp]),
+    "naz_ar_flow_pack": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
     "naz_ar_flow_log_prob_batched": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
                                                _i64, _i64, _i, _vp]),
-    "naz_ar_flow_pack_fwd": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _i64, _i64, _vp]),
+    "naz_ar_flow_pack_fwd": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _i64, _i64, _vp, _vp]),
     "naz_ar_flow_sample_batched": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
                                              _i64, _vp, _i64, _i64, _i64, _vp]),
     "naz_ar_flow_pack_fwd_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp]),

@@ -305,9 +305,9 @@ int naz_ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z,
 }
 
 int naz_ar_flow_pack_fwd(const naz_ar_desc* d, const float* flat, int64_t sflat, void* packed, int64_t spk, int64_t P,
-                         void* stream) {
+                         const float* mask, void* stream) {
   if (P < 0) return set_error("naz_ar_flow_pack_fwd: negative draw count");
-  return ar_flow_pack_fwd(d, flat, sflat, packed, spk, P, as_stream(stream));
+  return ar_flow_pack_fwd(d, flat, sflat, packed, spk, P, mask, as_stream(stream));
 }
 int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* z, int64_t ldz,
                                int64_t sz, const float* ctx, int64_t ldc, float* y, int64_t ldy, int64_t sy,
@@ -322,9 +322,9 @@ int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t
 
 int64_t naz_ar_flow_pass0_floats(const naz_ar_desc* d) { return ar_flow_pass0_floats(d); }
 int naz_ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
-                     int64_t P, const float* pass0, int64_t sp0, void* stream) {
+                     int64_t P, const float* pass0, int64_t sp0, const float* mask, void* stream) {
   if (P < 0) return set_error("naz_ar_flow_pack: negative draw count");
-  return ar_flow_pack(d, flat, sflat, perm, packed, spk, P, pass0, sp0, as_stream(stream));
+  return ar_flow_pack(d, flat, sflat, perm, packed, spk, P, pass0, sp0, mask, as_stream(stream));
 }
 int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                                  int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B,

@@ -1519,11 +1519,13 @@ struct AROps {
   }
   static int64_t pass0_floats() { return CF::C0; }
   static int pack_device(const float* flat, int64_t sflat, const int* perm, float* packed, int64_t spk, int L,
-                         int64_t P, hipStream_t s, const float* c0 = nullptr, int64_t sc0 = 0) {
+                         int64_t P, hipStream_t s, const float* c0 = nullptr, int64_t sc0 = 0,
+                         const float* mask = nullptr) {
     if (L == 0 || P == 0) return 0;
     if (P > 65535 || L > 65535) return set_error("naz_ar_flow_pack: at most 65535 draws / layers per call");
     const dim3 grid((unsigned)((CF::LAYER + 255) / 256), (unsigned)L, (unsigned)P);
-    hipLaunchKernelGGL((made_ar_pack_kernel<CF>), grid, dim3(256), 0, s, flat, sflat, perm, packed, spk, c0, sc0);
+    hipLaunchKernelGGL((made_ar_pack_kernel<CF>), grid, dim3(256), 0, s, flat, sflat, perm, packed, spk, c0, sc0,
+                       mask);
     return check_launch("made_ar_pack_kernel");
   }
   // forward (sample) direction: made_ar_fwd_kernel over CfgARF's per-layer image
@@ -1551,11 +1553,11 @@ struct AROps {
     return (int64_t)H * (C + D) + H + (int64_t)(CF::NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
   }
   static int pack_fwd_device(const float* flat, int64_t sflat, float* packed, int64_t spk, int L, int64_t P,
-                             hipStream_t s) {
+                             hipStream_t s, const float* mask = nullptr) {
     if (L == 0 || P == 0) return 0;
     if (P > 65535 || L > 65535) return set_error("naz_ar_flow_pack_fwd: at most 65535 draws / layers per call");
     const dim3 grid((unsigned)((FW::LAYER + 255) / 256), (unsigned)L, (unsigned)P);
-    hipLaunchKernelGGL((made_ar_pack_fwd_kernel<FW>), grid, dim3(256), 0, s, flat, sflat, packed, spk);
+    hipLaunchKernelGGL((made_ar_pack_fwd_kernel<FW>), grid, dim3(256), 0, s, flat, sflat, packed, spk, mask);
     return check_launch("made_ar_pack_fwd_kernel");
   }
 };
@@ -1642,13 +1644,13 @@ int ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z, int
 }
 
 int ar_flow_pack_fwd(const naz_ar_desc* d, const float* flat, int64_t sflat, void* packed, int64_t spk, int64_t P,
-                     hipStream_t s) {
+                     const float* mask, hipStream_t s) {
   if (flat == nullptr || packed == nullptr) return set_error("naz_ar_flow_pack_fwd: null pointer");
   const int rc = ar_dispatch(d, [&](auto ops) {
     using O = decltype(ops);
     if (sflat < O::flat_floats() * d->L || spk < O::fwd_layer_floats() * d->L)
       return set_error("naz_ar_flow_pack_fwd: draw strides shorter than one flow");
-    return O::pack_fwd_device(flat, sflat, static_cast<float*>(packed), spk, d->L, P, s);
+    return O::pack_fwd_device(flat, sflat, static_cast<float*>(packed), spk, d->L, P, s, mask);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }
@@ -1673,7 +1675,7 @@ int64_t ar_flow_pass0_floats(const naz_ar_desc* d) {
 }
 
 int ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
-                 int64_t P, const float* pass0, int64_t sp0, hipStream_t s) {
+                 int64_t P, const float* pass0, int64_t sp0, const float* mask, hipStream_t s) {
   if (flat == nullptr || perm == nullptr || packed == nullptr) return set_error("naz_ar_flow_pack: null pointer");
   if (pass0 != nullptr && (d == nullptr || d->C <= 0))
     return set_error("naz_ar_flow_pack: pass-0 constants need a conditional flow");
@@ -1683,7 +1685,7 @@ int ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const i
       return set_error("naz_ar_flow_pack: draw strides shorter than one flow");
     if (pass0 != nullptr && sp0 < O::pass0_floats() * d->L)
       return set_error("naz_ar_flow_pack: pass-0 stride shorter than one flow");
-    return O::pack_device(flat, sflat, perm, static_cast<float*>(packed), spk, d->L, P, s, pass0, sp0);
+    return O::pack_device(flat, sflat, perm, static_cast<float*>(packed), spk, d->L, P, s, pass0, sp0, mask);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }

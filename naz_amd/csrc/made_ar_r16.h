@@ -612,7 +612,7 @@ NAZ_DEV unsigned ar_piece_dev(float v, int piece) {
 
 template <class CF>
 __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t sflat, float* __restrict__ packed,
-                                        int64_t spk) {
+                                        int64_t spk, const float* __restrict__ mask) {
   constexpr int D = CF::D, C = CF::C, H = CF::H, P = CF::P, HB = CF::HB, KSH = CF::KSH, NHID = CF::NHID;
   constexpr int64_t per = (int64_t)H * (C + D) + H + (int64_t)(NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
   const int pos = blockIdx.x * blockDim.x + threadIdx.x;
@@ -627,6 +627,13 @@ __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t 
     return f + o;
   };
   auto bl = [&](int i) { return Wl(i) + (int64_t)(i < NHID ? H : D * P) * (i == 0 ? C + D : H); };
+  // weight idx of sub-layer i, times its mask entry when the caller passes the masks (per layer,
+  // the flat layout, shared by every draw) instead of pre-masked rows
+  const float* mk = mask == nullptr ? nullptr : mask + (int64_t)l * per;
+  auto wv = [&](int i, int64_t idx) {
+    const int64_t o = (Wl(i) - f) + idx;
+    return mk == nullptr ? f[o] : f[o] * mk[o];
+  };
   unsigned word = 0;
   bool done = false;
   static_for<0, CF::NU>([&](auto uc) {
@@ -661,14 +668,14 @@ __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t 
         if (un < H) {
           if constexpr (i > 0) {
             const int vv = r16_feat(t, kg, j);
-            if (vv < H) v = -2.f * kSigScale * Wl(i)[(int64_t)un * H + vv];
+            if (vv < H) v = -2.f * kSigScale * wv(i, (int64_t)un * H + vv);
           } else {
             if (t < CF::KC) {
               const int col = 32 * t + 8 * kg + j;
-              if (col < C) v = kSigScale * Wl(0)[(int64_t)un * (C + D) + col];
+              if (col < C) v = kSigScale * wv(0, (int64_t)un * (C + D) + col);
             } else {
               const int dd = 8 * kg + j;
-              if (dd < D) v = kSigScale * Wl(0)[(int64_t)un * (C + D) + C + dd];
+              if (dd < D) v = kSigScale * wv(0, (int64_t)un * (C + D) + C + dd);
             }
           }
         }
@@ -676,7 +683,7 @@ __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t 
         constexpr int d = u - NHID * HB;
         const int o = fr / KSH, t = fr % KSH;
         const int pi = 16 * o + m, vv = r16_feat(t, kg, j);
-        if (pi < P && vv < H) v = -2.f * Wl(NHID)[((int64_t)pi * D + d) * H + vv];
+        if (pi < P && vv < H) v = -2.f * wv(NHID, ((int64_t)pi * D + d) * H + vv);
       }
       word |= ar_piece_dev(v, piece) << (16 * e);
     }
@@ -690,7 +697,7 @@ __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t 
 template <class CF>
 __global__ void made_ar_pack_kernel(const float* __restrict__ flat, int64_t sflat, const int* __restrict__ perm,
                                     float* __restrict__ packed, int64_t spk, const float* __restrict__ c0,
-                                    int64_t sc0) {
+                                    int64_t sc0, const float* __restrict__ mask) {
   constexpr int D = CF::D, C = CF::C, H = CF::H, P = CF::P, NHID = CF::NHID;
   constexpr int64_t per = (int64_t)H * (C + D) + H + (int64_t)(NHID - 1) * (H * H + H) + (int64_t)D * P * H + D * P;
   const int pos = blockIdx.x * blockDim.x + threadIdx.x;
@@ -709,6 +716,13 @@ __global__ void made_ar_pack_kernel(const float* __restrict__ flat, int64_t sfla
     return f + o;
   };
   auto bl = [&](int i) { return Wl(i) + (int64_t)(i < NHID ? H : D * P) * (i == 0 ? C + D : H); };
+  // weight idx of sub-layer i, times its mask entry when the caller passes the masks (per layer,
+  // the flat layout, shared by every draw) instead of pre-masked rows
+  const float* mk = mask == nullptr ? nullptr : mask + (int64_t)l * per;
+  auto wv = [&](int i, int64_t idx) {
+    const int64_t o = (Wl(i) - f) + idx;
+    return mk == nullptr ? f[o] : f[o] * mk[o];
+  };
   unsigned word = 0;
   bool done = false;
   if (c0 != nullptr) {  // pass-0 stages: only the constants, compact per stage (CfgAR::c0_off)
@@ -756,20 +770,20 @@ __global__ void made_ar_pack_kernel(const float* __restrict__ flat, int64_t sfla
             if (u < H) {
               if constexpr (i > 0) {
                 const int vv = r16_feat(t, kg, j);
-                if (vv < H) v = -2.f * kSigScale * Wl(i)[(int64_t)u * H + vv];
+                if (vv < H) v = -2.f * kSigScale * wv(i, (int64_t)u * H + vv);
               } else if (t < CF::KC) {
                 const int col = 32 * t + 8 * kg + j;
-                if (col < C) v = kSigScale * Wl(0)[(int64_t)u * (C + D) + col];
+                if (col < C) v = kSigScale * wv(0, (int64_t)u * (C + D) + col);
               } else {
                 const int dd = 8 * kg + j;
-                if (dd < D) v = kSigScale * Wl(0)[(int64_t)u * (C + D) + C + dd];
+                if (dd < D) v = kSigScale * wv(0, (int64_t)u * (C + D) + C + dd);
               }
             }
           } else {
             constexpr int kts = CF::kt(p);
             const int o = fr / kts, t = fr % kts;
             const int pi = 16 * o + m, vv = r16_feat(t, kg, j);
-            if (pi < P && vv < H) v = -2.f * Wl(NHID)[((int64_t)pi * D + dp) * H + vv];
+            if (pi < P && vv < H) v = -2.f * wv(NHID, ((int64_t)pi * D + dp) * H + vv);
           }
           word |= ar_piece_dev(v, piece) << (16 * e);
         }

@@ -91,13 +91,13 @@ int ar_flow_pack_fwd_host(const naz_ar_desc* d, const float* flat, void* packed)
 int ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx, int64_t ldc,
                    const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B, hipStream_t s);
 int ar_flow_pack_fwd(const naz_ar_desc* d, const float* flat, int64_t sflat, void* packed, int64_t spk, int64_t P,
-                     hipStream_t s);
+                     const float* mask, hipStream_t s);
 int ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* z, int64_t ldz,
                            int64_t sz, const float* ctx, int64_t ldc, float* y, int64_t ldy, int64_t sy, float* out_ld,
                            int64_t sld, int64_t B, int64_t P, hipStream_t s);
 int64_t ar_flow_pass0_floats(const naz_ar_desc* d);
 int ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
-                 int64_t P, const float* pass0, int64_t sp0, hipStream_t s);
+                 int64_t P, const float* pass0, int64_t sp0, const float* mask, hipStream_t s);
 int ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                              int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B, int64_t P,
                              int pass0_const, hipStream_t s);

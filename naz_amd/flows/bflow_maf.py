@@ -525,13 +525,30 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
                                      ops.LD_ROWSUM_SUB)
         ops.base_log_prob(z.reshape(P * B, D), out=lp, accumulate=True)
 
+    ar_mask = torch.cat(ar_maskvec) if ar_desc is not None else None  # [L * per], the packers apply it
+
+    def _ar_flat(params: Params, P: int) -> Tensor:
+        """[P, L * per] unmasked flat rows in the packers' layout (ravel order): a zero-copy view
+        when the pytree is unravel()'s views of one [P, n] row buffer, else one concatenation."""
+        ts = [t for layer in params for (w, b) in layer for t in (w, b)]
+        base, off, ok = ts[0], 0, True
+        S = base.stride(0) if base.dim() else 0
+        for t in ts:
+            ok = ok and t.dtype == torch.float32 and t.device == base.device and t.dim() >= 1 and \
+                t.shape[0] == P and (P == 1 or t.stride(0) == S) and t[0].is_contiguous() and \
+                t.data_ptr() - base.data_ptr() == 4 * off
+            off += t[0].numel()
+        if ok and (P == 1 or S >= off):
+            return base.as_strided((P, off), (S if P > 1 else off, 1))
+        return torch.cat([t.reshape(P, -1).to(dev, torch.float32) for t in ts], 1)
+
     def _lp_chunk_ar(params: Params, out: Tensor):
         """Every draw's inverse image packed on the device (naz_ar_flow_pack), then the whole flow
         for all draws in one naz_ar_flow_log_prob_batched launch (csrc/made_ar_r16.h)."""
         P = _draws(params)
-        flat = torch.cat([_flat_layer(params[l], P, dev)[:, 1:] * ar_maskvec[l] for l in range(len(plans))], 1)
+        flat = _ar_flat(params, P)
         c0 = _ar_pass0(flat, P) if ar_pass0 else None
-        packed = ops.ar_flow_pack_batched(ar_desc, flat, ar_perm, pass0=c0)
+        packed = ops.ar_flow_pack_batched(ar_desc, flat, ar_perm, pass0=c0, mask=ar_mask)
         out.copy_(ops.ar_flow_log_prob_batched(ar_desc, packed, x, ctx, pass0_const=c0 is not None))
 
     def _ar_pass0_maps():
@@ -566,7 +583,7 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         nb = (e0 + 15) // 16
         h, pres = None, []
         for i, (wm, bm) in enumerate(ar_maps):
-            W = flat[:, wm].reshape(P * L, *wm.shape[1:])
+            W = (flat[:, wm] * ar_mask[wm]).reshape(P * L, *wm.shape[1:])
             b = flat[:, bm].reshape(P * L, -1)
             if i == nh:
                 o = ops.linear_act_batched(h, W, b, "identity")
@@ -611,8 +628,7 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         lj = lj_out.reshape(P * S)
         ops.base_log_prob(z.reshape(P * S, D), out=lj)
         if ar_desc is not None and (ctx_s is None or float(ctx_s.abs().max()) < 32768.0):
-            flat = torch.cat([_flat_layer(params[l], P, dev)[:, 1:] * ar_maskvec[l] for l in range(len(plans))], 1)
-            packed = ops.ar_flow_pack_fwd_batched(ar_desc, flat)
+            packed = ops.ar_flow_pack_fwd_batched(ar_desc, _ar_flat(params, P), mask=ar_mask)
             y, ld = ops.ar_flow_sample_batched(ar_desc, packed, z, ctx_s)
             y_out.copy_(y)
             lj_out.add_(ld)

@@ -611,17 +611,29 @@ def ar_flow_sample(d: ArDesc, packed_fwd: Tensor, z: Tensor, context: Optional[T
     return y, ld
 
 
-def ar_flow_pack_fwd_batched(d: ArDesc, flat: Tensor) -> Tensor:
+def _flat_rows(flat: Tensor):
+    """(flat, draw stride) of a [P, n] operand with unit column stride (rows may be strided)."""
+    if flat.dim() != 2:
+        raise ValueError("flat must be [P, L * per]")
+    if flat.stride(1) != 1 or (flat.shape[0] > 1 and flat.stride(0) < flat.shape[1]):
+        flat = flat.contiguous()
+    return flat, (flat.stride(0) if flat.shape[0] > 1 else flat.shape[1])
+
+
+def ar_flow_pack_fwd_batched(d: ArDesc, flat: Tensor, mask: Optional[Tensor] = None) -> Tensor:
     """Forward images of P weight draws packed on the device (naz_ar_flow_pack_fwd): flat [P, L * per]
-    (the naz_ar_flow_pack_host flat layout, masks applied) -> [P, image floats]."""
-    dev = _dev(flat)
-    flat = flat.contiguous()
+    (the naz_ar_flow_pack_host flat layout; masks applied, or given as ``mask`` [L * per]) ->
+    [P, image floats]."""
+    dev = _dev(flat, mask)
+    flat, sflat = _flat_rows(flat)
     P = flat.shape[0]
     n = int(lib().naz_ar_flow_fwd_packed_bytes(d)) // 4
     if n <= 0:
         raise RuntimeError("naz_amd ar_flow_pack_fwd: unsupported descriptor")
     out = torch.empty((P, n), device=dev, dtype=torch.float32)
-    check(lib().naz_ar_flow_pack_fwd(d, _p(flat), flat.shape[1], _p(out), n, P, _stream(dev)), "ar_flow_pack_fwd")
+    if mask is not None and (mask.numel() != flat.shape[1] or not mask.is_contiguous()):
+        raise ValueError("ar_flow_pack_fwd_batched: mask must be a contiguous [L * per] tensor")
+    check(lib().naz_ar_flow_pack_fwd(d, _p(flat), sflat, _p(out), n, P, _p(mask), _stream(dev)), "ar_flow_pack_fwd")
     return out
 
 
@@ -650,15 +662,18 @@ def ar_flow_pass0_floats(d: ArDesc) -> int:
     return int(lib().naz_ar_flow_pass0_floats(d))
 
 
-def ar_flow_pack_batched(d: ArDesc, flat: Tensor, perm, pass0: Optional[Tensor] = None) -> Tensor:
+def ar_flow_pack_batched(d: ArDesc, flat: Tensor, perm, pass0: Optional[Tensor] = None,
+                         mask: Optional[Tensor] = None) -> Tensor:
     """Inverse (log_prob) images of P weight draws packed on the device (naz_ar_flow_pack): flat
     [P, L * per] (the naz_ar_flow_pack_host flat layout, masks applied), perm [L, D] shared by the
     draws (checked here: the kernel indexes its registers by it) -> [P, image floats].  pass0
     [P, ar_flow_pass0_floats]: the first degree pass's per-draw constants (one context vector;
     include/naz_hip.h) written in place of that pass's weights."""
-    dev = _dev(flat)
-    flat = flat.contiguous()
+    dev = _dev(flat, mask)
+    flat, sflat = _flat_rows(flat)
     P = flat.shape[0]
+    if mask is not None and (mask.numel() != flat.shape[1] or not mask.is_contiguous()):
+        raise ValueError("ar_flow_pack_batched: mask must be a contiguous [L * per] tensor")
     pm = np.ascontiguousarray(np.asarray(perm), dtype=np.int32)
     key = (pm.shape, pm.tobytes(), str(dev))
     pmd = _AR_PERMS.get(key)
@@ -676,8 +691,8 @@ def ar_flow_pack_batched(d: ArDesc, flat: Tensor, perm, pass0: Optional[Tensor] 
         if pass0.shape != (P, sp0):
             raise ValueError(f"ar_flow_pack_batched: pass0 must be [{P}, {sp0}]")
     out = torch.empty((P, n), device=dev, dtype=torch.float32)
-    check(lib().naz_ar_flow_pack(d, _p(flat), flat.shape[1], _p(pmd), _p(out), n, P, _p(pass0), sp0, _stream(dev)),
-          "ar_flow_pack")
+    check(lib().naz_ar_flow_pack(d, _p(flat), sflat, _p(pmd), _p(out), n, P, _p(pass0), sp0, _p(mask),
+                                 _stream(dev)), "ar_flow_pack")
     return out
 
 

@@ -478,6 +478,10 @@ def test_lp_batched_fused_ar_paper_shape(_gpu, P, B):
         BM.ops.ar_flow_log_prob_batched = orig
     ref = _flow(spec, layers, x, ctx, "cuda", fused_ar=False)["lp_batched"](params)
     assert torch.allclose(lp, ref, rtol=1e-4, atol=1e-4), (lp - ref).abs().max()
+    # the same draws as unravel()'s views of one [P, n] buffer (the packers read it in place)
+    flat_draws = BM.ravel(params)
+    assert torch.equal(_flow(spec, layers, x, ctx, "cuda")["lp_batched"](BM.unravel(flat_draws, [
+        [tuple(t.shape[1:] for t in wb) for wb in layer] for layer in params])), lp)
     # fold_context=False: the first degree pass computed per row instead of packed as constants
     lp_rows = _flow(spec, layers, x, ctx, "cuda", fold_context=False)["lp_batched"](params)
     assert torch.allclose(lp, lp_rows, rtol=1e-4, atol=1e-4), (lp - lp_rows).abs().max()

@@ -209,6 +209,15 @@ def test_fused_ar_device_pack_and_batched_draws(spec):
     fwd = ops.ar_flow_pack_fwd_batched(plan.desc, torch.tensor(np.stack(flats), device=DEV))  # the sampler's
     for p, fl in enumerate(flats):
         assert torch.equal(fwd[p].view(torch.int32), ops.ar_flow_pack_fwd(plan.desc, fl, DEV).view(torch.int32))
+    # unmasked rows + the mask vector (the Bayesian front end's path): the packers' product equals
+    # packing the rows masked beforehand, bit for bit (same fp32 multiply)
+    ft = torch.tensor(np.stack(flats), device=DEV)
+    mask = (ft[0] != 0).float()
+    noisy = ft + torch.rand_like(ft) * (1 - mask)
+    assert torch.equal(ops.ar_flow_pack_batched(plan.desc, noisy, perm, mask=mask).view(torch.int32),
+                       ops.ar_flow_pack_batched(plan.desc, noisy * mask, perm).view(torch.int32))
+    assert torch.equal(ops.ar_flow_pack_fwd_batched(plan.desc, noisy, mask=mask).view(torch.int32),
+                       ops.ar_flow_pack_fwd_batched(plan.desc, noisy * mask).view(torch.int32))
     n, D, C = 777, spec["D"], spec["C"]
     x = torch.as_tensor(O.gaussian_mixture(n, D, seed=9)).to(DEV)
     xs = torch.stack([x, 0.9 * x, 1.1 * x])

@@ -110,6 +110,27 @@ def _slices(param_dims: Sequence[int]):
 # conditioner chains under autograd run as one ChainFn node (act' fused into the dX GEMMs);
 # NAZ_CHAIN_NODE=0 selects the LinearActFn-per-layer walk (A/B, tests)
 _CHAIN_NODE = os.environ.get("NAZ_CHAIN_NODE", "1") != "0"
+# run_grad's block gathers: every masked / padding entry gets its own zero slot, so a gather's
+# indices are unique and its backward is a plain scatter (NAZ_GATHER_SORT=1: torch's indexing
+# backward, which sorts the indices to accumulate the duplicates of a shared zero slot)
+_GATHER_UNIQUE = os.environ.get("NAZ_GATHER_SORT", "0") != "1"
+
+
+class _GatherUnique(torch.autograd.Function):
+    """F[idx] for indices without duplicates: backward scatters the gradient (no accumulation)."""
+
+    @staticmethod
+    def forward(ctx, F, idx):
+        ctx.save_for_backward(idx)
+        ctx.n = F.numel()
+        return F[idx]
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, = ctx.saved_tensors
+        gF = g.new_zeros(ctx.n)
+        gF[idx] = g
+        return gF, None
 
 
 def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Tensor], masked: bool,
@@ -502,10 +523,26 @@ class ARInversePlan:
         widths, hidden, outs = degree_schedule(arn.permutation.cpu(), [l.mask.detach().to(**cpu) for l in layers],
                                                wi, bi, arn.input_dim, arn.context_dim, arn.output_multiplier)
         dev = layers[0].weight.device
-        hidden = [[(li, a, b, n, w.round().long().to(dev), bb.round().long().to(dev)) for (li, a, b, n, w, bb) in g]
-                  for g in hidden]
-        outs = [(i, n, w.round().long().to(dev), bb.round().long().to(dev)) for (i, n, w, bb) in outs]
-        self._imap, self._imap_key = (widths, hidden, outs), key
+        nxt = [off]  # next zero slot past F's parameters
+
+        def ix(t):
+            t = t.round().long()
+            if _GATHER_UNIQUE:  # each masked / padding entry its own zero slot
+                z = t == 0
+                k = int(z.sum())
+                t[z] = torch.arange(nxt[0], nxt[0] + k)
+                nxt[0] += k
+            return t
+        hidden = [[(li, a, b, n, ix(w), ix(bb)) for (li, a, b, n, w, bb) in g] for g in hidden]
+        outs = [(i, n, ix(w), ix(bb)) for (i, n, w, bb) in outs]
+        if _GATHER_UNIQUE:
+            allix = torch.cat([t.reshape(-1) for g in hidden for blk in g for t in blk[4:]] +
+                              [t.reshape(-1) for o in outs for t in o[2:]])
+            assert allix.unique().numel() == allix.numel(), "degree schedule gathers a parameter twice"
+        to = lambda t: t.to(dev)  # noqa: E731
+        hidden = [[(li, a, b, n, to(w), to(bb)) for (li, a, b, n, w, bb) in g] for g in hidden]
+        outs = [(i, n, to(w), to(bb)) for (i, n, w, bb) in outs]
+        self._imap, self._imap_key, self._nzero = (widths, hidden, outs), key, nxt[0] - off
         return self._imap
 
     def run_grad(self, v: torch.Tensor, context: Optional[torch.Tensor], step):
@@ -516,7 +553,14 @@ class ARInversePlan:
         B, D = v.shape
         widths, hidden, outs = self.index_maps()
         layers = list(self.arn.layers)
-        F = torch.cat([v.new_zeros(1)] + [t.reshape(-1) for l in layers for t in (l.weight, l.bias)])
+        F = torch.cat([v.new_zeros(1)] + [t.reshape(-1) for l in layers for t in (l.weight, l.bias)] +
+                      [v.new_zeros(self._nzero)])
+        if _GATHER_UNIQUE:
+            def G(idx):
+                return _GatherUnique.apply(F, idx)
+        else:
+            def G(idx):
+                return F[idx]
         act = self.arn.act
         cols = [v.new_zeros(B, 1) for _ in range(D)]
         done = [[] for _ in widths]  # per hidden layer: its group outputs in degree order
@@ -525,15 +569,15 @@ class ARInversePlan:
             x = torch.cat(cols, 1)
             for (li, a, b, n, wi, bi) in hidden[k - 1]:
                 if li == 0:
-                    h = ag.linear_act(x, F[wi], F[bi], act, context=context)
+                    h = ag.linear_act(x, G(wi), G(bi), act, context=context)
                 else:
-                    h = ag.linear_act(torch.cat(done[li - 1], 1)[:, :n], F[wi], F[bi], act)
+                    h = ag.linear_act(torch.cat(done[li - 1], 1)[:, :n], G(wi), G(bi), act)
                 done[li].append(h)
             i, n, wi, bi = outs[k - 1]
             if n:
-                raw = ag.linear_act(torch.cat(done[-1], 1)[:, :n], F[wi], F[bi], "identity")
+                raw = ag.linear_act(torch.cat(done[-1], 1)[:, :n], G(wi), G(bi), "identity")
             else:
-                raw = F[bi].reshape(1, -1).expand(B, -1)
+                raw = G(bi).reshape(1, -1).expand(B, -1)
             xi, ldi = step(k, i, raw)
             cols[i] = xi
             ld = ldi if ld is None else ld + ldi

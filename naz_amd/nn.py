@@ -116,21 +116,26 @@ _CHAIN_NODE = os.environ.get("NAZ_CHAIN_NODE", "1") != "0"
 _GATHER_UNIQUE = os.environ.get("NAZ_GATHER_SORT", "0") != "1"
 
 
-class _GatherUnique(torch.autograd.Function):
-    """F[idx] for indices without duplicates: backward scatters the gradient (no accumulation)."""
+class _GatherBlocks(torch.autograd.Function):
+    """(F[idx_0], F[idx_1], ...) for index sets without duplicates (within and across sets):
+    backward scatters every block's gradient into ONE zero buffer (no per-block full-size
+    gradients for autograd to sum, no accumulation)."""
 
     @staticmethod
-    def forward(ctx, F, idx):
-        ctx.save_for_backward(idx)
+    def forward(ctx, F, *idxs):
+        ctx.save_for_backward(*idxs)
         ctx.n = F.numel()
-        return F[idx]
+        return tuple(F[i] for i in idxs)
 
     @staticmethod
-    def backward(ctx, g):
-        idx, = ctx.saved_tensors
-        gF = g.new_zeros(ctx.n)
-        gF[idx] = g
-        return gF, None
+    def backward(ctx, *grads):
+        idxs = ctx.saved_tensors
+        g0 = next(g for g in grads if g is not None)
+        gF = g0.new_zeros(ctx.n)
+        for i, g in zip(idxs, grads):
+            if g is not None:
+                gF[i] = g
+        return (gF,) + (None,) * len(idxs)
 
 
 def _run_chain(layers, f_name: str, x: torch.Tensor, context: Optional[torch.Tensor], masked: bool,
@@ -555,9 +560,12 @@ class ARInversePlan:
         layers = list(self.arn.layers)
         F = torch.cat([v.new_zeros(1)] + [t.reshape(-1) for l in layers for t in (l.weight, l.bias)] +
                       [v.new_zeros(self._nzero)])
-        if _GATHER_UNIQUE:
+        if _GATHER_UNIQUE:  # every block of the layer in one gather node
+            order = [t for g in hidden for blk in g for t in blk[4:]] + [t for o in outs for t in o[2:]]
+            got = dict(zip((id(t) for t in order), _GatherBlocks.apply(F, *order)))
+
             def G(idx):
-                return _GatherUnique.apply(F, idx)
+                return got[id(idx)]
         else:
             def G(idx):
                 return F[idx]

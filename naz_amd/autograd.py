@@ -69,11 +69,13 @@ class LinearActFn(Function):
                 if Kx:
                     parts.append(x)
                 K4, N4 = (Cd + Kx + 3) // 4 * 4, (N + 3) // 4 * 4
-                xin = torch.zeros((M, K4), device=W.device, dtype=torch.float32)
+                xin = torch.empty((M, K4), device=W.device, dtype=torch.float32)
+                xin[:, Cd + Kx:].zero_()  # only the padding columns
                 xin[:, :Cd + Kx] = torch.cat(parts, 1) if len(parts) > 1 else parts[0]
                 gp = gpre
                 if N4 != N:
-                    gp = torch.zeros((M, N4), device=W.device, dtype=torch.float32)
+                    gp = torch.empty((M, N4), device=W.device, dtype=torch.float32)
+                    gp[:, N:].zero_()
                     gp[:, :N] = gpre
                 gw4 = torch.empty((N4, K4), device=W.device, dtype=torch.float32)
                 gb4 = torch.empty(N4, device=W.device, dtype=torch.float32) if want_b else None

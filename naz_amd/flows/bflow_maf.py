@@ -33,6 +33,7 @@ from torch import Tensor
 
 from .. import ops
 from ..nn import create_mask, degree_schedule
+from .ar_pass0 import ArPass0
 
 __all__ = ["torch_to_jax", "make_conditional_autoregressive_nn", "make_masked_affine_autoregressive_transform",
            "make_normalizing_flow", "ravel", "unravel", "MAFSpec"]
@@ -276,7 +277,7 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
     # the whole log-density in ONE launch for all draws (naz_ar_flow_log_prob_batched): the
     # inverse kernel's degree passes assume pyro's create_mask for each layer's permutation, one
     # context vector (or none) and rows inside the f16x3 input split's range
-    ar_perm = ar_maps = None
+    ar_perm = ar_pass0 = None
     if ar_desc is not None and (C == 0 or ctx.dim() == 1) and float(x.abs().max()) < 32768.0 and \
             (C == 0 or float(ctx.abs().max()) < 32768.0):
         pm = [torch.as_tensor(p_).cpu().to(torch.int64) for p_ in perms]
@@ -290,11 +291,8 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             # one context vector: the first degree pass (units of mask index 0 see only the
             # context; the first dim's outputs see only them) is a per-draw constant, computed
             # once per draw below and packed in place of that pass's weights
-            ar_e0 = int((torch.as_tensor(ops.ar_flow_degrees(ar_desc)) == 0).sum()) if C else 0
-            ar_pass0 = C > 0 and ar_e0 > 0 and fold_context
-            assert not ar_pass0 or ops.ar_flow_pass0_floats(ar_desc) == \
-                len(masks) * 16 * (len(hd) * ((ar_e0 + 15) // 16) + 1), "pass-0 layout out of sync with made_ar_r16.h"
-            ar_first = [int(p_[0]) for p_ in pm]
+            if C > 0 and fold_context and int((torch.as_tensor(ops.ar_flow_degrees(ar_desc)) == 0).sum()):
+                ar_pass0 = ArPass0(ar_desc, [int(p_[0]) for p_ in pm], act, dev)
 
     def _chunks(P, rows, max_draws=65535):
         """Draw ranges per launch set: at most ``max_draws`` (the grid-z limit of the batched
@@ -547,54 +545,10 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         for all draws in one naz_ar_flow_log_prob_batched launch (csrc/made_ar_r16.h)."""
         P = _draws(params)
         flat = _ar_flat(params, P)
-        c0 = _ar_pass0(flat, P) if ar_pass0 else None
+        c0 = ar_pass0(flat, ctx, ar_mask) if ar_pass0 is not None else None
         packed = ops.ar_flow_pack_batched(ar_desc, flat, ar_perm, pass0=c0, mask=ar_mask)
         out.copy_(ops.ar_flow_log_prob_batched(ar_desc, packed, x, ctx, pass0_const=c0 is not None))
 
-    def _ar_pass0_maps():
-        """Index maps from a draw's masked flat row (all layers) to the pass-0 operands: per
-        hidden layer W [L, e0, C or e0] and b [L, e0], the first dim's output rows W [L, 2, e0]
-        and b [L, 2] (built once: the flat layout is naz_ar_flow_pack_host's)."""
-        L, e0, nh, H = len(plans), ar_e0, len(hd), hd[0]
-        per = H * (C + D) + H + (nh - 1) * (H * H + H) + 2 * D * H + 2 * D
-        maps = []
-        for i in range(nh):
-            o = 0 if i == 0 else H * (C + D) + H + (i - 1) * (H * H + H)
-            cols, ncols = (C, C + D) if i == 0 else (e0, H)
-            w = torch.stack([l * per + o + torch.arange(e0)[:, None] * ncols + torch.arange(cols)[None, :]
-                             for l in range(L)])
-            b = torch.stack([l * per + o + H * ncols + torch.arange(e0) for l in range(L)])
-            maps.append((w, b))
-        o = H * (C + D) + H + (nh - 1) * (H * H + H)
-        rows = [torch.tensor([ar_first[l], D + ar_first[l]]) for l in range(L)]
-        w = torch.stack([l * per + o + rows[l][:, None] * H + torch.arange(e0)[None, :] for l in range(L)])
-        b = torch.stack([l * per + o + 2 * D * H + rows[l] for l in range(L)])
-        maps.append((w, b))
-        return [(w.to(dev), b.to(dev)) for (w, b) in maps]
-
-    def _ar_pass0(flat: Tensor, P: int) -> Tensor:
-        """[P, L * C0] pass-0 constants (include/naz_hip.h naz_ar_flow_pack): the degree-0 units'
-        pre-activations of every hidden layer (x 2 / ln 2, the kernel's sigmoid-fold scale) and the
-        first dim's two ARN outputs, all draws and layers per naz_linear_act_batched launch."""
-        nonlocal ar_maps
-        if ar_maps is None:
-            ar_maps = _ar_pass0_maps()
-        L, e0, nh = len(plans), ar_e0, len(hd)
-        nb = (e0 + 15) // 16
-        h, pres = None, []
-        for i, (wm, bm) in enumerate(ar_maps):
-            W = (flat[:, wm] * ar_mask[wm]).reshape(P * L, *wm.shape[1:])
-            b = flat[:, bm].reshape(P * L, -1)
-            if i == nh:
-                o = ops.linear_act_batched(h, W, b, "identity")
-                break
-            pres.append(ops.linear_act_batched(h, W, b, "identity", context=ctx if i == 0 else None))
-            h = ops.linear_act_batched(h, W, b, act, context=ctx if i == 0 else None)
-        c0 = torch.zeros((P, L, 16 * (nh * nb + 1)), device=dev, dtype=torch.float32)
-        for i, z in enumerate(pres):
-            c0[:, :, 16 * nb * i:16 * nb * i + e0] = z.reshape(P, L, e0) * 2.8853900817779268
-        c0[:, :, 16 * nb * nh:16 * nb * nh + 2] = o.reshape(P, L, 2)
-        return c0.reshape(P, -1)
 
     def lp_batched(params: Params) -> Tensor:
         P = _draws(params)

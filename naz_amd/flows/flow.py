@@ -164,10 +164,12 @@ class _FusedAR:
         self.shape = (D, C, H, n_hidden, K)
         self.P = 2 if kind == "maf" else 3 * K - 1
         self.desc = ops.ar_flow_desc(kind, D, C, H, len(layers), n_hidden, K, act, bound)
+        self.act = act
         self._sig = None
         self._packed = None
         self._fsig, self._fpacked = None, None
         self._masks = None
+        self._p0sig, self._p0, self._p0fn = None, None, (None, None)
 
     def _nets(self):
         return [t.nn for t in self.layers]
@@ -257,10 +259,43 @@ class _FusedAR:
             low, high = bounds["low"].contiguous(), bounds["high"].contiguous()
         return ops.ar_flow_sample(self.desc, self.packed_fwd(), z, context, low, high, with_logdet=with_logdet)
 
+    def _pass0_operands(self):
+        """(unmasked flat rows [1, L per], mask vector, permutations, ArPass0) on the device, for
+        the one-context-vector path; re-read when a parameter, mask or permutation changes."""
+        nets = self._nets()
+        ts = [t for n in nets for l in n.layers for t in (l.weight, l.bias, l.mask)] + [n.permutation for n in nets]
+        sig = tuple((t.data_ptr(), t._version) for t in ts) + (cache_epoch(),)
+        if sig != self._p0sig:
+            flats, masks = [], []
+            for n in nets:
+                for l in n.layers:
+                    flats += [l.weight.detach().reshape(-1), l.bias.detach().reshape(-1)]
+                    masks += [l.mask.detach().reshape(-1), torch.ones_like(l.bias.detach()).reshape(-1)]
+            perm = np.stack([n.permutation.detach().cpu().numpy() for n in nets]).astype(np.int32)
+            flat = torch.cat(flats).to(torch.float32)[None].contiguous()
+            key = perm.tobytes()
+            if self._p0fn[0] != key:
+                from .ar_pass0 import ArPass0
+                self._p0fn = (key, ArPass0(self.desc, [int(p[0]) for p in perm], self.act, flat.device))
+            self._p0 = (flat, torch.cat(masks).to(torch.float32).contiguous(), perm, self._p0fn[1])
+            self._p0sig = sig
+        return self._p0
+
     def log_prob(self, x, context=None, bounds=None, out=None):
         low = high = None
         if bounds is not None:
             low, high = bounds["low"].to(x.device, torch.float32), bounds["high"].to(x.device, torch.float32)
+        if (_AR_PASS0 and bounds is None and self.shape[1] > 0 and context is not None and x.dim() == 2 and
+                x.shape[0] >= 4096 and (context.dim() == 1 or context.shape[0] == 1)):
+            # one condition vector (the density grid): the context-only first degree pass once,
+            # packed as constants in place of its weights (naz_ar_flow_pack pass0)
+            flat, mask, perm, p0 = self._pass0_operands()
+            img = ops.ar_flow_pack_batched(self.desc, flat, perm, pass0=p0(flat, context, mask), mask=mask)
+            lp = ops.ar_flow_log_prob_batched(self.desc, img, x, context.reshape(-1), pass0_const=True)[0]
+            if out is None:
+                return lp
+            out.copy_(lp)
+            return out
         return ops.ar_flow_log_prob(self.desc, self.packed(), x, context, low, high, out=out)
 
     def executed_flop_per_row(self) -> int:
@@ -283,6 +318,7 @@ class _FusedAR:
 
 _TRAIN_FUSED = __import__("os").environ.get("NAZ_TRAIN_FUSED", "1")
 _AR_FUSED = __import__("os").environ.get("NAZ_AR_FUSED", "1")
+_AR_PASS0 = __import__("os").environ.get("NAZ_AR_PASS0", "1") != "0"  # one-context-vector first-pass folding
 
 
 class _CouplingTrainFn(torch.autograd.Function):

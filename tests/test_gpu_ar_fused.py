@@ -229,3 +229,32 @@ def test_fused_ar_device_pack_and_batched_draws(spec):
         assert torch.equal(per[p], ops.ar_flow_log_prob(plan.desc, dev[p], xs[p], c1))
     with pytest.raises(ValueError):
         ops.ar_flow_pack_batched(plan.desc, torch.tensor(np.stack(flats), device=DEV), perm[:, ::-1] * 0)
+
+
+@pytest.mark.parametrize("spec", [CASES[4], CASES[3], CASES[0]], ids=_id)
+def test_fused_ar_one_context_vector_pass0(spec):
+    """One condition vector for every row (the density grid, naz plot.py:126-127): the
+    context-only first degree pass is computed once and packed as constants (naz_ar_flow_pack
+    pass0; the kernel skips the pass).  Same log_prob as the plain fused launch, and the oracle's."""
+    from naz_amd import ops
+    from naz_amd.flows import flow as FL
+    f, state = _flow(spec)
+    n, D, C = 5000, spec["D"], spec["C"]
+    x = torch.as_tensor(O.gaussian_mixture(n, D, seed=21))
+    c1 = torch.as_tensor(O.context_normal(1, C, seed=22)).reshape(-1)
+    calls, orig = [], ops.ar_flow_log_prob_batched
+    ops.ar_flow_log_prob_batched = lambda *a, **k: calls.append(k.get("pass0_const")) or orig(*a, **k)
+    try:
+        with torch.no_grad():
+            a = f.log_prob(x.to(DEV), condition=c1.to(DEV))
+            assert calls == [True], "the pass-0 path was not taken"
+            FL._AR_PASS0 = False
+            b = f.log_prob(x.to(DEV), condition=c1.to(DEV))
+    finally:
+        FL._AR_PASS0 = True
+        ops.ar_flow_log_prob_batched = orig
+    np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4)
+    cc = c1.reshape(1, -1).expand(n, -1)
+    lp64 = O.build_flow(spec, state, torch.float64).log_prob(x.double(), cc.double()).numpy()
+    lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, cc).numpy()
+    assert_parity(a.cpu().numpy(), lp64, lp32, what=f"pass0 {_id(spec)}")

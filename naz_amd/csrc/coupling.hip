@@ -186,8 +186,9 @@ __global__ void coupling_pack_kernel(const float* __restrict__ flat, float* __re
 // Stage copy HBM/L2 -> LDS (16-byte loads, all 256 threads)
 // ---------------------------------------------------------------------------
 // Asynchronous stage copy HBM/L2 -> LDS with LDS-DMA (global_load_lds_dwordx4): wave w
-// moves 1 KB chunks w, w+4, ...; no VGPRs hold the data.  Completion is awaited by the
-// next __syncthreads() (which waits vmcnt(0)).
+// moves 1 KB chunks w, w+4, ...; no VGPRs hold the data.  Completion is published by the
+// next ring_barrier() (naz_device.h: explicit vmcnt(0), then the barrier) — never by a bare
+// __syncthreads(), which hipcc does not always precede with vmcnt(0).
 template <int NFLOATS, int NW = 4>
 NAZ_DEV void stage_issue(float* lds, const float* __restrict__ src) {
 #ifdef NAZ_ABL_NOCOPY
@@ -343,7 +344,7 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
       logjac -= sl;
     }
   }
-  __syncthreads();  // stage A of the first layer has landed
+  ring_barrier();  // stage A of the first layer has landed
 
   for (int li = 0; li < L; ++li) {
     const int l = DIR_INV ? (L - 1 - li) : li;
@@ -390,7 +391,7 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
     __syncthreads();
     stage_issue<CF::B_SIZE>(lds, lp + CF::B_OFF);
     tanh_all<CF::HB>(acc1);
-    __syncthreads();
+    ring_barrier();
 
     // ---------------- stage B resident: GEMM2
     floatx16 acc2[CF::HB];
@@ -399,7 +400,7 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
     __syncthreads();
     stage_issue<CF::c_size(0)>(lds, lp + CF::c_off(0));
     tanh_all<CF::HB>(acc2);
-    __syncthreads();
+    ring_barrier();
 
     // ---------------- stages C_j resident: GEMM3 -> raw spline params in registers
     floatx16 acc3[CF::NO];
@@ -409,7 +410,7 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
       if constexpr (j > 0) {
         __syncthreads();
         stage_issue<CF::c_size(j)>(lds, lp + CF::c_off(j));
-        __syncthreads();
+        ring_barrier();
       }
       floatx16 part[cnt];
       init_bias<cnt>(part, lds + cnt * CF::PANEL1, h);
@@ -441,7 +442,7 @@ __global__ void __launch_bounds__(256, 2) coupling_flow_kernel(
       zu[q] = rqs_apply<CF::K, DIR_INV, true>(t, zu[q], bound, ld);
       ldsum += DIR_INV ? -ld : ld;
     }
-    __syncthreads();  // next layer's stage A has landed
+    ring_barrier();  // next layer's stage A has landed
   }
 
   if constexpr (DIR_INV) {
@@ -1056,7 +1057,7 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
     static_for<0, CF::NSTG>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
 #ifndef NAZ_ABL_NOBARRIER
-      __syncthreads();  // stage j has landed in slot (g&1); every wave is done with the other slot
+      ring_barrier();  // stage j has landed in slot (g&1); every wave is done with the other slot
 #endif
       const float* cur = (g & 1) ? slot1 : slot0;
       float* nxt = (g & 1) ? slot0 : slot1;

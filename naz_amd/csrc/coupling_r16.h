@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
     static_for<0, CF::NSTG>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
 #ifndef NAZ_ABL_NOBARRIER
-      __syncthreads();  // stage j has landed in slot (g&1); every wave is done with the other slot
+      ring_barrier();  // stage j has landed in slot (g&1); every wave is done with the other slot
 #endif
       const float* cur = (g & 1) ? slot1 : slot0;
       float* nxt = (g & 1) ? slot0 : slot1;

@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
 
     static_for<0, NSTG>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      __syncthreads();  // stage j has landed in slot (g&1); every wave is done with the other slot
+      ring_barrier();  // stage j has landed in slot (g&1); every wave is done with the other slot
       const float* cur = (g & 1) ? slot1 : slot0;
       float* nxt = (g & 1) ? slot0 : slot1;
       if constexpr (j + 1 < NSTG_F) {

@@ -639,7 +639,7 @@ __global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_t16_kernel(WGradArgs p
   int slot = 0;
   if (mb < me) fill(mb, tl);
   for (int64_t m0 = mb; m0 < me; m0 += R, slot ^= 1) {
-    __syncthreads();  // chunk m0 has landed (vmcnt drained); every wave is done with the other slot
+    ring_barrier();  // chunk m0 has landed (vmcnt drained); every wave is done with the other slot
     float* const Gs = tl + slot * CH;
     float* const Xs = Gs + R * N1;
     if (m0 + R < me) fill(m0 + R, tl + (slot ^ 1) * CH);

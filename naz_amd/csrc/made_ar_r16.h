@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
         constexpr bool NEW_STAGE = i == 0 || SID != CF::stage_id(p, i > 0 ? i - 1 : 0);
         if constexpr (NEW_STAGE) {  // it has landed in slot (g & 1)
           constexpr int SF_NEXT = SID + 1 < CF::NSTG ? CF::stage_floats(SID + 1) : CF::stage_floats(0);
-          __syncthreads();  // ... and every wave is done with the other slot
+          ring_barrier();  // ... and every wave is done with the other slot
           cur = (g & 1) ? slot1 : slot0;
           float* nxt = (g & 1) ? slot0 : slot1;
           if constexpr (SID + 1 < CF::NSTG) {
@@ -869,7 +869,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
       constexpr int SID = CF::stage_id(u), OFF = CF::unit_off(u);
       constexpr bool NEW_STAGE = u == 0 || SID != CF::stage_id(u > 0 ? u - 1 : 0);
       if constexpr (NEW_STAGE) {  // stage SID has landed in slot (g & 1)
-        __syncthreads();  // ... and every wave is done with the other slot
+        ring_barrier();  // ... and every wave is done with the other slot
         cur = (g & 1) ? slot1 : slot0;
         float* nxt = (g & 1) ? slot0 : slot1;
         if constexpr (SID + 1 < CF::NSTG) {

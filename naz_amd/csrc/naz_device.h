@@ -22,6 +22,19 @@ constexpr float kMinBinHeight = 1e-3f;
 constexpr float kMinDerivative = 1e-3f;
 constexpr float kSearchEps = 1e-6f;
 
+// Publish an LDS-DMA ring slot.  A global_load_lds write is pending on the issuing wave's
+// vmcnt until it lands in LDS; __syncthreads() alone does NOT reliably drain it: on a loop
+// back edge hipcc (ROCm 7.2) emitted only lgkmcnt(0) before the barrier, so a wave could read
+// a 1 KB chunk another wave's DMA had not written yet (the intermittent non-finite rows of
+// the coupling kernel at 2^20 rows, round 2).  Each wave waits for its OWN DMAs, then the
+// barrier makes every wave's chunks visible to all.  tests/test_isa_ring.py checks the built
+// code object: every s_barrier reachable with a global_load_lds in flight must be preceded
+// by an s_waitcnt vmcnt(0) on every path, loop back edges included.
+NAZ_DEV void ring_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 enum Act : int { ACT_IDENTITY = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SOFTPLUS = 3, ACT_SIGMOID = 4 };
 
 // Math policy.  ACCURATE = the ocml (libm-grade, ~1 ulp, many instructions) functions,

@@ -96,7 +96,9 @@ class _FusedCoupling:
             self.mode = self._resolve_mode()
             self.desc = ops.coupling_desc(D, C, S, K, len(self.layers), H, act, lower, bound, self.mode)
             flat = torch.cat([p.detach().reshape(-1) for p in ps])
-            self._packed = ops.coupling_pack(self.desc, flat, self._packed)
+            # a fresh image per repack: a training forward's backward (_CouplingTrainFn) still
+            # holds the previous one, which must not change under it
+            self._packed = ops.coupling_pack(self.desc, flat, None)
             self._flat, self._packed_bwd = flat, None
             self._sig = sig
         return self._packed
@@ -341,6 +343,7 @@ class _CouplingTrainFn(torch.autograd.Function):
         lp = ops.coupling_log_prob_train(d, packed, x.detach(), None if context is None else context.detach(),
                                          low, high, states)
         ctx.plan, ctx.packed, ctx.pbwd, ctx.flat = plan, packed, pbwd, flat
+        ctx.desc, ctx.shape = d, plan.shape  # the forward's; a later repack replaces plan.desc
         ctx.save_for_backward(states, context)
         ctx.n_params = len(params)
         return lp
@@ -349,8 +352,8 @@ class _CouplingTrainFn(torch.autograd.Function):
     def backward(ctx, g_lp):
         states, context = ctx.saved_tensors
         plan = ctx.plan
-        d = plan.desc
-        D, C, S, K, H, act, lower, bound = plan.shape
+        d = ctx.desc
+        D, C, S, K, H, act, lower, bound = ctx.shape
         L, B = d.L, states.shape[1]
         dev = states.device
         g_lp = g_lp.contiguous().float()
@@ -393,14 +396,29 @@ class _CouplingTrainFn(torch.autograd.Function):
         return (None, None, None, None, *grads)
 
 
+def _maker_args(flow_type, flow_args, flow_kwargs):
+    """The maker's arguments by name, however the caller passed them (positionally as naz's
+    examples do, or by keyword); None when they do not bind."""
+    import inspect
+    try:
+        b = inspect.signature(flow_makers[flow_type]).bind(*flow_args, **flow_kwargs)
+    except TypeError:
+        return None
+    b.apply_defaults()
+    return b.arguments
+
+
 def _fused_plan(flow_type, flow_args, flow_kwargs, transforms):
     if any(isinstance(t, Permute) for t in transforms):
         return None
+    a = _maker_args(flow_type, flow_args, flow_kwargs)
+    if a is None or "theta_dim" not in a:
+        return None
     if flow_type in ("nsa", "maf") and _AR_FUSED != "0":
-        D, C, hidden, L = flow_args[:4]
-        K = flow_args[4] if flow_type == "nsa" else 8
+        D, C, hidden, L = a["theta_dim"], a["condition_dim"], a["hidden_dim"], a["num_layers"]
+        K = a["count_bins"] if flow_type == "nsa" else 8
         hidden = list(hidden) if isinstance(hidden, (list, tuple)) else [hidden]
-        act = activation_name(flow_kwargs.get("activation", nn.Tanh()))
+        act = activation_name(a["activation"])
         if any(h != hidden[0] for h in hidden):
             return None
         try:
@@ -411,11 +429,12 @@ def _fused_plan(flow_type, flow_args, flow_kwargs, transforms):
             return None
     if flow_type != "nsc":
         return None
-    D, C, hidden, L, K, S = flow_args[:6]
+    D, C, hidden, L = a["theta_dim"], a["condition_dim"], a["hidden_dim"], a["num_layers"]
+    K, S = a["count_bins"], a["split_dim"]
     hidden = list(hidden) if isinstance(hidden, (list, tuple)) else [hidden]
     if len(hidden) != 2 or hidden[0] != hidden[1]:
         return None
-    act = activation_name(flow_kwargs.get("activation", nn.Tanh()))
+    act = activation_name(a["activation"])
     layers = list(transforms)
     inner = [t.module if isinstance(t, SplineCoupling) else t for t in layers]
     lower = all(t.lower_spline is not None for t in inner)

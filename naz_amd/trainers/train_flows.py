@@ -66,6 +66,18 @@ def _flow_parameters(flow) -> List[torch.Tensor]:
     return out
 
 
+def _module_parameters(flow) -> List[torch.Tensor]:
+    """train_flows.py:270 (Lightning ``Learner.configure_optimizers``): ``self.model.parameters()``
+    — every parameter of the flow module, the embedding net's included — deduplicated, plus any
+    transform parameter the module does not register."""
+    seen, out = set(), []
+    for p in list(flow.parameters()) + _flow_parameters(flow):
+        if id(p) not in seen:
+            seen.add(id(p))
+            out.append(p)
+    return out
+
+
 class DataParallel:
     """Rank layout and the gradient all-reduce.  ``group=None`` with an initialised default
     process group uses it; without torch.distributed this is the single-process identity."""
@@ -232,7 +244,7 @@ def train_lightning(flow, theta_train, condition_train, opt=optim.AdamW, lr=2e-3
     ``opt(params, lr, weight_decay=lambda_l2)``, no clipping (Lightning's default) — as the
     data-parallel NLL step (one process per GPU under torch.distributed).  Returns the flow."""
     dp = DataParallel(group)
-    params = _flow_parameters(flow)
+    params = _module_parameters(flow)
     dp.broadcast_params(params)
     optimizer = opt(params, lr=lr, weight_decay=lambda_l2)
     gen = torch.Generator().manual_seed(seed)

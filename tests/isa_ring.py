@@ -1,0 +1,153 @@
+"""Static check of the LDS-DMA ring protocol in the built gfx950 code objects (test helper).
+
+A `global_load_lds` (or `buffer_load ... lds`) write is pending on the issuing wave's vmcnt
+until it lands in LDS.  Every kernel that streams weights through an LDS ring publishes a slot
+with a workgroup barrier, so every `s_barrier` that a wave can reach with such a DMA in flight
+must be preceded by `s_waitcnt vmcnt(0)` on EVERY path — loop back edges included.  Round 2's
+headline kernel broke this on the layer loop's back edge (an intermittent NaN at 2^20 rows).
+
+The check: pull each gfx950 code object out of the library's `.hip_fatbin` (offload bundles),
+disassemble with llvm-objdump, build a per-kernel control-flow graph from the branch targets,
+and run a forward may-analysis of "a DMA may be in flight" to a fixed point.
+"""
+from __future__ import annotations
+
+import re
+import struct
+import subprocess
+import tempfile
+from pathlib import Path
+
+LLVM = Path("/opt/rocm/lib/llvm/bin")
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+_FUNC = re.compile(r"^([0-9a-f]+) <(.+)>:$")
+_ADDR = re.compile(r"//\s*([0-9A-F]+):")
+_TARGET = re.compile(r"<([^<>+]+)(?:\+0x([0-9a-f]+))?>\s*$")
+
+
+def code_objects(lib: Path, arch: str = "gfx950") -> list[bytes]:
+    """The `arch` device code objects of every offload bundle in `lib`'s .hip_fatbin."""
+    with tempfile.TemporaryDirectory() as td:
+        fb = Path(td) / "fb.bin"
+        subprocess.run([str(LLVM / "llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", str(lib),
+                        str(Path(td) / "junk")], check=True, capture_output=True)
+        b = fb.read_bytes()
+    out = []
+    i = b.find(MAGIC)
+    while i >= 0:
+        n = struct.unpack_from("<Q", b, i + 24)[0]
+        p = i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", b, p)
+            p += 24
+            triple = b[p:p + tl].decode()
+            p += tl
+            if triple.endswith(arch) and size:
+                out.append(b[i + off:i + off + size])
+        i = b.find(MAGIC, i + 1)
+    return out
+
+
+def disassemble(co: bytes) -> str:
+    with tempfile.NamedTemporaryFile(suffix=".co") as f:
+        f.write(co)
+        f.flush()
+        r = subprocess.run([str(LLVM / "llvm-objdump"), "-d", "--no-show-raw-insn", f.name],
+                           check=True, capture_output=True, text=True)
+    return r.stdout
+
+
+def functions(asm: str) -> dict[str, tuple[int, list[tuple[int, str]]]]:
+    """symbol -> (start address, [(address, instruction text)])."""
+    funcs: dict[str, tuple[int, list]] = {}
+    cur = None
+    for line in asm.splitlines():
+        m = _FUNC.match(line.strip())
+        if m:
+            cur = m.group(2)
+            funcs[cur] = (int(m.group(1), 16), [])
+            continue
+        if cur is None or not line.startswith("\t"):
+            continue
+        a = _ADDR.search(line)
+        if a:
+            funcs[cur][1].append((int(a.group(1), 16), line.strip()))
+    return funcs
+
+
+def is_dma(ins: str) -> bool:
+    op = ins.split(None, 1)[0]
+    return op.startswith("global_load_lds") or (op.startswith("buffer_load") and " lds" in ins.split("//")[0])
+
+
+def ring_violations(start: int, insns: list[tuple[int, str]]) -> list[str]:
+    """Barriers reachable with an LDS-DMA in flight and no vmcnt(0) on some path."""
+    if not any(is_dma(t) for _, t in insns):
+        return []
+    index = {a: k for k, (a, _) in enumerate(insns)}
+    succ: list[list[int]] = []
+    for k, (a, t) in enumerate(insns):
+        op = t.split(None, 1)[0]
+        nxt = [k + 1] if k + 1 < len(insns) else []
+        if op in ("s_endpgm", "s_endpgm_saved", "s_setpc_b64", "s_trap"):
+            succ.append([])
+            continue
+        if op.startswith("s_branch") or op.startswith("s_cbranch"):
+            m = _TARGET.search(t)
+            tgt = []
+            if m:
+                ta = start + int(m.group(2) or "0", 16)
+                if ta in index:
+                    tgt = [index[ta]]
+            if not tgt:
+                raise AssertionError(f"unresolved branch target: {t}")
+            succ.append(tgt if op.startswith("s_branch") else tgt + nxt)
+            continue
+        succ.append(nxt)
+    pending_in = [None] * len(insns)
+    work = [(0, False)]
+    bad: dict[int, str] = {}
+    while work:
+        k, st = work.pop()
+        if pending_in[k] is not None and (pending_in[k] or not st):
+            continue  # nothing new (the state only grows False -> True)
+        pending_in[k] = bool(pending_in[k]) or st
+        st = pending_in[k]
+        a, t = insns[k]
+        op = t.split(None, 1)[0]
+        if op == "s_barrier" and st:
+            bad[a] = t
+        if op == "s_waitcnt" and "vmcnt(0)" in t:
+            st = False
+        elif is_dma(t):
+            st = True
+        for s in succ[k]:
+            work.append((s, st))
+    return [f"+0x{a - start:x}: {t.split('//')[0].strip()}" for a, t in sorted(bad.items())]
+
+
+def check_library(lib: Path, arch: str = "gfx950") -> tuple[int, dict[str, list[str]]]:
+    """(number of DMA kernels checked, {kernel: violations})."""
+    checked = 0
+    out: dict[str, list[str]] = {}
+    for co in code_objects(lib, arch):
+        for name, (start, insns) in functions(disassemble(co)).items():
+            if not any(is_dma(t) for _, t in insns):
+                continue
+            checked += 1
+            v = ring_violations(start, insns)
+            if v:
+                out[name] = v
+    return checked, out
+
+
+if __name__ == "__main__":
+    import sys
+    lib = Path(sys.argv[1] if len(sys.argv) > 1 else Path(__file__).resolve().parents[1] / "naz_amd/lib/libnazhip.so")
+    n, bad = check_library(lib)
+    print(f"{n} LDS-DMA kernels checked, {len(bad)} with unguarded barriers")
+    for k, v in bad.items():
+        print(k)
+        for x in v[:8]:
+            print("   ", x)

@@ -183,6 +183,24 @@ def test_naz_compat_front_end_runs_unchanged():
     assert any(not torch.equal(a, p.detach()) for a, p in zip(before, model.parameters()))
 
 
+def test_train_lightning_updates_embedding_net():
+    """The Lightning Learner optimises ``self.model.parameters()`` (train_flows.py:269-270), the
+    embedding net included: its weights must move (they were left out)."""
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.trainers import train_lightning
+    torch.manual_seed(0)
+    emb = torch.nn.Linear(3, 2).to(DEV)
+    flow = NormalizingFlow('maf', None, 2, 2, [32, 32], 2, embedding_net=emb)
+    rng = np.random.default_rng(0)
+    lam = torch.as_tensor(rng.standard_normal((1024, 3)).astype(np.float32), device=DEV)
+    th = torch.as_tensor(rng.standard_normal((1024, 2)).astype(np.float32), device=DEV)
+    w0 = emb.weight.detach().clone()
+    t0 = [p.detach().clone() for p in flow.flow_dist.transforms[0].parameters()]
+    train_lightning(flow, th, lam, num_epochs=1, batch_size=256)
+    assert not torch.equal(w0, emb.weight.detach()), "embedding net not optimised"
+    assert any(not torch.equal(a, p.detach()) for a, p in zip(t0, flow.flow_dist.transforms[0].parameters()))
+
+
 def test_predict_batched_matches_oracle_per_draw():
     """predict (train_flows.py:384-422) for a maf: all posterior draws in one batched sampler
     call; draw p's samples equal the oracle flow under draw p's weights applied to the same

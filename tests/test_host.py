@@ -34,6 +34,18 @@ def test_flow_makers_and_signature():
     assert not g.conditional and len(g.flow_dist.transforms) == 1  # torch wraps a single compose transform
 
 
+def test_fused_plan_binds_keyword_maker_arguments():
+    """count_bins / split_dim / hidden_dim passed by keyword pick the same fused plan as the
+    positional form (they raised at construction)."""
+    from naz_amd.flows.flow import _FusedAR, _FusedCoupling
+    a = NormalizingFlow("nsa", None, 4, 2, [128, 128], 8, count_bins=8)
+    assert isinstance(a._plan, _FusedAR)
+    b = NormalizingFlow("nsc", None, 16, 32, [128, 128], 8, 8, split_dim=8)
+    assert isinstance(b._plan, _FusedCoupling)
+    c = NormalizingFlow("maf", None, 2, 2, hidden_dim=[150, 150, 150], num_layers=16)
+    assert isinstance(c._plan, _FusedAR)
+
+
 @pytest.mark.parametrize("ft,args", [("nsc", (6, 2, [32, 32], 3, 4, 2)), ("nsa", (4, 2, [32, 32], 2, 8)),
                                      ("maf", (3, 2, [16, 16], 3))])
 def test_state_roundtrip_and_oracle_masks(ft, args, tmp_path):

@@ -53,6 +53,10 @@ extern "C" {
 /* ---- library ------------------------------------------------------------ */
 const char* naz_last_error(void);
 int naz_abi_version(void); /* bumps on any signature change */
+/* Diagnostics (no reference counterpart): the first non-finite row state a fused log_prob
+ * kernel met, as {1, workgroup, layer, stage counter, row} ({0, ...} = none), optionally
+ * cleared.  Fails unless the library was built with -DNAZ_DEBUG_NONFINITE.               */
+int naz_debug_nonfinite(int64_t* out5, int clear);
 
 /* ---- a1+a2: conditional spline -------------------------------------------
  * Replaces [pyro] ConditionedSpline._call / ._inverse over a conditioner output,

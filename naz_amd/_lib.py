@@ -46,6 +46,7 @@ FLOW_COUPLING, FLOW_AR = 1, 2
 SIGNATURES = {
     "naz_last_error": (C.c_char_p, []),
     "naz_abi_version": (C.c_int, []),
+    "naz_debug_nonfinite": (C.c_int, [C.POINTER(C.c_int64), _i]),
     "naz_rqs_fwd": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _i64, _i, _i, _i, C.c_float, _vp]),
     "naz_rqs_inv": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _i64, _i, _i, _i, C.c_float, _vp]),
     "naz_spline_elementwise": (C.c_int, [_i, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i, _i, C.c_float,

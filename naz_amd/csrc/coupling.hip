@@ -209,6 +209,20 @@ NAZ_DEV void stage_issue(float* lds, const float* __restrict__ src) {
   }
 }
 
+// NAZ_DEBUG_NONFINITE builds (python -m naz_amd.build debug -DNAZ_DEBUG_NONFINITE): the fused
+// log_prob kernels record the FIRST non-finite row state as {1, workgroup, layer, stage counter,
+// row} (naz_debug_nonfinite reads and clears it).  The record exists in every build; only the
+// debug build writes it.
+__device__ int64_t g_nonfinite[5];
+NAZ_DEV void debug_nonfinite_probe(bool bad, int64_t row, int layer, int stage) {
+  if (bad && atomicCAS(reinterpret_cast<unsigned long long*>(&g_nonfinite[0]), 0ull, 1ull) == 0ull) {
+    g_nonfinite[1] = blockIdx.x;
+    g_nonfinite[2] = layer;
+    g_nonfinite[3] = stage;
+    g_nonfinite[4] = row;
+  }
+}
+
 // stage_issue of the first nch (wave-uniform, <= NFLOATS / 256) 1 KB chunks only
 template <int NFLOATS, int NW>
 NAZ_DEV void stage_issue_lim(float* lds, const float* __restrict__ src, int nch) {
@@ -1221,6 +1235,25 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
 #include "made_ar_r16.h"
 
 namespace naz {
+
+extern "C" int naz_debug_nonfinite(int64_t* out5, int clear) {
+#ifndef NAZ_DEBUG_NONFINITE
+  (void)out5;
+  (void)clear;
+  return naz::set_error("naz_debug_nonfinite: library not built with -DNAZ_DEBUG_NONFINITE");
+#else
+  if (out5 == nullptr) return naz::set_error("naz_debug_nonfinite: null output");
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpyFromSymbol(out5, HIP_SYMBOL(naz::g_nonfinite), 5 * sizeof(int64_t)) != hipSuccess)
+    return naz::set_error("naz_debug_nonfinite: reading the record failed");
+  if (clear) {
+    const int64_t zero[5] = {0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(naz::g_nonfinite), zero, sizeof(zero)) != hipSuccess)
+      return naz::set_error("naz_debug_nonfinite: clearing the record failed");
+  }
+  return 0;
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // Host dispatch over the compiled instantiations

@@ -622,6 +622,16 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
 
     // ---------------- upper spline on this quarter's remaining dims (next layer's stage A in flight)
     static_for<CF::SPLIT3 ? 1 : 0, CF::DQ>([&](auto uc) { upper(uc); });
+#ifdef NAZ_DEBUG_NONFINITE
+    {
+      bool fin = isfinite(ldsum);
+#pragma unroll
+      for (int u = 0; u < CF::SQ; ++u) fin = fin && isfinite(zl[u]);
+#pragma unroll
+      for (int u = 0; u < CF::DQ; ++u) fin = fin && isfinite(zu[u]);
+      debug_nonfinite_probe(valid && !fin, row, li, g);
+    }
+#endif
   }
   if constexpr (VAR == 1) {  // P[0] = z
     if (valid) {

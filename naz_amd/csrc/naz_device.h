@@ -31,7 +31,9 @@ constexpr float kSearchEps = 1e-6f;
 // code object: every s_barrier reachable with a global_load_lds in flight must be preceded
 // by an s_waitcnt vmcnt(0) on every path, loop back edges included.
 NAZ_DEV void ring_barrier() {
+#ifndef NAZ_ABL_RING_NOWAIT  // A/B only: the round-2 (racy) form
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   __syncthreads();
 }
 

@@ -354,3 +354,24 @@ def test_config3_gemm1_precision_paths(scale, mfma):
     lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, c).numpy()
     st = assert_parity(_np(lp), lp64, lp32, what=f"config3 gemm1 paths scale={scale}")
     print("gemm1 paths", scale, st)
+
+
+def test_full_size_debug_probe_build_clean():
+    """The NAZ_DEBUG_NONFINITE build of the library (when present: naz_amd/lib/libnazhip_debug.so)
+    at 2^20 rows, in its own process: every layer's row state stays finite in every workgroup
+    (the probe records the first non-finite (workgroup, layer, stage))."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    dbg = root / "naz_amd" / "lib" / "libnazhip_debug.so"
+    if not dbg.exists():
+        pytest.skip("debug library not built")
+    r = subprocess.run([sys.executable, str(root / "scripts" / "diag_nonfinite.py"), "2"], capture_output=True,
+                       text=True, timeout=110, env={**__import__("os").environ, "NAZ_LIB": str(dbg)}, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["debug_build"], res
+    for t in res["trials"]:
+        assert t["nonfinite_rows"] == 0 and t["record"]["hit"] == 0, res

@@ -362,12 +362,14 @@ def run_cnf(args, dev, rank, world, dist):
     eps = torch.randn(B, CNF_D, device=dev)
     lp = torch.empty(B, device=dev)
     dopri5 = args.cnf_solver == "dopri5"
-    nfe = torch.zeros((B + 15) // 16, device=dev, dtype=torch.int32)
+    glob = args.cnf_control == "global"
+    nfe = torch.zeros(1 if glob else (B + 15) // 16, device=dev, dtype=torch.int32)
 
     def solve():
         if dopri5:  # §8f rank 3: adaptive Dormand-Prince, atol = rtol = 1e-4 (naz's setting)
-            return ops.cnf_integrate_dopri5(plan.desc, packed, x, eps, 0.0, 1.0, 1e-4, 1e-4, ld_out=lp,
-                                            ld_mode=ops.LD_ROWSUM_SUB, nfe=nfe)[0]
+            fn = ops.cnf_integrate_dopri5_global if glob else ops.cnf_integrate_dopri5
+            return fn(plan.desc, packed, x, eps, 0.0, 1.0, 1e-4, 1e-4, ld_out=lp, ld_mode=ops.LD_ROWSUM_SUB,
+                      nfe=nfe)[0]
         return ops.cnf_integrate(plan.desc, packed, x, eps, 0.0, 1.0, CNF_STEPS, ld_out=lp,
                                  ld_mode=ops.LD_ROWSUM_SUB)[0]
 
@@ -430,8 +432,10 @@ def run_cnf(args, dev, rank, world, dist):
             "data": "synthetic: x ~ 0.5 x 8-component Gaussian mixture; random-init weights (nn.Linear default, "
                     "torch seed 1234); eps ~ N(0, I) redrawn per step",
             "config": {"workload": "BASELINE configs[4]: FFJORD block D=16, H=[128,128,128], softplus, " + (
-                                   "adaptive dopri5 atol=rtol=1e-4 per 16-row group (SURVEY.md §8f rank 3), "
-                                   "log_prob (naz_cnf_integrate_dopri5 t 0->1)" if dopri5 else
+                                   ("adaptive dopri5 atol=rtol=1e-4, torchdyn's batch-global step size "
+                                    "(SURVEY.md §8f rank 3), log_prob (naz_cnf_integrate_dopri5_global t 0->1)" if glob
+                                    else "adaptive dopri5 atol=rtol=1e-4 per 16-row group (SURVEY.md §8f rank 3), "
+                                    "log_prob (naz_cnf_integrate_dopri5 t 0->1)") if dopri5 else
                                    "fixed-step RK4 x 8 (NFE 32, SURVEY.md §8d pin), log_prob "
                                    "(naz_cnf_integrate t 0->1)"),
                        "batch_per_gpu": B, "global_batch": G,
@@ -441,7 +445,7 @@ def run_cnf(args, dev, rank, world, dist):
                          "peak_note": "f16x3: layer 0 at the exact-FP32 MFMA peak, the rest at the dense fp16 "
                                       "MFMA peak / 3 products, FLOP-weighted; f32: exact-FP32 MFMA peak "
                                       f"{FP32_PEAK_TFLOPS}",
-                         "kernel": f"{'cnf_dopri5_kernel' if dopri5 else 'cnf_kernel'}"
+                         "kernel": f"{('cnf_dp5g_step_kernel' if glob else 'cnf_dopri5_kernel') if dopri5 else 'cnf_kernel'}"
                                    f"<16,0,128,128,128,0,softplus,{mode}>",
                          "flop_per_row": flop_row, "avg_kernel_ms": kern_s * 1e3},
         }
@@ -943,6 +947,8 @@ def main():
     ap.add_argument("--cnf-train", action="store_true",
                     help="§8f rank 3: the CNF NLL training step (configs[4] block, RK4 x 8, discrete-adjoint "
                          "backward on the HIP walk) over 2^18 rows")
+    ap.add_argument("--cnf-control", choices=["global", "group"], default="global",
+                    help="--cnf-solver dopri5: torchdyn's batch-global step size (default) or per 16-row group")
     ap.add_argument("--cnf-solver", choices=["rk4", "dopri5"], default="rk4",
                     help="--cnf: pinned fixed-step RK4 x 8 (default) or adaptive dopri5 (atol = rtol = 1e-4)")
     ap.add_argument("--sample", action="store_true",

@@ -301,6 +301,18 @@ int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const fl
                              const float* ctx, int64_t ldc, const float* eps, int64_t lde, float t0, float t1,
                              float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
                              int* nfe, int64_t B, void* stream);
+/* The same solve with torchdyn's BATCH-GLOBAL step control, the reference's semantics (naz
+ * FFJORDTransform -> torchdyn odeint, continuous_transforms.py:73-82): one step size for the
+ * whole batch, the error norm = RMS over every element of the augmented state [B, D + 1].  Each
+ * attempted step is one launch over all rows plus a one-workgroup controller launch; the call
+ * polls the controller every 4 attempts, so it SYNCHRONISES `stream` (not graph-capturable).
+ * workspace: device buffer of naz_cnf_dopri5_global_workspace_bytes(d, B) bytes.  nfe
+ * (nullable, device int[1]): the batch's RHS evaluations, negated when max_steps ran out. */
+int64_t naz_cnf_dopri5_global_workspace_bytes(const naz_cnf_desc* d, int64_t B);
+int naz_cnf_integrate_dopri5_global(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx,
+                                    const float* ctx, int64_t ldc, const float* eps, int64_t lde, float t0, float t1,
+                                    float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld,
+                                    int ld_mode, int* nfe, void* workspace, int64_t B, void* stream);
 /* CNF training (§8f rank 3; replaces the autograd graph torchdyn's adjoint builds through naz's
  * hutch_trace, continuous_transforms.py:75-89): the input-adjoint GEMM of one vector-field layer
  * under the Hutchinson JVP, with the VJP of the layer's activation fused into its epilogue.  The

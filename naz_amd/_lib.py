@@ -88,6 +88,10 @@ SIGNATURES = {
                                     _i, _vp, _i64, _vp, _i, _i64, _vp]),
     "naz_cnf_integrate_dopri5": (C.c_int, [C.POINTER(CnfDesc), _vp, _vp, _i64, _vp, _i64, _vp, _i64, C.c_float,
                                            C.c_float, C.c_float, C.c_float, _i, _vp, _i64, _vp, _i, _vp, _i64, _vp]),
+    "naz_cnf_dopri5_global_workspace_bytes": (C.c_int64, [C.POINTER(CnfDesc), _i64]),
+    "naz_cnf_integrate_dopri5_global": (C.c_int, [C.POINTER(CnfDesc), _vp, _vp, _i64, _vp, _i64, _vp, _i64, C.c_float,
+                                                  C.c_float, C.c_float, C.c_float, _i, _vp, _i64, _vp, _i, _vp, _vp,
+                                                  _i64, _vp]),
     "naz_gemm_jvp_bwd": (C.c_int, [_vp, _i64, _i, _vp, _i64, _vp, _i64, _vp, _i64, _i, _i64, _i, _vp]),
     "naz_ar_flow_supported": (C.c_int, [C.POINTER(ArDesc)]),
     "naz_ar_flow_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),

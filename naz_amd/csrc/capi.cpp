@@ -217,6 +217,24 @@ int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const fl
                               ld_mode, nfe, B, as_stream(stream));
 }
 
+int64_t naz_cnf_dopri5_global_workspace_bytes(const naz_cnf_desc* d, int64_t B) {
+  if (B < 0) return -1;
+  return cnf_dopri5_global_workspace_bytes(d, B);
+}
+
+int naz_cnf_integrate_dopri5_global(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx,
+                                    const float* ctx, int64_t ldc, const float* eps, int64_t lde, float t0, float t1,
+                                    float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld,
+                                    int ld_mode, int* nfe, void* workspace, int64_t B, void* stream) {
+  if (B < 0) return set_error("naz_cnf_integrate_dopri5_global: negative batch");
+  if (B > 0 && (packed == nullptr || x == nullptr || eps == nullptr || y == nullptr))
+    return set_error("naz_cnf_integrate_dopri5_global: null pointer");
+  if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
+    return set_error("naz_cnf_integrate_dopri5_global: context required");
+  return cnf_integrate_dopri5_global(d, packed, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy,
+                                     ld, ld_mode, nfe, workspace, B, as_stream(stream));
+}
+
 int naz_gemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
                      const float* S, int64_t lds, int act, int64_t M, int N, void* stream) {
   if (M < 0 || N < 0 || K < 0) return set_error("naz_gemm_jvp_bwd: negative shape");

@@ -768,6 +768,319 @@ __global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_dopri5_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Batch-global dopri5: torchdyn's controller as naz configures it (ONE step size for the whole
+// batch; hairer_norm = the RMS over every element of the augmented state [B, D + 1]).  The grid
+// cannot agree on a step inside one launch without a grid barrier, so each attempted step is
+// one launch of cnf_dp5g_step_kernel (the six stages k1..k5, f(y5) for all rows, the rows' sum
+// of squared scaled errors as one partial per workgroup) followed by the one-workgroup
+// controller cnf_dp5g_ctrl_kernel (fixed-order reduction of the partials: deterministic;
+// accept / reject, next step size).  State and the FSAL stage live in HBM between launches in
+// two parities; the controller flips the parity on accept.  Launches after the solve has
+// finished return at once (ctrl->done); the host polls `done` every few attempts
+// (cnf_integrate_dopri5_global).  oracle/naz_oracle.py::dopri5_global restates it in fp64.
+// ---------------------------------------------------------------------------
+struct Dp5Ctrl {
+  float t, h, hh, h0, d1;
+  int cur, last, steps, nfe, done, exhausted, pad[5];
+};
+constexpr int kDp5MaxParts = 2048;
+
+template <class CF>
+NAZ_DEV void dp5g_load(const float* __restrict__ st, int64_t row, bool valid, int q, float (&xs)[CF::XS], float& a) {
+  constexpr int W = CF::D + 1;
+#pragma unroll
+  for (int s = 0; s < CF::XS; ++s) {
+    const int fi = q + 4 * s;
+    xs[s] = (valid && fi < CF::D) ? st[row * W + fi] : 0.f;
+  }
+  a = valid ? st[row * W + CF::D] : 0.f;
+}
+
+template <class CF>
+NAZ_DEV void dp5g_store(float* __restrict__ st, int64_t row, bool valid, int q, const float (&xs)[CF::XS], float a) {
+  constexpr int W = CF::D + 1;
+  if (!valid) return;
+#pragma unroll
+  for (int s = 0; s < CF::XS; ++s) {
+    const int fi = q + 4 * s;
+    if (fi < CF::D) st[row * W + fi] = xs[s];
+  }
+  if (q == 0) st[row * W + CF::D] = a;
+}
+
+// per-workgroup fixed-order sum of one value per wave (lane 0 holds the wave's total)
+NAZ_DEV float dp5g_block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+  return s;
+}
+
+// PHASE 0: k0 = f(x0), partials of |x0 / sc|^2 and |k0 / sc|^2 (sc = atol + rtol |x0|; a0 = 0)
+// PHASE 1: f1 = f(x0 + dir h0 k0), partial of |(f1 - k0) / sc|^2
+template <class CF, bool X3, int PHASE>
+__global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_dp5g_init_kernel(
+    const float* __restrict__ packed, const float* __restrict__ x, int64_t ldx, const float* __restrict__ ctx,
+    int64_t ldc, const float* __restrict__ eps, int64_t lde, float t0, float t1, float atol, float rtol,
+    float* __restrict__ st, float* __restrict__ kb, float* __restrict__ parts, const Dp5Ctrl* __restrict__ ctrl,
+    int64_t B) {
+  __shared__ __attribute__((aligned(16))) float lds[CF::TOTAL];
+  __shared__ float red[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4;
+  for (int i = tid * 4; i < CF::TOTAL; i += blockDim.x * 4)
+    *reinterpret_cast<floatx4*>(lds + i) = *reinterpret_cast<const floatx4*>(packed + i);
+  __syncthreads();
+  constexpr int CSR = CF::CS > 0 ? CF::CS : 1, XS = CF::XS;
+  const float dir = t1 > t0 ? 1.f : -1.f;
+  const float h0 = PHASE == 1 ? ctrl->h0 : 0.f;
+  float acc0 = 0.f, acc1 = 0.f;
+  for (int64_t tile = blockIdx.x; tile * kCnfRows < B; tile += gridDim.x) {
+    const int64_t row = tile * kCnfRows + wave * 16 + (lane & 15);
+    const bool valid = row < B;
+    float xs[XS], es[XS], cs[CSR], f[XS], g;
+    bool live[XS];
+#pragma unroll
+    for (int s = 0; s < XS; ++s) {
+      const int fi = q + 4 * s;
+      live[s] = valid && fi < CF::D;
+      xs[s] = live[s] ? x[row * ldx + fi] : 0.f;
+      es[s] = live[s] ? eps[row * lde + fi] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < CSR; ++s) {
+      const int fi = q + 4 * s;
+      cs[s] = (CF::CS > 0 && valid && fi < CF::C) ? ctx[(ldc ? row * ldc : 0) + fi] : 0.f;
+    }
+    const bool alive = valid && q == 0;
+    if constexpr (PHASE == 0) {
+      cnf_rhs<CF, X3>(lds, xs, es, cs, f, g, lane);
+      dp5g_store<CF>(st, row, valid, q, xs, 0.f);
+      dp5g_store<CF>(kb, row, valid, q, f, g);
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {
+        const float sc = atol + rtol * fabsf(xs[s]);
+        acc0 += live[s] ? (xs[s] / sc) * (xs[s] / sc) : 0.f;
+        acc1 += live[s] ? (f[s] / sc) * (f[s] / sc) : 0.f;
+      }
+      acc1 += alive ? (g / atol) * (g / atol) : 0.f;  // a0 = 0: |a0 / sca|^2 = 0
+    } else {
+      float k0[XS], k0a, xin[XS];
+      dp5g_load<CF>(kb, row, valid, q, k0, k0a);
+#pragma unroll
+      for (int s = 0; s < XS; ++s) xin[s] = xs[s] + dir * h0 * k0[s];
+      cnf_rhs<CF, X3>(lds, xin, es, cs, f, g, lane);
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {
+        const float sc = atol + rtol * fabsf(xs[s]), r = (f[s] - k0[s]) / sc;
+        acc0 += live[s] ? r * r : 0.f;
+      }
+      acc0 += alive ? ((g - k0a) / atol) * ((g - k0a) / atol) : 0.f;
+    }
+  }
+  const float s0 = dp5g_block_sum(wave_sum(acc0), red);
+  const float s1 = PHASE == 0 ? dp5g_block_sum(wave_sum(acc1), red) : 0.f;
+  if (tid == 0) {
+    parts[blockIdx.x] = s0;
+    if (PHASE == 0) parts[kDp5MaxParts + blockIdx.x] = s1;
+  }
+}
+
+template <class CF, bool X3>
+__global__ void __launch_bounds__(kCnfRows * 4, 1) cnf_dp5g_step_kernel(
+    const float* __restrict__ packed, const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ eps,
+    int64_t lde, float atol, float rtol, float* __restrict__ st0, float* __restrict__ st1, float* __restrict__ kb0,
+    float* __restrict__ kb1, float* __restrict__ parts, const Dp5Ctrl* __restrict__ ctrl, int64_t B) {
+  if (ctrl->done) return;
+  __shared__ __attribute__((aligned(16))) float lds[CF::TOTAL];
+  __shared__ float red[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4;
+  for (int i = tid * 4; i < CF::TOTAL; i += blockDim.x * 4)
+    *reinterpret_cast<floatx4*>(lds + i) = *reinterpret_cast<const floatx4*>(packed + i);
+  __syncthreads();
+  constexpr int CSR = CF::CS > 0 ? CF::CS : 1, XS = CF::XS;
+  constexpr float b0 = 35.f / 384, b2 = 500.f / 1113, b3 = 125.f / 192, b4 = -2187.f / 6784, b5 = 11.f / 84;
+  constexpr float e0 = 35.f / 384 - 5179.f / 57600, e2 = 500.f / 1113 - 7571.f / 16695,
+                  e3 = 125.f / 192 - 393.f / 640, e4 = -2187.f / 6784 + 92097.f / 339200,
+                  e5 = 11.f / 84 - 187.f / 2100, e6 = -1.f / 40;
+  const int cur = ctrl->cur;
+  const float hh = ctrl->hh;
+  const float* sc_ = cur ? st1 : st0;  // current state / FSAL stage
+  const float* kc_ = cur ? kb1 : kb0;
+  float* sn_ = cur ? st0 : st1;        // candidate
+  float* kn_ = cur ? kb0 : kb1;
+  float acc = 0.f;
+  for (int64_t tile = blockIdx.x; tile * kCnfRows < B; tile += gridDim.x) {
+    const int64_t row = tile * kCnfRows + wave * 16 + (lane & 15);
+    const bool valid = row < B;
+    float xs[XS], es[XS], cs[CSR], a;
+    bool live[XS];
+    dp5g_load<CF>(sc_, row, valid, q, xs, a);
+#pragma unroll
+    for (int s = 0; s < XS; ++s) {
+      const int fi = q + 4 * s;
+      live[s] = valid && fi < CF::D;
+      es[s] = live[s] ? eps[row * lde + fi] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < CSR; ++s) {
+      const int fi = q + 4 * s;
+      cs[s] = (CF::CS > 0 && valid && fi < CF::C) ? ctx[(ldc ? row * ldc : 0) + fi] : 0.f;
+    }
+    const bool alive = valid && q == 0;
+    float k0[XS], k1[XS], k2[XS], k3[XS], k4[XS], k5[XS], xin[XS], x5[XS], f[XS];
+    float k0a, k1a = 0.f, k2a = 0.f, k3a = 0.f, k4a = 0.f, k5a = 0.f, a5 = 0.f, g;
+    dp5g_load<CF>(kc_, row, valid, q, k0, k0a);
+#pragma unroll
+    for (int s = 0; s < XS; ++s) xin[s] = xs[s] + hh * kDpA[0] * k0[s];
+    // one RHS call site; the stage machine of cnf_dopri5_kernel (phases 1..6)
+    for (int phase = 1; phase <= 6; ++phase) {
+      cnf_rhs<CF, X3>(lds, xin, es, cs, f, g, lane);
+      if (phase == 1) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k1[s] = f[s];
+          xin[s] = xs[s] + hh * (kDpA[1] * k0[s] + kDpA[2] * k1[s]);
+        }
+        k1a = g;
+      } else if (phase == 2) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k2[s] = f[s];
+          xin[s] = xs[s] + hh * (kDpA[3] * k0[s] + kDpA[4] * k1[s] + kDpA[5] * k2[s]);
+        }
+        k2a = g;
+      } else if (phase == 3) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k3[s] = f[s];
+          xin[s] = xs[s] + hh * (kDpA[6] * k0[s] + kDpA[7] * k1[s] + kDpA[8] * k2[s] + kDpA[9] * k3[s]);
+        }
+        k3a = g;
+      } else if (phase == 4) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k4[s] = f[s];
+          xin[s] = xs[s] + hh * (kDpA[10] * k0[s] + kDpA[11] * k1[s] + kDpA[12] * k2[s] + kDpA[13] * k3[s] +
+                                 kDpA[14] * k4[s]);
+        }
+        k4a = g;
+      } else if (phase == 5) {
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+          k5[s] = f[s];
+          x5[s] = xs[s] + hh * (b0 * k0[s] + b2 * k2[s] + b3 * k3[s] + b4 * k4[s] + b5 * k5[s]);
+          xin[s] = x5[s];
+        }
+        k5a = g;
+        a5 = a + hh * (b0 * k0a + b2 * k2a + b3 * k3a + b4 * k4a + b5 * k5a);
+      }
+    }
+    // f is now f(y5) (FSAL); the error of this row's elements
+#pragma unroll
+    for (int s = 0; s < XS; ++s) {
+      const float err = hh * (e0 * k0[s] + e2 * k2[s] + e3 * k3[s] + e4 * k4[s] + e5 * k5[s] + e6 * f[s]);
+      const float r = err / (atol + rtol * fmaxf(fabsf(xs[s]), fabsf(x5[s])));
+      acc += live[s] ? r * r : 0.f;
+    }
+    {
+      const float erra = hh * (e0 * k0a + e2 * k2a + e3 * k3a + e4 * k4a + e5 * k5a + e6 * g);
+      const float r = erra / (atol + rtol * fmaxf(fabsf(a), fabsf(a5)));
+      acc += alive ? r * r : 0.f;
+    }
+    dp5g_store<CF>(sn_, row, valid, q, x5, a5);
+    dp5g_store<CF>(kn_, row, valid, q, f, g);
+  }
+  const float sum = dp5g_block_sum(wave_sum(acc), red);
+  if (tid == 0) parts[blockIdx.x] = sum;
+}
+
+// one 256-thread workgroup: fixed-order sum of `nparts` partials (twice for PHASE 0)
+NAZ_DEV float dp5g_sum_parts(const float* __restrict__ p, int n, float* red) {
+  float v = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) v += p[i];
+  return dp5g_block_sum(wave_sum(v), red);
+}
+
+// MODE 0: after init PHASE 0 (h0); 1: after PHASE 1 (h, first attempt); 2: after a step attempt
+template <int MODE>
+__global__ void __launch_bounds__(256, 1) cnf_dp5g_ctrl_kernel(Dp5Ctrl* __restrict__ ctrl,
+                                                                 const float* __restrict__ parts, int nparts,
+                                                                 double n_elem, float t0, float t1, int max_steps) {
+  __shared__ float red[16];
+  if (MODE == 2 && ctrl->done) return;
+  const float s0 = dp5g_sum_parts(parts, nparts, red);
+  const float s1 = MODE == 0 ? dp5g_sum_parts(parts + kDp5MaxParts, nparts, red) : 0.f;
+  if (threadIdx.x != 0) return;
+  const float dir = t1 > t0 ? 1.f : -1.f;
+  const float inv_n = (float)(1.0 / n_elem);
+  bool start = false;
+  if constexpr (MODE == 0) {
+    const float d0 = sqrtf(s0 * inv_n), d1 = sqrtf(s1 * inv_n);
+    ctrl->t = t0;
+    ctrl->d1 = d1;
+    ctrl->h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : 0.01f * d0 / d1;
+    ctrl->cur = 0;
+    ctrl->steps = 0;
+    ctrl->nfe = 1;
+    ctrl->done = 0;
+    ctrl->exhausted = 0;
+  } else if constexpr (MODE == 1) {
+    const float h0 = ctrl->h0, d1 = ctrl->d1;
+    const float d2 = sqrtf(s0 * inv_n) / h0, dm = fmaxf(d1, d2);
+    const float h1 = dm <= 1e-15f ? fmaxf(1e-6f, h0 * 1e-3f) : powf(0.01f / dm, 1.f / 6.f);
+    ctrl->h = fminf(100.f * h0, h1);
+    ctrl->nfe = 2;
+    start = true;
+  } else {
+    const float en = sqrtf(s0 * inv_n);
+    const bool accept = en <= 1.f;
+    const float hh = ctrl->hh;
+    if (accept) {
+      ctrl->cur ^= 1;
+      ctrl->t = ctrl->last ? t1 : ctrl->t + hh;
+    }
+    const float fac = en == 0.f ? 10.f : fminf(10.f, fmaxf(0.9f * powf(en, -0.2f), accept ? 1.f : 0.2f));
+    ctrl->h = fabsf(hh) * fac;
+    ctrl->steps += 1;
+    ctrl->nfe += 6;
+    if (ctrl->t == t1) {
+      ctrl->done = 1;
+    } else if (ctrl->steps >= max_steps) {
+      ctrl->done = 1;
+      ctrl->exhausted = 1;
+    } else {
+      start = true;
+    }
+  }
+  if (start) {  // the next attempt's step, clipped to end at t1
+    const float rem = fabsf(t1 - ctrl->t);
+    ctrl->last = ctrl->h >= rem ? 1 : 0;
+    ctrl->hh = dir * (ctrl->last ? rem : ctrl->h);
+  }
+}
+
+template <class CF>
+__global__ void cnf_dp5g_finish_kernel(const float* __restrict__ st0, const float* __restrict__ st1,
+                                       const Dp5Ctrl* __restrict__ ctrl, float* __restrict__ y, int64_t ldy,
+                                       float* __restrict__ ld, int ld_mode, int* __restrict__ nfe_out, int64_t B) {
+  const float* st = ctrl->cur ? st1 : st0;
+  constexpr int W = CF::D + 1;
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < B; row += (int64_t)gridDim.x * blockDim.x) {
+    for (int d = 0; d < CF::D; ++d) y[row * ldy + d] = st[row * W + d];
+    if (ld != nullptr) {
+      const float a = st[row * W + CF::D];
+      if (ld_mode == NAZ_LD_ROWSUM_ADD) ld[row] += a;
+      else if (ld_mode == NAZ_LD_ROWSUM_SUB) ld[row] -= a;
+      else ld[row] = a;
+    }
+  }
+  if (nfe_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) nfe_out[0] = ctrl->exhausted ? -ctrl->nfe : ctrl->nfe;
+}
+
+// ---------------------------------------------------------------------------
 // Instantiations and dispatch
 // ---------------------------------------------------------------------------
 template <class CF>
@@ -831,6 +1144,68 @@ struct CnfOps {
                          y, ldy, ld, ld_mode, nfe, B);
     }
     return check_launch("cnf_dopri5_kernel");
+  }
+  // workspace floats: two state parities and two FSAL parities [B][D + 1], the partials, the control block
+  static int64_t dp5g_workspace_floats(int64_t B) { return 4 * B * (CF::D + 1) + 2 * kDp5MaxParts + 64; }
+  static int run_dopri5_global(const void* packed, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
+                               const float* eps, int64_t lde, float t0, float t1, float atol, float rtol, int max_steps,
+                               float* y, int64_t ldy, float* ld, int ld_mode, int* nfe, void* work, int64_t B,
+                               int mode, hipStream_t s) {
+    if constexpr (!kX3) {
+      if (mode == NAZ_CNF_F16X3) return set_error("naz_cnf: f16x3 not available for this shape");
+    }
+    const int64_t tiles = (B + kCnfRows - 1) / kCnfRows;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess)
+      cus = 256;
+    const int per_cu = (160 * 1024) / (CF::TOTAL * 4) >= 2 ? 2 : 1;
+    int64_t grid = tiles < (int64_t)cus * per_cu ? tiles : (int64_t)cus * per_cu;
+    if (grid > kDp5MaxParts) grid = kDp5MaxParts;
+    const int64_t n = B * (CF::D + 1);
+    float* w = static_cast<float*>(work);
+    float *st0 = w, *st1 = w + n, *kb0 = w + 2 * n, *kb1 = w + 3 * n, *parts = w + 4 * n;
+    Dp5Ctrl* ctrl = reinterpret_cast<Dp5Ctrl*>(parts + 2 * kDp5MaxParts);
+    const float* pk = static_cast<const float*>(packed);
+    const dim3 g((unsigned)grid), b(kCnfRows * 4);
+    const double n_elem = (double)n;
+    auto launch = [&](auto x3) {
+      constexpr bool X3 = decltype(x3)::value;
+      hipLaunchKernelGGL((cnf_dp5g_init_kernel<CF, X3, 0>), g, b, 0, s, pk, x, ldx, ctx, ldc, eps, lde, t0, t1, atol,
+                         rtol, st0, kb0, parts, ctrl, B);
+      hipLaunchKernelGGL((cnf_dp5g_ctrl_kernel<0>), dim3(1), dim3(256), 0, s, ctrl, parts, (int)grid, n_elem, t0, t1,
+                         max_steps);
+      hipLaunchKernelGGL((cnf_dp5g_init_kernel<CF, X3, 1>), g, b, 0, s, pk, x, ldx, ctx, ldc, eps, lde, t0, t1, atol,
+                         rtol, st0, kb0, parts, ctrl, B);
+      hipLaunchKernelGGL((cnf_dp5g_ctrl_kernel<1>), dim3(1), dim3(256), 0, s, ctrl, parts, (int)grid, n_elem, t0, t1,
+                         max_steps);
+      if (check_launch("cnf_dp5g_init") != 0) return -1;
+      // attempts in rounds of 4, then one poll of `done` (torchdyn's controller is host-driven too)
+      int done = 0;
+      for (int issued = 0; issued < max_steps && !done;) {
+        const int k = max_steps - issued < 4 ? max_steps - issued : 4;
+        for (int i = 0; i < k; ++i) {
+          hipLaunchKernelGGL((cnf_dp5g_step_kernel<CF, X3>), g, b, 0, s, pk, ctx, ldc, eps, lde, atol, rtol, st0, st1,
+                             kb0, kb1, parts, ctrl, B);
+          hipLaunchKernelGGL((cnf_dp5g_ctrl_kernel<2>), dim3(1), dim3(256), 0, s, ctrl, parts, (int)grid, n_elem, t0,
+                             t1, max_steps);
+        }
+        issued += k;
+        if (check_launch("cnf_dp5g_step") != 0) return -1;
+        if (hipMemcpyAsync(&done, &ctrl->done, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+          return set_error("naz_cnf_integrate_dopri5_global: polling the controller failed");
+      }
+      const int64_t fg = (B + 255) / 256 < 4096 ? (B + 255) / 256 : 4096;
+      hipLaunchKernelGGL((cnf_dp5g_finish_kernel<CF>), dim3((unsigned)fg), dim3(256), 0, s, st0, st1, ctrl, y, ldy, ld,
+                         ld_mode, nfe, B);
+      return check_launch("cnf_dp5g_finish_kernel");
+    };
+    if (mode == NAZ_CNF_F16X3) {
+      if constexpr (kX3) return launch(std::integral_constant<bool, true>{});
+      return -1;
+    }
+    return launch(std::integral_constant<bool, false>{});
   }
 };
 
@@ -918,6 +1293,31 @@ int cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const float*
   return cnf_dispatch(d, [&](auto ops) {
     return decltype(ops)::run_dopri5(packed, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy, ld,
                                      ld_mode, nfe, B, d->mfma_mode, s);
+  });
+}
+
+int64_t cnf_dopri5_global_workspace_bytes(const naz_cnf_desc* d, int64_t B) {
+  int64_t n = -1;
+  if (cnf_dispatch(d, [&](auto ops) {
+        n = decltype(ops)::dp5g_workspace_floats(B) * 4;
+        return 0;
+      }) != 0)
+    return -1;
+  return n;
+}
+
+int cnf_integrate_dopri5_global(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx,
+                                const float* ctx, int64_t ldc, const float* eps, int64_t lde, float t0, float t1,
+                                float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
+                                int* nfe, void* work, int64_t B, hipStream_t s) {
+  if (B == 0) return 0;
+  if (!(atol > 0.f) || !(rtol >= 0.f)) return set_error("naz_cnf_integrate_dopri5_global: atol must be > 0, rtol >= 0");
+  if (max_steps < 1) return set_error("naz_cnf_integrate_dopri5_global: max_steps must be >= 1");
+  if (t0 == t1) return set_error("naz_cnf_integrate_dopri5_global: empty interval");
+  if (work == nullptr) return set_error("naz_cnf_integrate_dopri5_global: workspace required");
+  return cnf_dispatch(d, [&](auto ops) {
+    return decltype(ops)::run_dopri5_global(packed, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy,
+                                            ld, ld_mode, nfe, work, B, d->mfma_mode, s);
   });
 }
 

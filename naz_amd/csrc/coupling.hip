@@ -223,6 +223,37 @@ NAZ_DEV void debug_nonfinite_probe(bool bad, int64_t row, int layer, int stage) 
   }
 }
 
+// The same copy through a buffer resource (buffer_load_dwordx4 ... lds): the per-lane offset is
+// one VGPR set once (lane * 16) and each chunk's offset is scalar (soffset), so a chunk costs no
+// 64-bit VALU address add (global_load_lds needs one per chunk and lane).  `off` = the stage's
+// float offset from the resource base (wave-uniform).  Out-of-range chunks read zeros, never fault.
+struct RingSrc {
+  const float* base;
+  __amdgpu_buffer_rsrc_t r;
+  NAZ_DEV RingSrc(const float* base_, int64_t nfloats)
+      : base(base_), r(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base_), 0,
+                                            (int)(nfloats * 4 < 0x7fffffff ? nfloats * 4 : 0x7fffffff), 0x00020000)) {}
+};
+
+template <int NFLOATS, int NW>
+NAZ_DEV void stage_issue(float* lds, const RingSrc& src, int off) {
+#ifdef NAZ_RING_GLDS
+  return stage_issue<NFLOATS, NW>(lds, src.base + off);
+#endif
+  static_assert(NFLOATS % 256 == 0, "stage must be whole 1 KB chunks");
+  constexpr int CHUNKS = NFLOATS / 256;
+  const int vo = (threadIdx.x & 63) * 16;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int c0 = 0; c0 < CHUNKS; c0 += NW) {
+    const int c = c0 + wave;
+    if (c0 + NW - 1 < CHUNKS || c < CHUNKS) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(src.r, (__attribute__((address_space(3))) void*)(lds + c * 256), 16, vo,
+                                               (off + c * 256) * 4, 0, 0);
+    }
+  }
+}
+
 // stage_issue of the first nch (wave-uniform, <= NFLOATS / 256) 1 KB chunks only
 template <int NFLOATS, int NW>
 NAZ_DEV void stage_issue_lim(float* lds, const float* __restrict__ src, int nch) {
@@ -614,14 +645,28 @@ NAZ_DEV unsigned pack_f16x2(float a, float b) {
 }
 #endif
 
+// the lo pieces of a packed pair: f16(v0 - hi0) | f16(v1 - hi1) << 16 in TWO instructions
+// (v_fma_mixlo_f16 / v_fma_mixhi_f16 round the exact f32 residual to f16 in the same op, RNE as
+// v_cvt_pk_f16_f32) instead of two v_fma_mix_f32 + one v_cvt_pk_f16_f32
+NAZ_DEV unsigned lo_pair_f16(float v0, float v1, unsigned hp) {
+  unsigned lo;
+  asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hp), "v"(v0));
+  asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hp), "v"(v1));
+  return lo;
+}
+
 NAZ_DEV Frag2 split8_f16(const float (&v)[8]) {
   u32x4 H, Lo;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const unsigned hp = pack_f16x2(v[2 * q], v[2 * q + 1]);
-    const float r0 = sub_f16_piece<false>(v[2 * q], hp), r1 = sub_f16_piece<true>(v[2 * q + 1], hp);
     H[q] = hp;
+#ifdef NAZ_SPLIT_MIX32
+    const float r0 = sub_f16_piece<false>(v[2 * q], hp), r1 = sub_f16_piece<true>(v[2 * q + 1], hp);
     Lo[q] = pack_f16x2(r0, r1);
+#else
+    Lo[q] = lo_pair_f16(v[2 * q], v[2 * q + 1], hp);
+#endif
   }
   return Frag2{__builtin_bit_cast(half8, H), __builtin_bit_cast(half8, Lo)};
 }

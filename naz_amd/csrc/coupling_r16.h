@@ -410,7 +410,8 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
   const bool g1f16 = ok;
   const int a_off = g1f16 ? 0 : CF::A32_OFF;
 
-  stage_issue<CF::A_SIZE, kR16Waves>(slot0, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER + a_off);
+  const RingSrc ring(packed, (int64_t)L * CF::LAYER);
+  stage_issue<CF::A_SIZE, kR16Waves>(slot0, ring, (DIR_INV ? (L - 1) : 0) * CF::LAYER + a_off);
 
   const RqsConsts<CF::K, DIR_INV> rc(bound);
   int g = 0;  // global stage counter: stage g lives in slot (g & 1)
@@ -425,8 +426,6 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
         for (int u = 0; u < CF::DQ; ++u) st[CF::S + q * CF::DQ + u] = zu[u];
       }
     }
-    const float* lp = packed + (int64_t)l * CF::LAYER;
-    const float* lnext = packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER;
     floatx4 acc1[CF::HB], acc2[CF::HB], acc3[CF::NO];
     Frag2 f3[CF::KS2];  // GEMM3's B fragments (half 0 forms them, half 1 reuses them)
     // upper spline on this quarter's dim u (parameters in acc3 slots u P .. u P + P - 1)
@@ -473,9 +472,9 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
       const float* cur = (g & 1) ? slot1 : slot0;
       float* nxt = (g & 1) ? slot0 : slot1;
       if constexpr (j + 1 < CF::NSTG) {
-        stage_issue<CF::stage_size(j + 1), kR16Waves>(nxt, lp + CF::stage_off(j + 1));
+        stage_issue<CF::stage_size(j + 1), kR16Waves>(nxt, ring, l * CF::LAYER + CF::stage_off(j + 1));
       } else {
-        if (li + 1 < L) stage_issue<CF::A_SIZE, kR16Waves>(nxt, lnext + a_off);
+        if (li + 1 < L) stage_issue<CF::A_SIZE, kR16Waves>(nxt, ring, (DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER + a_off);
       }
       ++g;
 

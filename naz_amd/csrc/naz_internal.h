@@ -115,6 +115,11 @@ int cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const float*
                          int64_t ldc, const float* eps, int64_t lde, float t0, float t1, float atol, float rtol,
                          int max_steps, float* y, int64_t ldy, float* ld, int ld_mode, int* nfe, int64_t B,
                          hipStream_t s);
+int64_t cnf_dopri5_global_workspace_bytes(const naz_cnf_desc* d, int64_t B);
+int cnf_integrate_dopri5_global(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx,
+                                const float* ctx, int64_t ldc, const float* eps, int64_t lde, float t0, float t1,
+                                float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
+                                int* nfe, void* work, int64_t B, hipStream_t s);
 int rowgemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
                     const float* S, int64_t lds, int act, int64_t M, int N, hipStream_t s);
 

@@ -10,7 +10,8 @@ registers, the MLP resident in LDS (csrc/cnf.hip).
 Solver: naz constructs torchdyn ``NeuralODE(solver='dopri5', atol=rtol=1e-4, sensitivity=
 'adjoint')`` (:73-81).  SURVEY.md §8d pins config 5 to fixed-step classical RK4 with 8 steps
 (NFE 32) — the default here (``solver='rk4', steps=8``); ``solver='dopri5'`` runs the adaptive
-Dormand-Prince solve (naz_cnf_integrate_dopri5, one step size per 16-row group).  Under autograd
+Dormand-Prince solve (``step_control="global"``, the default: torchdyn's one step size for the
+batch, naz_cnf_integrate_dopri5_global; ``"group"``: naz_cnf_integrate_dopri5, one per 16 rows).  Under autograd
 the solve is one ``CnfSolveFn`` node (flows/cnf_adjoint.py, §8f rank 3): rk4 backpropagates by the
 discrete adjoint of the pinned solve from per-step checkpoints, dopri5 by the continuous adjoint
 (``adjoint_steps`` RK4 steps back from t1), every RHS and VJP on HIP kernels.  The Hutchinson probe eps ~ N(0, I)
@@ -124,15 +125,20 @@ class _FFJORDCore:
         return self.noise if self.noise is not None else torch.randn(v.shape, device=v.device, dtype=torch.float32)
 
     def _dopri5(self, desc, packed, v, noise, t0, t1, ld_buf, ld_mode):
-        """§8f rank 3: adaptive Dormand-Prince, per-16-row step control."""
-        nfe = self._nfe_buffer(v)
-        y, ld = ops.cnf_integrate_dopri5(desc, packed, v, noise, t0, t1, self.atol, self.rtol, self.max_steps,
-                                         context=self._context, ld_out=ld_buf, ld_mode=ld_mode, nfe=nfe)
-        # a group that hit max_steps before t1 writes a negative count (cnf.hip): its state and
+        """§8f rank 3: adaptive Dormand-Prince.  ``step_control="global"`` (default): torchdyn's
+        one step size for the whole batch (naz_cnf_integrate_dopri5_global); ``"group"``: one per
+        16-row group (naz_cnf_integrate_dopri5, one launch, no host sync)."""
+        glob = self.step_control == "global"
+        nfe = self._nfe_buffer(v, glob)
+        fn = ops.cnf_integrate_dopri5_global if glob else ops.cnf_integrate_dopri5
+        y, ld = fn(desc, packed, v, noise, t0, t1, self.atol, self.rtol, self.max_steps, context=self._context,
+                   ld_out=ld_buf, ld_mode=ld_mode, nfe=nfe)
+        # a solve that hit max_steps before t1 writes a negative count (cnf.hip): its state and
         # log-det are from partway through the interval, so fail loudly (strict, the default)
         if self.strict and nfe.numel() and bool((nfe < 0).any()):
             bad = int((nfe < 0).sum())
-            raise RuntimeError(f"naz_amd CNF dopri5: {bad} of {nfe.numel()} 16-row groups reached max_steps="
+            what = "the batch" if glob else f"{bad} of {nfe.numel()} 16-row groups"
+            raise RuntimeError(f"naz_amd CNF dopri5: {what} reached max_steps="
                                f"{self.max_steps} before t1 (step size collapsed or non-finite state); "
                                "raise max_steps, loosen atol/rtol, or set strict=False to accept partial solves")
         return y, ld
@@ -151,9 +157,10 @@ class _FFJORDCore:
         return ops.cnf_integrate(self._plan.desc, packed, v, noise, t0, t1, self.steps,
                                  context=self._context, ld_out=ld_buf, ld_mode=ld_mode)
 
-    def _nfe_buffer(self, v):
-        """RHS evaluations per 16-row group of the last dopri5 solve (``last_nfe``)."""
-        n = (v.shape[0] + 15) // 16
+    def _nfe_buffer(self, v, glob=False):
+        """RHS evaluations of the last dopri5 solve (``last_nfe``): one count for the batch
+        (global step control) or one per 16-row group."""
+        n = 1 if glob else (v.shape[0] + 15) // 16
         self.last_nfe = torch.empty(n, device=v.device, dtype=torch.int32)
         return self.last_nfe
 
@@ -184,7 +191,9 @@ class _FFJORDCore:
         return self._solve(y, 0.0, 1.0, None, ops.LD_ROWSUM)
 
 
-def _check_solver(solver, steps):
+def _check_solver(solver, steps, step_control="global"):
+    if step_control not in ("global", "group"):
+        raise ValueError("step_control must be 'global' (torchdyn's batch step size) or 'group' (per 16 rows)")
     if solver not in ("rk4", "dopri5"):
         raise NotImplementedError(f"naz_amd CNF: solver {solver!r}: fixed-step 'rk4' (SURVEY.md §8d config 5) and "
                                   "adaptive 'dopri5' are built")
@@ -200,9 +209,10 @@ class FFJORDTransform(_FFJORDCore, TransformModule):
     bijective = True
 
     def __init__(self, net, input_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4, steps=8,
-                 max_steps=1000, strict=True, adjoint_steps=16):
+                 max_steps=1000, strict=True, adjoint_steps=16, step_control="global"):
         super().__init__()
-        _check_solver(solver, steps)
+        _check_solver(solver, steps, step_control)
+        self.step_control = step_control
         self.net, self.input_dim, self.steps = net, input_dim, int(steps)
         self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
         self.max_steps = int(max_steps)
@@ -249,7 +259,7 @@ class _ConditionedFFJORD(_FFJORDCore, Transform):
         return self.module.noise
 
     def __getattr__(self, name):  # solver settings live on the module
-        if name in ("solver", "atol", "rtol", "max_steps", "strict", "adjoint_steps"):
+        if name in ("solver", "atol", "rtol", "max_steps", "strict", "adjoint_steps", "step_control"):
             return getattr(self.module, name)
         raise AttributeError(name)
 
@@ -259,9 +269,10 @@ class ConditionalFFJORDTransform(ConditionalTransformModule):
     monkey-patch of the vector field's ``forward``."""
 
     def __init__(self, net, input_dim, context_dim, solver="rk4", sensitivity="adjoint", atol=1e-4, rtol=1e-4,
-                 steps=8, max_steps=1000, strict=True, adjoint_steps=16):
+                 steps=8, max_steps=1000, strict=True, adjoint_steps=16, step_control="global"):
         super().__init__()
-        _check_solver(solver, steps)
+        _check_solver(solver, steps, step_control)
+        self.step_control = step_control
         self.net, self.input_dim, self.context_dim, self.steps = net, input_dim, context_dim, int(steps)
         self.solver, self.sensitivity, self.atol, self.rtol = solver, sensitivity, atol, rtol
         self.max_steps = int(max_steps)

@@ -21,7 +21,7 @@ Tensor = torch.Tensor
 __all__ = ["rqs", "rqs_bwd", "spline_elementwise", "linear_act", "linear_act_batched", "made_packed_floats", "made_affine_fwd", "made_affine_inv1", "gemm_dact", "affine_ar", "affine_ar_bwd", "base_log_prob",
            "base_log_prob_bwd", "gemm", "colsum", "act_bwd", "bounding_fwd", "bounding_inv",
            "coupling_desc", "coupling_supported", "coupling_param_count", "coupling_pack", "coupling_log_prob",
-           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5", "gemm_jvp_bwd", "flow_desc", "flow_log_prob", "flow_sample",
+           "coupling_sample", "cnf_desc", "cnf_supported", "cnf_param_count", "cnf_pack", "cnf_integrate", "cnf_integrate_dopri5", "cnf_integrate_dopri5_global", "gemm_jvp_bwd", "flow_desc", "flow_log_prob", "flow_sample",
            "LAYOUT_ARN", "LAYOUT_DENSE", "LD_PERDIM", "LD_ROWSUM", "LD_ROWSUM_ADD",
            "LD_ROWSUM_SUB"]
 
@@ -934,4 +934,39 @@ def cnf_integrate_dopri5(d: CnfDesc, packed: Tensor, x: Tensor, eps: Tensor, t0:
     check(lib().naz_cnf_integrate_dopri5(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(eps), lde, float(t0),
                                          float(t1), float(atol), float(rtol), int(max_steps), _p(out), out.stride(0),
                                          _p(ld_out), ld_mode, _p(nfe), B, _stream(dev)), "cnf_integrate_dopri5")
+    return out, ld_out
+
+
+def cnf_integrate_dopri5_global(d: CnfDesc, packed: Tensor, x: Tensor, eps: Tensor, t0: float, t1: float,
+                                atol: float = 1e-4, rtol: float = 1e-4, max_steps: int = 1000,
+                                context: Optional[Tensor] = None, ld_out: Optional[Tensor] = None,
+                                ld_mode: int = LD_ROWSUM, out: Optional[Tensor] = None,
+                                nfe: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """dopri5 FFJORD block solve with torchdyn's batch-global step control
+    (naz_cnf_integrate_dopri5_global: one step size for the batch, the reference's semantics).
+    ``nfe`` (int32 [1], optional) receives the batch's RHS evaluations (negative: max_steps ran
+    out).  Synchronises the current stream (the controller is polled)."""
+    dev = _dev(packed, x, eps, context, ld_out, out)
+    x, ldx = _rows(x)
+    eps, lde = _rows(eps)
+    B = x.shape[0]
+    if eps.shape != x.shape:
+        raise ValueError("eps must match x")
+    context, ldc = _ctx_arg(context, B)
+    if out is None:
+        out = torch.empty_like(x)
+    if ld_out is None:
+        ld_out = torch.empty((B,), device=dev, dtype=torch.float32)
+        if ld_mode in (LD_ROWSUM_ADD, LD_ROWSUM_SUB):
+            ld_out.zero_()
+    if nfe is not None and (nfe.dtype != torch.int32 or nfe.numel() < 1 or nfe.device != dev):
+        raise ValueError("nfe must be a device int32 tensor with one entry")
+    nbytes = int(lib().naz_cnf_dopri5_global_workspace_bytes(d, B))
+    if nbytes < 0:
+        check(-1, "cnf_dopri5_global_workspace_bytes")
+    work = torch.empty((max(nbytes, 4) + 3) // 4, device=dev, dtype=torch.float32)
+    check(lib().naz_cnf_integrate_dopri5_global(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(eps), lde, float(t0),
+                                                float(t1), float(atol), float(rtol), int(max_steps), _p(out),
+                                                out.stride(0), _p(ld_out), ld_mode, _p(nfe), _p(work), B,
+                                                _stream(dev)), "cnf_integrate_dopri5_global")
     return out, ld_out

@@ -279,12 +279,72 @@ def test_cnf_dopri5_vs_oracle(D, C, hidden, act, direction, mfma):
     assert np.all(np.abs(a - ag) <= 20 * (atol + rtol * np.abs(ag))), np.abs(a - ag).max()
 
 
+@pytest.mark.parametrize("D,C,hidden,act", [(4, 2, [32, 32], "softplus"), (2, 2, [128, 64, 64], "softplus"),
+                                            (16, 0, [128, 128, 128], "softplus")])
+@pytest.mark.parametrize("direction", [(0.0, 1.0), (1.0, 0.0)])
+@pytest.mark.parametrize("mfma", ["f32", "f16x3"])
+def test_cnf_dopri5_global_vs_oracle(D, C, hidden, act, direction, mfma):
+    """torchdyn's batch-global step control (naz_cnf_integrate_dopri5_global, the reference's
+    semantics: continuous_transforms.py:73-82) vs oracle.dopri5_global in fp64: the same number
+    of RHS evaluations (= the same accepted/rejected step sequence), the same solution within
+    atol = rtol = 1e-4 (2e-4 absolute), and within the tolerance of the converged solution."""
+    from naz_amd import ops
+    B, atol, rtol = 200, 1e-4, 1e-4
+    rng = np.random.default_rng(D * 10 + C + 1)
+    x = (rng.standard_normal((B, D)) * 0.8).astype(np.float32)
+    c = rng.standard_normal((B, C)).astype(np.float32) if C else None
+    eps = rng.standard_normal((B, D)).astype(np.float32)
+    t0, t1 = direction
+    yg, ag, nfe64 = _oracle_dopri5_global(D, C, hidden, act, x, c, eps, t0, t1, atol, rtol)
+    _, _, _, yr, ar = _oracle_dopri5(D, C, hidden, act, x, c, eps, t0, t1, atol, rtol)
+    _, _, flat = _oracle_block(D, C, hidden, act, x, c, eps, t0, t1, 1, torch.float64)
+    d = ops.cnf_desc(D, C, hidden, act, mfma)
+    if not ops.cnf_supported(d):
+        pytest.skip("mode not available for this shape")
+    packed = ops.cnf_pack(d, _cuda(flat))
+    nfe = torch.zeros(1, device=DEV, dtype=torch.int32)
+    y, a = ops.cnf_integrate_dopri5_global(d, packed, _cuda(x), _cuda(eps), t0, t1, atol, rtol,
+                                           context=None if c is None else _cuda(c), nfe=nfe)
+    y, a, n = _np(y), _np(a), int(nfe.item())
+    assert n == nfe64, (n, nfe64)
+    assert np.abs(y - yg).max() <= 2e-4 and np.abs(a - ag).max() <= 2e-4, (np.abs(y - yg).max(), np.abs(a - ag).max())
+    assert np.all(np.abs(y - yr) <= 20 * (atol + rtol * np.abs(yr))), np.abs(y - yr).max()
+    assert np.all(np.abs(a - ar) <= 20 * (atol + rtol * np.abs(ar))), np.abs(a - ar).max()
+
+
+def test_cnf_dopri5_global_ragged_and_max_steps():
+    """Batch-global control: ragged batch sizes (partial waves and workgroups) agree with the fp64
+    oracle's step count; max_steps exhaustion is reported (negative count)."""
+    from naz_amd import ops
+    D, C, hidden, act = 4, 2, [32, 32], "softplus"
+    for B in (1, 37, 1000):
+        rng = np.random.default_rng(B)
+        x = (rng.standard_normal((B, D)) * 0.8).astype(np.float32)
+        c = rng.standard_normal((B, C)).astype(np.float32)
+        eps = rng.standard_normal((B, D)).astype(np.float32)
+        yg, ag, nfe64 = _oracle_dopri5_global(D, C, hidden, act, x, c, eps, 0.0, 1.0, 1e-4, 1e-4)
+        _, _, flat = _oracle_block(D, C, hidden, act, x, c, eps, 0.0, 1.0, 1, torch.float64)
+        d = ops.cnf_desc(D, C, hidden, act, "f32")
+        packed = ops.cnf_pack(d, _cuda(flat))
+        nfe = torch.zeros(1, device=DEV, dtype=torch.int32)
+        y, a = ops.cnf_integrate_dopri5_global(d, packed, _cuda(x), _cuda(eps), 0.0, 1.0, context=_cuda(c), nfe=nfe)
+        assert int(nfe.item()) == nfe64 and np.abs(_np(y) - yg).max() <= 2e-4, (B, int(nfe.item()), nfe64)
+        y, a = ops.cnf_integrate_dopri5_global(d, packed, _cuda(x), _cuda(eps), 0.0, 1.0, 1e-9, 1e-9, max_steps=2,
+                                               context=_cuda(c), nfe=nfe)
+        assert int(nfe.item()) < 0, "max_steps exhaustion must be reported"
+
+
 def test_cnf_dopri5_flow_api_and_ragged():
-    """NormalizingFlow("cnf", ..., solver="dopri5") log_prob runs the adaptive kernel; ragged
-    batches (the last wave partially filled) give the same per-row result as a full batch."""
+    """NormalizingFlow("cnf", ..., solver="dopri5", step_control="group") log_prob runs the
+    per-group adaptive kernel; ragged batches (the last wave partially filled) give the same
+    per-row result as a full batch.  The default (batch-global control) runs and is finite."""
     from naz_amd.flows import NormalizingFlow
     rng = np.random.default_rng(4)
-    f = NormalizingFlow("cnf", None, 4, 2, [32, 32], 2, solver="dopri5").to(DEV)
+    g = NormalizingFlow("cnf", None, 4, 2, [32, 32], 2, solver="dopri5").to(DEV)
+    xg = _cuda(rng.standard_normal((200, 4)) * 0.8)
+    assert bool(torch.isfinite(g.log_prob(xg, condition=_cuda(rng.standard_normal((200, 2))))).all())
+    assert all(t.step_control == "global" for t in g.transforms)
+    f = NormalizingFlow("cnf", None, 4, 2, [32, 32], 2, solver="dopri5", step_control="group").to(DEV)
     x = _cuda(rng.standard_normal((200, 4)) * 0.8)
     c = _cuda(rng.standard_normal((200, 2)))
     for t in f.transforms:

@@ -4,7 +4,7 @@ from pathlib import Path
 
 import pytest
 
-from tests.isa_ring import check_library, code_objects, disassemble, functions, ring_violations
+from tests.isa_ring import check_library, code_objects, disassemble, functions, is_dma, ring_violations
 
 LIB = Path(__file__).resolve().parents[1] / "naz_amd" / "lib" / "libnazhip.so"
 HEADLINE = "_ZN3naz19coupling_r16_kernelINS_6CfgR16ILi16ELi32ELi8ELi8ELi128ELb1EEELb1ELi0EEEvPKfiS4_lS4_lS4_S4_PfS5_llfS5_"
@@ -31,7 +31,7 @@ def test_headline_kernel_present_and_checked(lib):
         fs = functions(disassemble(co))
         if HEADLINE in fs:
             start, insns = fs[HEADLINE]
-            assert any(t.startswith("global_load_lds") for _, t in insns)
+            assert any(is_dma(t) for _, t in insns)
             assert ring_violations(start, insns) == []
             found = True
     assert found, "the config-3 log_prob kernel is not in the library"

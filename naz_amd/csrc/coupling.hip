@@ -647,7 +647,11 @@ NAZ_DEV unsigned pack_f16x2(float a, float b) {
 
 // the lo pieces of a packed pair: f16(v0 - hi0) | f16(v1 - hi1) << 16 in TWO instructions
 // (v_fma_mixlo_f16 / v_fma_mixhi_f16 round the exact f32 residual to f16 in the same op, RNE as
-// v_cvt_pk_f16_f32) instead of two v_fma_mix_f32 + one v_cvt_pk_f16_f32
+// v_cvt_pk_f16_f32) instead of two v_fma_mix_f32 + one v_cvt_pk_f16_f32.  OFF by default
+// (NAZ_SPLIT_MIXLO): the compiler's hazard recognizer does not see the inline-asm write of the
+// B fragment, so an MFMA issued 1-2 instructions later can read the register before the VALU
+// write lands (measured: nsc D=8 flows off by 1e-2 relative; the D=16 image happened to pass).
+// The default keeps the last writer a compiler-visible v_cvt_pk_f16_f32.
 NAZ_DEV unsigned lo_pair_f16(float v0, float v1, unsigned hp) {
   unsigned lo;
   asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hp), "v"(v0));
@@ -661,7 +665,7 @@ NAZ_DEV Frag2 split8_f16(const float (&v)[8]) {
   for (int q = 0; q < 4; ++q) {
     const unsigned hp = pack_f16x2(v[2 * q], v[2 * q + 1]);
     H[q] = hp;
-#ifdef NAZ_SPLIT_MIX32
+#ifndef NAZ_SPLIT_MIXLO
     const float r0 = sub_f16_piece<false>(v[2 * q], hp), r1 = sub_f16_piece<true>(v[2 * q + 1], hp);
     Lo[q] = pack_f16x2(r0, r1);
 #else

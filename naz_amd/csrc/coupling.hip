@@ -235,9 +235,12 @@ struct RingSrc {
                                             (int)(nfloats * 4 < 0x7fffffff ? nfloats * 4 : 0x7fffffff), 0x00020000)) {}
 };
 
+// Default OFF (NAZ_RING_BUF enables it): same-box A/B on the headline kernel, 2^20 rows, two
+// repetitions: global_load_lds 2.242 / 2.243 ms, buffer_load ... lds 2.284 / 2.290 ms
+// (profiles/r03_s3_ab_ring.txt) — the saved 64-bit address adds do not pay for the slower form.
 template <int NFLOATS, int NW>
 NAZ_DEV void stage_issue(float* lds, const RingSrc& src, int off) {
-#ifdef NAZ_RING_GLDS
+#ifndef NAZ_RING_BUF
   return stage_issue<NFLOATS, NW>(lds, src.base + off);
 #endif
   static_assert(NFLOATS % 256 == 0, "stage must be whole 1 KB chunks");

@@ -414,6 +414,22 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
   stage_issue<CF::A_SIZE, kR16Waves>(slot0, ring, (DIR_INV ? (L - 1) : 0) * CF::LAYER + a_off);
 
   const RqsConsts<CF::K, DIR_INV> rc(bound);
+  // GEMM1's context k-slots of this lane, loaded for layer li + 1 before layer li's upper spline
+  // (and for layer 0 here).  vmcnt retires in order: a context load issued AFTER a stage's
+  // LDS-DMA (as when it sits in stage A) can only be waited for together with that DMA, so
+  // stage A would stall on stage B's weights (3 % of the kernel, same-box A/B).  Issued before
+  // the stage-A barrier, the barrier's vmcnt(0) covers them with the stage-A weights.
+  float cpre[CF::KS1 * 8];
+  auto load_ctx = [&]() {
+#pragma unroll
+    for (int t = 0; t < CF::KS1; ++t)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int col = r16_in_col<CF>(t, q, jj);
+        cpre[8 * t + jj] = (col >= 0 && col < CF::C) ? ctx[crow * ldc + col] : 0.f;
+      }
+  };
+  load_ctx();
   int g = 0;  // global stage counter: stage g lives in slot (g & 1)
   for (int li = 0; li < L; ++li) {
     const int l = DIR_INV ? (L - 1 - li) : li;
@@ -513,7 +529,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
             const int col = r16_in_col<CF>(t, q, jj);
             float v = 0.f;
             if (col >= CF::C) v = zl[(col - CF::C - q * CF::SQ) < CF::SQ ? (col - CF::C - q * CF::SQ) : 0];
-            else if (col >= 0) v = ctx[crow * ldc + col];
+            else if (col >= 0) v = cpre[8 * t + jj];
             in[8 * t + jj] = v;
           }
         {
@@ -620,6 +636,7 @@ __global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_k
     });
 
     // ---------------- upper spline on this quarter's remaining dims (next layer's stage A in flight)
+    if (li + 1 < L) load_ctx();
     static_for<CF::SPLIT3 ? 1 : 0, CF::DQ>([&](auto uc) { upper(uc); });
 #ifdef NAZ_DEBUG_NONFINITE
     {

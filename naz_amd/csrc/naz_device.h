@@ -30,9 +30,13 @@ constexpr float kSearchEps = 1e-6f;
 // barrier makes every wave's chunks visible to all.  tests/test_isa_ring.py checks the built
 // code object: every s_barrier reachable with a global_load_lds in flight must be preceded
 // by an s_waitcnt vmcnt(0) on every path, loop back edges included.
+// The wait is the s_waitcnt builtin (gfx9 encoding 0x0F70 = vmcnt(0), expcnt/lgkmcnt unchanged),
+// not inline asm: the compiler's waitcnt pass sees it and drops the loads it covers from its
+// scoreboard (after an opaque asm wait it re-waits vmcnt(0) at the first use of a register loaded
+// before the barrier — which then also waits for the DMAs issued after it).
 NAZ_DEV void ring_barrier() {
 #ifndef NAZ_ABL_RING_NOWAIT  // A/B only: the round-2 (racy) form
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);
 #endif
   __syncthreads();
 }

@@ -13,7 +13,7 @@ step() {  # step <name> <timeout> <cmd...>
   tail -n 4 "gpurun_out/s2_$name.log" | cut -c1-600
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step parity 400 python -u -m pytest -m gpu -x -q --timeout 150 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_flow_abi.py tests/test_gpu_cnf.py
+step parity 500 python -u -m pytest -m gpu -x -q --timeout 150 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_flow_abi.py tests/test_gpu_cnf.py
 VARIANTS="base glds nowait nocopy" step ab 600 bash scripts/ab.sh
 step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_s2 -o run --output-format csv -- python3 bench.py --steps 30 --warmup 10 --no-cpu-baseline
 TAG=r03_headline ARGS="--steps 3 --warmup 2 --no-cpu-baseline" step pmc 600 bash scripts/pmc.sh

@@ -596,6 +596,10 @@ FLOW_CASES = {
     # SURVEY.md §8d's config-3 autoregressive variant: the config-3 flow with nsa layers
     "nsa16": ("nsa", 16, 32, [128, 128], 8, (8,), 1 << 18,
               "naz nsa at SURVEY §8d's config-3 AR variant: D=16 | C=32, K=8, L=8, H=[128,128], D-pass inverse"),
+    # naz's 4-parameter MLE MAF (examples/papers/2506.05657/train_mle_all_data_4param.py:87-92):
+    # D=4 | C=2, H=[512]*5, L=18 — the posterior-predictive workhorse (calibrate_4p.py:130-136)
+    "maf4": ("maf", 4, 2, [512] * 5, 18, (), 1 << 18,
+             "naz 4-parameter MLE maf (train_mle_all_data_4param.py:87-92): D=4, C=2, H=[512]*5, L=18"),
     # the density-grid use (plot.py:126-127): one context vector for every row
     "maf_grid": ("maf", 2, 2, [150, 150, 150], 16, (), 1 << 18,
                  "naz maf at the paper shape with ONE context vector (density grid, plot.py:126-127): "
@@ -626,8 +630,10 @@ def run_flow_case(args, dev, rank, world, dist):
         passes = Dd
     fl_ref = 2 * passes * Ld * sum(a * b for a, b in zip(dims[:-1], dims[1:]))  # the reference's work
     fl_row = fl_ref
-    ar_fused = ftype in ("nsa", "maf") and getattr(f, "_plan", None) is not None and hasattr(f._plan, "executed_flop_per_row")
-    if ar_fused:  # the fused autoregressive kernel's executed work (made_ar_r16.h)
+    plan_ = getattr(f, "_plan", None)
+    ar_fused = (ftype in ("nsa", "maf") and plan_ is not None and hasattr(plan_, "executed_flop_per_row") and
+                (args.sample or plan_.inverse))  # the wide MAFs fuse the sampling direction only
+    if ar_fused and not args.sample:  # the fused autoregressive kernel's executed work (made_ar_r16.h)
         fl_row = f._plan.executed_flop_per_row()
     elif ftype != "nsc":  # executed work of the degree-scheduled inverse (padded blocks included)
         fl_row = 0
@@ -678,7 +684,7 @@ def run_flow_case(args, dev, rank, world, dist):
     if rank == 0:
         step_s = elapsed / args.steps
         achieved = fl_row * B / step_s / 1e12
-        fused = getattr(f, "fused", False)
+        fused = ar_fused or (ftype == "nsc" and getattr(f, "fused", False))
         rec = {
             "metric": (f"samples/sec through sample (forward transform + log|detJ|), naz {ftype} flow (NormalizingFlow "
                        "API)" if args.sample else
@@ -746,10 +752,18 @@ def run_flow_case(args, dev, rank, world, dist):
 # (examples/papers/2506.05657: D=2 (m1, m2), C=2 (chi_b, alpha), hidden [150]*3, 16 layers):
 # lp = density grid under P posterior draws (plot.py:192-204), sample = posterior-predictive
 # draws (calibrate.py:145-151).  One step = one batched call over all P draws.
-BAYES = dict(D=2, C=2, hidden=[150, 150, 150], L=16)
+BAYES_SHAPES = {
+    "paper": dict(D=2, C=2, hidden=[150, 150, 150], L=16),
+    # the 4-parameter MLE MAF (train_mle_all_data_4param.py:87-92) whose posterior-predictive loop
+    # draws 800k samples per posterior draw (calibrate_4p.py:130-136)
+    "maf4": dict(D=4, C=2, hidden=[512] * 5, L=18),
+}
+BAYES = BAYES_SHAPES["paper"]
 
 
 def run_bayes(args, dev, rank, world, dist):
+    global BAYES
+    BAYES = BAYES_SHAPES[args.bayes_shape]
     from naz_amd.flows import bflow_maf as BM
     from oracle import jax_maf_np as J  # checker + cpu_baseline only
     from oracle import naz_oracle as O
@@ -770,8 +784,11 @@ def run_bayes(args, dev, rank, world, dist):
                for i in range(len(BAYES["hidden"]) + 1)] for l in range(BAYES["L"])]
     g = np.linspace(-3, 3, int(round(B ** 0.5)))
     grid = np.stack(np.meshgrid(g, g), -1).reshape(-1, 2).astype(np.float32)
-    x = np.concatenate([grid, gaussian_mixture(B - grid.shape[0], D, seed=rank)]) if grid.shape[0] < B else grid[:B]
-    ctx = np.array([0.3, -1.2], dtype=np.float32)
+    if D == 2:
+        x = np.concatenate([grid, gaussian_mixture(B - grid.shape[0], D, seed=rank)]) if grid.shape[0] < B else grid[:B]
+    else:
+        x = gaussian_mixture(B, D, seed=rank)
+    ctx = np.array([0.3, -1.2], dtype=np.float32)[:C]
     if grad_mode:  # NUTS over the training set: per-row contexts (hmc_maf_exact.py:128)
         ctx = np.random.default_rng(7).standard_normal((B, C)).astype(np.float32)
     nn_spec, _, _ = BM.make_conditional_autoregressive_nn(D, C, BAYES["hidden"])
@@ -839,8 +856,9 @@ def run_bayes(args, dev, rank, world, dist):
                 "(bflow_jax_maf.py:224-226); random-init MLE weights (torch seed 1234)",
         "config": {"workload": f"SURVEY.md §8f rank {2 if args.bayes == 'sample' else 1}: naz JAX-MAF front end "
                                f"({ {'lp': 'lp', 'grad': 'NUTS potential + gradient', 'sample': 'sampler'}[args.bayes] })"
-                               f" at the 2506.05657 paper shape D=2, C=2, "
-                               f"H=[150]*3, L=16; {P} draws x {B} rows per step (pack included)",
+                               f" at D={D}, C={C}, H={BAYES['hidden']}, L={BAYES['L']} "
+                               f"({'the 2506.05657 paper shape' if args.bayes_shape == 'paper' else 'the 4-parameter MLE MAF'})"
+                               f"; {P} draws x {B} rows per step (pack included)",
                    "draws": P, "rows_per_draw": B, "parallelism": f"dp{world} (independent draw sets, no collective)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "whole batched call",
@@ -959,6 +977,8 @@ def main():
     ap.add_argument("--bayes", choices=["lp", "sample", "grad"], default=None,
                     help="§8f ranks 1-2: the Bayesian MAF front end batched over weight draws (lp over a grid, "
                          "posterior-predictive sampling) at the paper shape")
+    ap.add_argument("--bayes-shape", choices=sorted(BAYES_SHAPES), default="paper",
+                    help="--bayes: the paper MAF (D=2, H=[150]*3, L=16) or the 4-parameter MLE MAF (D=4, H=[512]*5, L=18)")
     ap.add_argument("--mfma", choices=["auto", "f16x3", "f16x3r16", "bf16x6", "f32"], default="auto",
                     help="auto (default): f16x3r16 (16-row waves) when the packed hidden-layer weights fit fp16 and "
                          "the shape allows, else f16x3, else bf16x6; f32: exact FP32 MFMA")

@@ -345,6 +345,10 @@ typedef struct naz_ar_desc {
   int kind;          /* NAZ_AR_SPLINE | NAZ_AR_AFFINE */
   int reserved[6];
 } naz_ar_desc;
+/* 1: both directions fused (log_prob + sample); 2: the forward (sample) direction only — the
+ * wide production MAFs (D=4 | C=2, H=[512]x5), whose log_prob keeps the per-layer path and whose
+ * inverse-direction entry points (packed_bytes, pack_host, pack, log_prob*) report the shape as
+ * unsupported; 0: not instantiated */
 int naz_ar_flow_supported(const naz_ar_desc* d);
 int64_t naz_ar_flow_packed_bytes(const naz_ar_desc* d);
 /* deg[u] (u < H) = mask index of hidden unit u in every hidden layer (pyro create_mask) */

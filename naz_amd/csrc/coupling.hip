@@ -185,6 +185,15 @@ __global__ void coupling_pack_kernel(const float* __restrict__ flat, float* __re
 // ---------------------------------------------------------------------------
 // Stage copy HBM/L2 -> LDS (16-byte loads, all 256 threads)
 // ---------------------------------------------------------------------------
+// LDS (address space 3) pointer of a generic pointer into __shared__ memory: the low 32 bits
+// of a flat LDS address are the LDS offset.  An addrspacecast would instead emit a null check
+// against src_shared_base, which hipcc (ROCm 7.2) mis-encodes (v_cmp_ne_u32_e32 with
+// src_shared_base as src1: "Operand has incorrect register class") once the address space
+// cannot be inferred (the wide H = 512 forward kernel).
+NAZ_DEV __attribute__((address_space(3))) void* to_lds(const void* p) {
+  return (__attribute__((address_space(3))) void*)(uint32_t)(uintptr_t)p;
+}
+
 // Asynchronous stage copy HBM/L2 -> LDS with LDS-DMA (global_load_lds_dwordx4): wave w
 // moves 1 KB chunks w, w+4, ...; no VGPRs hold the data.  Completion is published by the
 // next ring_barrier() (naz_device.h: explicit vmcnt(0), then the barrier) — never by a bare
@@ -204,7 +213,7 @@ NAZ_DEV void stage_issue(float* lds, const float* __restrict__ src) {
     if (c0 + NW - 1 < CHUNKS || c < CHUNKS) {
       __builtin_amdgcn_global_load_lds(
           (const void __attribute__((address_space(1)))*)(src + c * 256 + lane * 4),
-          (void __attribute__((address_space(3)))*)(lds + c * 256), 16, 0, 0);
+          to_lds(lds + c * 256), 16, 0, 0);
     }
   }
 }
@@ -251,7 +260,7 @@ NAZ_DEV void stage_issue(float* lds, const RingSrc& src, int off) {
   for (int c0 = 0; c0 < CHUNKS; c0 += NW) {
     const int c = c0 + wave;
     if (c0 + NW - 1 < CHUNKS || c < CHUNKS) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(src.r, (__attribute__((address_space(3))) void*)(lds + c * 256), 16, vo,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(src.r, to_lds(lds + c * 256), 16, vo,
                                                (off + c * 256) * 4, 0, 0);
     }
   }
@@ -271,7 +280,7 @@ NAZ_DEV void stage_issue_lim(float* lds, const float* __restrict__ src, int nch)
     if (c < nch) {
       __builtin_amdgcn_global_load_lds(
           (const void __attribute__((address_space(1)))*)(src + c * 256 + lane * 4),
-          (void __attribute__((address_space(3)))*)(lds + c * 256), 16, 0, 0);
+          to_lds(lds + c * 256), 16, 0, 0);
     }
   }
 }
@@ -1648,6 +1657,57 @@ struct AROps {
   }
 };
 
+// wide affine MADE, forward (sample) direction only (CfgARW): the inverse-direction entry points
+// report the shape as unsupported, so log_prob keeps the degree-scheduled per-layer path
+template <class CW>
+struct AROpsW {
+  using FW = CfgARF<CW>;
+  static int64_t layer_floats() { return -1; }
+  static int degrees(int* deg) {
+    for (int u = 0; u < CW::H; ++u) deg[u] = CW::deg(u);
+    return 0;
+  }
+  static int inverse_unsupported() {
+    return set_error("naz_ar_flow: D=%d C=%d H=%d x %d: fused forward (sample) direction only", CW::D, CW::C, CW::H,
+                     CW::NHID);
+  }
+  static int pack_host(const float*, const int*, int, float*) { return inverse_unsupported(); }
+  template <class... A>
+  static int log_prob(A...) { return inverse_unsupported(); }
+  static int64_t pass0_floats() { return -1; }
+  template <class... A>
+  static int pack_device(A...) { return inverse_unsupported(); }
+  static constexpr int64_t per() {
+    return (int64_t)CW::H * (CW::C + CW::D) + CW::H + (int64_t)(CW::NHID - 1) * (CW::H * CW::H + CW::H) +
+           (int64_t)CW::D * CW::P * CW::H + CW::D * CW::P;
+  }
+  static int64_t fwd_layer_floats() { return FW::LAYER; }
+  static int64_t flat_floats() { return per(); }
+  static int pack_fwd_host(const float* flat, int L, float* out) {
+    for (int l = 0; l < L; ++l) made_ar_pack_fwd_layer<FW>(flat + l * per(), out + (int64_t)l * FW::LAYER);
+    return 0;
+  }
+  static int sample(const float* packed, int L, const float* z, int64_t ldz, const float* ctx, int64_t ldc,
+                    const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B, float bound,
+                    hipStream_t s, int64_t P = 1, int64_t spk = 0, int64_t sz = 0, int64_t sy = 0, int64_t sld = 0) {
+    if (B == 0 || P == 0) return 0;
+    if (P > 65535) return set_error("naz_ar_flow_sample_batched: at most 65535 draws per call");
+    const int64_t rows = 16 * FW::NW, grid = (B + rows - 1) / rows;
+    const size_t lds = (size_t)2 * FW::STG * 4;
+    hipLaunchKernelGGL((made_ar_fwd_kernel<FW>), dim3((unsigned)grid, (unsigned)P), dim3(64 * FW::NW), lds, s, packed,
+                       L, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, bound, spk, sz, sy, sld);
+    return check_launch("made_ar_fwd_kernel");
+  }
+  static int pack_fwd_device(const float* flat, int64_t sflat, float* packed, int64_t spk, int L, int64_t P,
+                             hipStream_t s, const float* mask = nullptr) {
+    if (L == 0 || P == 0) return 0;
+    if (P > 65535 || L > 65535) return set_error("naz_ar_flow_pack_fwd: at most 65535 draws / layers per call");
+    const dim3 grid((unsigned)((FW::LAYER + 255) / 256), (unsigned)L, (unsigned)P);
+    hipLaunchKernelGGL((made_ar_pack_fwd_kernel<FW>), grid, dim3(256), 0, s, flat, sflat, packed, spk, mask);
+    return check_launch("made_ar_pack_fwd_kernel");
+  }
+};
+
 template <class F>
 static int ar_dispatch(const naz_ar_desc* d, F&& f) {
   if (d == nullptr || d->act != NAZ_ACT_TANH || d->L < 0) return -2;
@@ -1664,13 +1724,17 @@ static int ar_dispatch(const naz_ar_desc* d, F&& f) {
     // SURVEY §8d's config-3 AR variant
     if (d->D == 2 && d->C == 2 && d->H == 150 && d->n_hidden == 3) return f(AROps<CfgAR<2, 2, 150, 8, 3, true>>{});
     if (d->D == 16 && d->C == 32 && d->H == 128 && d->n_hidden == 2) return f(AROps<CfgAR<16, 32, 128, 8, 2, true>>{});
+    // naz's production MAFs (4-parameter MLE, POSYDON): forward direction only (AROpsW)
+    if (d->D == 4 && d->C == 2 && d->H == 512 && d->n_hidden == 5) return f(AROpsW<CfgARW<4, 2, 512, 5>>{});
     return -2;
   }
   return -2;
 }
 
+// 1: both directions fused; 2: the forward (sample) direction only (AROpsW); 0: neither
 int ar_flow_supported(const naz_ar_desc* d) {
-  return ar_dispatch(d, [](auto) { return 1; }) == 1 ? 1 : 0;
+  const int r = ar_dispatch(d, [](auto ops) { return decltype(ops)::layer_floats() < 0 ? 2 : 1; });
+  return r > 0 ? r : 0;
 }
 
 int64_t ar_flow_packed_bytes(const naz_ar_desc* d) {

@@ -486,6 +486,27 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
 // stages of <= kARCap floats.  Forward values can grow through the layers (affine scales up to
 // e^3 per layer), so the layer input is split into f16 pieces at a per-row power-of-two scale and
 // the x part of hidden layer 1 rescaled in fp32 (the context keeps the caller's |ctx| < 2^15).
+// Wide affine MADE (naz's production MAFs: the 4-parameter MLE flow D=4 | C=2, H=[512]x5, L=18,
+// examples/papers/2506.05657/train_mle_all_data_4param.py:87-92; POSYDON D=4, 512x5, L=16,
+// eposydon/train_maf_mle.py:84-90), forward (sample) direction only: CfgARF over this gives
+// made_ar_fwd_kernel's per-layer image and schedule.  Two hidden layers of B fragments are 256
+// VGPRs at H = 512, so one 4-wave workgroup per CU (one wave per SIMD, AGPRs in use) with 64
+// rows per weight stream; each ring stage carries two 16-unit blocks (2 x 32 KB of f16 pieces).
+template <int D_, int C_, int H_, int NHID_>
+struct CfgARW {
+  static constexpr int D = D_, C = C_, H = H_, K = 8, NHID = NHID_;
+  static constexpr bool AFFINE = true;
+  static constexpr int P = 2, HP = (H + 31) / 32 * 32, HB = HP / 16, KSH = HP / 32;
+  static constexpr int KC = (C + 31) / 32, KI = KC + 1, NOB = 1, OT = 2 * kChunk;
+  static constexpr int deg(int u) {
+    if (C > 0) return ar_round_half_even(1.0 + (double)u * (double)(D - 1) / (double)(H - 1)) - 1;
+    return ar_round_half_even(1.0 + (double)u * (double)(D - 2) / (double)(H - 1));
+  }
+  static constexpr int pad(int n) { return (n + 255) / 256 * 256; }
+  static constexpr int NW = 4;
+  static_assert(H > 256 && H % 32 == 0 && D >= 2 && D <= 8 && NHID >= 1, "wide MADE instances only");
+};
+
 template <class G>
 struct CfgARF {
   static constexpr int D = G::D, C = G::C, H = G::H, K = G::K, NHID = G::NHID, P = G::P;
@@ -840,9 +861,11 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
   for (int l = 0; l < L; ++l) {
     const float* lp = packed + (int64_t)l * CF::LAYER;
     const float* lnext = packed + (int64_t)(l + 1) * CF::LAYER;
-    Frag2 hf[NHID][KSH];
+    // hidden layer i's B fragments in hf[i & 1]: only two layers are ever live (the wide H = 512
+    // instances hold 2 x 128 VGPRs of them)
+    Frag2 hf[2][KSH];
 #pragma unroll
-    for (int i = 0; i < NHID; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int t = 0; t < KSH; ++t) hf[i][t] = Frag2{half8{}, half8{}};
     // the layer input's f16 split at a per-row power-of-two scale (|x| sc < 2^14)
@@ -896,9 +919,9 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
           for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(ax[r], us, acc[r]);
         } else {
 #pragma unroll
-          for (int t = 0; t < KSH; ++t) acc = mfma3_16(afrag(t), hf[i - 1][t], acc);
+          for (int t = 0; t < KSH; ++t) acc = mfma3_16(afrag(t), hf[(i - 1) & 1][t], acc);
         }
-        ar_split4<b & 1>(hf[i][b >> 1], acc);
+        ar_split4<b & 1>(hf[i & 1][b >> 1], acc);
       } else {
         constexpr int d = u - NHID * HB;
         floatx4 o3[CF::NOB];
@@ -911,7 +934,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
 #pragma unroll
         for (int t = 0; t < KSH; ++t)
 #pragma unroll
-          for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KSH + t), hf[NHID - 1][t], o3[o]);
+          for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KSH + t), hf[(NHID - 1) & 1][t], o3[o]);
         if constexpr (CF::AFFINE) {
           // pyro AffineAutoregressive._call: y = exp(clamp(ls)) x + mean, log|det| = clamp(ls)
           const float mean = __shfl(o3[0][0], lane & 15);

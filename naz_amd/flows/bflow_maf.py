@@ -268,7 +268,7 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
     hd = list(spec.hidden_dims)
     if fused_ar and act == "tanh" and len(set(hd)) == 1:
         d_ = ops.ar_flow_desc("maf", D, C, hd[0], len(masks), len(hd))
-        if ops.ar_flow_supported(d_):
+        if ops.ar_flow_fwd_supported(d_):
             ar_desc = d_
             # per layer: F[:, 1:] * mask-vector = the flat layout naz_ar_flow_pack_fwd reads
             ar_maskvec = [torch.cat([t for m, (ws, bs) in zip(ms, spec.param_shapes)
@@ -278,7 +278,8 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
     # inverse kernel's degree passes assume pyro's create_mask for each layer's permutation, one
     # context vector (or none) and rows inside the f16x3 input split's range
     ar_perm = ar_pass0 = None
-    if ar_desc is not None and (C == 0 or ctx.dim() == 1) and float(x.abs().max()) < 32768.0 and \
+    if ar_desc is not None and ops.ar_flow_supported(ar_desc) and (C == 0 or ctx.dim() == 1) and \
+            float(x.abs().max()) < 32768.0 and \
             (C == 0 or float(ctx.abs().max()) < 32768.0):
         pm = [torch.as_tensor(p_).cpu().to(torch.int64) for p_ in perms]
         ok = True

@@ -157,6 +157,7 @@ class _FusedAR:
     checked against them once per parameter change."""
 
     can_sample = True  # sample(): naz_ar_flow_sample (the forward direction, one launch)
+    inverse = True  # log_prob fused too (False for the forward-only wide instances: per-layer log_prob)
     F16_DATA_LIMIT = 32768.0  # the kernel's f16x3 input split (|x|, |ctx| < 2^15)
 
     def __init__(self, layers: List[nn.Module], kind: str, D: int, C: int, H: int, n_hidden: int, K: int, act: str,
@@ -204,7 +205,7 @@ class _FusedAR:
         return self.masks_ok() and not any(n.dropout_active() for n in self._nets())
 
     def log_prob_ready(self, x, context) -> bool:
-        if x.dim() != 2:
+        if not self.inverse or x.dim() != 2:
             return False
         m = x.detach().abs().amax() if x.numel() else torch.zeros((), device=x.device)
         if context is not None and context.numel():
@@ -424,7 +425,10 @@ def _fused_plan(flow_type, flow_args, flow_kwargs, transforms):
         try:
             bound = transforms[0].bound if flow_type == "nsa" else 3.0
             plan = _FusedAR(list(transforms), flow_type, D, C, hidden[0], len(hidden), K, act, bound)
-            return plan if ops.ar_flow_supported(plan.desc) and plan.masks_ok() else None
+            if not ops.ar_flow_fwd_supported(plan.desc) or not plan.masks_ok():
+                return None
+            plan.inverse = ops.ar_flow_supported(plan.desc)  # False: fused sampling only (wide MAFs)
+            return plan
         except Exception:
             return None
     if flow_type != "nsc":

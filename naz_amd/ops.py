@@ -561,7 +561,14 @@ def ar_flow_desc(kind: str, D: int, C: int, H: int, L: int, n_hidden: int = 2, K
 
 
 def ar_flow_supported(d: ArDesc) -> bool:
-    return bool(lib().naz_ar_flow_supported(d))
+    """Both directions (log_prob and sample) run fused for this shape."""
+    return int(lib().naz_ar_flow_supported(d)) == 1
+
+
+def ar_flow_fwd_supported(d: ArDesc) -> bool:
+    """The sampling direction runs fused (naz_ar_flow_sample*): every fused shape, including the
+    forward-only wide production MAFs (naz_ar_flow_supported == 2)."""
+    return int(lib().naz_ar_flow_supported(d)) in (1, 2)
 
 
 def ar_flow_degrees(d: ArDesc) -> np.ndarray:

@@ -107,6 +107,8 @@ SAMPLE_CASES = [
     dict(flow_type="nsa", D=4, C=2, hidden=[128, 128], L=3, K=8),
     dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=16),
     dict(flow_type="maf", D=16, C=32, hidden=[128, 128], L=3),
+    # naz's 4-parameter MLE MAF (train_mle_all_data_4param.py:87-92): the wide forward-only instance
+    dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=18),
 ]
 
 
@@ -306,3 +308,30 @@ def test_fused_ar_full_size_properties_maf_paper():
     c = torch.as_tensor(O.context_normal(B, 2, seed=24), device=DEV)
     with torch.no_grad():
         _full_size_properties(lambda a, b: f.log_prob(a, condition=b), x, c, "maf log_prob")
+
+
+def test_wide_maf_forward_only_plan_and_log_prob():
+    """The production MAF shapes (D=4 | C=2, H=[512]x5; L=18 MLE, L=16 POSYDON) sample through
+    the fused wide kernel, while log_prob (no fused inverse at H = 512) takes the degree-scheduled
+    per-layer path: parity vs the fp64 oracle on both, and the sampler's y round-trips through
+    log_prob (base(z) - ld(z) == log_prob(y))."""
+    from naz_amd import ops
+    for L in (16, 18):
+        spec = dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=L)
+        f, state = _flow(spec)
+        assert f.fused and f._plan.inverse is False and ops.ar_flow_fwd_supported(f._plan.desc)
+        assert not ops.ar_flow_supported(f._plan.desc)
+        n = 600
+        x = torch.as_tensor(O.gaussian_mixture(n, 4, seed=7))
+        c = torch.as_tensor(O.context_normal(n, 2, seed=8))
+        with torch.no_grad():
+            lp = f.log_prob(x.to(DEV), condition=c.to(DEV)).cpu().numpy()
+        lp64 = O.build_flow(spec, state, torch.float64).log_prob(x.double(), c.double()).numpy()
+        lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, c).numpy()
+        assert_parity(lp, lp64, lp32, what=f"wide maf L={L} log_prob (per-layer path)")
+        z = torch.randn(n, 4, generator=torch.Generator().manual_seed(L)).to(DEV)
+        y, ld = ops.ar_flow_sample(f._plan.desc, f._plan.packed_fwd(), z, c.to(DEV), with_logdet=True)
+        with torch.no_grad():
+            lpy = f.log_prob(y, condition=c.to(DEV))
+        rt = (lpy - (ops.base_log_prob(z) - ld)).abs() / lpy.abs().clamp_min(1.0)
+        assert float(rt.max()) < 1e-4, float(rt.max())

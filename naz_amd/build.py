@@ -24,6 +24,9 @@ ARCH = os.environ.get("NAZ_OFFLOAD_ARCH", "gfx950")
 SOURCE_FLAGS = {"coupling.hip": ["-fno-slp-vectorize"], "cnf.hip": ["-fno-slp-vectorize"],
                 "made.hip": ["-fno-slp-vectorize"]}
 SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "gemm_rows.hip", "elementwise.hip", "made.hip", "coupling.hip", "cnf.hip", "capi.cpp"]
+# sources compiled more than once with a part macro (object name suffix, extra flags): coupling.hip
+# holds the coupling and the autoregressive kernels, ~5 min of device compile in one object
+PARTS = {"coupling.hip": [("", ["-DNAZ_PART=1"]), ("_ar", ["-DNAZ_PART=2"])]}
 
 
 def hipcc() -> str:
@@ -63,12 +66,13 @@ def build(verbose: bool = False, jobs: int = 4, extra: list | None = None, varia
     objs = []
     for s in SOURCES:
         src = CSRC / s
-        obj = obj_dir / (src.stem + ".o")
-        objs.append(obj)
-        if not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hm):
-            todo.append((src, obj))
+        for suffix, flags in PARTS.get(s, [("", [])]):
+            obj = obj_dir / (src.stem + suffix + ".o")
+            objs.append(obj)
+            if not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hm):
+                todo.append((src, obj, flags))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        for (src, obj), warn in zip(todo, ex.map(lambda t: _compile(t[0], t[1], extra), todo)):
+        for (src, obj, _), warn in zip(todo, ex.map(lambda t: _compile(t[0], t[1], extra + t[2]), todo)):
             if verbose:
                 print(f"[naz_amd.build] {src.name} -> {obj.name}", file=sys.stderr)
                 if warn.strip():

@@ -23,6 +23,12 @@
 //   * weights (the A operands, exact fp32 MFMA) are staged per GEMM into LDS as
 //     [block][k/4][lane][4] panels read by ds_read_b128; one stage <= 64 KB so two
 //     workgroups share a CU and overlap each other's VALU (spline/tanh) with MFMA.
+// Compiled twice by naz_amd/build.py (two objects, built in parallel): NAZ_PART=1 the coupling
+// flows' dispatch and kernels, NAZ_PART=2 the autoregressive (made_ar_r16.h) ones; both parts
+// share the device helpers above the dispatch sections.  Without NAZ_PART both are built.
+#ifndef NAZ_PART
+#define NAZ_PART 0
+#endif
 #include "naz_device.h"
 #include "naz_internal.h"
 
@@ -222,7 +228,11 @@ NAZ_DEV void stage_issue(float* lds, const float* __restrict__ src) {
 // log_prob kernels record the FIRST non-finite row state as {1, workgroup, layer, stage counter,
 // row} (naz_debug_nonfinite reads and clears it).  The record exists in every build; only the
 // debug build writes it.
+#if NAZ_PART != 2
 __device__ int64_t g_nonfinite[5];
+#else
+extern __device__ int64_t g_nonfinite[5];
+#endif
 NAZ_DEV void debug_nonfinite_probe(bool bad, int64_t row, int layer, int stage) {
   if (bad && atomicCAS(reinterpret_cast<unsigned long long*>(&g_nonfinite[0]), 0ull, 1ull) == 0ull) {
     g_nonfinite[1] = blockIdx.x;
@@ -1297,6 +1307,7 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
 
 namespace naz {
 
+#if NAZ_PART != 2  // ---------------- part 1: the coupling flows (build.py compiles this file twice)
 extern "C" int naz_debug_nonfinite(int64_t* out5, int clear) {
 #ifndef NAZ_DEBUG_NONFINITE
   (void)out5;
@@ -1577,6 +1588,9 @@ int coupling_dp3_columns(const naz_coupling_desc* d, int* rows) {
   return rc == -2 ? unsupported(d) : rc;
 }
 
+#endif  // NAZ_PART != 2
+
+#if NAZ_PART != 1  // ---------------- part 2: the autoregressive flows
 // ---- fused autoregressive inverse (made_ar_r16.h): naz nsa / maf log_prob -------------
 template <class CF>
 struct AROps {
@@ -1861,5 +1875,7 @@ int ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, i
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }
+
+#endif  // NAZ_PART != 1
 
 }  // namespace naz

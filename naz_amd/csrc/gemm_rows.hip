@@ -752,6 +752,214 @@ static bool wgrad_t16(WGradArgs p, hipStream_t s) {
   }
 }
 
+// wgrad_x6: the same reduction on the bf16 matrix pipe, exact to fp32 products.  Every operand
+// value is split EXACTLY into three bf16 pieces by truncation (hi = the top 16 bits, mid = those of
+// v - hi, lo = v - hi - mid, which fits 8 bits) and C += sum of the six largest piece products
+// (hh, hm, mh, hl, mm, lh; the dropped ml, lm, ll are <= 2^-24 relative) on
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation: 6 x 16 = 96 cycles per 32 rows against 8 x 32 =
+// 256 for the fp32 16x16x4 form (2.67x the matrix rate), so the reduction becomes bound by the
+// HBM stream of G and X.  No range limit (bf16 keeps fp32's exponent).  Same chunking, ring and
+// write-back as wgrad_t16; a 32-row step takes rows 8 kq .. 8 kq + 7 of lane (m, kq) from LDS.
+typedef short wg_bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned wg_u32x4 __attribute__((ext_vector_type(4)));
+struct WgFrag3 {
+  wg_bf16x8 h, m, l;
+};
+NAZ_DEV WgFrag3 wg_split8(const float (&v)[8]) {
+  wg_u32x4 H, M, L;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned hb[2], mb[2], lb[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float x = v[2 * q + e];
+      hb[e] = __float_as_uint(x);
+      const float r1 = x - __uint_as_float(hb[e] & 0xffff0000u);
+      mb[e] = __float_as_uint(r1);
+      lb[e] = __float_as_uint(r1 - __uint_as_float(mb[e] & 0xffff0000u));
+    }
+    H[q] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+    M[q] = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
+    L[q] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+  }
+  return WgFrag3{__builtin_bit_cast(wg_bf16x8, H), __builtin_bit_cast(wg_bf16x8, M), __builtin_bit_cast(wg_bf16x8, L)};
+}
+NAZ_DEV floatx4w wg_mfma6(const WgFrag3& a, const WgFrag3& b, floatx4w c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);  // small terms first
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.m, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+}
+
+template <int NOW, int NB2, int JS>
+__global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_x6_kernel(WGradArgs p, int R) {
+  extern __shared__ float tl[];
+  constexpr int NT = 256 * JS, NBW = NB2 / JS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, jh = tid >> 8, m = lane & 15,
+            kq = lane >> 4;
+  const int N1 = p.N1, N2 = p.N2;
+  const int64_t mb = (int64_t)blockIdx.x * p.rows_per_wg;
+  const int64_t me = (mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M;
+  floatx4w acc[NOW][NBW];
+#pragma unroll
+  for (int i = 0; i < NOW; ++i)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) acc[i][j] = floatx4w{0.f, 0.f, 0.f, 0.f};
+  float dsum[NOW];
+#pragma unroll
+  for (int i = 0; i < NOW; ++i) dsum[i] = 0.f;
+  const int CH = R * (N1 + N2);
+  const int nw = NT / 64, wv = tid >> 6;
+  auto issue = [&](int64_t m0, float* dst) {
+    const float* src[2] = {p.g + m0 * N1, p.x + m0 * N2};
+    const int cnt[2] = {R * N1 / 256, R * N2 / 256};
+    float* d = dst;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      for (int c = wv; c < cnt[h]; c += nw)
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src[h] + c * 256 + lane * 4),
+                                         (void __attribute__((address_space(3)))*)(uint32_t)(uintptr_t)(d + c * 256), 16, 0, 0);
+      d += R * (h == 0 ? N1 : N2);
+    }
+  };
+  auto copy_tail = [&](int64_t m0, float* dst) {  // zero-filled past me: padding rows add nothing
+    const int64_t rows = me - m0;
+    const int lg = (int)(rows * N1 / 4), lx = (int)(rows * N2 / 4), fg = R * N1 / 4;
+    const float4* gp = reinterpret_cast<const float4*>(p.g + m0 * N1);
+    const float4* xp = reinterpret_cast<const float4*>(p.x + m0 * N2);
+    float4* l4 = reinterpret_cast<float4*>(dst);
+    for (int q = tid; q < CH / 4; q += NT) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < fg) {
+        if (q < lg) v = gp[q];
+      } else if (q - fg < lx) {
+        v = xp[q - fg];
+      }
+      l4[q] = v;
+    }
+  };
+  auto fill = [&](int64_t m0, float* dst) {
+    if (m0 + R <= me) issue(m0, dst);
+    else copy_tail(m0, dst);
+  };
+  int slot = 0;
+  if (mb < me) fill(mb, tl);
+  for (int64_t m0 = mb; m0 < me; m0 += R, slot ^= 1) {
+    ring_barrier();  // chunk m0 has landed; every wave is done with the other slot
+    const float* const Gs = tl + slot * CH;
+    const float* const Xs = Gs + R * N1;
+    if (m0 + R < me) fill(m0 + R, tl + (slot ^ 1) * CH);
+    // lane (m, kq) of a 32-row step reads rows 8 kq .. 8 kq + 7; past-the-end blocks read LDS
+    // slack / neighbours and only feed dropped accumulator rows or columns (as wgrad_t16)
+    const float* pa = Gs + (8 * kq) * N1 + wave * 16 + m;
+    const float* pb = Xs + (8 * kq) * N2 + jh * NBW * 16 + m;
+    for (int st = 0; st < R / 32; ++st) {
+      WgFrag3 fa[NOW], fb[NBW];
+#pragma unroll
+      for (int i = 0; i < NOW; ++i) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = pa[j * N1 + 64 * i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum[i] += v[j];
+        fa[i] = wg_split8(v);
+      }
+#pragma unroll
+      for (int jb = 0; jb < NBW; ++jb) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = pb[j * N2 + 16 * jb];
+        fb[jb] = wg_split8(v);
+      }
+      pa += 32 * N1;
+      pb += 32 * N2;
+#pragma unroll
+      for (int i = 0; i < NOW; ++i)
+#pragma unroll
+        for (int jb = 0; jb < NBW; ++jb) acc[i][jb] = wg_mfma6(fa[i], fb[jb], acc[i][jb]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NOW; ++i) {
+    const int ob = wave + 4 * i;
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const int n2 = 16 * (jh * NBW + j) + m;
+      if (n2 >= N2) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n1 = 16 * ob + 4 * kq + r;
+        if (n1 >= N1) continue;
+        float v = acc[i][j][r];
+        if (p.mask != nullptr) v *= p.mask[(int64_t)n1 * p.smm + (int64_t)n2 * p.smn];
+        atomicAdd(p.c + (int64_t)n1 * p.scm + (int64_t)n2 * p.scn, v);
+      }
+    }
+    if (p.ones && jh == 0) {  // db: lane (m, kq) summed rows 8 kq .. of column 16 ob + m
+      float v = dsum[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      const int o = 16 * ob + m;
+      if (kq == 0 && o < N1) atomicAdd(p.rowsum + o, v);
+    }
+  }
+}
+
+template <int NOW, int NB2>
+static void wgrad_x6_go(const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s) {
+  constexpr int JS = (NOW * NB2 > 12 && NB2 % 2 == 0) ? 2 : 1;
+  hipLaunchKernelGGL((wgrad_x6_kernel<NOW, NB2, JS>), dim3(gx), dim3(256 * JS), lds, s, q, R);
+}
+
+template <int NOW>
+static bool wgrad_x6_launch(int nb2, const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s) {
+  switch (nb2) {
+    case 1: wgrad_x6_go<NOW, 1>(q, R, lds, gx, s); return true;
+    case 2: wgrad_x6_go<NOW, 2>(q, R, lds, gx, s); return true;
+    case 3: wgrad_x6_go<NOW, 3>(q, R, lds, gx, s); return true;
+    case 4: wgrad_x6_go<NOW, 4>(q, R, lds, gx, s); return true;
+    case 6: wgrad_x6_go<NOW, 6>(q, R, lds, gx, s); return true;
+    case 8: wgrad_x6_go<NOW, 8>(q, R, lds, gx, s); return true;
+    default: return false;
+  }
+}
+
+// wgrad on the bf16x6 kernel for the shapes wgrad_t16 takes (R a multiple of 32 here)
+static bool wgrad_x6(WGradArgs p, hipStream_t s) {
+  const int nb1 = (p.N1 + 15) / 16, now = (nb1 + 3) / 4;
+  int nb2 = (p.N2 + 15) / 16;
+  nb2 = nb2 <= 4 ? nb2 : (nb2 <= 6 ? 6 : (nb2 <= 8 ? 8 : 0));
+  if (now < 1 || now > 4 || nb2 == 0) return false;
+  const bool js2 = now * nb2 > 12 && nb2 % 2 == 0;
+  int R = 0;
+  for (int r = 32; r <= 128; r += 32)
+    if ((r * p.N1) % 256 == 0 && (r * p.N2) % 256 == 0 && 2 * r * (p.N1 + p.N2) * 4 <= (js2 ? 147456 : 49152)) R = r;
+  if (R == 0) return false;
+  // + slack for the unmasked past-the-end reads (a 16-wide block past N2 / the last rows' padding)
+  const size_t lds = ((size_t)2 * R * (p.N1 + p.N2) + 16 * p.N2 + 16 * nb2 + 64 * nb1 + 64) * 4;
+  int64_t rpw = (p.M + (js2 ? 511 : 767)) / (js2 ? 512 : 768);
+  rpw = (rpw + R - 1) / R * R;
+  if (rpw < 4 * R) rpw = 4 * R;
+  p.rows_per_wg = rpw;
+  const unsigned gx = (unsigned)((p.M + rpw - 1) / rpw);
+  switch (now) {
+    case 1: return wgrad_x6_launch<1>(nb2, p, R, lds, gx, s);
+    case 2: return wgrad_x6_launch<2>(nb2, p, R, lds, gx, s);
+    case 3: return wgrad_x6_launch<3>(nb2, p, R, lds, gx, s);
+    default: return wgrad_x6_launch<4>(nb2, p, R, lds, gx, s);
+  }
+}
+
+static bool wgrad_x6_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("NAZ_WGRAD_X6");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 __global__ void zero2d_kernel(float* c, int64_t scm, int64_t scn, int M, int N) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)M * N) return;
@@ -781,6 +989,7 @@ int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
   const bool flat = p.sgm == p.N1 && p.sxm == p.N2 && p.N1 % 4 == 0 && p.N2 % 4 == 0 && p.N2 > 0 &&
                     (reinterpret_cast<uintptr_t>(p.g) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.x) & 15) == 0 &&
                     p.N1 <= 256 && p.N2 <= 256;
+  if (flat && p.N2 <= 128 && wgrad_x6_enabled() && wgrad_x6(p, s)) return check_launch("wgrad_x6_kernel");
   if (flat && p.N2 <= 128 && wgrad_t16_enabled() && wgrad_t16(p, s)) return check_launch("wgrad_t16_kernel");
   if (flat) {
     // rows per chunk: ~8192 floats of G + X (a multiple of 16, <= 128); ~1024 workgroups

@@ -908,20 +908,25 @@ __global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_x6_kernel(WGradArgs p,
 }
 
 template <int NOW, int NB2>
-static void wgrad_x6_go(const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s) {
-  constexpr int JS = (NOW * NB2 > 12 && NB2 % 2 == 0) ? 2 : 1;
-  hipLaunchKernelGGL((wgrad_x6_kernel<NOW, NB2, JS>), dim3(gx), dim3(256 * JS), lds, s, q, R);
+static void wgrad_x6_go(const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s, bool js2) {
+  if constexpr (NOW * NB2 > 12 && NB2 % 2 == 0) {
+    if (js2) {
+      hipLaunchKernelGGL((wgrad_x6_kernel<NOW, NB2, 2>), dim3(gx), dim3(512), lds, s, q, R);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((wgrad_x6_kernel<NOW, NB2, 1>), dim3(gx), dim3(256), lds, s, q, R);
 }
 
 template <int NOW>
-static bool wgrad_x6_launch(int nb2, const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s) {
+static bool wgrad_x6_launch(int nb2, const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s, bool js2) {
   switch (nb2) {
-    case 1: wgrad_x6_go<NOW, 1>(q, R, lds, gx, s); return true;
-    case 2: wgrad_x6_go<NOW, 2>(q, R, lds, gx, s); return true;
-    case 3: wgrad_x6_go<NOW, 3>(q, R, lds, gx, s); return true;
-    case 4: wgrad_x6_go<NOW, 4>(q, R, lds, gx, s); return true;
-    case 6: wgrad_x6_go<NOW, 6>(q, R, lds, gx, s); return true;
-    case 8: wgrad_x6_go<NOW, 8>(q, R, lds, gx, s); return true;
+    case 1: wgrad_x6_go<NOW, 1>(q, R, lds, gx, s, js2); return true;
+    case 2: wgrad_x6_go<NOW, 2>(q, R, lds, gx, s, js2); return true;
+    case 3: wgrad_x6_go<NOW, 3>(q, R, lds, gx, s, js2); return true;
+    case 4: wgrad_x6_go<NOW, 4>(q, R, lds, gx, s, js2); return true;
+    case 6: wgrad_x6_go<NOW, 6>(q, R, lds, gx, s, js2); return true;
+    case 8: wgrad_x6_go<NOW, 8>(q, R, lds, gx, s, js2); return true;
     default: return false;
   }
 }
@@ -932,23 +937,32 @@ static bool wgrad_x6(WGradArgs p, hipStream_t s) {
   int nb2 = (p.N2 + 15) / 16;
   nb2 = nb2 <= 4 ? nb2 : (nb2 <= 6 ? 6 : (nb2 <= 8 ? 8 : 0));
   if (now < 1 || now > 4 || nb2 == 0) return false;
-  const bool js2 = now * nb2 > 12 && nb2 % 2 == 0;
-  int R = 0;
-  for (int r = 32; r <= 128; r += 32)
-    if ((r * p.N1) % 256 == 0 && (r * p.N2) % 256 == 0 && 2 * r * (p.N1 + p.N2) * 4 <= (js2 ? 147456 : 49152)) R = r;
-  if (R == 0) return false;
-  // + slack for the unmasked past-the-end reads (a 16-wide block past N2 / the last rows' padding)
-  const size_t lds = ((size_t)2 * R * (p.N1 + p.N2) + 16 * p.N2 + 16 * nb2 + 64 * nb1 + 64) * 4;
-  int64_t rpw = (p.M + (js2 ? 511 : 767)) / (js2 ? 512 : 768);
+  // 4-wave workgroups, two per CU (two DMA rings in flight per CU: one 8-wave workgroup with a
+  // single ring streamed G + X at ~3.7 TB/s) when two rings of 32-row chunks fit the LDS; else one
+  // 8-wave workgroup per CU (the wide 192 x 128 reduction)
+  auto lds_of = [&](int r) {  // + slack for the unmasked past-the-end reads
+    return ((size_t)2 * r * (p.N1 + p.N2) + 16 * p.N2 + 16 * nb2 + 64 * nb1 + 64) * 4;
+  };
+  const bool whole = (32 * p.N1) % 256 == 0 && (32 * p.N2) % 256 == 0;
+  if (!whole) return false;
+  bool js2 = 2 * lds_of(32) > 160 * 1024;
+  if (js2 && !(now * nb2 > 12 && nb2 % 2 == 0)) return false;
+  int R = 32;
+  for (int r = 64; r <= 128; r += 32)
+    if ((r * p.N1) % 256 == 0 && (r * p.N2) % 256 == 0 && lds_of(r) * (js2 ? 1 : 2) <= 160 * 1024) R = r;
+  if (lds_of(R) * (js2 ? 1 : 2) > 160 * 1024) return false;
+  const size_t lds = lds_of(R);
+  // two rounds of resident workgroups (one per CU for 8-wave ones, two per CU for 4-wave ones)
+  int64_t rpw = (p.M + (js2 ? 511 : 1023)) / (js2 ? 512 : 1024);
   rpw = (rpw + R - 1) / R * R;
   if (rpw < 4 * R) rpw = 4 * R;
   p.rows_per_wg = rpw;
   const unsigned gx = (unsigned)((p.M + rpw - 1) / rpw);
   switch (now) {
-    case 1: return wgrad_x6_launch<1>(nb2, p, R, lds, gx, s);
-    case 2: return wgrad_x6_launch<2>(nb2, p, R, lds, gx, s);
-    case 3: return wgrad_x6_launch<3>(nb2, p, R, lds, gx, s);
-    default: return wgrad_x6_launch<4>(nb2, p, R, lds, gx, s);
+    case 1: return wgrad_x6_launch<1>(nb2, p, R, lds, gx, s, js2);
+    case 2: return wgrad_x6_launch<2>(nb2, p, R, lds, gx, s, js2);
+    case 3: return wgrad_x6_launch<3>(nb2, p, R, lds, gx, s, js2);
+    default: return wgrad_x6_launch<4>(nb2, p, R, lds, gx, s, js2);
   }
 }
 

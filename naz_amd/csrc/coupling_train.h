@@ -273,6 +273,19 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
 #pragma unroll
     for (int u = 0; u < CF::DQ; ++u) y2[u] = valid ? state[crow * D + S + q * CF::DQ + u] : 0.f;
     const float gl = valid ? g_lp[crow] : 0.f;
+    // GEMM1's context k-slots and the upper dims' incoming gradients, loaded here, before the
+    // stage-0 barrier: vmcnt retires in order, so a load issued after a stage's LDS-DMA (as when
+    // these sat in stages 0 and C) is waited for together with that DMA
+    float cpre[CF::KS1 * 8], gin[CF::DQ];
+#pragma unroll
+    for (int t = 0; t < CF::KS1; ++t)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int col = r16_in_col<CF>(t, q, jj);
+        cpre[8 * t + jj] = (col >= 0 && col < C) ? ctx[crow * ldc + col] : 0.f;
+      }
+#pragma unroll
+    for (int u = 0; u < CF::DQ; ++u) gin[u] = valid ? g_in[crow * D + S + q * CF::DQ + u] : 0.f;
 
     floatx4 h1[CF::HB], h2[CF::HB], a3[CF::NO];
     float in[CF::KS1 * 8];
@@ -331,7 +344,11 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
 #pragma unroll
               for (int u = 0; u < CF::SQ; ++u) v = di == u ? x1[u] : v;
             } else if (col >= 0) {
+#ifdef NAZ_BWD_LATE_LOADS  // A/B only: the round-2 placement
               v = ctx[crow * ldc + col];
+#else
+              v = cpre[8 * t + jj];
+#endif
             }
             in[8 * t + jj] = v;
             if (valid && col >= 0) o.x0[row * (C + S) + col] = v;
@@ -410,7 +427,11 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
             }
 #pragma unroll
             for (int k = 0; k < K - 1; ++k) ud[k] = a3[(u * P + 2 * K + k) >> 2][(u * P + 2 * K + k) & 3];
+#ifdef NAZ_BWD_LATE_LOADS
             const float go = valid ? g_in[crow * D + S + q * CF::DQ + u] : 0.f;
+#else
+            const float go = gin[u];
+#endif
             gy2[u] = train_vjp_inv<K>(uw, uh, ud, bound, y2[u], go, gl, rc, gw, gh, gd);
 #pragma unroll
             for (int k = 0; k < K; ++k) {

@@ -864,6 +864,10 @@ def run_bayes(args, dev, rank, world, dist):
                      "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "whole batched call",
                      "flop_per_row": fl_row, "reference_flop_per_row": fl_ref},
     }
+    if grad_mode and flow["grad_fused"]:  # maf_grad.py: fused inverse + per-layer fused backward + dW GEMMs
+        rec["roofline"].update(path="fused maf backward (f16x3 MADE passes and chains, bf16x6 dW reductions)",
+                               peak_note="FP32 MFMA peak on the reference's FLOPs (D-pass forward + 2x backward); "
+                                         f"vs the 833 TF split f16x3 ceiling: {achieved / (BF16_PEAK_TFLOPS / 3):.3f}")
     if lp_mode and flow["lp_fused_ar"]:  # the whole flow per draw in one naz_ar_flow_log_prob_batched launch
         peak = BF16_PEAK_TFLOPS / 3
         rec["roofline"].update(peak=peak, frac=achieved / peak, peak_note="split f16x3 ceiling (2.5 PF / 3 products)")

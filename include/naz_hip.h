@@ -412,6 +412,34 @@ int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64
                                  int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B,
                                  int64_t P, int pass0_const, void* stream);
 
+/* ---- fused maf backward: the NUTS potential's gradient ------------------
+ * Replaces jax.grad of bayesian_normalizing_flow's potential Σ_rows flow_lp(unravel(p))
+ * (naz/flows/bflow_jax_maf.py:231-235; examples/papers/2506.05657/hmc_maf_exact.py:118-133) and
+ * loss.backward() of a maf NLL (naz/trainers/train_flows.py:194-213).  Affine autoregressive flows
+ * at the compiled shapes (naz_ar_flow_bwd_packed_bytes < 0 otherwise; today the paper shape
+ * D=2 | C=2, H=[150]x3).
+ *   naz_ar_flow_log_prob_train: naz_ar_flow_log_prob (one draw, no bounding) that also writes
+ *     states [L][B][D]: states[l] = s_l, layer l's output (layer l maps s_{l+1} -> s_l; s_0 = z).
+ *   naz_ar_flow_pack_bwd: per-layer backward images (naz_ar_flow_bwd_packed_bytes) from the
+ *     naz_ar_flow_pack_host flat layout on the device; mask (nullable, same layout) multiplies.
+ *   naz_ar_flow_bwd_dims: dims[6] = {n_hidden, HP, XA, XB, X0W, rows per tile}.
+ *   naz_ar_flow_bwd_layer: layer `layer`'s backward (call l = 0 .. L-1): g_in [B][D] = dL/ds_l,
+ *     g_lp [B] = dL/dlog p (nullable: 1), state = states[layer], packed_fwd = the
+ *     naz_ar_flow_pack_fwd image, perm = [L][D] dim of order p; writes g_out [B][D] = dL/ds_{l+1}
+ *     and the weight-gradient operands bufs[2 + 3 n_hidden]: x0 [B][X0W] = [ctx | s_l | 0], per
+ *     hidden layer i (h_i [B][XA] units < XA, [B][XB] units >= XA; natural tanh), then per hidden
+ *     layer i dp_i [B][HP] = dL/d pre-activation, then gout [B][X0W] = dL/d ARN output row
+ *     (pi D + d), zero padded.  dW_0 = dp_1ᵀ x0, dW_i = dp_{i+1}ᵀ h_i, dW_out = goutᵀ h_n,
+ *     biases = column sums of dp_i / gout (naz_gemm), then times the masks. */
+int naz_ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                               int64_t ldc, float* out_lp, float* states, int64_t B, void* stream);
+int64_t naz_ar_flow_bwd_packed_bytes(const naz_ar_desc* d);
+int naz_ar_flow_bwd_dims(const naz_ar_desc* d, int* dims);
+int naz_ar_flow_pack_bwd(const naz_ar_desc* d, const float* flat, const float* mask, void* packed, void* stream);
+int naz_ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* packed_bwd, const int* perm,
+                          int layer, const float* state, const float* ctx, int64_t ldc, const float* g_in,
+                          const float* g_lp, float* const* bufs, float* g_out, int64_t B, void* stream);
+
 /* ---- §8b: whole-flow entries over the fused kinds -------------------------------------
  * One descriptor for the flows whose whole log_prob is one launch: the spline coupling flow (naz
  * "nsc": naz_coupling_*) and the autoregressive flows (naz "nsa" / "maf": naz_ar_flow_*).  The

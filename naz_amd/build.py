@@ -25,8 +25,9 @@ SOURCE_FLAGS = {"coupling.hip": ["-fno-slp-vectorize"], "cnf.hip": ["-fno-slp-ve
                 "made.hip": ["-fno-slp-vectorize"]}
 SOURCES = ["rqs.hip", "dense.hip", "gemm.hip", "gemm_rows.hip", "elementwise.hip", "made.hip", "coupling.hip", "cnf.hip", "capi.cpp"]
 # sources compiled more than once with a part macro (object name suffix, extra flags): coupling.hip
-# holds the coupling and the autoregressive kernels, ~5 min of device compile in one object
-PARTS = {"coupling.hip": [("", ["-DNAZ_PART=1"]), ("_ar", ["-DNAZ_PART=2"])]}
+# holds the coupling, the autoregressive and the autoregressive-backward kernels, ~5 min of device
+# compile in one object
+PARTS = {"coupling.hip": [("", ["-DNAZ_PART=1"]), ("_ar", ["-DNAZ_PART=2"]), ("_arb", ["-DNAZ_PART=3"])]}
 
 
 def hipcc() -> str:

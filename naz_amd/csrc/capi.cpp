@@ -356,6 +356,35 @@ int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64
                                   as_stream(stream));
 }
 
+// ---- fused maf backward (made_ar_bwd.h): NUTS potential gradient / maf NLL step ----------
+int naz_ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                               int64_t ldc, float* out_lp, float* states, int64_t B, void* stream) {
+  if (B < 0) return set_error("naz_ar_flow_log_prob_train: negative batch");
+  if (B > 0 && (packed == nullptr || x == nullptr || out_lp == nullptr))
+    return set_error("naz_ar_flow_log_prob_train: null pointer");
+  if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
+    return set_error("naz_ar_flow_log_prob_train: conditional flow needs ctx");
+  if (naz_ar_flow_bwd_packed_bytes(d) < 0) return set_error("naz_ar_flow_log_prob_train: no fused backward for this flow");
+  return ar_flow_log_prob_train(d, packed, x, ldx, ctx, ldc, out_lp, states, B, as_stream(stream));
+}
+int64_t naz_ar_flow_bwd_packed_bytes(const naz_ar_desc* d) { return ar_flow_bwd_packed_bytes(d); }
+int naz_ar_flow_bwd_dims(const naz_ar_desc* d, int* dims) { return ar_flow_bwd_dims(d, dims); }
+int naz_ar_flow_pack_bwd(const naz_ar_desc* d, const float* flat, const float* mask, void* packed, void* stream) {
+  return ar_flow_pack_bwd(d, flat, mask, packed, as_stream(stream));
+}
+int naz_ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* packed_bwd, const int* perm,
+                          int layer, const float* state, const float* ctx, int64_t ldc, const float* g_in,
+                          const float* g_lp, float* const* bufs, float* g_out, int64_t B, void* stream) {
+  if (B < 0) return set_error("naz_ar_flow_bwd_layer: negative batch");
+  if (B > 0 && (packed_fwd == nullptr || packed_bwd == nullptr || perm == nullptr || state == nullptr ||
+                g_in == nullptr || bufs == nullptr || g_out == nullptr))
+    return set_error("naz_ar_flow_bwd_layer: null pointer");
+  if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
+    return set_error("naz_ar_flow_bwd_layer: conditional flow needs ctx");
+  return ar_flow_bwd_layer(d, packed_fwd, packed_bwd, perm, layer, state, ctx, ldc, g_in, g_lp, bufs, g_out, B,
+                           as_stream(stream));
+}
+
 // ---- §8b whole-flow entries over the fused kinds ----------------------------------------
 int64_t naz_flow_packed_bytes(const naz_flow_desc* d) {
   if (d == nullptr) return -1;

@@ -23,9 +23,10 @@
 //   * weights (the A operands, exact fp32 MFMA) are staged per GEMM into LDS as
 //     [block][k/4][lane][4] panels read by ds_read_b128; one stage <= 64 KB so two
 //     workgroups share a CU and overlap each other's VALU (spline/tanh) with MFMA.
-// Compiled twice by naz_amd/build.py (two objects, built in parallel): NAZ_PART=1 the coupling
-// flows' dispatch and kernels, NAZ_PART=2 the autoregressive (made_ar_r16.h) ones; both parts
-// share the device helpers above the dispatch sections.  Without NAZ_PART both are built.
+// Compiled three times by naz_amd/build.py (objects built in parallel): NAZ_PART=1 the coupling
+// flows' dispatch and kernels, NAZ_PART=2 the autoregressive (made_ar_r16.h) ones, NAZ_PART=3 the
+// autoregressive backward (made_ar_bwd.h); the parts share the device helpers above the dispatch
+// sections.  Without NAZ_PART all are built.
 #ifndef NAZ_PART
 #define NAZ_PART 0
 #endif
@@ -228,7 +229,7 @@ NAZ_DEV void stage_issue(float* lds, const float* __restrict__ src) {
 // log_prob kernels record the FIRST non-finite row state as {1, workgroup, layer, stage counter,
 // row} (naz_debug_nonfinite reads and clears it).  The record exists in every build; only the
 // debug build writes it.
-#if NAZ_PART != 2
+#if NAZ_PART == 0 || NAZ_PART == 1
 __device__ int64_t g_nonfinite[5];
 #else
 extern __device__ int64_t g_nonfinite[5];
@@ -1304,10 +1305,11 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
 #include "coupling_r16.h"
 #include "coupling_train.h"
 #include "made_ar_r16.h"
+#include "made_ar_bwd.h"
 
 namespace naz {
 
-#if NAZ_PART != 2  // ---------------- part 1: the coupling flows (build.py compiles this file twice)
+#if NAZ_PART == 0 || NAZ_PART == 1  // ---------------- part 1: the coupling flows (build.py compiles this file twice)
 extern "C" int naz_debug_nonfinite(int64_t* out5, int clear) {
 #ifndef NAZ_DEBUG_NONFINITE
   (void)out5;
@@ -1588,9 +1590,9 @@ int coupling_dp3_columns(const naz_coupling_desc* d, int* rows) {
   return rc == -2 ? unsupported(d) : rc;
 }
 
-#endif  // NAZ_PART != 2
+#endif  // part 1
 
-#if NAZ_PART != 1  // ---------------- part 2: the autoregressive flows
+#if NAZ_PART == 0 || NAZ_PART == 2  // ---------------- part 2: the autoregressive flows
 // ---- fused autoregressive inverse (made_ar_r16.h): naz nsa / maf log_prob -------------
 template <class CF>
 struct AROps {
@@ -1616,14 +1618,15 @@ struct AROps {
   }
   static int log_prob(const float* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
                       const float* low, const float* high, float* out_lp, int64_t B, float bound, hipStream_t s,
-                      int64_t P = 1, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0, int c0mode = 0) {
+                      int64_t P = 1, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0, int c0mode = 0,
+                      float* states = nullptr) {
     static_assert(2 * CF::STG * 4 <= 160 * 1024, "two weight stages exceed the LDS");
     if (B == 0 || L == 0 || P == 0) return 0;
     if (P > 65535) return set_error("naz_ar_flow_log_prob_batched: at most 65535 draws per call");
     const int64_t rows = 16 * CF::NW, grid = (B + rows - 1) / rows;
     const size_t lds = (size_t)2 * CF::STG * 4;
     hipLaunchKernelGGL((made_ar_r16_kernel<CF>), dim3((unsigned)grid, (unsigned)P), dim3(64 * CF::NW), lds, s, packed,
-                       L, x, ldx, ctx, ldc, low, high, out_lp, B, bound, spk, sx, slp, c0mode);
+                       L, x, ldx, ctx, ldc, low, high, out_lp, B, bound, spk, sx, slp, c0mode, states);
     return check_launch("made_ar_r16_kernel");
   }
   static int64_t pass0_floats() { return CF::C0; }
@@ -1876,6 +1879,116 @@ int ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, i
   return rc == -2 ? ar_unsupported(d) : rc;
 }
 
-#endif  // NAZ_PART != 1
+int ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                           int64_t ldc, float* out_lp, float* states, int64_t B, hipStream_t s) {
+  if (states == nullptr) return set_error("naz_ar_flow_log_prob_train: null states");
+  const int rc = ar_dispatch(d, [&](auto ops) {
+    return decltype(ops)::log_prob(static_cast<const float*>(packed), d->L, x, ldx, ctx, ldc, nullptr, nullptr, out_lp,
+                                   B, d->bound, s, 1, 0, 0, 0, 0, states);
+  });
+  return rc == -2 ? ar_unsupported(d) : rc;
+}
+
+#endif  // part 2
+
+#if NAZ_PART == 0 || NAZ_PART == 3  // ---------------- part 3: the autoregressive backward
+// ---- fused maf backward (made_ar_bwd.h): the NUTS potential's gradient / the maf NLL step --------
+template <class CF>
+struct ARBwdOps {
+  using CB = CfgARB<CF>;
+  static int64_t layer_floats() { return CB::LAYER; }
+  static int dims(int* w) {  // operand widths: n_hidden, HP, XA, XB, X0W, rows per tile
+    w[0] = CB::NHID;
+    w[1] = CB::HP;
+    w[2] = CB::XA;
+    w[3] = CB::XB;
+    w[4] = CB::X0W;
+    w[5] = 16 * CB::NW;
+    return 0;
+  }
+  static int pack(const float* flat, const float* mask, float* packed, int L, hipStream_t s) {
+    if (L == 0) return 0;
+    if (L > 65535) return set_error("naz_ar_flow_pack_bwd: at most 65535 layers");
+    const dim3 grid((unsigned)((CB::LAYER + 255) / 256), (unsigned)L);
+    hipLaunchKernelGGL((made_ar_pack_bwd_kernel<CB>), grid, dim3(256), 0, s, flat, mask, packed);
+    return check_launch("made_ar_pack_bwd_kernel");
+  }
+  static int layer(const float* fimg, const float* bimg, const int* perm, const float* s_in, const float* ctx,
+                   int64_t ldc, const float* g_in, const float* g_lp, const ArBwdOut& o, int64_t B, hipStream_t s) {
+    if (B == 0) return 0;
+    const int64_t grid = (B + 16 * CB::NW - 1) / (16 * CB::NW);  // one workgroup per CU at a time (160 KB ring)
+    if (grid > 0x7fffffff) return set_error("naz_ar_flow_bwd_layer: batch too large for one launch");
+    const size_t lds = (size_t)2 * CB::SLOT * 4;
+    hipLaunchKernelGGL((made_ar_bwd_kernel<CB>), dim3((unsigned)grid), dim3(64 * CB::NW), lds, s, fimg, bimg, perm,
+                       s_in, ctx, ldc, g_in, g_lp, o, B);
+    return check_launch("made_ar_bwd_kernel");
+  }
+};
+
+template <class F>
+static int ar_bwd_dispatch(const naz_ar_desc* d, F&& f) {
+  if (d == nullptr || d->act != NAZ_ACT_TANH || d->L < 0 || d->kind != NAZ_AR_AFFINE) return -2;
+  // the maf paper shape (train_mle_all_data.py:62-70; the NUTS potential of hmc_maf_exact.py)
+  if (d->D == 2 && d->C == 2 && d->H == 150 && d->n_hidden == 3) return f(ARBwdOps<CfgAR<2, 2, 150, 8, 3, true>>{});
+  return -2;
+}
+
+static int ar_bwd_unsupported(const naz_ar_desc* d) {
+  if (d == nullptr) return set_error("naz_ar_flow_bwd: null descriptor");
+  return set_error("naz_ar_flow_bwd: no fused backward for kind=%d D=%d C=%d H=%d x %d act=%d", d->kind, d->D, d->C,
+                   d->H, d->n_hidden, d->act);
+}
+
+int64_t ar_flow_bwd_packed_bytes(const naz_ar_desc* d) {
+  int64_t v = -1;
+  ar_bwd_dispatch(d, [&](auto ops) {
+    v = decltype(ops)::layer_floats() * d->L * 4;
+    return 0;
+  });
+  return v;
+}
+
+int ar_flow_bwd_dims(const naz_ar_desc* d, int* dims) {
+  if (dims == nullptr) return set_error("naz_ar_flow_bwd_dims: null output");
+  const int rc = ar_bwd_dispatch(d, [&](auto ops) { return decltype(ops)::dims(dims); });
+  return rc == -2 ? ar_bwd_unsupported(d) : rc;
+}
+
+int ar_flow_pack_bwd(const naz_ar_desc* d, const float* flat, const float* mask, void* packed, hipStream_t s) {
+  if (flat == nullptr || packed == nullptr) return set_error("naz_ar_flow_pack_bwd: null pointer");
+  const int rc = ar_bwd_dispatch(d, [&](auto ops) {
+    return decltype(ops)::pack(flat, mask, static_cast<float*>(packed), d->L, s);
+  });
+  return rc == -2 ? ar_bwd_unsupported(d) : rc;
+}
+
+int ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* packed_bwd, const int* perm, int layer,
+                      const float* state, const float* ctx, int64_t ldc, const float* g_in, const float* g_lp,
+                      float* const* bufs, float* g_out, int64_t B, hipStream_t s) {
+  if (d == nullptr || layer < 0 || layer >= d->L) return set_error("naz_ar_flow_bwd_layer: layer out of range");
+  const int rc = ar_bwd_dispatch(d, [&](auto ops) {
+    using O = decltype(ops);
+    using CB = typename O::CB;
+    // bufs: x0, then per hidden layer i (ha_i, hb_i), then dp_i, then gout
+    ArBwdOut o{};
+    o.x0 = bufs[0];
+    for (int i = 0; i < CB::NHID; ++i) {
+      o.ha[i] = bufs[1 + 2 * i];
+      o.hb[i] = bufs[2 + 2 * i];
+      o.dp[i] = bufs[1 + 2 * CB::NHID + i];
+    }
+    o.gout = bufs[1 + 3 * CB::NHID];
+    o.g_next = g_out;
+    for (int k = 0; k < 2 + 3 * CB::NHID; ++k)
+      if (bufs[k] == nullptr && !(k >= 1 && k <= 2 * CB::NHID && (k & 1) == 0 && CB::XB == 0))
+        return set_error("naz_ar_flow_bwd_layer: null operand buffer %d", k);
+    const float* fimg = static_cast<const float*>(packed_fwd) + (int64_t)layer * CB::FW::LAYER;
+    const float* bimg = static_cast<const float*>(packed_bwd) + (int64_t)layer * CB::LAYER;
+    return O::layer(fimg, bimg, perm + (int64_t)layer * CB::D, state, ctx, ldc, g_in, g_lp, o, B, s);
+  });
+  return rc == -2 ? ar_bwd_unsupported(d) : rc;
+}
+
+#endif  // part 3
 
 }  // namespace naz

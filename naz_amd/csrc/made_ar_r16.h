@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, int64_t B, float bound, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0,
-    int c0mode = 0) {
+    int c0mode = 0, float* __restrict__ states = nullptr) {
   constexpr int D = CF::D, K = CF::K, P = CF::P, NW = CF::NW, NHID = CF::NHID;
   {  // blockIdx.y = draw (naz_ar_flow_log_prob_batched): image packed + draw spk, rows x + draw sx
     const int64_t dz = blockIdx.y;
@@ -466,6 +466,12 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
         }
       });
     });
+    // the training forward (naz_ar_flow_log_prob_train, one draw): layer l's output s_l for the
+    // backward (made_ar_bwd.h)
+    if (states != nullptr && q == 0 && valid) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) states[((int64_t)l * B + row) * D + d] = v[d];
+    }
   }
   constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
   float base = 0.f;

@@ -103,6 +103,14 @@ int ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t s
                              int pass0_const, hipStream_t s);
 int ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
                        int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s);
+int ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
+                           int64_t ldc, float* out_lp, float* states, int64_t B, hipStream_t s);
+int64_t ar_flow_bwd_packed_bytes(const naz_ar_desc* d);
+int ar_flow_bwd_dims(const naz_ar_desc* d, int* dims);
+int ar_flow_pack_bwd(const naz_ar_desc* d, const float* flat, const float* mask, void* packed, hipStream_t s);
+int ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* packed_bwd, const int* perm, int layer,
+                      const float* state, const float* ctx, int64_t ldc, const float* g_in, const float* g_lp,
+                      float* const* bufs, float* g_out, int64_t B, hipStream_t s);
 
 int cnf_supported(const naz_cnf_desc* d);
 int64_t cnf_param_count(const naz_cnf_desc* d);

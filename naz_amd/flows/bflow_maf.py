@@ -223,7 +223,8 @@ def _flat_layer(layer, P, dev):
 
 def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bounds=None, context=None,
                           rows_per_chunk: int = 1 << 23, fold_context: bool = True,
-                          fuse_pass2: bool = True, batch_layers: bool = True, fused_ar: bool = True) -> Dict[str, object]:
+                          fuse_pass2: bool = True, batch_layers: bool = True, fused_ar: bool = True,
+                          fused_grad: bool = True) -> Dict[str, object]:
     """naz ``make_normalizing_flow`` (bflow_jax_maf.py:196-225) on MI355X.  Returns
     ``{"lp": f(params) -> [B], "sampler": f(params, rng_key, size) -> (y, log_j),
     "lp_batched": f(params_P) -> [P, B], "sampler_batched": f(params_P, rng_key, size)}``.
@@ -277,8 +278,8 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
     # the whole log-density in ONE launch for all draws (naz_ar_flow_log_prob_batched): the
     # inverse kernel's degree passes assume pyro's create_mask for each layer's permutation, one
     # context vector (or none) and rows inside the f16x3 input split's range
-    ar_perm = ar_pass0 = None
-    if ar_desc is not None and ops.ar_flow_supported(ar_desc) and (C == 0 or ctx.dim() == 1) and \
+    ar_perm = ar_pass0 = ar_grad_perm = None
+    if ar_desc is not None and ops.ar_flow_supported(ar_desc) and \
             float(x.abs().max()) < 32768.0 and \
             (C == 0 or float(ctx.abs().max()) < 32768.0):
         pm = [torch.as_tensor(p_).cpu().to(torch.int64) for p_ in perms]
@@ -287,7 +288,10 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             ref, _ = create_mask(D, C, hd, p_, 2)
             ok = ok and len(ref) == len(ms) and all(
                 torch.equal(r.to(torch.float32), m.detach().cpu().to(torch.float32)) for r, m in zip(ref, ms))
-        if ok:
+        # the NUTS potential's gradient (lp_and_grad) on the fused maf backward: any context rows
+        if ok and ops.ar_flow_bwd_supported(ar_desc):
+            ar_grad_perm = torch.stack(pm).numpy()
+        if ok and (C == 0 or ctx.dim() == 1):
             ar_perm = torch.stack(pm).numpy()
             # one context vector: the first degree pass (units of mask index 0 see only the
             # context; the first dim's outputs see only them) is a per-draw constant, computed
@@ -653,7 +657,11 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         return f
 
     def _grad_step(flat: Tensor):
-        """flat θ -> (Σ lp, ∇θ): weights copied in, the NLL training walk forward + backward."""
+        """flat θ -> (Σ lp, ∇θ): MafGrad, or the weights copied into a naz_amd maf and the NLL
+        training walk forward + backward."""
+        mg = _fused_grad()
+        if mg is not None:
+            return mg(flat)
         f = _grad_model()
         params = unravel(flat, [spec.param_shapes] * len(plans))
         with torch.no_grad():
@@ -667,36 +675,51 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         g = [[(lin.weight.grad, lin.bias.grad) for lin in t.nn.layers] for t in f.transforms]
         return total.detach(), ravel(g)
 
-    def _capture():
-        """The whole gradient step as one HIP graph (it is ~1,000 small launches eager)."""
-        f = _grad_model()
-        n = sum(p.numel() for p in f.parameters())
-        static = torch.zeros(n, device=dev, dtype=torch.float32)
-        static.copy_(ravel([[(lin.weight.detach(), lin.bias.detach()) for lin in t.nn.layers] for t in f.transforms]))
+    def _capture(flat0: Tensor):
+        """The whole gradient step as one HIP graph (the walk is ~1,000 small launches eager)."""
+        fused = _fused_grad() is not None
+        f = None if fused else _grad_model()
+        static = flat0.detach().clone()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(2):  # warm the caches (schedules, packs) outside the capture
-                f.zero_grad(set_to_none=True)
+                if f is not None:
+                    f.zero_grad(set_to_none=True)
                 _grad_step(static)
         torch.cuda.current_stream(dev).wait_stream(side)
-        f.zero_grad(set_to_none=True)
+        if f is not None:
+            f.zero_grad(set_to_none=True)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out = _grad_step(static)
         grad_flow["graph"] = (graph, static, out)
 
+    def _fused_grad():
+        """MafGrad over these rows (maf_grad.py: the fused inverse with saved states, one fused
+        backward launch per layer, bf16x6 batch reductions), or None where it does not apply."""
+        if ar_grad_perm is None or not fused_grad:
+            return None
+        mg = grad_flow.get("mafgrad")
+        if mg is None:
+            from .maf_grad import MafGrad
+            c = None if ctx is None else (ctx.reshape(1, -1) if ctx.dim() == 1 else ctx)
+            mg = grad_flow["mafgrad"] = MafGrad(ar_desc, ar_grad_perm, torch.cat(ar_maskvec), x, c)
+        return mg
+
     def lp_and_grad(params, use_graph: bool = True) -> Tuple[Tensor, Tensor]:
         """(Σ_rows log p(x | θ), ∇θ of it in ``ravel`` order): the NUTS / HMC potential of
         ``bayesian_normalizing_flow`` (bflow_jax_maf.py:233-235: ``flow_lp(unravel(p)).sum()``
-        and its gradient).  One draw (pytree or flat [n]); runs the NLL training walk (HIP
-        forward + backward kernels, nn autograd) on a naz_amd maf with these weights, replayed as
-        one captured HIP graph after the first call (``use_graph=False``: eager launches)."""
+        and its gradient).  One draw (pytree or flat [n]).  At the fused backward's shapes (the
+        paper maf, pyro masks, rows inside the f16 split's range): MafGrad.  Otherwise the NLL
+        training walk (HIP forward + backward kernels, nn autograd) on a naz_amd maf with these
+        weights.  Either is replayed as one captured HIP graph after the first call
+        (``use_graph=False``: eager launches)."""
         flat = params if torch.is_tensor(params) else ravel(params)
         flat = flat.to(dev, torch.float32).reshape(-1)
         if use_graph and "graph" not in grad_flow and not grad_flow.get("no_graph"):
             try:
-                _capture()
+                _capture(flat)
             except RuntimeError:  # capture unsupported here: eager launches (same kernels)
                 grad_flow["no_graph"] = True
                 torch.cuda.synchronize(dev)
@@ -705,7 +728,8 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             static.copy_(flat)
             graph.replay()
             return total.clone(), grad.clone()
-        _grad_model().zero_grad(set_to_none=True)
+        if _fused_grad() is None:
+            _grad_model().zero_grad(set_to_none=True)
         return _grad_step(flat)
 
     def _one(params):
@@ -736,4 +760,5 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
 
     return {"lp": lp, "sampler": sampler, "lp_batched": lp_batched, "sampler_batched": sampler_batched,
             "lp_and_grad": lp_and_grad, "grad_state": grad_flow, "lp_flops_per_row": lp_flops_per_row,
+            "grad_fused": ar_grad_perm is not None and fused_grad,
             "plans": plans, "fused_fwd": fused_fwd, "lp_fused_ar": ar_perm is not None}

@@ -8,7 +8,7 @@ without copies.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -739,6 +739,67 @@ def ar_flow_log_prob(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Ten
     check(lib().naz_ar_flow_log_prob(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out), B,
                                      _stream(dev)), "ar_flow_log_prob")
     return out
+
+
+# ----------------------------------------------------------------------------- fused maf backward (§8f rank 1)
+def ar_flow_bwd_supported(d: ArDesc) -> bool:
+    """The fused maf backward (made_ar_bwd.h) is compiled for this shape."""
+    return int(lib().naz_ar_flow_bwd_packed_bytes(d)) > 0
+
+
+def ar_flow_bwd_dims(d: ArDesc) -> dict:
+    """Operand widths of naz_ar_flow_bwd_layer (include/naz_hip.h)."""
+    out = np.zeros(6, dtype=np.int32)
+    check(lib().naz_ar_flow_bwd_dims(d, out.ctypes.data), "ar_flow_bwd_dims")
+    return dict(zip(("n_hidden", "HP", "XA", "XB", "X0W", "rows"), (int(v) for v in out)))
+
+
+def ar_flow_pack_bwd(d: ArDesc, flat: Tensor, mask: Optional[Tensor] = None) -> Tensor:
+    """Per-layer backward images (naz_ar_flow_pack_bwd) of one flow's flat [L * per] parameters."""
+    dev = _dev(flat, mask)
+    flat = flat.reshape(-1).contiguous()
+    n = int(lib().naz_ar_flow_bwd_packed_bytes(d)) // 4
+    if n <= 0:
+        raise RuntimeError("naz_amd ar_flow_pack_bwd: unsupported descriptor")
+    if mask is not None and (mask.numel() != flat.numel() or not mask.is_contiguous()):
+        raise ValueError("ar_flow_pack_bwd: mask must be a contiguous tensor shaped like flat")
+    out = torch.empty(n, device=dev, dtype=torch.float32)
+    check(lib().naz_ar_flow_pack_bwd(d, _p(flat), _p(mask), _p(out), _stream(dev)), "ar_flow_pack_bwd")
+    return out
+
+
+def ar_flow_log_prob_train(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor], states: Tensor,
+                           out: Optional[Tensor] = None) -> Tensor:
+    """log p(x | ctx) (naz_ar_flow_log_prob on the inverse image) also writing states [L, B, D]:
+    layer l's output s_l, for naz_ar_flow_bwd_layer."""
+    dev = _dev(packed, x, context, states, out)
+    x, ldx = _rows(x)
+    B = x.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    if states.shape != (d.L, B, d.D) or not states.is_contiguous():
+        raise ValueError(f"ar_flow_log_prob_train: states must be contiguous {(d.L, B, d.D)}")
+    if out is None:
+        out = torch.empty((B,), device=dev, dtype=torch.float32)
+    check(lib().naz_ar_flow_log_prob_train(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(out), _p(states), B,
+                                           _stream(dev)), "ar_flow_log_prob_train")
+    return out
+
+
+def ar_flow_bwd_layer(d: ArDesc, packed_fwd: Tensor, packed_bwd: Tensor, perm: Tensor, layer: int, state: Tensor,
+                      context: Optional[Tensor], g_in: Tensor, g_lp: Optional[Tensor], bufs: List[Tensor],
+                      g_out: Tensor) -> None:
+    """Layer ``layer``'s fused maf backward (naz_ar_flow_bwd_layer): g_in = dL/ds_l -> g_out =
+    dL/ds_{l+1} and the weight-gradient operands ``bufs`` (include/naz_hip.h order)."""
+    dev = _dev(packed_fwd, packed_bwd, perm, state, context, g_in, g_lp, g_out)
+    B = state.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    for t in (state, g_in, g_out, perm) + tuple(b for b in bufs if b is not None) + ((g_lp,) if g_lp is not None else ()):
+        if not t.is_contiguous():
+            raise ValueError("ar_flow_bwd_layer: buffers must be contiguous")
+    ptrs = (C.c_void_p * len(bufs))(*[_p(b) for b in bufs])
+    check(lib().naz_ar_flow_bwd_layer(d, _p(packed_fwd), _p(packed_bwd), _p(perm), int(layer), _p(state),
+                                      _p(context), ldc, _p(g_in), _p(g_lp), ptrs, _p(g_out), B, _stream(dev)),
+          "ar_flow_bwd_layer")
 
 
 # ----------------------------------------------------------------------------- a10: fused NLL step

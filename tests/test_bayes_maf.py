@@ -490,3 +490,87 @@ def test_lp_batched_fused_ar_paper_shape(_gpu, P, B):
         ol = _oracle_layers(layers, d)
         assert_parity(lp[p], J.log_prob(x, ol, ctx), J.log_prob(x, J.cast_layers(ol, np.float32), ctx, np.float32),
                       what=f"fused-AR lp draw {p}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ctx_kind,B", [("rows", 1500), ("vec", 700), ("rows", 64)])
+def test_lp_and_grad_fused_maf_backward_vs_oracle(_gpu, ctx_kind, B):
+    """The NUTS potential's gradient on the fused maf backward (maf_grad.py: the inverse kernel
+    with saved states, made_ar_bwd_kernel per layer, batch-reduction dW) at the paper shape (D=2 |
+    C=2, H=[150]x3) vs the fp64 oracle's torch autograd (ref32 = its fp32 run), vs the training
+    walk, graph replay vs eager, and new weights through the replay; ragged row counts."""
+    from naz_amd.flows import bflow_maf as BM
+    spec = dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=3, P=2, B=B, ctx=ctx_kind)
+    layers, draws, x, ctx = _setup(spec, seed=11)
+    flow = _flow(spec, layers, x, ctx, "cuda")
+    assert flow["grad_fused"], "the paper shape must take the fused maf backward"
+    walk = _flow(spec, layers, x, ctx, "cuda", fused_grad=False)
+    assert not walk["grad_fused"]
+
+    def flat_of(d):
+        return BM.ravel([[(torch.tensor(W, dtype=torch.float32, device="cuda"),
+                           torch.tensor(b, dtype=torch.float32, device="cuda")) for (W, b) in lay] for lay in d])
+    p1 = flat_of(draws[0])
+    total, grad = flow["lp_and_grad"](p1)
+    assert "graph" in flow["grad_state"] and "mafgrad" in flow["grad_state"]
+    t_e, g_e = flow["lp_and_grad"](p1, use_graph=False)
+    assert torch.allclose(total, t_e, rtol=1e-6) and torch.allclose(grad, g_e, rtol=1e-5,
+                                                                     atol=1e-6 * float(g_e.abs().max()))
+    t_w, g_w = walk["lp_and_grad"](p1, use_graph=False)
+    assert abs(total.item() - t_w.item()) <= 1e-5 * abs(t_w.item())
+    assert torch.allclose(grad, g_w, rtol=1e-3, atol=1e-4 * float(g_w.abs().max())), \
+        float((grad - g_w).abs().max() / g_w.abs().max())
+    p2 = flat_of(draws[1])  # the replay follows new weights
+    t_g, g_g = flow["lp_and_grad"](p2)
+    t_e2, g_e2 = flow["lp_and_grad"](p2, use_graph=False)
+    assert torch.allclose(t_g, t_e2, rtol=1e-6) and torch.allclose(g_g, g_e2, rtol=1e-5,
+                                                                    atol=1e-6 * float(g_e2.abs().max()))
+    d = draws[0]
+
+    def oracle(dtype):
+        st = {}
+        for l, lay in enumerate(d):
+            for i, (W, b) in enumerate(lay):
+                st[f"layers.{l}.nn.layers.{i}.weight"] = torch.tensor(W, dtype=dtype, requires_grad=True)
+                st[f"layers.{l}.nn.layers.{i}.bias"] = torch.tensor(b, dtype=dtype, requires_grad=True)
+            st[f"layers.{l}.nn.permutation"] = torch.tensor(layers[l][1])
+        f = O.build_flow(spec, st, dtype)
+        xc = torch.tensor(x, dtype=dtype)
+        cc = torch.tensor(ctx, dtype=dtype)
+        cc = cc.expand(len(x), -1) if cc.dim() == 1 else cc
+        lp = f.log_prob(xc, cc).sum()
+        lp.backward()
+        g = torch.cat([t.grad.reshape(-1) for l in range(len(d)) for i in range(len(d[0]))
+                       for t in (st[f"layers.{l}.nn.layers.{i}.weight"], st[f"layers.{l}.nn.layers.{i}.bias"])])
+        return lp.item(), g.numpy()
+    lp64, g64 = oracle(torch.float64)
+    lp32, g32 = oracle(torch.float32)
+    assert abs(total.item() - lp64) / abs(lp64) < 1e-5
+    from tests.parity import grad_floor
+    assert_parity(grad.cpu().numpy(), g64, g32, what="fused NUTS potential gradient", floor=grad_floor(g64),
+                  count_factor=None)
+
+
+@pytest.mark.gpu
+def test_lp_and_grad_fused_full_size_properties(_gpu):
+    """The §8f rank-1 workload (paper shape, L=16, 2^16 training rows, per-row contexts): the fused
+    potential and gradient are finite, the potential bitwise reproducible, the gradient equal up to
+    the dW reductions' summation order, and the potential equals the fused log-density's sum."""
+    from naz_amd.flows import bflow_maf as BM
+    spec = dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=16, P=1, B=1 << 16, ctx="rows")
+    layers, draws, x, ctx = _setup(spec, seed=5)
+    flow = _flow(spec, layers, x, ctx, "cuda")
+    assert flow["grad_fused"]
+    p = BM.ravel([[(torch.tensor(W, dtype=torch.float32, device="cuda"),
+                    torch.tensor(b, dtype=torch.float32, device="cuda")) for (W, b) in lay] for lay in draws[0]])
+    t1, g1 = flow["lp_and_grad"](p)
+    t2, g2 = flow["lp_and_grad"](p)
+    assert bool(torch.isfinite(t1)) and bool(torch.isfinite(g1).all())
+    assert torch.equal(t1, t2)
+    assert torch.allclose(g1, g2, rtol=1e-5, atol=1e-6 * float(g1.abs().max()))
+    mg = flow["grad_state"]["mafgrad"]
+    lp_rows = mg.lp.clone()
+    from naz_amd import ops
+    ref = ops.ar_flow_log_prob(mg.desc, ops.ar_flow_pack_batched(mg.desc, p[None], mg.perms, mask=mg.mask)[0],
+                               mg.x, mg.ctx)
+    assert torch.equal(lp_rows, ref), "the training forward must be the log_prob kernel's arithmetic"

@@ -173,6 +173,15 @@ int naz_rqs_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int6
 int naz_gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
              int64_t sbn, float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn,
              int mask_b, int accumulate, int split_k, float* rowsum, void* stream);
+/* nbatch weight-gradient reductions in one launch (bf16x6 MFMA, exact to fp32 products):
+ * C[b][n1][n2] += sum_m G[b][m][n1] X[b][m][n2] and (rowsum != NULL) rowsum[b][n1] += sum_m G[b][m][n1],
+ * with G[b] = g + b*bg (row stride sgm = N1), X[b] = x + b*bx (row stride sxm = N2), C[b] = c + b*bc
+ * (row stride scm, unit column stride), rowsum[b] = rowsum + b*br; 16-byte aligned rows,
+ * N1 <= 256, N2 <= 160, both multiples of 4.  Accumulates (zero C / rowsum first).  The fused maf
+ * backward's dW of all layers (flows/maf_grad.py), replacing per-layer jax.grad reductions. */
+int naz_wgrad_batched(int64_t M, int N1, int N2, int nbatch, const float* g, int64_t sgm, int64_t bg, const float* x,
+                      int64_t sxm, int64_t bx, float* c, int64_t scm, int64_t bc, float* rowsum, int64_t br,
+                      void* stream);
 /* VJP of naz_affine_ar (the kernel reports the FORWARD log-det sum(clamp(ls)) in both
  * directions).  x = the map's input, y = its output, g_ld [B] = dL/d(row ld) (may be NULL).
  * pyro clamps log_scale with clamp_preserve_gradients: the clamp passes gradients through.

@@ -107,6 +107,8 @@ SIGNATURES = {
     "naz_ar_flow_sample_batched": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
                                              _i64, _vp, _i64, _i64, _i64, _vp]),
     "naz_ar_flow_pack_fwd_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp]),
+    "naz_wgrad_batched": (C.c_int, [_i64, _i, _i, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64,
+                                    _vp]),
     "naz_ar_flow_log_prob_train": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
     "naz_ar_flow_bwd_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),
     "naz_ar_flow_bwd_dims": (C.c_int, [C.POINTER(ArDesc), _vp]),

@@ -156,6 +156,14 @@ int naz_gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, 
               as_stream(stream));
 }
 
+int naz_wgrad_batched(int64_t M, int N1, int N2, int nbatch, const float* g, int64_t sgm, int64_t bg, const float* x,
+                      int64_t sxm, int64_t bx, float* c, int64_t scm, int64_t bc, float* rowsum, int64_t br,
+                      void* stream) {
+  if (M > 0 && nbatch > 0 && (g == nullptr || x == nullptr || c == nullptr))
+    return set_error("naz_wgrad_batched: null pointer");
+  return wgrad_batched(M, N1, N2, nbatch, g, sgm, bg, x, sxm, bx, c, scm, bc, rowsum, br, as_stream(stream));
+}
+
 int naz_affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y,
                       int64_t ldy, const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx,
                       float* g_raw, int64_t ldgr, int64_t B, int D, void* stream) {

@@ -355,6 +355,8 @@ struct WGradArgs {
   float* rowsum;
   int64_t rows_per_wg;
   int blk0;        // first output block (of NB1 x NB2, n2-fastest) this launch owns
+  // batched reductions (wgrad_x6 only, blockIdx.y = batch b): g, x, c, rowsum advance by b times these
+  int64_t bg, bx, bc, br;
 };
 
 // one workgroup: rows [mb, me) of G and X -> its share of every output block, added atomically
@@ -586,6 +588,13 @@ __global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_t16_kernel(WGradArgs p
   const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, jh = tid >> 8, m = lane & 15,
             kq = lane >> 4;
   const int N1 = p.N1, N2 = p.N2;
+  {
+    const int64_t bz = blockIdx.y;
+    p.g += bz * p.bg;
+    p.x += bz * p.bx;
+    p.c += bz * p.bc;
+    if (p.rowsum != nullptr) p.rowsum += bz * p.br;
+  }
   const int64_t mb = (int64_t)blockIdx.x * p.rows_per_wg;
   const int64_t me = (mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M;
   floatx4w acc[NOW][NBW];
@@ -800,6 +809,13 @@ __global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_x6_kernel(WGradArgs p,
   const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, jh = tid >> 8, m = lane & 15,
             kq = lane >> 4;
   const int N1 = p.N1, N2 = p.N2;
+  {
+    const int64_t bz = blockIdx.y;
+    p.g += bz * p.bg;
+    p.x += bz * p.bx;
+    p.c += bz * p.bc;
+    if (p.rowsum != nullptr) p.rowsum += bz * p.br;
+  }
   const int64_t mb = (int64_t)blockIdx.x * p.rows_per_wg;
   const int64_t me = (mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M;
   floatx4w acc[NOW][NBW];
@@ -908,34 +924,36 @@ __global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_x6_kernel(WGradArgs p,
 }
 
 template <int NOW, int NB2>
-static void wgrad_x6_go(const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s, bool js2) {
+static void wgrad_x6_go(const WGradArgs& q, int R, size_t lds, dim3 grid, hipStream_t s, bool js2) {
   if constexpr (NOW * NB2 > 12 && NB2 % 2 == 0) {
     if (js2) {
-      hipLaunchKernelGGL((wgrad_x6_kernel<NOW, NB2, 2>), dim3(gx), dim3(512), lds, s, q, R);
+      hipLaunchKernelGGL((wgrad_x6_kernel<NOW, NB2, 2>), grid, dim3(512), lds, s, q, R);
       return;
     }
   }
-  hipLaunchKernelGGL((wgrad_x6_kernel<NOW, NB2, 1>), dim3(gx), dim3(256), lds, s, q, R);
+  hipLaunchKernelGGL((wgrad_x6_kernel<NOW, NB2, 1>), grid, dim3(256), lds, s, q, R);
 }
 
 template <int NOW>
-static bool wgrad_x6_launch(int nb2, const WGradArgs& q, int R, size_t lds, unsigned gx, hipStream_t s, bool js2) {
+static bool wgrad_x6_launch(int nb2, const WGradArgs& q, int R, size_t lds, dim3 grid, hipStream_t s, bool js2) {
   switch (nb2) {
-    case 1: wgrad_x6_go<NOW, 1>(q, R, lds, gx, s, js2); return true;
-    case 2: wgrad_x6_go<NOW, 2>(q, R, lds, gx, s, js2); return true;
-    case 3: wgrad_x6_go<NOW, 3>(q, R, lds, gx, s, js2); return true;
-    case 4: wgrad_x6_go<NOW, 4>(q, R, lds, gx, s, js2); return true;
-    case 6: wgrad_x6_go<NOW, 6>(q, R, lds, gx, s, js2); return true;
-    case 8: wgrad_x6_go<NOW, 8>(q, R, lds, gx, s, js2); return true;
+    case 1: wgrad_x6_go<NOW, 1>(q, R, lds, grid, s, js2); return true;
+    case 2: wgrad_x6_go<NOW, 2>(q, R, lds, grid, s, js2); return true;
+    case 3: wgrad_x6_go<NOW, 3>(q, R, lds, grid, s, js2); return true;
+    case 4: wgrad_x6_go<NOW, 4>(q, R, lds, grid, s, js2); return true;
+    case 6: wgrad_x6_go<NOW, 6>(q, R, lds, grid, s, js2); return true;
+    case 8: wgrad_x6_go<NOW, 8>(q, R, lds, grid, s, js2); return true;
+    case 10: wgrad_x6_go<NOW, 10>(q, R, lds, grid, s, js2); return true;
     default: return false;
   }
 }
 
-// wgrad on the bf16x6 kernel for the shapes wgrad_t16 takes (R a multiple of 32 here)
-static bool wgrad_x6(WGradArgs p, hipStream_t s) {
+// wgrad on the bf16x6 kernel for the shapes wgrad_t16 takes (R a multiple of 32 here), plus
+// N2 <= 160 (the maf's 150-wide layers); nbatch independent reductions (blockIdx.y)
+static bool wgrad_x6(WGradArgs p, hipStream_t s, int nbatch = 1) {
   const int nb1 = (p.N1 + 15) / 16, now = (nb1 + 3) / 4;
   int nb2 = (p.N2 + 15) / 16;
-  nb2 = nb2 <= 4 ? nb2 : (nb2 <= 6 ? 6 : (nb2 <= 8 ? 8 : 0));
+  nb2 = nb2 <= 4 ? nb2 : (nb2 <= 6 ? 6 : (nb2 <= 8 ? 8 : (nb2 <= 10 ? 10 : 0)));
   if (now < 1 || now > 4 || nb2 == 0) return false;
   // 4-wave workgroups, two per CU (two DMA rings in flight per CU: one 8-wave workgroup with a
   // single ring streamed G + X at ~3.7 TB/s) when two rings of 32-row chunks fit the LDS; else one
@@ -953,16 +971,18 @@ static bool wgrad_x6(WGradArgs p, hipStream_t s) {
   if (lds_of(R) * (js2 ? 1 : 2) > 160 * 1024) return false;
   const size_t lds = lds_of(R);
   // two rounds of resident workgroups (one per CU for 8-wave ones, two per CU for 4-wave ones)
-  int64_t rpw = (p.M + (js2 ? 511 : 1023)) / (js2 ? 512 : 1024);
+  // over all nbatch reductions
+  const int64_t slots = js2 ? 512 : 1024;
+  int64_t rpw = (p.M * nbatch + slots - 1) / slots;
   rpw = (rpw + R - 1) / R * R;
   if (rpw < 4 * R) rpw = 4 * R;
   p.rows_per_wg = rpw;
-  const unsigned gx = (unsigned)((p.M + rpw - 1) / rpw);
+  const dim3 grid((unsigned)((p.M + rpw - 1) / rpw), (unsigned)nbatch);
   switch (now) {
-    case 1: return wgrad_x6_launch<1>(nb2, p, R, lds, gx, s, js2);
-    case 2: return wgrad_x6_launch<2>(nb2, p, R, lds, gx, s, js2);
-    case 3: return wgrad_x6_launch<3>(nb2, p, R, lds, gx, s, js2);
-    default: return wgrad_x6_launch<4>(nb2, p, R, lds, gx, s, js2);
+    case 1: return wgrad_x6_launch<1>(nb2, p, R, lds, grid, s, js2);
+    case 2: return wgrad_x6_launch<2>(nb2, p, R, lds, grid, s, js2);
+    case 3: return wgrad_x6_launch<3>(nb2, p, R, lds, grid, s, js2);
+    default: return wgrad_x6_launch<4>(nb2, p, R, lds, grid, s, js2);
   }
 }
 
@@ -997,13 +1017,16 @@ int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
       hipLaunchKernelGGL(zero2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p.c, p.scm, p.scn, p.N1,
                          p.N2);
     }
-    if (p.ones) (void)hipMemsetAsync(p.rowsum, 0, sizeof(float) * p.N1, s);
+    // the db vector zeroed by a kernel too: a hipMemsetAsync captured into a HIP graph was measured
+    // to leave stale sums on replay (tests/test_bayes_maf.py, fused maf gradient)
+    if (p.ones) hipLaunchKernelGGL(zero2d_kernel, dim3((unsigned)((p.N1 + 255) / 256)), dim3(256), 0, s, p.rowsum,
+                                   (int64_t)1, (int64_t)0, p.N1, 1);
   }
   if (p.M <= 0) return check_launch("zero2d_kernel");
   const bool flat = p.sgm == p.N1 && p.sxm == p.N2 && p.N1 % 4 == 0 && p.N2 % 4 == 0 && p.N2 > 0 &&
                     (reinterpret_cast<uintptr_t>(p.g) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.x) & 15) == 0 &&
                     p.N1 <= 256 && p.N2 <= 256;
-  if (flat && p.N2 <= 128 && wgrad_x6_enabled() && wgrad_x6(p, s)) return check_launch("wgrad_x6_kernel");
+  if (flat && p.N2 <= 160 && wgrad_x6_enabled() && wgrad_x6(p, s)) return check_launch("wgrad_x6_kernel");
   if (flat && p.N2 <= 128 && wgrad_t16_enabled() && wgrad_t16(p, s)) return check_launch("wgrad_t16_kernel");
   if (flat) {
     // rows per chunk: ~8192 floats of G + X (a multiple of 16, <= 128); ~1024 workgroups
@@ -1051,7 +1074,47 @@ int wgrad(WGradArgs p, int accumulate, hipStream_t s) {
   return check_launch("wgrad_kernel");
 }
 
+// nbatch independent dW-type reductions C[b] += G[b]ᵀ X[b] (+ rowsum[b] += column sums of G[b]) in
+// ONE bf16x6 launch (blockIdx.y = b): the maf backward's per-layer dW over all layers at once.
+// Row-major G [M, N1] / X [M, N2] with unit column stride, 16-byte aligned, C unit column stride.
+int wgrad_batched_impl(int64_t M, int N1, int N2, int nbatch, const float* g, int64_t sgm, int64_t bg,
+                       const float* x, int64_t sxm, int64_t bx, float* c, int64_t scm, int64_t bc, float* rowsum,
+                       int64_t br, hipStream_t s) {
+  if (M < 0 || N1 <= 0 || N2 <= 0 || nbatch < 0) return set_error("naz_wgrad_batched: bad shape");
+  if (M == 0 || nbatch == 0) return 0;
+  if (nbatch > 65535) return set_error("naz_wgrad_batched: at most 65535 reductions per call");
+  WGradArgs p{};
+  p.g = g;
+  p.sgm = sgm;
+  p.x = x;
+  p.sxm = sxm;
+  p.M = M;
+  p.N1 = N1;
+  p.N2 = N2;
+  p.ones = rowsum != nullptr;
+  p.c = c;
+  p.scm = scm;
+  p.scn = 1;
+  p.rowsum = rowsum;
+  p.bg = bg;
+  p.bx = bx;
+  p.bc = bc;
+  p.br = br;
+  const bool aligned = (reinterpret_cast<uintptr_t>(g) & 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                       bg % 4 == 0 && bx % 4 == 0;
+  if (!(sgm == N1 && sxm == N2 && N1 % 4 == 0 && N2 % 4 == 0 && N1 <= 256 && N2 <= 160 && aligned))
+    return set_error("naz_wgrad_batched: operands must be contiguous, 16-byte aligned rows of N1, N2 <= 160 (N %% 4 == 0)");
+  if (!wgrad_x6(p, s, nbatch)) return set_error("naz_wgrad_batched: no bf16x6 instance for N1=%d N2=%d", N1, N2);
+  return check_launch("wgrad_x6_kernel (batched)");
+}
+
 }  // namespace
+
+int wgrad_batched(int64_t M, int N1, int N2, int nbatch, const float* g, int64_t sgm, int64_t bg, const float* x,
+                  int64_t sxm, int64_t bx, float* c, int64_t scm, int64_t bc, float* rowsum, int64_t br,
+                  hipStream_t s) {
+  return wgrad_batched_impl(M, N1, N2, nbatch, g, sgm, bg, x, sxm, bx, c, scm, bc, rowsum, br, s);
+}
 
 // ------------------------------------------------------------------------------------------
 // Entry points used by dense.hip / gemm.hip

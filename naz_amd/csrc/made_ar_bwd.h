@@ -42,7 +42,7 @@ struct CfgARB {
   static constexpr int NW = 8;           // 2 waves per SIMD, one workgroup per CU (two 80 KB ring slots)
   static constexpr int NO = 2 * D;       // ARN outputs (mean, log_scale) x D, row pi D + d
   static constexpr int X0W = 8;          // [ctx | s | 0] operand width (wgrad's whole-chunk rule)
-  static constexpr int XA = HP > 128 ? 128 : HP, XB = HP - XA;  // h operands in two column groups
+  static constexpr int XA = HP, XB = 0;  // h operand column groups (one: naz_wgrad_batched takes N2 <= 160)
   // backward image units: 0 = W_out (natural fp32 [NO][HP]); 1 .. (NHID-1) HB = (W_iᵀ, output
   // block b) for i = NHID-1 down to 1; last = the input unit W_0[:, C:]ᵀ (one block, rows = dims)
   static constexpr int NUB = 2 + (NHID - 1) * HB;

@@ -128,6 +128,9 @@ int cnf_integrate_dopri5_global(const naz_cnf_desc* d, const void* packed, const
                                 const float* ctx, int64_t ldc, const float* eps, int64_t lde, float t0, float t1,
                                 float atol, float rtol, int max_steps, float* y, int64_t ldy, float* ld, int ld_mode,
                                 int* nfe, void* work, int64_t B, hipStream_t s);
+int wgrad_batched(int64_t M, int N1, int N2, int nbatch, const float* g, int64_t sgm, int64_t bg, const float* x,
+                  int64_t sxm, int64_t bx, float* c, int64_t scm, int64_t bc, float* rowsum, int64_t br,
+                  hipStream_t s);
 int rowgemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
                     const float* S, int64_t lds, int act, int64_t M, int N, hipStream_t s);
 

@@ -7,13 +7,14 @@ forward over the whole training set and one backward per leapfrog step.  Here th
   * the fused inverse kernel with every layer's output saved (naz_ar_flow_log_prob_train);
   * per layer l = 0 .. L-1 one fused backward launch (naz_ar_flow_bwd_layer, csrc/made_ar_bwd.h:
     dense MADE recompute, the affine VJP, the D-order chain of input gradients, the total δ's)
-    writing the weight-gradient operands;
-  * per layer the batch reductions dW = δᵀ·h (+ bias column sums) on naz_gemm's bf16x6 wgrad
-    kernel, into a padded per-layer workspace;
+    writing that layer's weight-gradient operands into its own slice of [L, rows, ...] buffers;
+  * per weight matrix ONE batched reduction over all layers (naz_wgrad_batched, bf16x6 MFMA):
+    dW_l = δ_lᵀ·h_l and the bias column sums into a padded per-layer workspace;
   * ONE gather of the workspace into ``ravel`` order times the masks (pyro MaskedLinear's
     gradient is mask ⊙ (δᵀ h)).
 
-No autograd graph, no per-block gathers: ~10 launches per layer.
+Rows are processed in chunks so the operands stay within ``operand_bytes`` (4 KB per row and layer
+at the paper shape).  No autograd graph, no per-block gathers: L + NHID + 5 launches per chunk.
 """
 from __future__ import annotations
 
@@ -28,10 +29,11 @@ from .. import ops
 
 class MafGrad:
     """(Σ lp, ∇θ) of one flat θ (``ravel`` order = the naz_ar_flow_pack_host flat layout) over
-    fixed rows ``x`` [B, D] and ``ctx`` ([B, C], [C] or None).  ``mask`` [L * per]: the MADE
+    fixed rows ``x`` [B, D] and ``ctx`` ([B, C], [1, C] or None).  ``mask`` [L * per]: the MADE
     masks in the flat layout (1 on biases); ``perms`` [L, D]: dim of order p per layer."""
 
-    def __init__(self, desc, perms: np.ndarray, mask: Tensor, x: Tensor, ctx: Optional[Tensor]):
+    def __init__(self, desc, perms: np.ndarray, mask: Tensor, x: Tensor, ctx: Optional[Tensor],
+                 operand_bytes: int = 8 << 30):
         if not ops.ar_flow_bwd_supported(desc):
             raise RuntimeError("MafGrad: no fused maf backward for this shape")
         self.desc = desc
@@ -40,6 +42,8 @@ class MafGrad:
         D, C, H, L = desc.D, desc.C, desc.H, desc.L
         dm = ops.ar_flow_bwd_dims(desc)
         NH, HP, XA, XB, X0W = dm["n_hidden"], dm["HP"], dm["XA"], dm["XB"], dm["X0W"]
+        if XB:
+            raise RuntimeError("MafGrad: split hidden operands are not supported")
         self.dims = dm
         self.x = x.to(torch.float32).contiguous()
         self.ctx = None if ctx is None else ctx.to(dev, torch.float32).contiguous()
@@ -53,13 +57,15 @@ class MafGrad:
         self.lp = torch.empty((B,), **f32)
         self.g = torch.empty((B, D), **f32)
         self.g_next = torch.empty((B, D), **f32)
-        self.x0 = torch.empty((B, X0W), **f32)
-        self.ha = [torch.empty((B, XA), **f32) for _ in range(NH)]
-        self.hb = [torch.empty((B, XB), **f32) if XB else None for _ in range(NH)]
-        self.dp = [torch.empty((B, HP), **f32) for _ in range(NH)]
-        self.gout = torch.empty((B, X0W), **f32)
-        self.bufs = [self.x0] + [t for i in range(NH) for t in (self.ha[i], self.hb[i])] + self.dp + [self.gout]
-        # padded per-layer dW workspace and its gather map into the flat (ravel) order
+        per_row = L * 4 * (2 * X0W + 2 * NH * HP)
+        rows = max(dm["rows"], min(B, operand_bytes // per_row) // dm["rows"] * dm["rows"])
+        self.chunk = min(B, rows)
+        Bc = self.chunk
+        self.x0 = torch.empty((L, Bc, X0W), **f32)
+        self.h = [torch.empty((L, Bc, HP), **f32) for _ in range(NH)]
+        self.dp = [torch.empty((L, Bc, HP), **f32) for _ in range(NH)]
+        self.gout = torch.empty((L, Bc, X0W), **f32)
+        # padded per-layer dW workspace [L, ws_per] and its gather map into the flat (ravel) order
         shapes = [(HP, X0W)] + [(HP, HP)] * (NH - 1) + [(X0W, HP)]
         nat = [(H, C + D)] + [(H, H)] * (NH - 1) + [(2 * D, H)]
         offs, o = [], 0
@@ -68,12 +74,8 @@ class MafGrad:
             o += r * c + r
         self.ws_per = o
         self.ws = torch.zeros((L, o), **f32)
-        self.views = []
-        for l in range(L):
-            v = []
-            for (r, c), (ow, ob) in zip(shapes, offs):
-                v.append((self.ws[l, ow:ow + r * c].view(r, c), self.ws[l, ob:ob + r]))
-            self.views.append(v)
+        self.views = [(self.ws[:, ow:ow + r * c].view(L, r, c), self.ws[:, ob:ob + r])
+                      for (r, c), (ow, ob) in zip(shapes, offs)]
         idx = []
         for l in range(L):
             for (r, c), (nr, nc), (ow, ob) in zip(shapes, nat, offs):
@@ -92,23 +94,27 @@ class MafGrad:
         bwd = ops.ar_flow_pack_bwd(d, flat, self.mask)
         ops.ar_flow_log_prob_train(d, inv, self.x, self.ctx, self.states, out=self.lp)
         torch.neg(self.states[0], out=self.g)  # d/dz of the Normal(0, I) base log-density
-        g, g_next = self.g, self.g_next
-        NH, XA = self.dims["n_hidden"], self.dims["XA"]
-        for l in range(d.L):
-            ops.ar_flow_bwd_layer(d, fwd, bwd, self.perm_dev, l, self.states[l], self.ctx, g, None, self.bufs,
-                                  g_next)
-            v = self.views[l]
-            W, b = v[0]
-            ops.gemm(self.dp[0].t(), self.x0, out=W, rowsum=b, split_k=1)
+        NH = self.dims["n_hidden"]
+        # one fill for every layer's dW / db, then the reductions accumulate into it
+        self.ws.zero_()
+        for r0 in range(0, self.B, self.chunk):
+            r1 = min(self.B, r0 + self.chunk)
+            n = r1 - r0
+            g, g_next = self.g[r0:r1], self.g_next[r0:r1]
+            ctx = None if self.ctx is None else (self.ctx if self.ctx.shape[0] == 1 else self.ctx[r0:r1])
+            for l in range(d.L):
+                bufs = [self.x0[l, :n]] + [t for i in range(NH) for t in (self.h[i][l, :n], None)] + \
+                       [self.dp[i][l, :n] for i in range(NH)] + [self.gout[l, :n]]
+                ops.ar_flow_bwd_layer(d, fwd, bwd, self.perm_dev, l, self.states[l, r0:r1], ctx, g, None, bufs,
+                                      g_next)
+                g, g_next = g_next, g
+            # dW of every layer: one batched reduction per weight matrix
+            W, b = self.views[0]
+            ops.wgrad_batched(self.dp[0][:, :n], self.x0[:, :n], W, b)
             for i in range(1, NH):
-                W, b = v[i]
-                ops.gemm(self.dp[i].t(), self.ha[i - 1], out=W[:, :XA], rowsum=b, split_k=1)
-                if self.hb[i - 1] is not None:
-                    ops.gemm(self.dp[i].t(), self.hb[i - 1], out=W[:, XA:], split_k=1)
-            W, b = v[NH]
-            ops.gemm(self.gout.t(), self.ha[NH - 1], out=W[:, :XA], rowsum=b, split_k=1)
-            if self.hb[NH - 1] is not None:
-                ops.gemm(self.gout.t(), self.hb[NH - 1], out=W[:, XA:], split_k=1)
-            g, g_next = g_next, g
+                W, b = self.views[i]
+                ops.wgrad_batched(self.dp[i][:, :n], self.h[i - 1][:, :n], W, b)
+            W, b = self.views[NH]
+            ops.wgrad_batched(self.gout[:, :n], self.h[NH - 1][:, :n], W, b)
         grad = self.ws.view(-1)[self.idx] * self.mask
         return self.lp.sum(), grad

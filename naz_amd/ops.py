@@ -398,6 +398,25 @@ def gemm(a: Tensor, b: Tensor, out: Optional[Tensor] = None, mask: Optional[Tens
     return out
 
 
+def wgrad_batched(g: Tensor, x: Tensor, c: Tensor, rowsum: Optional[Tensor] = None) -> Tensor:
+    """c[b] += g[b]ᵀ @ x[b] and rowsum[b] += g[b].sum(0) for every b in ONE launch (naz_wgrad_batched,
+    bf16x6 MFMA): g [nb, M, N1], x [nb, M, N2] with contiguous rows; c [nb, N1, N2] with unit column
+    stride (a strided view of a workspace is fine); rowsum [nb, N1] with unit stride."""
+    dev = _dev(g, x, c, rowsum)
+    nb, M, N1 = g.shape
+    if x.shape[:2] != (nb, M) or c.shape != (nb, N1, x.shape[2]):
+        raise ValueError("wgrad_batched: shapes must be g [nb, M, N1], x [nb, M, N2], c [nb, N1, N2]")
+    for t in (g, x):
+        if t.stride(2) != 1 or t.stride(1) != t.shape[2]:
+            raise ValueError("wgrad_batched: g and x need contiguous rows")
+    if c.stride(2) != 1 or (rowsum is not None and (rowsum.shape != (nb, N1) or rowsum.stride(1) != 1)):
+        raise ValueError("wgrad_batched: c / rowsum need a unit column stride")
+    check(lib().naz_wgrad_batched(M, N1, x.shape[2], nb, _p(g), g.stride(1), g.stride(0), _p(x), x.stride(1),
+                                  x.stride(0), _p(c), c.stride(1), c.stride(0), _p(rowsum),
+                                  0 if rowsum is None else rowsum.stride(0), _stream(dev)), "wgrad_batched")
+    return c
+
+
 def gemm_dact(a: Tensor, weight: Tensor, y: Tensor, act: str, mask: Optional[Tensor] = None,
               out: Optional[Tensor] = None) -> Tensor:
     """(a @ (weight * mask)) * act'(y) in one batch-row GEMM (naz_gemm_dact): the input
@@ -790,7 +809,9 @@ def ar_flow_bwd_layer(d: ArDesc, packed_fwd: Tensor, packed_bwd: Tensor, perm: T
                       g_out: Tensor) -> None:
     """Layer ``layer``'s fused maf backward (naz_ar_flow_bwd_layer): g_in = dL/ds_l -> g_out =
     dL/ds_{l+1} and the weight-gradient operands ``bufs`` (include/naz_hip.h order)."""
-    dev = _dev(packed_fwd, packed_bwd, perm, state, context, g_in, g_lp, g_out)
+    dev = _dev(packed_fwd, packed_bwd, state, context, g_in, g_lp, g_out)
+    if perm.dtype != torch.int32 or perm.device != dev or perm.shape != (d.L, d.D):
+        raise ValueError(f"ar_flow_bwd_layer: perm must be an int32 [{d.L}, {d.D}] tensor on {dev}")
     B = state.shape[0]
     context, ldc = _ctx_arg(context, B)
     for t in (state, g_in, g_out, perm) + tuple(b for b in bufs if b is not None) + ((g_lp,) if g_lp is not None else ()):

@@ -12,7 +12,7 @@ step() {
   tail -n 25 "gpurun_out/s10_$name.log" | cut -c1-600
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step tests 400 python -u -m pytest tests/test_bayes_maf.py -x -v -m gpu --timeout 120 --timeout-method thread -k "fused_maf_backward or fused_full_size or lp_and_grad_vs_oracle"
+step tests 400 python -u -m pytest tests/test_bayes_maf.py -x -v -m gpu --timeout 120 --timeout-method thread -k "fused_maf_backward or fused_full_size or lp_and_grad_vs_oracle"; step tests2 400 python -u -m pytest tests/test_gpu_grad.py -x -q -m gpu --timeout 120 --timeout-method thread -k "wgrad or gemm"
 step bench 300 python bench.py --bayes grad --steps 10 --warmup 3 --no-cpu-baseline
-step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_s10 -o run -- python bench.py --bayes grad --steps 10 --warmup 3 --no-cpu-baseline
+step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_s10 -o run --output-format csv -- python bench.py --bayes grad --steps 10 --warmup 3 --no-cpu-baseline
 exit 0

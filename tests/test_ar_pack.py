@@ -78,7 +78,7 @@ def test_fused_maf_backward_host_queries():
     widths include/naz_hip.h documents; every other shape / kind reports itself unsupported."""
     d = ops.ar_flow_desc("maf", 2, 2, 150, 16, 3)
     assert ops.ar_flow_bwd_supported(d)
-    assert ops.ar_flow_bwd_dims(d) == dict(n_hidden=3, HP=160, XA=128, XB=32, X0W=8, rows=128)
+    assert ops.ar_flow_bwd_dims(d) == dict(n_hidden=3, HP=160, XA=160, XB=0, X0W=8, rows=128)
     per_layer = int(ops.lib().naz_ar_flow_bwd_packed_bytes(ops.ar_flow_desc("maf", 2, 2, 150, 1, 3)))
     assert per_layer > 0 and int(ops.lib().naz_ar_flow_bwd_packed_bytes(d)) == 16 * per_layer
     for bad in (ops.ar_flow_desc("nsa", 16, 32, 128, 1), ops.ar_flow_desc("maf", 16, 32, 128, 1, 2),

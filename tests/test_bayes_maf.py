@@ -523,8 +523,10 @@ def test_lp_and_grad_fused_maf_backward_vs_oracle(_gpu, ctx_kind, B):
     p2 = flat_of(draws[1])  # the replay follows new weights
     t_g, g_g = flow["lp_and_grad"](p2)
     t_e2, g_e2 = flow["lp_and_grad"](p2, use_graph=False)
-    assert torch.allclose(t_g, t_e2, rtol=1e-6) and torch.allclose(g_g, g_e2, rtol=1e-5,
-                                                                    atol=1e-6 * float(g_e2.abs().max()))
+    # the dW reductions add per-workgroup partials with fp32 atomics: equal up to summation order
+    err = float((g_g - g_e2).abs().max() / g_e2.abs().max())
+    assert torch.allclose(t_g, t_e2, rtol=1e-6) and err < 1e-5, err
+    assert not torch.allclose(g_g, grad, rtol=1e-3), "the replay must follow the new weights"
     d = draws[0]
 
     def oracle(dtype):

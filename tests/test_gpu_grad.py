@@ -200,6 +200,27 @@ def test_wgrad_t16_shapes(N1, N2, M):
 
 
 # ------------------------------------------------------------------ a5 affine step VJP
+@pytest.mark.parametrize("N1,N2,M,nb", [(160, 160, 65536, 3), (160, 8, 3000, 3), (8, 160, 4097, 5), (160, 144, 517, 2),
+                                        (128, 128, 70001, 1)])
+def test_wgrad_batched_shapes(N1, N2, M, nb):
+    """naz_wgrad_batched (the fused maf backward's dW of all layers in one launch, bf16x6): every
+    reduction c[b] += G[b]^T X[b], rowsum[b] += column sums of G[b], into strided workspace views,
+    vs fp64; N2 up to 160 (the maf's 150-wide hidden layers padded) and ragged row counts."""
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(N1 * 7 + N2 + M + nb)
+    a = torch.randn(nb, M, N1, generator=g)
+    b = torch.randn(nb, M, N2, generator=g)
+    ws = torch.zeros(nb, N1 * N2 + N1 + 4, device=DEV)  # padded workspace rows, as flows/maf_grad.py
+    c = ws[:, :N1 * N2].view(nb, N1, N2)
+    rs = ws[:, N1 * N2:N1 * N2 + N1]
+    ops.wgrad_batched(_cuda(a), _cuda(b), c, rs)
+    ops.wgrad_batched(_cuda(a), _cuda(b), c, rs)  # accumulates
+    for k in range(nb):
+        _check(c[k] / 2, a[k].double().t() @ b[k].double(), a[k].t() @ b[k], f"wgrad batch {k} {N1}x{N2} M={M}")
+        _check(rs[k] / 2, a[k].double().sum(0), a[k].sum(0), f"wgrad batch {k} row sums")
+    assert float(ws[:, -4:].abs().max()) == 0.0, "wrote past the reduction"
+
+
 @pytest.mark.parametrize("inverse", [False, True])
 def test_affine_ar_grad(inverse):
     from naz_amd import autograd as ag

@@ -661,7 +661,7 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         training walk forward + backward."""
         mg = _fused_grad()
         if mg is not None:
-            return mg(flat)
+            return mg(flat, x, None if ctx is None else (ctx.reshape(1, -1) if ctx.dim() == 1 else ctx))
         f = _grad_model()
         params = unravel(flat, [spec.param_shapes] * len(plans))
         with torch.no_grad():
@@ -703,8 +703,7 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         mg = grad_flow.get("mafgrad")
         if mg is None:
             from .maf_grad import MafGrad
-            c = None if ctx is None else (ctx.reshape(1, -1) if ctx.dim() == 1 else ctx)
-            mg = grad_flow["mafgrad"] = MafGrad(ar_desc, ar_grad_perm, torch.cat(ar_maskvec), x, c)
+            mg = grad_flow["mafgrad"] = MafGrad(ar_desc, ar_grad_perm, torch.cat(ar_maskvec))
         return mg
 
     def lp_and_grad(params, use_graph: bool = True) -> Tuple[Tensor, Tensor]:

@@ -213,7 +213,38 @@ class _FusedAR:
         return float(m) < self.F16_DATA_LIMIT
 
     def train_ready(self, x, context) -> bool:
-        return False
+        """The maf NLL step on the fused backward (made_ar_bwd.h, flows/maf_grad.py): an affine flow
+        at a compiled shape, rows inside the f16 split's range, no gradient wanted for x or the
+        context (train's data).  NAZ_TRAIN_FUSED=0 keeps the autograd walk."""
+        if self.kind != "maf" or _TRAIN_FUSED == "0" or x.dim() != 2 or x.requires_grad or \
+                (context is not None and context.requires_grad) or not ops.ar_flow_bwd_supported(self.desc):
+            return False
+        return self.log_prob_ready(x, context)
+
+    def maf_grad(self):
+        """MafGrad for the current permutations and masks (rebuilt when one of them changes)."""
+        nets = self._nets()
+        ts = [t for n in nets for l in n.layers for t in (l.mask,)] + [n.permutation for n in nets]
+        sig = tuple((t.data_ptr(), t._version) for t in ts) + (cache_epoch(),)
+        if getattr(self, "_mg", None) is None or self._mg[0] != sig:
+            from .maf_grad import MafGrad
+            mask = torch.cat([t for n in nets for l in n.layers
+                              for t in (l.mask.detach().reshape(-1).float(), torch.ones_like(l.bias.detach()))])
+            perm = np.stack([n.permutation.detach().cpu().numpy() for n in nets]).astype(np.int32)
+            self._mg = (sig, MafGrad(self.desc, perm, mask.contiguous()))
+        return self._mg[1]
+
+    def train_params(self) -> List[torch.Tensor]:
+        return [p for n in self._nets() for l in n.layers for p in (l.weight, l.bias)]
+
+    def train_log_prob(self, x, context=None, bounds=None):
+        """log p(x | ctx) recorded as ONE autograd node whose backward is the fused maf backward."""
+        lj = None
+        if bounds is not None:  # naz bounding_transform: a constant of the parameters here
+            with torch.no_grad():
+                x, lj = ops.bounding_fwd(x.detach(), bounds["low"], bounds["high"])
+        lp = _MafTrainFn.apply(x, context, self, *self.train_params())
+        return lp if lj is None else lp + lj
 
     def packed(self) -> torch.Tensor:
         ps = [p for n in self._nets() for l in n.layers for p in (l.weight, l.bias, l.mask)]
@@ -322,6 +353,35 @@ class _FusedAR:
 _TRAIN_FUSED = __import__("os").environ.get("NAZ_TRAIN_FUSED", "1")
 _AR_FUSED = __import__("os").environ.get("NAZ_AR_FUSED", "1")
 _AR_PASS0 = __import__("os").environ.get("NAZ_AR_PASS0", "1") != "0"  # one-context-vector first-pass folding
+
+
+class _MafTrainFn(torch.autograd.Function):
+    """NormalizingFlow.log_prob of a maf flow under autograd at the fused backward's shapes (naz
+    train's loss, train_flows.py:195, 208): forward = the fused inverse kernel with every layer's
+    output saved; backward = one fused backward launch per layer + batched dW (flows/maf_grad.py)."""
+
+    @staticmethod
+    def forward(ctx, x, context, plan, *params):
+        mg = plan.maf_grad()
+        flat = torch.cat([p.detach().reshape(-1) for p in params])
+        imgs = mg.images(flat)
+        c = None if context is None else (context.detach().reshape(1, -1) if context.dim() == 1 else context.detach())
+        lp, states = mg.forward(imgs, x.detach().float().contiguous(), c)
+        ctx.mg, ctx.imgs, ctx.c = mg, imgs, c
+        ctx.shapes = [p.shape for p in params]
+        ctx.save_for_backward(states.clone())  # the buffer is reused by the next forward of this size
+        return lp.clone()
+
+    @staticmethod
+    def backward(ctx, g_lp):
+        (states,) = ctx.saved_tensors
+        grad, _ = ctx.mg.backward(ctx.imgs, states, ctx.c, g_lp.contiguous().float())
+        outs, o = [], 0
+        for shp in ctx.shapes:
+            n = int(np.prod(shp))
+            outs.append(grad[o:o + n].view(shp))
+            o += n
+        return (None, None, None, *outs)
 
 
 class _CouplingTrainFn(torch.autograd.Function):

@@ -571,8 +571,9 @@ def test_lp_and_grad_fused_full_size_properties(_gpu):
     assert torch.equal(t1, t2)
     assert torch.allclose(g1, g2, rtol=1e-5, atol=1e-6 * float(g1.abs().max()))
     mg = flow["grad_state"]["mafgrad"]
-    lp_rows = mg.lp.clone()
+    lp_rows = mg._buffers(spec["B"])["lp"].clone()
     from naz_amd import ops
+    xd, cd = torch.tensor(x, device="cuda"), torch.tensor(ctx, device="cuda")
     ref = ops.ar_flow_log_prob(mg.desc, ops.ar_flow_pack_batched(mg.desc, p[None], mg.perms, mask=mg.mask)[0],
-                               mg.x, mg.ctx)
+                               xd, cd)
     assert torch.equal(lp_rows, ref), "the training forward must be the log_prob kernel's arithmetic"

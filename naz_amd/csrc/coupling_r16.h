@@ -342,8 +342,15 @@ constexpr bool kTrainFast = true;
 #endif
 NAZ_DEV float acc_fold(float v) { return -0.5f * tanh_f<kTrainFast>(v * kInvSigScale); }
 
+// waves per SIMD: the training forward (VAR = 1) as inference, 4 (128 VGPRs, 12 B of scratch at
+// config 3); NAZ_R16_TRAIN_W2: 2, the round-2 form (A/B)
+#ifdef NAZ_R16_TRAIN_W2
+#define NAZ_R16_TRAIN_WAVES_PER_SIMD_SEL(VAR) ((VAR) == 0 ? 4 : 2)
+#else
+#define NAZ_R16_TRAIN_WAVES_PER_SIMD_SEL(VAR) 4
+#endif
 template <class CF, bool DIR_INV, int VAR = 0>
-__global__ void __launch_bounds__(kR16Rows * 4, VAR == 0 ? 4 : 2) coupling_r16_kernel(
+__global__ void __launch_bounds__(kR16Rows * 4, NAZ_R16_TRAIN_WAVES_PER_SIMD_SEL(VAR)) coupling_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound,

@@ -1412,7 +1412,7 @@ struct CouplingOps {
       if (B == 0) return 0;
       const int64_t ntiles = (B + 16 * kBwdWaves - 1) / (16 * kBwdWaves);
       const int64_t grid = std::min<int64_t>(ntiles, 2048);
-      const size_t lds = (size_t)(2 * BwdSlot<CR>::v + CR::S * (3 * CR::K - 1)) * 4;
+      const size_t lds = (size_t)(2 * BwdSlot<CR>::v + 2 * CR::S * (3 * CR::K - 1)) * 4;  // ring, glow, lowp
       hipLaunchKernelGGL((coupling_bwd_r16_kernel<CR>), dim3((unsigned)grid), dim3(kBwdWaves * 64), lds, s,
                          reinterpret_cast<const float*>(packed), reinterpret_cast<const float*>(bwd), flat, l, state,
                          ctx, ldc, g_in, g_lp, o, B, bound);

@@ -250,11 +250,17 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int q = lane >> 4;
+  // the layer's raw lower-spline parameters, staged once per workgroup into LDS (read by the lower
+  // spline VJP at the end of every tile: as global loads there they queued behind the next
+  // tile's stage-0 LDS-DMA, vmcnt retiring in order)
+  float* const lowp = glow + NLOW;
   for (int i = threadIdx.x; i < NLOW; i += blockDim.x) glow[i] = 0.f;
 
   const float* lp = packed + (int64_t)l * CF::LAYER;
   const float* lb = bwd + (int64_t)l * BW::LAYER;
   const float* low = flat + (int64_t)l * CF::FLAT + CF::N_W0 + CF::N_B0 + CF::N_W1 + CF::N_B1 + CF::N_W2 + CF::N_B2;
+  if constexpr (CF::LOWER)
+    for (int i = threadIdx.x; i < NLOW; i += blockDim.x) lowp[i] = low[i];  // published by the first ring barrier
   const int64_t ntiles = (B + ROWS - 1) / ROWS;
   const RqsConsts<K, true> rc(bound);
   constexpr int NSTG_F = CF::NSTG, NSTG = NSTG_F + BW::NSTG;
@@ -276,7 +282,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
     // GEMM1's context k-slots and the upper dims' incoming gradients, loaded here, before the
     // stage-0 barrier: vmcnt retires in order, so a load issued after a stage's LDS-DMA (as when
     // these sat in stages 0 and C) is waited for together with that DMA
-    float cpre[CF::KS1 * 8], gin[CF::DQ];
+    float cpre[CF::KS1 * 8], gin[CF::DQ], ginl[CF::SQ];
 #pragma unroll
     for (int t = 0; t < CF::KS1; ++t)
 #pragma unroll
@@ -286,6 +292,8 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
       }
 #pragma unroll
     for (int u = 0; u < CF::DQ; ++u) gin[u] = valid ? g_in[crow * D + S + q * CF::DQ + u] : 0.f;
+#pragma unroll
+    for (int u = 0; u < CF::SQ; ++u) ginl[u] = valid ? g_in[crow * D + q * CF::SQ + u] : 0.f;
 
     floatx4 h1[CF::HB], h2[CF::HB], a3[CF::NO];
     float in[CF::KS1 * 8];
@@ -297,9 +305,43 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
     float gy2[CF::DQ];
     const bool has_next = tile + gridDim.x < ntiles;
 
+    // tanh' epilogues of the dH2 / dH1 GEMMs: H re-read from this lane's own stores.  vmcnt
+    // retires in order, so a load issued after a stage's LDS-DMA is waited for together with that
+    // DMA: the epilogue of the last dH2 (dH1) stage therefore runs at the head of the NEXT stage,
+    // after its barrier and before its DMA is issued (NAZ_BWD_EPI_LATE: at the stage's end, r02).
+    auto epi_dh2 = [&]() {
+#pragma unroll
+      for (int b = 0; b < CF::HB; ++b) {
+        // H2 re-read from this lane's own store (frees 32 VGPRs across the dH2 GEMM)
+        const float4 hv = valid ? *reinterpret_cast<const float4*>(o.h2 + row * H + 16 * b + 4 * q)
+                                : float4{0.f, 0.f, 0.f, 0.f};
+        const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dp2[b][r] = (dacc[b][r] * gscale) * (1.f - hh[r] * hh[r]);
+        dacc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    auto epi_dh1 = [&]() {
+#pragma unroll
+      for (int b = 0; b < CF::HB; ++b) {
+        const float4 hv = valid ? *reinterpret_cast<const float4*>(o.h1 + row * H + 16 * b + 4 * q)
+                                : float4{0.f, 0.f, 0.f, 0.f};
+        const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dp2[b][r] = (dacc[b][r] * gscale) * (1.f - hh[r] * hh[r]);  // now dPre1
+      }
+    };
+#ifdef NAZ_BWD_EPI_LATE
+    constexpr bool kEpiEarly = false;
+#else
+    constexpr bool kEpiEarly = true;
+#endif
+
     static_for<0, NSTG>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       ring_barrier();  // stage j has landed in slot (g&1); every wave is done with the other slot
+      if constexpr (kEpiEarly && j == NSTG_F + BW::NB3) epi_dh2();
+      if constexpr (kEpiEarly && j == NSTG_F + BW::NB3 + BW::NB2) epi_dh1();
       const float* cur = (g & 1) ? slot1 : slot0;
       float* nxt = (g & 1) ? slot0 : slot1;
       if constexpr (j + 1 < NSTG_F) {
@@ -463,18 +505,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         } else {
           bwd_gemm_stage<CF::HB, BW::U3, sb * BW::U3>(dacc, cur, lane, a3);
         }
-        if constexpr (sb == BW::NB3 - 1) {
-#pragma unroll
-          for (int b = 0; b < CF::HB; ++b) {
-            // H2 re-read from this lane's own store (frees 32 VGPRs across the dH2 GEMM)
-            const float4 hv = valid ? *reinterpret_cast<const float4*>(o.h2 + row * H + 16 * b + 4 * q)
-                                    : float4{0.f, 0.f, 0.f, 0.f};
-            const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dp2[b][r] = (dacc[b][r] * gscale) * (1.f - hh[r] * hh[r]);
-            dacc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
+        if constexpr (!kEpiEarly && sb == BW::NB3 - 1) epi_dh2();
       } else if constexpr (j < NSTG_F + BW::NB3 + BW::NB2) {
         // ---- dH1 = dPre2 · W1
         constexpr int sb = j - NSTG_F - BW::NB3;
@@ -487,16 +518,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         }
         if constexpr (kBwdF16) gemm_r16_lazy<CF::HB, BW::KB2, sb * BW::KB2, false>(dacc, cur, lane, dp2);
         else bwd_gemm_stage<CF::HB, BW::U2, sb * BW::U2>(dacc, cur, lane, dp2);
-        if constexpr (sb == BW::NB2 - 1) {
-#pragma unroll
-          for (int b = 0; b < CF::HB; ++b) {
-            const float4 hv = valid ? *reinterpret_cast<const float4*>(o.h1 + row * H + 16 * b + 4 * q)
-                                    : float4{0.f, 0.f, 0.f, 0.f};
-            const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dp2[b][r] = (dacc[b][r] * gscale) * (1.f - hh[r] * hh[r]);  // now dPre1
-          }
-        }
+        if constexpr (!kEpiEarly && sb == BW::NB2 - 1) epi_dh1();
       } else {
         // ---- dx1 = dPre1 · W0[:, C:], lower spline VJP, g(P[l + 1])
         if (valid)
@@ -518,17 +540,21 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         for (int u = 0; u < CF::SQ; ++u) {
           __builtin_amdgcn_sched_barrier(0);  // one dim's VJP at a time (its temporaries are large)
           const int dim = q * CF::SQ + u;
+#ifdef NAZ_BWD_LATE_LOADS
           const float go = (valid ? g_in[crow * D + dim] : 0.f) + dx1[u];
+#else
+          const float go = ginl[u] + dx1[u];
+#endif
           gy1[u] = go;
           if constexpr (CF::LOWER) {
             float uw[K], uh[K], ud[K - 1], gw[K], gh[K], gd[K - 1];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-              uw[k] = low[dim * K + k];
-              uh[k] = low[S * K + dim * K + k];
+              uw[k] = lowp[dim * K + k];
+              uh[k] = lowp[S * K + dim * K + k];
             }
 #pragma unroll
-            for (int k = 0; k < K - 1; ++k) ud[k] = low[2 * S * K + dim * (K - 1) + k];
+            for (int k = 0; k < K - 1; ++k) ud[k] = lowp[2 * S * K + dim * (K - 1) + k];
             gy1[u] = train_vjp_inv<K>(uw, uh, ud, bound, y1[u], go, gl, rc, gw, gh, gd);
             // sum over the wave's 16 rows (lanes of this quarter), then one LDS add per value
             auto red = [&](float v) {

@@ -45,6 +45,31 @@ def test_host_side_errors_have_messages():
     assert rc != 0 and b"no fused instantiation" in L.naz_last_error()
 
 
+def test_maf_backward_and_batched_wgrad_host_errors():
+    """The fused maf backward's and the batched dW reduction's host-side checks (no GPU: every
+    call below fails before a launch)."""
+    import ctypes
+    from naz_amd import _lib, ops
+    L = _lib.lib()
+    d = ops.ar_flow_desc("maf", 2, 2, 150, 4, 3)
+    rc = L.naz_ar_flow_bwd_layer(d, None, None, None, 0, None, None, 0, None, None, None, None, 128, None)
+    assert rc != 0 and b"null pointer" in L.naz_last_error()
+    bufs = (ctypes.c_void_p * 11)(*([16] * 11))
+    rc = L.naz_ar_flow_bwd_layer(d, 16, 16, 16, 4, 16, 16, 0, 16, None, bufs, 16, 128, None)  # layer == L
+    assert rc != 0 and b"layer out of range" in L.naz_last_error()
+    bad = ops.ar_flow_desc("maf", 16, 32, 128, 4, 2)
+    rc = L.naz_ar_flow_bwd_layer(bad, 16, 16, 16, 0, 16, 16, 0, 16, None, bufs, 16, 128, None)
+    assert rc != 0 and b"no fused backward" in L.naz_last_error()
+    rc = L.naz_ar_flow_log_prob_train(bad, 16, 16, 2, 16, 2, 16, 16, 128, None)
+    assert rc != 0 and b"no fused backward" in L.naz_last_error()
+    # batched dW: widths beyond the bf16x6 instances, misaligned rows
+    rc = L.naz_wgrad_batched(1024, 160, 168, 2, 16, 160, 1 << 20, 16, 168, 1 << 20, 16, 168, 0, None, 0, None)
+    assert rc != 0 and b"naz_wgrad_batched" in L.naz_last_error()
+    rc = L.naz_wgrad_batched(1024, 160, 160, 2, 16, 161, 1 << 20, 16, 160, 1 << 20, 16, 160, 0, None, 0, None)
+    assert rc != 0 and b"contiguous" in L.naz_last_error()
+    assert L.naz_wgrad_batched(0, 160, 160, 2, 16, 160, 0, 16, 160, 0, 16, 160, 0, None, 0, None) == 0  # no rows
+
+
 def test_fused_descriptor_matches_flow_parameters():
     from naz_amd import ops
     from naz_amd.flows import NormalizingFlow

@@ -294,13 +294,20 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
           f.h = __builtin_bit_cast(half8, Hh);
           f.l = __builtin_bit_cast(half8, Lo);
         } else {
-          constexpr int d = u - NHID * HB;
+          // dims 4 g + qq: quarter qq's registers 0, 1 hold that dim's (mean, log_scale) (the
+          // forward image's dim groups); every lane takes all of the group's
+          constexpr int g = u - NHID * HB;
+          static_assert(FW::NOG == 1, "affine: one output block per dim group");
           const float4 bv = reinterpret_cast<const float4*>(cur + OFF + KSH * CB::OT)[q];
           floatx4 o3 = floatx4{bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
           for (int t = 0; t < KSH; ++t) o3 = mfma3_16(afrag(t), hf[(NHID - 1) & 1][t], o3);
-          mu[d] = __shfl(o3[0], lane & 15);
-          la[d] = __shfl(o3[1], lane & 15);
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq)
+            if (4 * g + qq < D) {
+              mu[4 * g + qq < D ? 4 * g + qq : 0] = __shfl(o3[0], (lane & 15) + 16 * qq);
+              la[4 * g + qq < D ? 4 * g + qq : 0] = __shfl(o3[1], (lane & 15) + 16 * qq);
+            }
         }
       });
     }

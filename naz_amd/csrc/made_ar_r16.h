@@ -516,13 +516,17 @@ struct CfgARW {
 template <class G>
 struct CfgARF {
   static constexpr int D = G::D, C = G::C, H = G::H, K = G::K, NHID = G::NHID, P = G::P;
-  static constexpr int HB = G::HB, KSH = G::KSH, KC = G::KC, KI = G::KI, NOB = G::NOB, OT = G::OT;
+  static constexpr int HB = G::HB, KSH = G::KSH, KC = G::KC, KI = G::KI, OT = G::OT;
+  // output units: dims in groups of four, one per row quarter — output row 4 q + i of block o is
+  // parameter 4 o + i of dim 4 g + q, so every lane receives ITS dim's parameters in its own
+  // accumulator registers and runs one dim's map (no gather, no 4x redundant spline)
+  static constexpr int NG = (D + 3) / 4, NOG = (P + 3) / 4;
   // the forward spline's live set at D = 16 exceeds the 168 VGPRs of 12-wave workgroups (spilled
   // 352-468 B/lane): 8 waves (2 per SIMD) there
   static constexpr int NW = (G::AFFINE || D <= 8) ? G::NW : 8;
   static constexpr bool AFFINE = G::AFFINE;
-  static constexpr int NU = NHID * HB + D;  // units: hidden (i, b) row-major, then one per dim
-  static constexpr int unit_blocks(int u) { return u < NHID * HB ? 1 : NOB; }
+  static constexpr int NU = NHID * HB + NG;  // units: hidden (i, b) row-major, then one per dim group
+  static constexpr int unit_blocks(int u) { return u < NHID * HB ? 1 : NOG; }
   static constexpr int unit_kts(int u) { return u < HB ? KI : KSH; }
   static constexpr int unit_floats(int u) { return unit_blocks(u) * (unit_kts(u) * OT + 16); }
   struct Layout {
@@ -605,15 +609,19 @@ static void made_ar_pack_fwd_layer(const float* flat, float* out) {
       float* bias = out + base + kts * CF::OT;
       for (int r = 0; r < 16; ++r) bias[r] = 16 * b + r < H ? kSigScale * bl[i][16 * b + r] : 0.f;
     } else {
-      const int d = u - CF::NHID * HB;
-      for (int o = 0; o < CF::NOB; ++o)
+      const int g = u - CF::NHID * HB;  // dims 4 g + q, quarter q: row 4 q + i = parameter 4 o + i
+      for (int o = 0; o < CF::NOG; ++o)
         for (int t = 0; t < KSH; ++t)
           frag(st + (o * KSH + t) * CF::OT, [&](int m, int kg, int j) -> float {
-            const int pi = 16 * o + m, v = r16_feat(t, kg, j);
-            return (pi < P && v < H) ? -2.f * Wl[CF::NHID][(pi * D + d) * H + v] : 0.f;
+            const int d = 4 * g + (m >> 2), pi = 4 * o + (m & 3), v = r16_feat(t, kg, j);
+            return (d < D && pi < P && v < H) ? -2.f * Wl[CF::NHID][(pi * D + d) * H + v] : 0.f;
           });
-      float* bias = out + base + CF::NOB * KSH * CF::OT;
-      for (int r = 0; r < 16 * CF::NOB; ++r) bias[r] = r < P ? bl[CF::NHID][r * D + d] : 0.f;
+      float* bias = out + base + CF::NOG * KSH * CF::OT;
+      for (int o = 0; o < CF::NOG; ++o)
+        for (int m = 0; m < 16; ++m) {
+          const int d = 4 * g + (m >> 2), pi = 4 * o + (m & 3);
+          bias[16 * o + m] = (d < D && pi < P) ? bl[CF::NHID][pi * D + d] : 0.f;
+        }
     }
   }
 }
@@ -677,8 +685,9 @@ __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t 
         constexpr int i = u / HB, b = u % HB;
         if (16 * b + r < H) v = kSigScale * bl(i)[16 * b + r];
       } else {
-        constexpr int d = u - NHID * HB;
-        if (r < P) v = bl(NHID)[r * D + d];
+        constexpr int g = u - NHID * HB;
+        const int d = 4 * g + ((r & 15) >> 2), pi = 4 * (r >> 4) + (r & 3);
+        if (d < D && pi < P) v = bl(NHID)[pi * D + d];
       }
       word = __builtin_bit_cast(unsigned, v);
       return;
@@ -707,10 +716,10 @@ __global__ void made_ar_pack_fwd_kernel(const float* __restrict__ flat, int64_t 
           }
         }
       } else {
-        constexpr int d = u - NHID * HB;
+        constexpr int g = u - NHID * HB;
         const int o = fr / KSH, t = fr % KSH;
-        const int pi = 16 * o + m, vv = r16_feat(t, kg, j);
-        if (pi < P && vv < H) v = -2.f * wv(NHID, ((int64_t)pi * D + d) * H + vv);
+        const int d = 4 * g + (m >> 2), pi = 4 * o + (m & 3), vv = r16_feat(t, kg, j);
+        if (d < D && pi < P && vv < H) v = -2.f * wv(NHID, ((int64_t)pi * D + d) * H + vv);
       }
       word |= ar_piece_dev(v, piece) << (16 * e);
     }
@@ -929,39 +938,49 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
         }
         ar_split4<b & 1>(hf[i & 1][b >> 1], acc);
       } else {
-        constexpr int d = u - NHID * HB;
-        floatx4 o3[CF::NOB];
-        const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF + CF::NOB * KSH * CF::OT);
+        // dims 4 g .. 4 g + 3: quarter q's lanes map dim 4 g + q with its parameters in their own
+        // accumulator registers (register i of block o = parameter 4 o + i), then every lane
+        // takes the group's new values from the owning quarters (four shuffles)
+        constexpr int g = u - NHID * HB, NOG = CF::NOG;
+        floatx4 o3[NOG];
+        const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF + NOG * KSH * CF::OT);
 #pragma unroll
-        for (int o = 0; o < CF::NOB; ++o) {
+        for (int o = 0; o < NOG; ++o) {
           const float4 bv = bias4[4 * o + q];
           o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
         }
 #pragma unroll
         for (int t = 0; t < KSH; ++t)
 #pragma unroll
-          for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KSH + t), hf[(NHID - 1) & 1][t], o3[o]);
+          for (int o = 0; o < NOG; ++o) o3[o] = mfma3_16(afrag(o * KSH + t), hf[(NHID - 1) & 1][t], o3[o]);
+        float xv = 0.f;  // this quarter's dim
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          if (4 * g + qq < D) xv = q == qq ? v[4 * g + qq < D ? 4 * g + qq : 0] : xv;
+        const bool own = 4 * g + q < D;
+        float yv, ld;
         if constexpr (CF::AFFINE) {
           // pyro AffineAutoregressive._call: y = exp(clamp(ls)) x + mean, log|det| = clamp(ls)
-          const float mean = __shfl(o3[0][0], lane & 15);
-          const float ls = fminf(fmaxf(__shfl(o3[0][1], lane & 15), -5.f), 3.f);
-          v[d] = __builtin_fmaf(v[d], __expf(ls), mean);
-          ldsum += ls;
+          const float ls = fminf(fmaxf(o3[0][1], -5.f), 3.f);
+          yv = __builtin_fmaf(xv, __expf(ls), o3[0][0]);
+          ld = ls;
         } else {
           float uw[K], uh[K], ud[K - 1];
 #pragma unroll
           for (int pi = 0; pi < P; ++pi) {
-            const float val = __shfl(o3[pi >> 4][pi & 3], (lane & 15) + 16 * ((pi & 15) >> 2));
+            const float val = o3[pi >> 2][pi & 3];
             if (pi < K) uw[pi] = val;
             else if (pi < 2 * K) uh[pi - K] = val;
             else ud[pi - 2 * K] = val;
           }
-          float ld;
-          v[d] = rqs_select<K, false>(uw, uh, ud, v[d], bound, rc, ld);
-          ldsum += ld;
+          yv = rqs_select<K, false>(uw, uh, ud, xv, bound, rc, ld);
         }
-        // the dims are independent: unpinned, the scheduler hoists later dims' output MFMAs over
-        // this dim's spline and their accumulators spill (460 B/lane at D = 16)
+        ldsum += own ? ld : 0.f;  // summed over the quarters at the end
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          if (4 * g + qq < D) v[4 * g + qq < D ? 4 * g + qq : 0] = __shfl(yv, (lane & 15) + 16 * qq);
+        // the groups are independent: unpinned, the scheduler hoists later groups' output MFMAs
+        // over this group's map and their accumulators spill
         __builtin_amdgcn_sched_barrier(0);
       }
     });
@@ -970,6 +989,8 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
 #pragma unroll
     for (int d = 0; d < D; ++d) v[d] = (1.f / (1.f + expf(-v[d]))) * (high[d] - low[d]) + low[d];
   }
+  ldsum += __shfl_xor(ldsum, 16);  // each quarter summed its own dims' log-dets
+  ldsum += __shfl_xor(ldsum, 32);
   if (q == 0 && valid) {
 #pragma unroll
     for (int d = 0; d < D; ++d) y[row * ldy + d] = v[d];

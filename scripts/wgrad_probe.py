@@ -1,5 +1,6 @@
 """Probe: the NLL step's weight-gradient GEMMs (dW = dPre^T X over 2^20 rows) — naz_gemm
 (wgrad_flat) vs torch.mm (rocBLAS / hipBLASLt) for reference."""
+import os
 import sys
 from pathlib import Path
 
@@ -10,12 +11,19 @@ from naz_amd import ops  # noqa: E402
 
 B = 1 << 20
 dev = "cuda"
-for (n1, n2) in [(192, 128), (128, 128), (128, 40)]:
+SHAPES = [(192, 128), (128, 128), (128, 40)]
+if os.environ.get("WG_SHAPES"):  # e.g. "192x128,128x40"
+    SHAPES = [tuple(int(v) for v in t.split("x")) for t in os.environ["WG_SHAPES"].split(",")]
+MM = os.environ.get("WG_TORCH", "1") != "0"
+for (n1, n2) in SHAPES:
     g = torch.randn(B, n1, device=dev)
     x = torch.randn(B, n2, device=dev)
     out = torch.empty(n1, n2, device=dev)
     rs = torch.empty(n1, device=dev)
-    for name, fn in [("naz_gemm", lambda: ops.gemm(g.t(), x, out=out, rowsum=rs)), ("torch.mm", lambda: torch.mm(g.t(), x))]:
+    fns = [("naz_gemm", lambda: ops.gemm(g.t(), x, out=out, rowsum=rs))]
+    if MM:
+        fns.append(("torch.mm", lambda: torch.mm(g.t(), x)))
+    for name, fn in fns:
         for _ in range(3):
             fn()
         torch.cuda.synchronize()

@@ -185,10 +185,14 @@ def test_gemm_strided_split_k(M, N, K, split):
 
 
 @pytest.mark.parametrize("N1,N2,M", [(192, 128, 70001), (128, 128, 4096), (128, 40, 33333), (184, 128, 517),
-                                     (60, 20, 1000), (256, 96, 20000), (100, 52, 16), (4, 4, 9), (128, 8, 1 << 18)])
+                                     (60, 20, 1000), (256, 96, 20000), (100, 52, 16), (4, 4, 9), (128, 8, 1 << 18),
+                                     # the deep-ring (3-4 slot) instances: fewer chunks than slots,
+                                     # a ragged last chunk, one or two chunks per workgroup, full size
+                                     (192, 128, 32), (192, 128, 95), (128, 128, 33), (128, 128, 200),
+                                     (128, 40, 100), (160, 8, 64), (192, 128, (1 << 20) + 77)])
 def test_wgrad_t16_shapes(N1, N2, M):
-    """dW = G^T X (+ column sums of G) on contiguous row-major operands: the 16x16x4 LDS-ring kernel
-    (unmasked padding blocks, one-step-ahead prefetch, partial tail chunk) vs fp64."""
+    """dW = G^T X (+ column sums of G) on contiguous row-major operands: the LDS-ring reductions
+    (bf16x6 with two- or deep rings, fp32 16x16x4; unmasked padding blocks, partial tail chunk) vs fp64."""
     from naz_amd import ops
     g = torch.Generator().manual_seed(N1 * 131 + N2 + M)
     a = torch.randn(M, N1, generator=g)

@@ -357,6 +357,9 @@ struct WGradArgs {
   int blk0;        // first output block (of NB1 x NB2, n2-fastest) this launch owns
   // batched reductions (wgrad_x6 only, blockIdx.y = batch b): g, x, c, rowsum advance by b times these
   int64_t bg, bx, bc, br;
+  // wgrad_x6 only: > 0 = workgroup w takes the R-row chunks starting at w R, w R + chunk_stride, ...
+  // (interleaved over the grid) instead of the contiguous rows_per_wg block
+  int64_t chunk_stride;
 };
 
 // one workgroup: rows [mb, me) of G and X -> its share of every output block, added atomically
@@ -816,8 +819,13 @@ __global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_x6_kernel(WGradArgs p,
     p.c += bz * p.bc;
     if (p.rowsum != nullptr) p.rowsum += bz * p.br;
   }
-  const int64_t mb = (int64_t)blockIdx.x * p.rows_per_wg;
-  const int64_t me = (mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M;
+  // rows: the contiguous block [mb, me) in steps of R, or (chunk_stride > 0) the chunks mb, mb +
+  // chunk_stride, ... of all M rows: the grid's concurrently streamed chunks then lie side by side
+  // in HBM instead of rows_per_wg apart
+  const bool il = p.chunk_stride > 0;
+  const int64_t mb = (int64_t)blockIdx.x * (il ? R : p.rows_per_wg);
+  const int64_t me = il ? p.M : ((mb + p.rows_per_wg) < p.M ? (mb + p.rows_per_wg) : p.M);
+  const int64_t step = il ? p.chunk_stride : R;
   floatx4w acc[NOW][NBW];
 #pragma unroll
   for (int i = 0; i < NOW; ++i)
@@ -862,11 +870,11 @@ __global__ void __launch_bounds__(256 * JS, 2 / JS) wgrad_x6_kernel(WGradArgs p,
   };
   int slot = 0;
   if (mb < me) fill(mb, tl);
-  for (int64_t m0 = mb; m0 < me; m0 += R, slot ^= 1) {
+  for (int64_t m0 = mb; m0 < me; m0 += step, slot ^= 1) {
     ring_barrier();  // chunk m0 has landed; every wave is done with the other slot
     const float* const Gs = tl + slot * CH;
     const float* const Xs = Gs + R * N1;
-    if (m0 + R < me) fill(m0 + R, tl + (slot ^ 1) * CH);
+    if (m0 + step < me) fill(m0 + step, tl + (slot ^ 1) * CH);
     // lane (m, kq) of a 32-row step reads rows 8 kq .. 8 kq + 7; past-the-end blocks read LDS
     // slack / neighbours and only feed dropped accumulator rows or columns (as wgrad_t16)
     const float* pa = Gs + (8 * kq) * N1 + wave * 16 + m;
@@ -948,6 +956,14 @@ static bool wgrad_x6_launch(int nb2, const WGradArgs& q, int R, size_t lds, dim3
   }
 }
 
+static bool wgrad_x6_interleave() {
+  static const bool on = [] {
+    const char* e = getenv("NAZ_WGRAD_INTERLEAVE");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 // wgrad on the bf16x6 kernel for the shapes wgrad_t16 takes (R a multiple of 32 here), plus
 // N2 <= 160 (the maf's 150-wide layers); nbatch independent reductions (blockIdx.y)
 static bool wgrad_x6(WGradArgs p, hipStream_t s, int nbatch = 1) {
@@ -978,6 +994,7 @@ static bool wgrad_x6(WGradArgs p, hipStream_t s, int nbatch = 1) {
   if (rpw < 4 * R) rpw = 4 * R;
   p.rows_per_wg = rpw;
   const dim3 grid((unsigned)((p.M + rpw - 1) / rpw), (unsigned)nbatch);
+  p.chunk_stride = wgrad_x6_interleave() ? (int64_t)grid.x * R : 0;
   switch (now) {
     case 1: return wgrad_x6_launch<1>(nb2, p, R, lds, grid, s, js2);
     case 2: return wgrad_x6_launch<2>(nb2, p, R, lds, grid, s, js2);

@@ -486,10 +486,10 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
 // per layer over the layer input, then every dim's map — y_d = spline(x_d) or x_d exp(ls_d) + m_d —
 // all of a layer's dims from the same hidden activations (no sequential dependence: the masks
 // already encode the order).  The whole flow is one launch: per layer, all hidden blocks (f16x3
-// MFMA, register-resident B fragments, the inverse kernel's machinery), then per dim its output
-// rows and the elementwise map.  Weights: per layer "units" — (hidden layer i, 16-unit block b)
-// with its k-steps and bias, then (dim d) with its output blocks — grouped greedily into LDS-ring
-// stages of <= kARCap floats.  Forward values can grow through the layers (affine scales up to
+// MFMA, register-resident B fragments, the inverse kernel's machinery), then per group of four
+// dims their output rows and the elementwise maps (one dim per row quarter).  Weights: per layer
+// "units" — (hidden layer i, 16-unit block b) with its k-steps and bias, then (dim group g) with
+// its output blocks — grouped greedily into LDS-ring stages of <= kARCap floats.  Forward values can grow through the layers (affine scales up to
 // e^3 per layer), so the layer input is split into f16 pieces at a per-row power-of-two scale and
 // the x part of hidden layer 1 rescaled in fp32 (the context keeps the caller's |ctx| < 2^15).
 // Wide affine MADE (naz's production MAFs: the 4-parameter MLE flow D=4 | C=2, H=[512]x5, L=18,

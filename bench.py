@@ -210,14 +210,19 @@ def parity_record(gpu, ref64, ref32) -> dict:
     return rec
 
 
-def load_traffic(mode: str):
+def load_traffic(mode: str, rows: int = None):
     """HBM bytes per launch measured with rocprofv3 PMC passes for this kernel variant
-    (profiles/traffic_config3_<mode>.json, written by scripts/pmc_summary.py), if present."""
+    (profiles/traffic_config3_<mode>.json, written by scripts/pmc_summary.py /
+    scripts/pmc_step_traffic.py), if present.  A file that records the rows it was measured on
+    (``rows_per_launch``) is scaled linearly to ``rows`` (the traffic of a step is per row)."""
     p = ROOT / "profiles" / f"traffic_config3_{mode}.json"
     if p.exists():
         try:
             d = json.loads(p.read_text())
-            return d.get("hbm_bytes_per_launch"), str(p.relative_to(ROOT))
+            v = d.get("hbm_bytes_per_launch")
+            if v is not None and rows is not None and d.get("rows_per_launch"):
+                v = v * rows / d["rows_per_launch"]
+            return v, str(p.relative_to(ROOT))
         except Exception:
             pass
     return None, None
@@ -270,12 +275,18 @@ def run_train(args, dev, rank, world, dist):
         step_s = elapsed / args.steps
         flop = 3 * flops_per_row() * B  # per rank: fwd GEMMs + dX + dW
         achieved = flop / step_s / 1e12
-        traffic, traffic_src = load_traffic("train")
-        # ceiling of the fused step's arithmetic: forward and dX GEMMs on the f16x3 split pipe
-        # (2.5 PF / 3 products), dW on exact FP32 MFMA; equal FLOPs in each third
-        peak = 3.0 / (2.0 * 3 / BF16_PEAK_TFLOPS + 1.0 / FP32_PEAK_TFLOPS)
+        traffic, traffic_src = load_traffic("train", rows=B)
+        # ceiling of the fused step's arithmetic, each third of the FLOPs on the pipe it runs on:
+        # forward and dX GEMMs on the f16x3 split (2.5 PF / 3 products = 833 TF), dW on the bf16x6
+        # split (wgrad_x6: 2.5 PF / 6 = 417 TF; NAZ_WGRAD_X6=0: exact FP32 MFMA) -> 625 TF
+        dw_peak = FP32_PEAK_TFLOPS if os.environ.get("NAZ_WGRAD_X6", "1") == "0" else BF16_PEAK_TFLOPS / X6_PRODUCTS
+        dx_peak = FP32_PEAK_TFLOPS if os.environ.get("NAZ_BWD_EXACT_F32") else BF16_PEAK_TFLOPS / 3
+        peak = 3.0 / (3.0 / BF16_PEAK_TFLOPS + 1.0 / dx_peak + 1.0 / dw_peak)
+        peak_note = (f"harmonic FLOP-weighted ceiling: fwd on the f16x3 split ({BF16_PEAK_TFLOPS / 3:.0f} TF), "
+                     f"dX at {dx_peak:.0f} TF, dW at {dw_peak:.0f} TF (equal FLOPs in each third)")
         if args.train_walk:
             peak = FP32_PEAK_TFLOPS
+            peak_note = "exact FP32 MFMA peak (the per-node walk's GEMMs)"
         rec = {
             "metric": "samples/sec through the NLL training step (log_prob fwd + backward + grad all-reduce + "
                       "clip + Adam), 16-dim RQ-spline flow",
@@ -288,7 +299,7 @@ def run_train(args, dev, rank, world, dist):
                        "parallelism": f"dp{world} (RCCL all-reduce, one flat bucket)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
-                         "peak_note": "fwd + dX on the f16x3 split pipe (833 TF), dW on FP32 MFMA (157.3 TF)",
+                         "peak_note": peak_note,
                          "kernel": "whole step", "flop_per_row": 3 * flops_per_row()},
             "final_loss": float(loss),
         }
@@ -757,6 +768,10 @@ BAYES_SHAPES = {
     # the 4-parameter MLE MAF (train_mle_all_data_4param.py:87-92) whose posterior-predictive loop
     # draws 800k samples per posterior draw (calibrate_4p.py:130-136)
     "maf4": dict(D=4, C=2, hidden=[512] * 5, L=18),
+    # the 4-parameter BAYESIAN MAF: calibrate_4p.py:75,90-96 builds make_conditional_autoregressive_nn(
+    # 4, 2, [150, 150, 150]) over 16 layers; its NUTS potential (hmc_maf_exact.py:101-133) and
+    # posterior-predictive loop (calibrate_4p.py:129-135) run at this shape
+    "4p150": dict(D=4, C=2, hidden=[150] * 3, L=16),
 }
 BAYES = BAYES_SHAPES["paper"]
 
@@ -837,7 +852,7 @@ def run_bayes(args, dev, rank, world, dist):
     if lp_mode:
         fl_ref = D * full  # the reference's D full MADE passes per layer
         fl_row = flow["lp_flops_per_row"]()  # executed: context-only units folded into per-draw biases
-    elif grad_mode:  # forward D passes + backward (2x the GEMM work of the forward)
+    elif grad_mode:  # the reference's work: forward D passes + backward (2x the GEMM work of the forward)
         fl_ref = fl_row = 3 * D * full
     else:
         fl_ref = fl_row = full
@@ -857,7 +872,7 @@ def run_bayes(args, dev, rank, world, dist):
         "config": {"workload": f"SURVEY.md §8f rank {2 if args.bayes == 'sample' else 1}: naz JAX-MAF front end "
                                f"({ {'lp': 'lp', 'grad': 'NUTS potential + gradient', 'sample': 'sampler'}[args.bayes] })"
                                f" at D={D}, C={C}, H={BAYES['hidden']}, L={BAYES['L']} "
-                               f"({'the 2506.05657 paper shape' if args.bayes_shape == 'paper' else 'the 4-parameter MLE MAF'})"
+                               f"({ {'paper': 'the 2506.05657 paper shape', 'maf4': 'the 4-parameter MLE MAF', '4p150': 'the 4-parameter Bayesian MAF, calibrate_4p.py:75'}[args.bayes_shape] })"
                                f"; {P} draws x {B} rows per step (pack included)",
                    "draws": P, "rows_per_draw": B, "parallelism": f"dp{world} (independent draw sets, no collective)"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -865,9 +880,24 @@ def run_bayes(args, dev, rank, world, dist):
                      "flop_per_row": fl_row, "reference_flop_per_row": fl_ref},
     }
     if grad_mode and flow["grad_fused"]:  # maf_grad.py: fused inverse + per-layer fused backward + dW GEMMs
-        rec["roofline"].update(path="fused maf backward (f16x3 MADE passes and chains, bf16x6 dW reductions)",
-                               peak_note="FP32 MFMA peak on the reference's FLOPs (D-pass forward + 2x backward); "
-                                         f"vs the 833 TF split f16x3 ceiling: {achieved / (BF16_PEAK_TFLOPS / 3):.3f}")
+        # the FLOPs the kernels EXECUTE, each against the pipe it runs on: inverse + backward on
+        # the f16x3 split (833 TF; the backward's W_out^T g is fp32 VALU, counted there too), the
+        # dW reductions on bf16x6 (417 TF); harmonic FLOP-weighted ceiling
+        from naz_amd import ops as _ops
+        ex = _ops.ar_executed_flop_per_row(flow["grad_state"]["mafgrad"].desc)
+        f_split, f_dw = ex["inverse"] + ex["bwd"], ex["dw"]
+        fl_row = f_split + f_dw
+        achieved = fl_row * P * B / step_s / 1e12
+        peak = fl_row / (f_split / (BF16_PEAK_TFLOPS / 3) + f_dw / (BF16_PEAK_TFLOPS / X6_PRODUCTS))
+        rec["roofline"].update(achieved=achieved, peak=peak, frac=achieved / peak, flop_per_row=fl_row,
+                               executed_flop_per_row={"inverse": ex["inverse"], "bwd": ex["bwd"], "dw": ex["dw"]},
+                               reference_flop_per_row=fl_ref,
+                               reference_tflops=fl_ref * P * B / step_s / 1e12,
+                               path="fused maf backward (f16x3 MADE passes and chains, bf16x6 dW reductions)",
+                               peak_note=f"executed FLOPs: inverse + backward on the f16x3 split ({BF16_PEAK_TFLOPS / 3:.0f} "
+                                         f"TF), dW on bf16x6 ({BF16_PEAK_TFLOPS / X6_PRODUCTS:.0f} TF), FLOP-weighted; "
+                                         "reference_flop_per_row = the reference's D-pass forward + 2x backward (not "
+                                         "executed here)")
     if lp_mode and flow["lp_fused_ar"]:  # the whole flow per draw in one naz_ar_flow_log_prob_batched launch
         peak = BF16_PEAK_TFLOPS / 3
         rec["roofline"].update(peak=peak, frac=achieved / peak, peak_note="split f16x3 ceiling (2.5 PF / 3 products)")

@@ -52,7 +52,8 @@ extern "C" {
 
 /* ---- library ------------------------------------------------------------ */
 const char* naz_last_error(void);
-int naz_abi_version(void); /* bumps on any signature change */
+int naz_abi_version(void); /* bumps on any signature or contract change (2: naz_ar_desc.flags, affine clip modes,
+                             * naz_ar_flow_supported = 2 for forward-only shapes) */
 /* Diagnostics (no reference counterpart): the first non-finite row state a fused log_prob
  * kernel met, as {1, workgroup, layer, stage counter, row} ({0, ...} = none), optionally
  * cleared.  Fails unless the library was built with -DNAZ_DEBUG_NONFINITE.               */
@@ -185,8 +186,11 @@ int naz_wgrad_batched(int64_t M, int N1, int N2, int nbatch, const float* g, int
 /* VJP of naz_affine_ar (the kernel reports the FORWARD log-det sum(clamp(ls)) in both
  * directions).  x = the map's input, y = its output, g_ld [B] = dL/d(row ld) (may be NULL).
  * pyro clamps log_scale with clamp_preserve_gradients: the clamp passes gradients through.
+ * `mode`: bit 0 = inverse direction; bit 1 (NAZ_AFFINE_CLIP_ZERO_GRAD) = differentiate the clamp
+ * as jnp.clip instead (zero gradient outside [-5, 3]; the JAX Bayesian MAF, bflow_jax_maf.py:177-192).
  * Writes g_x [B, D] (may be NULL) and g_raw [B, 2D].                                       */
-int naz_affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y,
+#define NAZ_AFFINE_CLIP_ZERO_GRAD 2
+int naz_affine_ar_bwd(int mode, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y,
                       int64_t ldy, const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx,
                       float* g_raw, int64_t ldgr, int64_t B, int D, void* stream);
 /* out[n] += sum_m A[m*lda + n]  (atomic; zero `out` first for a plain column sum)         */
@@ -352,8 +356,14 @@ typedef struct naz_ar_desc {
   float bound;       /* spline box half-width (spline only) */
   int n_hidden;      /* hidden layers, all of width H */
   int kind;          /* NAZ_AR_SPLINE | NAZ_AR_AFFINE */
-  int reserved[6];
+  int flags;         /* NAZ_AR_CLIP_ZERO_GRAD (affine backward only); 0 = pyro semantics */
+  int reserved[5];
 } naz_ar_desc;
+/* flags: the affine backward (naz_ar_flow_bwd_layer) differentiates the log_scale clip to [-5, 3]
+ * as jnp.clip (zero gradient outside the range: the reference's JAX Bayesian MAF,
+ * bflow_jax_maf.py:177,188,192, whose potential NUTS differentiates) instead of pyro's
+ * clamp_preserve_gradients (identity gradient: naz's torch maf, transforms.py:133-160). */
+#define NAZ_AR_CLIP_ZERO_GRAD 1
 /* 1: both directions fused (log_prob + sample); 2: the forward (sample) direction only — the
  * wide production MAFs (D=4 | C=2, H=[512]x5), whose log_prob keeps the per-layer path and whose
  * inverse-direction entry points (packed_bytes, pack_host, pack, log_prob*) report the shape as

@@ -28,7 +28,8 @@ class CouplingDesc(C.Structure):
 
 class ArDesc(C.Structure):
     _fields_ = [("D", C.c_int), ("C", C.c_int), ("H", C.c_int), ("K", C.c_int), ("L", C.c_int), ("act", C.c_int),
-                ("bound", C.c_float), ("n_hidden", C.c_int), ("kind", C.c_int), ("reserved", C.c_int * 6)]
+                ("bound", C.c_float), ("n_hidden", C.c_int), ("kind", C.c_int), ("flags", C.c_int),
+                ("reserved", C.c_int * 5)]
 
 
 class CnfDesc(C.Structure):

@@ -231,9 +231,9 @@ class AffineARFn(Function):
     """(y, forward ld_row) of pyro's AffineAutoregressive step over MADE output ``raw``."""
 
     @staticmethod
-    def forward(ctx, x, raw, inverse: bool):
+    def forward(ctx, x, raw, inverse: bool, clip_zero: bool = False):
         y, ld = ops.affine_ar(x, raw, inverse, ops.LD_ROWSUM)
-        ctx.inverse = inverse
+        ctx.inverse, ctx.clip_zero = inverse, clip_zero
         ctx.save_for_backward(x, raw, y)
         return y, ld
 
@@ -242,12 +242,15 @@ class AffineARFn(Function):
         x, raw, y = ctx.saved_tensors
         if g_y is None:
             g_y = torch.zeros_like(y)
-        g_x, g_raw = ops.affine_ar_bwd(x, raw, y, ctx.inverse, g_y, g_ld, need_g_x=_needs(ctx, 0))
-        return g_x, g_raw, None
+        g_x, g_raw = ops.affine_ar_bwd(x, raw, y, ctx.inverse, g_y, g_ld, need_g_x=_needs(ctx, 0),
+                                       clip_zero=ctx.clip_zero)
+        return g_x, g_raw, None, None
 
 
-def affine_ar(x, raw, inverse):
-    return AffineARFn.apply(x, raw, inverse)
+def affine_ar(x, raw, inverse, clip_zero: bool = False):
+    """``clip_zero``: jnp.clip's gradient for the log_scale clip (the JAX Bayesian MAF) instead of
+    pyro's clamp_preserve_gradients."""
+    return AffineARFn.apply(x, raw, inverse, clip_zero)
 
 
 class BaseLogProbFn(Function):

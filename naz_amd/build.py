@@ -86,9 +86,41 @@ def build(verbose: bool = False, jobs: int = 4, extra: list | None = None, varia
     return lib_path
 
 
+DEBUG_LIB = LIB.with_name("libnazhip_debug.so")
+
+
+def build_debug(verbose: bool = False) -> Path:
+    """naz_amd/lib/libnazhip_debug.so: the library with the fused coupling kernels built with
+    -DNAZ_DEBUG_NONFINITE (the first non-finite row state recorded as (workgroup, layer, stage,
+    row), naz_debug_nonfinite).  Only coupling.hip's part 1 reads the flag, so the other objects
+    are the default build's (built first if needed)."""
+    build(verbose=verbose)
+    obj_dir = OBJ / "debug"
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    src = CSRC / "coupling.hip"
+    dobj = obj_dir / "coupling.o"
+    if not dobj.exists() or dobj.stat().st_mtime < max(src.stat().st_mtime, _headers_mtime()):
+        _compile(src, dobj, ["-DNAZ_DEBUG_NONFINITE", "-DNAZ_PART=1"])
+        if verbose:
+            print(f"[naz_amd.build] coupling.hip -> debug/{dobj.name}", file=sys.stderr)
+    objs = [dobj if o.name == "coupling.o" else o for o in _objects(OBJ)]
+    if not DEBUG_LIB.exists() or DEBUG_LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(DEBUG_LIB)] + [str(o) for o in objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return DEBUG_LIB
+
+
+def _objects(obj_dir: Path) -> list:
+    return [obj_dir / (CSRC.joinpath(s).stem + suffix + ".o") for s in SOURCES for suffix, _ in PARTS.get(s, [("", [])])]
+
+
 if __name__ == "__main__":
-    # python -m naz_amd.build [variant -DFLAG ...]
-    if len(sys.argv) > 1:
+    # python -m naz_amd.build [variant -DFLAG ... | debug]
+    if sys.argv[1:] == ["debug"]:
+        print(build_debug(verbose=True))
+    elif len(sys.argv) > 1:
         print(build(verbose=True, variant=sys.argv[1], extra=sys.argv[2:]))
     else:
         print(build(verbose=True))

@@ -41,7 +41,7 @@ using namespace naz;
 extern "C" {
 
 const char* naz_last_error(void) { return g_err; }
-int naz_abi_version(void) { return 1; }
+int naz_abi_version(void) { return 2; }
 
 int naz_rqs_fwd(const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy, float* ld,
                 int ld_mode, int64_t B, int Dt, int K, int layout, float bound, void* stream) {

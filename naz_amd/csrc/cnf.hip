@@ -1154,6 +1154,12 @@ struct CnfOps {
     if constexpr (!kX3) {
       if (mode == NAZ_CNF_F16X3) return set_error("naz_cnf: f16x3 not available for this shape");
     }
+    // the host polls the controller (hipMemcpyAsync + hipStreamSynchronize every few attempts), which
+    // a stream capture cannot record
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+      return set_error("naz_cnf_integrate_dopri5_global: the batch-global controller polls the host and cannot be "
+                       "captured into a HIP graph; use step_control='group' (one launch per solve) under capture");
     const int64_t tiles = (B + kCnfRows - 1) / kCnfRows;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=

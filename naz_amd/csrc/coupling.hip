@@ -1740,6 +1740,8 @@ static int ar_dispatch(const naz_ar_desc* d, F&& f) {
     // K is unused (the instances carry 8); the maf paper shape (train_mle_all_data.py:62-70) and
     // SURVEY §8d's config-3 AR variant
     if (d->D == 2 && d->C == 2 && d->H == 150 && d->n_hidden == 3) return f(AROps<CfgAR<2, 2, 150, 8, 3, true>>{});
+    // the 4-parameter Bayesian MAF (calibrate_4p.py:75,90-96; hmc_maf_exact.py:101-133)
+    if (d->D == 4 && d->C == 2 && d->H == 150 && d->n_hidden == 3) return f(AROps<CfgAR<4, 2, 150, 8, 3, true>>{});
     if (d->D == 16 && d->C == 32 && d->H == 128 && d->n_hidden == 2) return f(AROps<CfgAR<16, 32, 128, 8, 2, true>>{});
     // naz's production MAFs (4-parameter MLE, POSYDON): forward direction only (AROpsW)
     if (d->D == 4 && d->C == 2 && d->H == 512 && d->n_hidden == 5) return f(AROpsW<CfgARW<4, 2, 512, 5>>{});
@@ -1914,13 +1916,14 @@ struct ARBwdOps {
     return check_launch("made_ar_pack_bwd_kernel");
   }
   static int layer(const float* fimg, const float* bimg, const int* perm, const float* s_in, const float* ctx,
-                   int64_t ldc, const float* g_in, const float* g_lp, const ArBwdOut& o, int64_t B, hipStream_t s) {
+                   int64_t ldc, const float* g_in, const float* g_lp, const ArBwdOut& o, int64_t B, int clip_zero,
+                   hipStream_t s) {
     if (B == 0) return 0;
     const int64_t grid = (B + 16 * CB::NW - 1) / (16 * CB::NW);  // one workgroup per CU at a time (160 KB ring)
     if (grid > 0x7fffffff) return set_error("naz_ar_flow_bwd_layer: batch too large for one launch");
     const size_t lds = (size_t)2 * CB::SLOT * 4;
     hipLaunchKernelGGL((made_ar_bwd_kernel<CB>), dim3((unsigned)grid), dim3(64 * CB::NW), lds, s, fimg, bimg, perm,
-                       s_in, ctx, ldc, g_in, g_lp, o, B);
+                       s_in, ctx, ldc, g_in, g_lp, o, B, clip_zero);
     return check_launch("made_ar_bwd_kernel");
   }
 };
@@ -1930,6 +1933,8 @@ static int ar_bwd_dispatch(const naz_ar_desc* d, F&& f) {
   if (d == nullptr || d->act != NAZ_ACT_TANH || d->L < 0 || d->kind != NAZ_AR_AFFINE) return -2;
   // the maf paper shape (train_mle_all_data.py:62-70; the NUTS potential of hmc_maf_exact.py)
   if (d->D == 2 && d->C == 2 && d->H == 150 && d->n_hidden == 3) return f(ARBwdOps<CfgAR<2, 2, 150, 8, 3, true>>{});
+  // the 4-parameter Bayesian MAF's NUTS potential (calibrate_4p.py:75,90-96; hmc_maf_exact.py:101-133)
+  if (d->D == 4 && d->C == 2 && d->H == 150 && d->n_hidden == 3) return f(ARBwdOps<CfgAR<4, 2, 150, 8, 3, true>>{});
   return -2;
 }
 
@@ -1984,7 +1989,8 @@ int ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* 
         return set_error("naz_ar_flow_bwd_layer: null operand buffer %d", k);
     const float* fimg = static_cast<const float*>(packed_fwd) + (int64_t)layer * CB::FW::LAYER;
     const float* bimg = static_cast<const float*>(packed_bwd) + (int64_t)layer * CB::LAYER;
-    return O::layer(fimg, bimg, perm + (int64_t)layer * CB::D, state, ctx, ldc, g_in, g_lp, o, B, s);
+    return O::layer(fimg, bimg, perm + (int64_t)layer * CB::D, state, ctx, ldc, g_in, g_lp, o, B,
+                    (d->flags & NAZ_AR_CLIP_ZERO_GRAD) ? 1 : 0, s);
   });
   return rc == -2 ? ar_bwd_unsupported(d) : rc;
 }

@@ -19,7 +19,8 @@ __global__ void affine_ar_kernel(int inverse, const float* __restrict__ x, int64
   float s = 0.f;
   for (int i = 0; i < D; ++i) {
     const float mean = raw[r * ldr + i];
-    const float ls = fminf(fmaxf(raw[r * ldr + D + i], -5.f), 3.f);
+    const float raw_ls = raw[r * ldr + D + i];
+  const float ls = fminf(fmaxf(raw_ls, -5.f), 3.f);
     const float xv = x[r * ldx + i];
     y[r * ldy + i] = inverse ? (xv - mean) * expf(-ls) : expf(ls) * xv + mean;
     if (ld_mode == NAZ_LD_PERDIM) ld[r * D + i] = ls;
@@ -93,11 +94,12 @@ __global__ void affine_ar_bwd_kernel(int inverse, const float* __restrict__ x, i
   const int64_t r = e / D;
   const int i = (int)(e - r * D);
   const float mean = raw[r * ldr + i];
-  const float ls = fminf(fmaxf(raw[r * ldr + D + i], -5.f), 3.f);
+  const float raw_ls = raw[r * ldr + D + i];
+  const float ls = fminf(fmaxf(raw_ls, -5.f), 3.f);
   const float gy = g_y[r * ldgy + i], yv = y[r * ldy + i];
   const float gl = g_ld != nullptr ? g_ld[r] : 0.f;
   float gx, gm, gs;
-  if (inverse) {
+  if (inverse & 1) {
     const float sc = expf(-ls);
     gx = gy * sc;
     gm = -gx;
@@ -108,6 +110,7 @@ __global__ void affine_ar_bwd_kernel(int inverse, const float* __restrict__ x, i
     gm = gy;
     gs = gy * (yv - mean) + gl;
   }
+  if ((inverse & 2) && !(raw_ls >= -5.f && raw_ls <= 3.f)) gs = 0.f;  // jnp.clip's gradient
   (void)x;
   (void)ldx;
   if (g_x != nullptr) g_x[r * ldgx + i] = gx;

@@ -16,6 +16,8 @@
 //   2. the affine step's VJP per dim: s_d = (y_d - m_d) e^{-c(a_d)}, c = clamp(., -5, 3) with
 //      pyro's clamp_preserve_gradients (identity gradient), and log p gaining -c(a_d):
 //        dL/dm_d = -g_d e^{-c},  dL/da_d = -g_lp - g_d s_d,  dL/dy_d = g_d e^{-c};
+//      with clip_zero (NAZ_AR_CLIP_ZERO_GRAD: jnp.clip, bflow_jax_maf.py:177,188,192) dL/da_d = 0
+//      wherever a_d lies outside [-5, 3];
 //   3. the D sequential dependencies of the inverse, in reverse: for order p = D-1 .. 1, the output
 //      gradient of dim d_p alone is backpropagated through the MADE (δ_NHID = W_outᵀ g ⊙ tanh',
 //      δ_i = W_iᵀ δ_{i+1} ⊙ tanh', dx = W_0[:, C:]ᵀ δ_1) and dx added to g of the dims of order < p
@@ -162,7 +164,7 @@ template <class CB>
 __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
     const float* __restrict__ fimg, const float* __restrict__ bimg, const int* __restrict__ perm,
     const float* __restrict__ s_in, const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ g_in,
-    const float* __restrict__ g_lp, ArBwdOut o, int64_t B) {
+    const float* __restrict__ g_lp, ArBwdOut o, int64_t B, int clip_zero) {
   using FW = typename CB::FW;
   constexpr int D = CB::D, C = CB::C, NW = CB::NW, NHID = CB::NHID, HB = CB::HB, KSH = CB::KSH, HP = CB::HP;
   constexpr int NO = CB::NO, ROWS = 16 * NW, SLOT = CB::SLOT, NUF = FW::NU;
@@ -173,9 +175,6 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int q = lane >> 4;
-  int dps[D];  // dim of order p (wave-uniform)
-#pragma unroll
-  for (int p = 0; p < D; ++p) dps[p] = __builtin_amdgcn_readfirstlane(perm[p]);
 
   // one 128-row tile per workgroup (a persistent tile loop lets the compiler hoist ~60 per-unit LDS
   // addresses out of it, which then spill)
@@ -239,9 +238,8 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
       constexpr int kn = k + 1;
       if constexpr (kn < NSF) {
         stage_issue<FW::stage_floats(kn), NW>(nxt, fimg + kn * FW::STG);
-      } else if constexpr (kn < NSF + D * NSB) {
-        constexpr int sb = (kn - NSF) % NSB;
-        stage_issue<CB::stage_floats(sb), NW>(nxt, bimg + sb * CB::STG);
+      } else {  // the first backward stage (the chains' own advances issue the rest)
+        stage_issue<CB::stage_floats(0), NW>(nxt, bimg);
       }
       ++g;
     };
@@ -311,20 +309,54 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
         }
       });
     }
+    // ex[d] = e^{-c(a_d)} > 0; with clip_zero its SIGN carries whether a_d lies inside [-5, 3] (the
+    // jnp.clip gradient's support), so no per-dim flag stays live through the chains
 #pragma unroll
-    for (int d = 0; d < D; ++d) ex[d] = __expf(-fminf(fmaxf(la[d], -5.f), 3.f));
+    for (int d = 0; d < D; ++d) {
+      const float e = __expf(-fminf(fmaxf(la[d], -5.f), 3.f));
+      ex[d] = (clip_zero && !(la[d] >= -5.f && la[d] <= 3.f)) ? -e : e;
+    }
 
-    // ---- 2./3. the chains: orders p = D-1 .. 1 for the input gradients, then the final one
-    static_for<0, D>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      constexpr bool FINAL = c == D - 1;
-      const int dsel = dps[D - 1 - c];  // dim of order D-1-c (unused in the final chain)
+    // ---- 2./3. the chains: orders p = D-1 .. 1 for the input gradients, then the final one with
+    // every dim's output gradient.  The input chains run as a RUNTIME loop (one chain's code and
+    // operands live at a time: unrolled over D = 4 the compiler interleaved the chains' LDS reads and
+    // needed ~470 registers); a chain streams the NSB backward stages, its last one issuing stage 0
+    // of the next chain.
+    auto advance_b = [&](auto sc, auto morec) {
+      constexpr int sb = decltype(sc)::value;
+      ring_barrier();  // backward stage sb has landed in slot (g & 1); every wave is done with the other
+      cur = (g & 1) ? slot1 : slot0;
+      float* nxt = (g & 1) ? slot0 : slot1;
+      if constexpr (sb + 1 < NSB) {
+        stage_issue<CB::stage_floats(sb + 1), NW>(nxt, bimg + (sb + 1) * CB::STG);
+      } else if constexpr (decltype(morec)::value) {
+        stage_issue<CB::stage_floats(0), NW>(nxt, bimg);
+      }
+      ++g;
+    };
+    auto chain = [&](auto finalc, const int dsel) {  // dsel: dim of this chain's order (input chains)
+      constexpr bool FINAL = decltype(finalc)::value;
+      // dL/d (mean_d, log_scale_d); with clip_zero the clip's gradient is jnp.clip's (0 outside
+      // [-5, 3]).  Input chain: go[0], go[1] = dim dsel's pair (the others are zero).
       float go[NO];
+      if constexpr (FINAL) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const bool on = FINAL || dsel == d;
-        go[d] = on ? -gs[d] * ex[d] : 0.f;                 // dL/d mean_d
-        go[D + d] = on ? -gl - gs[d] * s[d] : 0.f;         // dL/d log_scale_d
+        for (int d = 0; d < D; ++d) {
+          go[d] = -gs[d] * fabsf(ex[d]);
+          go[D + d] = ex[d] > 0.f ? -gl - gs[d] * s[d] : 0.f;
+        }
+      } else {
+        float gsd = gs[0], sd = s[0], exd = ex[0];
+#pragma unroll
+        for (int d = 1; d < D; ++d) {
+          gsd = dsel == d ? gs[d] : gsd;
+          sd = dsel == d ? s[d] : sd;
+          exd = dsel == d ? ex[d] : exd;
+        }
+        go[0] = -gsd * fabsf(exd);
+        go[1] = exd > 0.f ? -gl - gsd * sd : 0.f;
+#pragma unroll
+        for (int k = 2; k < NO; ++k) go[k] = 0.f;
       }
       if constexpr (FINAL) {
         if (valid && q == 0) {
@@ -343,7 +375,7 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
         constexpr int j = decltype(jc)::value;
         constexpr int SID = CB::stage_id(j), OFF = CB::unit_off(j);
         if constexpr (j == 0 || SID != CB::stage_id(j > 0 ? j - 1 : 0))
-          advance(std::integral_constant<int, NSF + c * NSB + SID>{});
+          advance_b(std::integral_constant<int, SID>{}, std::integral_constant<bool, !FINAL>{});
         if constexpr (FINAL && j == CB::NUB - 1) return;  // no input gradient after the last chain
         __builtin_amdgcn_sched_barrier(0);
         const u32x4* c4 = reinterpret_cast<const u32x4*>(cur);
@@ -354,17 +386,37 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
         if constexpr (j == 0) {
           // δ_NHID = (W_outᵀ go) ⊙ (1 - h²), exact fp32 from the natural W_out rows
           const float4* tb = reinterpret_cast<const float4*>(cur + OFF);
+          // an input chain has only dim dsel's two outputs (mean, log_scale) nonzero
+          const float gm = FINAL ? 0.f : go[0], gsl = FINAL ? 0.f : go[1];
+          floatx4 tie1 = floatx4{0.f, 0.f, 0.f, 0.f}, tie2 = tie1;  // the final chain's last two blocks' products
           static_for<0, HB>([&](auto bc) {
             constexpr int b = decltype(bc)::value;
             __builtin_amdgcn_sched_barrier(0);
             float a[4] = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (FINAL) {
+              // block b's NO float4 reads of W_out take their address through a register tied to
+              // block b - 2's products: at most two blocks' reads in flight.  Untied, the scheduler
+              // issued all HB x NO reads ahead of the products (320 VGPRs at D = 4: spills), across
+              // sched_barrier and asm memory fences alike.
+              int woff = 0;
+              asm volatile("" : "+v"(woff) : "v"(tie2[0]), "v"(tie2[1]), "v"(tie2[2]), "v"(tie2[3]));
+              const float4* tbb = tb + woff;
 #pragma unroll
-            for (int oo = 0; oo < NO; ++oo) {
-              const float4 w = tb[(oo * HP + 16 * b) / 4 + q];
-              a[0] = __builtin_fmaf(w.x, go[oo], a[0]);
-              a[1] = __builtin_fmaf(w.y, go[oo], a[1]);
-              a[2] = __builtin_fmaf(w.z, go[oo], a[2]);
-              a[3] = __builtin_fmaf(w.w, go[oo], a[3]);
+              for (int oo = 0; oo < NO; ++oo) {
+                const float4 w = tbb[(oo * HP + 16 * b) / 4 + q];
+                a[0] = __builtin_fmaf(w.x, go[oo], a[0]);
+                a[1] = __builtin_fmaf(w.y, go[oo], a[1]);
+                a[2] = __builtin_fmaf(w.z, go[oo], a[2]);
+                a[3] = __builtin_fmaf(w.w, go[oo], a[3]);
+              }
+              tie2 = tie1;
+              tie1 = floatx4{a[0], a[1], a[2], a[3]};
+            } else {
+              const float4 w0 = tb[(dsel * HP + 16 * b) / 4 + q], w1 = tb[((D + dsel) * HP + 16 * b) / 4 + q];
+              a[0] = __builtin_fmaf(w1.x, gsl, w0.x * gm);
+              a[1] = __builtin_fmaf(w1.y, gsl, w0.y * gm);
+              a[2] = __builtin_fmaf(w1.z, gsl, w0.z * gm);
+              a[3] = __builtin_fmaf(w1.w, gsl, w0.w * gm);
             }
             const float4 hv = valid ? *ar_h_ptr<CB, NHID - 1, b>(o, row, q) : float4{0.f, 0.f, 0.f, 0.f};
             dcur[b] = floatx4{a[0] * (1.f - hv.x * hv.x), a[1] * (1.f - hv.y * hv.y), a[2] * (1.f - hv.z * hv.z),
@@ -418,10 +470,13 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
           }
         }
       });
-    });
+    };
+#pragma unroll 1
+    for (int c = 0; c < D - 1; ++c) chain(std::false_type{}, __builtin_amdgcn_readfirstlane(perm[D - 1 - c]));
+    chain(std::true_type{}, -1);
     if (valid && q == 0) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) o.g_next[row * D + d] = gs[d] * ex[d];
+      for (int d = 0; d < D; ++d) o.g_next[row * D + d] = gs[d] * fabsf(ex[d]);
     }
   }
 }

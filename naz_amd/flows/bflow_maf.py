@@ -653,6 +653,7 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             f = NormalizingFlow("maf", None, D, C, spec.hidden_dims, len(plans), activation=acts[act]).to(dev)
             for t, perm in zip(f.transforms, perms):
                 t.nn.set_permutation(torch.as_tensor(perm))
+                t.nn.clip_zero_grad = True  # the potential differentiates jnp.clip (bflow_jax_maf.py:177-192)
             grad_flow["f"] = f
         return f
 
@@ -703,7 +704,8 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         mg = grad_flow.get("mafgrad")
         if mg is None:
             from .maf_grad import MafGrad
-            mg = grad_flow["mafgrad"] = MafGrad(ar_desc, ar_grad_perm, torch.cat(ar_maskvec))
+            # jnp.clip's gradient for the log_scale clip, as jax.grad of the reference's potential
+            mg = grad_flow["mafgrad"] = MafGrad(ar_desc, ar_grad_perm, torch.cat(ar_maskvec), clip_zero=True)
         return mg
 
     def lp_and_grad(params, use_graph: bool = True) -> Tuple[Tensor, Tensor]:

@@ -11,7 +11,9 @@ Solver: naz constructs torchdyn ``NeuralODE(solver='dopri5', atol=rtol=1e-4, sen
 'adjoint')`` (:73-81).  SURVEY.md §8d pins config 5 to fixed-step classical RK4 with 8 steps
 (NFE 32) — the default here (``solver='rk4', steps=8``); ``solver='dopri5'`` runs the adaptive
 Dormand-Prince solve (``step_control="global"``, the default: torchdyn's one step size for the
-batch, naz_cnf_integrate_dopri5_global; ``"group"``: naz_cnf_integrate_dopri5, one per 16 rows).  Under autograd
+batch, naz_cnf_integrate_dopri5_global — one launch per attempted step, the host polling the
+controller every 4 attempts, so the call blocks the host and cannot be captured into a HIP graph;
+``"group"``: naz_cnf_integrate_dopri5, one launch per solve, one step size per 16 rows, capturable).  Under autograd
 the solve is one ``CnfSolveFn`` node (flows/cnf_adjoint.py, §8f rank 3): rk4 backpropagates by the
 discrete adjoint of the pinned solve from per-step checkpoints, dopri5 by the continuous adjoint
 (``adjoint_steps`` RK4 steps back from t1), every RHS and VJP on HIP kernels.  The Hutchinson probe eps ~ N(0, I)

@@ -225,13 +225,14 @@ class _FusedAR:
         """MafGrad for the current permutations and masks (rebuilt when one of them changes)."""
         nets = self._nets()
         ts = [t for n in nets for l in n.layers for t in (l.mask,)] + [n.permutation for n in nets]
-        sig = tuple((t.data_ptr(), t._version) for t in ts) + (cache_epoch(),)
+        cz = any(bool(getattr(n, "clip_zero_grad", False)) for n in nets)  # jnp.clip's gradient (bflow)
+        sig = tuple((t.data_ptr(), t._version) for t in ts) + (cache_epoch(), cz)
         if getattr(self, "_mg", None) is None or self._mg[0] != sig:
             from .maf_grad import MafGrad
             mask = torch.cat([t for n in nets for l in n.layers
                               for t in (l.mask.detach().reshape(-1).float(), torch.ones_like(l.bias.detach()))])
             perm = np.stack([n.permutation.detach().cpu().numpy() for n in nets]).astype(np.int32)
-            self._mg = (sig, MafGrad(self.desc, perm, mask.contiguous()))
+            self._mg = (sig, MafGrad(self.desc, perm, mask.contiguous(), clip_zero=cz))
         return self._mg[1]
 
     def train_params(self) -> List[torch.Tensor]:
@@ -333,21 +334,8 @@ class _FusedAR:
         return ops.ar_flow_log_prob(self.desc, self.packed(), x, context, low, high, out=out)
 
     def executed_flop_per_row(self) -> int:
-        """FP32-equivalent FLOPs the kernel executes per row (an f16x3 product counted once; the
-        16-unit block recomputations and zero-padded k-slots included): per pass, the first hidden
-        layer's blocks over [ctx | x], the further hidden layers' blocks over the units of degree
-        <= p, and the output blocks."""
-        D, C, H, NH, K = self.shape
-        deg = ops.ar_flow_degrees(self.desc)
-        E = [int((deg <= p).sum()) for p in range(D)]
-        KI, NOB = (C + 31) // 32 + 1, (self.P + 15) // 16
-        per_layer = 0
-        for p in range(D):
-            e0 = E[p - 1] if p else 0
-            nb = ((E[p] - 1) >> 4) - (e0 >> 4) + 1 if E[p] > e0 else 0
-            kt = (E[p] + 31) // 32
-            per_layer += (nb * (KI + (NH - 1) * kt) + NOB * kt) * 16 * 32 * 2  # 16 outputs x 32 k per block-step
-        return per_layer * len(self.layers)
+        """FP32-equivalent FLOPs the inverse kernel executes per row (ops.ar_executed_flop_per_row)."""
+        return ops.ar_executed_flop_per_row(self.desc)["inverse"]
 
 
 _TRAIN_FUSED = __import__("os").environ.get("NAZ_TRAIN_FUSED", "1")

@@ -31,12 +31,18 @@ class MafGrad:
     """The fused maf log-density and its backward for one flow structure: ``desc`` (an affine
     naz_ar_desc at a compiled shape), ``perms`` [L, D] (dim of order p per layer) and ``mask``
     [L * per] (the MADE masks in the naz_ar_flow_pack_host flat layout, 1 on biases).  Weights
-    come as flat rows in that layout (= ``ravel`` order of the JAX front end)."""
+    come as flat rows in that layout (= ``ravel`` order of the JAX front end).  ``clip_zero``: the
+    log_scale clip differentiates as jnp.clip (zero outside [-5, 3]: the JAX MAF's potential,
+    bflow_jax_maf.py:177-192) instead of pyro's clamp_preserve_gradients (naz's torch maf)."""
 
-    def __init__(self, desc, perms: np.ndarray, mask: Tensor, operand_bytes: int = 8 << 30):
+    def __init__(self, desc, perms: np.ndarray, mask: Tensor, operand_bytes: int = 4 << 30,
+                 clip_zero: bool = False, keep_sizes: int = 2):
         if not ops.ar_flow_bwd_supported(desc):
             raise RuntimeError("MafGrad: no fused maf backward for this shape")
+        desc = type(desc).from_buffer_copy(desc)
+        desc.flags = ops.AR_CLIP_ZERO_GRAD if clip_zero else 0
         self.desc = desc
+        self.keep_sizes = max(1, int(keep_sizes))
         dev = mask.device
         self.dev = dev
         D, C, H, L = desc.D, desc.C, desc.H, desc.L
@@ -71,9 +77,16 @@ class MafGrad:
             raise ValueError("MafGrad: mask does not match the flow's flat parameter count")
 
     def _buffers(self, B: int) -> dict:
-        """Per-row-count buffers (kept: a captured graph replays the same addresses)."""
-        b = self._bufs.get(B)
-        if b is None:
+        """Per-row-count buffers.  The most recent ``keep_sizes`` row counts stay allocated (a
+        captured graph replays the same addresses; a training loop alternates the full batch and
+        a ragged last batch); older ones are released, so a run of distinct batch sizes does not
+        pin one operand set each."""
+        b = self._bufs.pop(B, None)
+        if b is not None:
+            self._bufs[B] = b  # most recently used last
+        else:
+            while len(self._bufs) >= self.keep_sizes:
+                self._bufs.pop(next(iter(self._bufs)))
             d, dm = self.desc, self.dims
             NH, HP, X0W = dm["n_hidden"], dm["HP"], dm["X0W"]
             f32 = dict(device=self.dev, dtype=torch.float32)

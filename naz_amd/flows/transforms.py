@@ -546,13 +546,14 @@ class _ConditionedAffineAutoregressive(_LDCache, Transform):
         scheduled (every MADE unit once, ARInversePlan.run_grad) unless the conditioner's
         degree_schedule is off, then pyro's D full passes."""
         plan = self.arn.inverse_plan() if y.dim() == 2 else None
+        cz = bool(getattr(self.arn, "clip_zero_grad", False))  # the JAX MAF's jnp.clip gradient
         if plan is not None:
-            return plan.run_grad(y, self.context, lambda k, i, raw: ag.affine_ar(y[:, i:i + 1], raw, True))
+            return plan.run_grad(y, self.context, lambda k, i, raw: ag.affine_ar(y[:, i:i + 1], raw, True, cz))
         x = torch.zeros_like(y)
         ld = None
         for _ in range(y.shape[-1]):
             raw = self.arn.raw(x, self.context)
-            x, ld = ag.affine_ar(y, raw, True)
+            x, ld = ag.affine_ar(y, raw, True, cz)
         return x, ld
 
 

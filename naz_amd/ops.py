@@ -333,8 +333,10 @@ def rqs_bwd(x: Tensor, raw: Tensor, count_bins: int, layout: int, inverse: bool,
 
 
 def affine_ar_bwd(x: Tensor, raw: Tensor, y: Tensor, inverse: bool, g_y: Tensor, g_ld: Optional[Tensor],
-                  need_g_x: bool = True) -> Tuple[Optional[Tensor], Tensor]:
-    """VJP of ``affine_ar`` with a row-sum ld (naz_affine_ar_bwd)."""
+                  need_g_x: bool = True, clip_zero: bool = False) -> Tuple[Optional[Tensor], Tensor]:
+    """VJP of ``affine_ar`` with a row-sum ld (naz_affine_ar_bwd).  ``clip_zero``: the log_scale
+    clip differentiates as jnp.clip (0 outside [-5, 3], bflow_jax_maf.py:177-192) instead of pyro's
+    clamp_preserve_gradients."""
     dev = _dev(x, raw, y, g_y, g_ld)
     x, ldx = _rows(x)
     raw, ldr = _rows(raw)
@@ -344,7 +346,7 @@ def affine_ar_bwd(x: Tensor, raw: Tensor, y: Tensor, inverse: bool, g_y: Tensor,
     g_ld = None if g_ld is None else g_ld.contiguous()
     g_x = torch.empty((B, D), device=dev, dtype=torch.float32) if need_g_x else None
     g_raw = torch.empty((B, 2 * D), device=dev, dtype=torch.float32)
-    check(lib().naz_affine_ar_bwd(int(inverse), _p(x), ldx, _p(raw), ldr, _p(y), ldy, _p(g_y), ldgy, _p(g_ld),
+    check(lib().naz_affine_ar_bwd(int(bool(inverse)) | (2 if clip_zero else 0), _p(x), ldx, _p(raw), ldr, _p(y), ldy, _p(g_y), ldgy, _p(g_ld),
                                   _p(g_x), D, _p(g_raw), 2 * D, B, D, _stream(dev)), "affine_ar_bwd")
     return g_x, g_raw
 
@@ -567,6 +569,7 @@ def coupling_log_prob(d: CouplingDesc, packed: Tensor, x: Tensor, context: Optio
 
 # ----------------------------------------------------------------------------- §8b naz_{spline,affine}_ar_inv
 AR_KIND = {"nsa": 0, "maf": 1}  # NAZ_AR_SPLINE, NAZ_AR_AFFINE
+AR_CLIP_ZERO_GRAD = 1  # naz_ar_desc.flags: NAZ_AR_CLIP_ZERO_GRAD
 
 
 def ar_flow_desc(kind: str, D: int, C: int, H: int, L: int, n_hidden: int = 2, K: int = 8, act: str = "tanh",
@@ -594,6 +597,42 @@ def ar_flow_degrees(d: ArDesc) -> np.ndarray:
     """The hidden-unit mask indices the fused kernel is compiled for (pyro create_mask's)."""
     out = np.zeros(d.H, dtype=np.int32)
     check(lib().naz_ar_flow_degrees(d, out.ctypes.data), "ar_flow_degrees")
+    return out
+
+
+def ar_executed_flop_per_row(d: ArDesc) -> dict:
+    """FP32-equivalent FLOPs per row the fused autoregressive kernels EXECUTE (a split f16x3 /
+    bf16x6 product counted once; the 16-unit block recomputation and zero padding included), for
+    roofline accounting against the pipe each runs on:
+
+      inverse  made_ar_r16_kernel (log_prob): per pass p, hidden layer 1's blocks holding units of
+               degree p over [ctx | x], the further hidden layers' over the units of degree <= p,
+               and the output blocks of dim p (made_ar_r16.h; f16x3);
+      bwd      made_ar_bwd_kernel, all layers (maf only): one dense MADE pass plus D chains
+               (W_out^T g on the VALU in fp32, the W_i^T chain and the input unit on f16x3);
+      dw       the batched weight-gradient reductions over the padded operands (bf16x6).
+    """
+    D, C, H, NH, L = d.D, d.C, d.H, d.n_hidden, d.L
+    P = 2 if d.kind == AR_KIND["maf"] else 3 * d.K - 1
+    HP = (H + 31) // 32 * 32
+    HB, KSH, KI, NOB = HP // 16, HP // 32, (C + 31) // 32 + 1, (P + 15) // 16
+    blk = 16 * 32 * 2  # one 16-unit block over one 32-deep k-step, per row
+    deg = ar_flow_degrees(d)
+    E = [int((deg <= p).sum()) for p in range(D)]
+    inv = 0
+    for p in range(D):
+        e0 = E[p - 1] if p else 0
+        nb = ((E[p] - 1) >> 4) - (e0 >> 4) + 1 if E[p] > e0 else 0
+        kt = (E[p] + 31) // 32
+        inv += (nb * (KI + (NH - 1) * kt) + NOB * kt) * blk
+    out = {"inverse": inv * L}
+    if d.kind == AR_KIND["maf"] and int(lib().naz_ar_flow_bwd_packed_bytes(d)) > 0:
+        X0W = ar_flow_bwd_dims(d)["X0W"]
+        dense = (HB * KI + (NH - 1) * HB * KSH + (D + 3) // 4 * KSH) * blk
+        chains = D * (2 * 2 * D * HP + (NH - 1) * HB * KSH * blk) + (D - 1) * KSH * blk
+        out["bwd"] = (dense + chains) * L
+        out["bwd_valu"] = D * 2 * 2 * D * HP * L  # the W_out^T g part, in "bwd"
+        out["dw"] = 2 * (HP * X0W + (NH - 1) * HP * HP + X0W * HP) * L
     return out
 
 
@@ -817,6 +856,27 @@ def ar_flow_bwd_layer(d: ArDesc, packed_fwd: Tensor, packed_bwd: Tensor, perm: T
     for t in (state, g_in, g_out, perm) + tuple(b for b in bufs if b is not None) + ((g_lp,) if g_lp is not None else ()):
         if not t.is_contiguous():
             raise ValueError("ar_flow_bwd_layer: buffers must be contiguous")
+    if not (0 <= int(layer) < d.L):
+        raise ValueError(f"ar_flow_bwd_layer: layer {layer} outside [0, {d.L})")
+    for name, t in (("state", state), ("g_in", g_in), ("g_out", g_out)):
+        if t.dim() != 2 or t.shape[0] != B or t.shape[1] != d.D or t.dtype != torch.float32:
+            raise ValueError(f"ar_flow_bwd_layer: {name} must be float32 [{B}, {d.D}], got {tuple(t.shape)}")
+    if g_lp is not None and (g_lp.numel() != B or g_lp.dtype != torch.float32):
+        raise ValueError(f"ar_flow_bwd_layer: g_lp must be float32 [{B}]")
+    # bufs (include/naz_hip.h): x0, then per hidden layer (h_i, h_i split tail), then dp_i, then gout
+    dm = ar_flow_bwd_dims(d)
+    NH, HP, X0W, XA, XB = dm["n_hidden"], dm["HP"], dm["X0W"], dm["XA"], dm["XB"]
+    if len(bufs) != 2 + 3 * NH:
+        raise ValueError(f"ar_flow_bwd_layer: {2 + 3 * NH} operand buffers expected, got {len(bufs)}")
+    widths = [X0W] + [w for _ in range(NH) for w in (XA, XB)] + [HP] * NH + [X0W]
+    for k, (t, w) in enumerate(zip(bufs, widths)):
+        if t is None:
+            if w != 0 and not (1 <= k <= 2 * NH and k % 2 == 0 and XB == 0):
+                raise ValueError(f"ar_flow_bwd_layer: operand buffer {k} is required")
+            continue
+        if t.dim() != 2 or t.shape[0] < B or t.shape[1] != w or t.dtype != torch.float32 or t.device != dev:
+            raise ValueError(f"ar_flow_bwd_layer: operand buffer {k} must be float32 [>= {B}, {w}] on {dev}, "
+                             f"got {tuple(t.shape)}")
     ptrs = (C.c_void_p * len(bufs))(*[_p(b) for b in bufs])
     check(lib().naz_ar_flow_bwd_layer(d, _p(packed_fwd), _p(packed_bwd), _p(perm), int(layer), _p(state),
                                       _p(context), ldc, _p(g_in), _p(g_lp), ptrs, _p(g_out), B, _stream(dev)),

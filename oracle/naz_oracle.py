@@ -312,12 +312,23 @@ def _clamp(t: Tensor, lo: float, hi: float) -> Tensor:
     return t + (t.clamp(min=lo, max=hi) - t).detach()
 
 
+def _clip(t: Tensor, lo: float, hi: float) -> Tensor:
+    """jnp.clip as the reference's JAX MAF applies it to log_scale (bflow_jax_maf.py:177,188,192):
+    clamped value, ZERO gradient outside [lo, hi] (torch.clamp's gradient)."""
+    return t.clamp(min=lo, max=hi)
+
+
 class AffineAutoregressive:
     """a5: [pyro] affine_autoregressive.py::AffineAutoregressive(stable=False) with clip
-    (-5, 3) (naz ``maf``: transforms.py:133-160; JAX restatement bflow_jax_maf.py:169-194)."""
+    (-5, 3) (naz ``maf``: transforms.py:133-160; JAX restatement bflow_jax_maf.py:169-194).
+    ``clip_grad``: "preserve" = pyro's clamp_preserve_gradients (naz's torch flows), "zero" =
+    jnp.clip's gradient (the JAX Bayesian MAF whose potential NUTS differentiates)."""
 
-    def __init__(self, D: int, arn: MLP, permutation: Tensor):
+    def __init__(self, D: int, arn: MLP, permutation: Tensor, clip_grad: str = "preserve"):
         self.D, self.nn, self.permutation = D, arn, permutation
+        if clip_grad not in ("preserve", "zero"):
+            raise ValueError(f"clip_grad must be 'preserve' or 'zero', not {clip_grad!r}")
+        self._cl = _clamp if clip_grad == "preserve" else _clip
 
     def _mean_logscale(self, x, ctx):
         out = self.nn(x, ctx).reshape(x.shape[:-1] + (2, self.D))
@@ -325,7 +336,7 @@ class AffineAutoregressive:
 
     def forward(self, x, ctx=None):
         mean, log_scale = self._mean_logscale(x, ctx)
-        log_scale = _clamp(log_scale, LOG_SCALE_MIN_CLIP, LOG_SCALE_MAX_CLIP)
+        log_scale = self._cl(log_scale, LOG_SCALE_MIN_CLIP, LOG_SCALE_MAX_CLIP)
         return torch.exp(log_scale) * x + mean, log_scale
 
     def inverse(self, y, ctx=None):
@@ -333,9 +344,9 @@ class AffineAutoregressive:
         log_scale = None
         for idx in self.permutation.tolist():
             mean, log_scale = self._mean_logscale(torch.stack(xs, dim=-1), ctx)
-            inverse_scale = torch.exp(-_clamp(log_scale[..., idx], LOG_SCALE_MIN_CLIP, LOG_SCALE_MAX_CLIP))
+            inverse_scale = torch.exp(-self._cl(log_scale[..., idx], LOG_SCALE_MIN_CLIP, LOG_SCALE_MAX_CLIP))
             xs[idx] = (y[..., idx] - mean[..., idx]) * inverse_scale
-        return torch.stack(xs, dim=-1), _clamp(log_scale, LOG_SCALE_MIN_CLIP, LOG_SCALE_MAX_CLIP)
+        return torch.stack(xs, dim=-1), self._cl(log_scale, LOG_SCALE_MIN_CLIP, LOG_SCALE_MAX_CLIP)
 
 
 class Permute:
@@ -430,6 +441,37 @@ DOPRI5_E = [35 / 384 - 5179 / 57600, 0.0, 500 / 1113 - 7571 / 16695, 125 / 192 -
             -2187 / 6784 + 92097 / 339200, 11 / 84 - 187 / 2100, -1 / 40]
 
 
+def _rms(u: Tensor, ua: Tensor) -> float:
+    """RMS over the augmented state's elements ([x] and [a] together)."""
+    return float(torch.sqrt((torch.sum(u ** 2) + torch.sum(ua ** 2)) / (u.numel() + ua.numel())))
+
+
+def dopri5_step(net: FCNN, y: Tensor, a: Tensor, ctx: Optional[Tensor], eps: Tensor, hh: float,
+                atol: float, rtol: float, k0: Optional[Tuple[Tensor, Tensor]] = None):
+    """One Dormand-Prince 5(4) step of the augmented field, naz's in-tree ``Dopri5._step_fn``
+    (neural_nets/__deprecated__/neural_odes/odeint.py:96-112 with the tableau :136-160): stages
+    k_i = f(y + hh sum_j a_ij k_j), the 5th-order update y5 = y + hh sum b_i k_i, the FSAL stage
+    f(y5), the embedded error hh sum e_i k_i and its RMS norm over err / (atol + rtol max(|y|, |y5|)).
+    Returns (y5, a5, k6 = f(y5) pair, error norm).  Pinned to the reference's own step by
+    tests/golden/cnf_refode_*.npz (oracle/gen_refode_fixtures.py)."""
+    f0, f0a = hutchinson_rhs(net, y, ctx, eps) if k0 is None else k0
+    ks, kas = [f0], [f0a]
+    for row in DOPRI5_A:
+        ki, kia = hutchinson_rhs(net, y + hh * sum(c * k for c, k in zip(row, ks)), ctx, eps)
+        ks.append(ki)
+        kas.append(kia)
+    y5 = y + hh * sum(c * k for c, k in zip(DOPRI5_B, ks))
+    a5 = a + hh * sum(c * k for c, k in zip(DOPRI5_B, kas))
+    k6, k6a = hutchinson_rhs(net, y5, ctx, eps)
+    ks.append(k6)
+    kas.append(k6a)
+    err = hh * sum(c * k for c, k in zip(DOPRI5_E, ks))
+    erra = hh * sum(c * k for c, k in zip(DOPRI5_E, kas))
+    en = _rms(err / (atol + rtol * torch.maximum(y.abs(), y5.abs())),
+              erra / (atol + rtol * torch.maximum(a.abs(), a5.abs())))
+    return y5, a5, (k6, k6a), en
+
+
 def dopri5_augmented(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor, t0: float, t1: float,
                      atol: float = 1e-4, rtol: float = 1e-4, group: int = 16, max_steps: int = 1000):
     """Adaptive Dormand-Prince 5(4) on the augmented state [x, a] (naz
@@ -453,9 +495,7 @@ def dopri5_augmented(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor, t
 
         def f(v):
             return hutchinson_rhs(net, v, cg, e)
-
-        def rms(u, ua):
-            return float(torch.sqrt((torch.sum(u ** 2) + torch.sum(ua ** 2)) / (u.numel() + ua.numel())))
+        rms = _rms
         direction = 1.0 if t1 > t0 else -1.0
         k0, k0a = f(y)
         sc, sca = atol + rtol * y.abs(), atol + rtol * a.abs()
@@ -470,21 +510,8 @@ def dopri5_augmented(net: FCNN, x: Tensor, ctx: Optional[Tensor], eps: Tensor, t
             rem = abs(t1 - t)
             last = h >= rem
             hh = direction * (rem if last else h)
-            ks, kas = [k0], [k0a]
-            for row in DOPRI5_A:
-                ki, kia = f(y + hh * sum(c * k for c, k in zip(row, ks)))
-                ks.append(ki)
-                kas.append(kia)
-            y5 = y + hh * sum(c * k for c, k in zip(DOPRI5_B, ks))
-            a5 = a + hh * sum(c * k for c, k in zip(DOPRI5_B, kas))
-            k6, k6a = f(y5)
-            ks.append(k6)
-            kas.append(k6a)
+            y5, a5, (k6, k6a), en = dopri5_step(net, y, a, cg, e, hh, atol, rtol, k0=(k0, k0a))
             nfe += 6
-            err = hh * sum(c * k for c, k in zip(DOPRI5_E, ks))
-            erra = hh * sum(c * k for c, k in zip(DOPRI5_E, kas))
-            en = rms(err / (atol + rtol * torch.maximum(y.abs(), y5.abs())),
-                     erra / (atol + rtol * torch.maximum(a.abs(), a5.abs())))
             if en <= 1.0:
                 y, a, k0, k0a = y5, a5, k6, k6a
                 t = t1 if last else t + hh
@@ -597,7 +624,7 @@ def _hidden_list(hidden) -> List[int]:
 
 def build_flow(spec: dict, state: Dict[str, Tensor], dtype=torch.float64) -> Flow:
     """Build an oracle flow from ``spec`` (flow_type, D, C, hidden, L, K, split, activation,
-    bounds) and a canonical state dict (numpy or torch values):
+    bounds, clip_grad for maf) and a canonical state dict (numpy or torch values):
 
       layers.{l}.nn.layers.{i}.weight/bias                      conditioner
       layers.{l}.nn.permutation                                 ARN variable order (maf/nsa)
@@ -633,7 +660,7 @@ def build_flow(spec: dict, state: Dict[str, Tensor], dtype=torch.float64) -> Flo
             if ft == "nsa":
                 layers.append(SplineAutoregressive(D, K, arn, bound))
             else:
-                layers.append(AffineAutoregressive(D, arn, perm))
+                layers.append(AffineAutoregressive(D, arn, perm, spec.get("clip_grad", "preserve")))
         else:
             raise ValueError(f"oracle: unsupported flow_type {ft!r}")
         if (p + "perm") in t:

@@ -28,7 +28,27 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared_functions() if not hasattr(L, n)]
     assert not missing, missing
     assert set(declared_functions()) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
-    assert L.naz_abi_version() == 1
+    # 2: naz_ar_desc.flags (NAZ_AR_CLIP_ZERO_GRAD), naz_affine_ar_bwd's mode bits, and
+    # naz_ar_flow_supported's 0 / 1 / 2 contract (2 = forward direction only)
+    assert L.naz_abi_version() == 2
+
+
+def test_ar_flow_supported_contract():
+    """naz_ar_flow_supported: 1 = both directions fused, 2 = the sampling direction only (the
+    wide production MAFs), 0 = not instantiated; the inverse entry points of a 2-shape report it."""
+    from naz_amd import _lib, ops
+    L = _lib.lib()
+    assert L.naz_ar_flow_supported(ops.ar_flow_desc("maf", 2, 2, 150, 16, 3)) == 1
+    assert L.naz_ar_flow_supported(ops.ar_flow_desc("maf", 4, 2, 150, 16, 3)) == 1  # the 4-parameter Bayesian MAF
+    assert L.naz_ar_flow_supported(ops.ar_flow_desc("nsa", 16, 32, 128, 8, 2)) == 1
+    wide = ops.ar_flow_desc("maf", 4, 2, 512, 18, 5)
+    assert L.naz_ar_flow_supported(wide) == 2
+    assert L.naz_ar_flow_packed_bytes(wide) < 0 and L.naz_ar_flow_fwd_packed_bytes(wide) > 0
+    assert L.naz_ar_flow_supported(ops.ar_flow_desc("maf", 3, 2, 150, 4, 3)) == 0
+    # the fused maf backward exists at both Bayesian shapes
+    assert ops.ar_flow_bwd_supported(ops.ar_flow_desc("maf", 4, 2, 150, 16, 3))
+    assert ops.ar_flow_bwd_supported(ops.ar_flow_desc("maf", 2, 2, 150, 16, 3))
+    assert not ops.ar_flow_bwd_supported(ops.ar_flow_desc("maf", 16, 32, 128, 4, 2))
 
 
 def test_host_side_errors_have_messages():

@@ -339,7 +339,7 @@ def test_lp_and_grad_vs_oracle_autograd(_gpu, ctx_kind):
     """The NUTS potential Σ_rows lp(θ) and its gradient (bflow_jax_maf.py:233-235) from the HIP
     training walk vs the fp64 oracle's torch autograd (and its fp32 run as ref32)."""
     from naz_amd.flows import bflow_maf as BM
-    spec = dict(flow_type="maf", D=2, C=2, hidden=[48, 48], L=3, P=2, B=1500, ctx=ctx_kind)
+    spec = dict(flow_type="maf", D=2, C=2, hidden=[48, 48], L=3, P=2, B=1500, ctx=ctx_kind, clip_grad="zero")
     layers, draws, x, ctx = _setup(spec)
     flow = _flow(spec, layers, x, ctx, "cuda")
     d = draws[0]
@@ -428,17 +428,27 @@ def test_lp_layer_batched_many_draws_few_rows():
 
 
 @pytest.mark.gpu
-def test_sampler_batched_fused_ar_paper_shape(_gpu):
-    """At the paper shape (D=2 | C=2, H=[150]*3) the batched sampler runs the whole flow for every
-    draw in ONE naz_ar_flow_sample_batched launch (weights packed on the device per draw); against
-    the numpy restatement of the reference's JAX sampler and the per-layer fused-MADE path."""
-    spec = dict(D=2, C=2, hidden=[150, 150, 150], L=4, P=5, B=64, ctx="vec", flow_type="maf")
+@pytest.mark.parametrize("D", [2, 4])
+def test_sampler_batched_fused_ar_paper_shape(_gpu, D):
+    """At the paper shape (D=2 | C=2, H=[150]*3) and the 4-parameter Bayesian MAF (D=4,
+    calibrate_4p.py:75) the batched sampler runs the whole flow for every draw in ONE
+    naz_ar_flow_sample_batched launch (weights packed on the device per draw); against the numpy
+    restatement of the reference's JAX sampler and the per-layer fused-MADE path."""
+    spec = dict(D=D, C=2, hidden=[150, 150, 150], L=4, P=5, B=64, ctx="vec", flow_type="maf")
     layers, draws, x, ctx = _setup(spec)
     S = 700
     z = np.random.default_rng(4).standard_normal((spec["P"], S, spec["D"])).astype(np.float32)
     params = _batched_params(draws, "cuda")
     flow = _flow(spec, layers, x, ctx, "cuda")
-    y, lj = flow["sampler_batched"](params, size=S, z=torch.tensor(z, device="cuda"))
+    calls = []
+    from naz_amd.flows import bflow_maf as BM
+    orig = BM.ops.ar_flow_sample_batched
+    BM.ops.ar_flow_sample_batched = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        y, lj = flow["sampler_batched"](params, size=S, z=torch.tensor(z, device="cuda"))
+    finally:
+        BM.ops.ar_flow_sample_batched = orig
+    assert calls, "the fused batched AR sampler was not used"
     flow_made = _flow(spec, layers, x, ctx, "cuda", fused_ar=False)
     y_m, lj_m = flow_made["sampler_batched"](params, size=S, z=torch.tensor(z, device="cuda"))
     y, lj = y.cpu().numpy(), lj.cpu().numpy()
@@ -452,14 +462,14 @@ def test_sampler_batched_fused_ar_paper_shape(_gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,B", [(5, 700), (3, 1)])
-def test_lp_batched_fused_ar_paper_shape(_gpu, P, B):
+@pytest.mark.parametrize("D,P,B", [(2, 5, 700), (2, 3, 1), (4, 4, 900)])
+def test_lp_batched_fused_ar_paper_shape(_gpu, D, P, B):
     """At the paper shape the batched log-density packs every draw's inverse image on the device
     (naz_ar_flow_pack) and runs the whole flow for all draws in ONE naz_ar_flow_log_prob_batched
     launch; against the numpy restatement of the reference's JAX log_prob, the layer-batched
     MADE path, and a flow whose masks are not pyro's create_mask (must not take the fused path)."""
     from naz_amd.flows import bflow_maf as BM
-    spec = dict(D=2, C=2, hidden=[150, 150, 150], L=5, P=P, B=B, ctx="vec", flow_type="maf")
+    spec = dict(D=D, C=2, hidden=[150, 150, 150], L=5, P=P, B=B, ctx="vec", flow_type="maf")
     layers, draws, x, ctx = _setup(spec)
     params = _batched_params(draws, "cuda")
     calls = []
@@ -493,14 +503,16 @@ def test_lp_batched_fused_ar_paper_shape(_gpu, P, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ctx_kind,B", [("rows", 1500), ("vec", 700), ("rows", 64)])
-def test_lp_and_grad_fused_maf_backward_vs_oracle(_gpu, ctx_kind, B):
+@pytest.mark.parametrize("D,ctx_kind,B", [(2, "rows", 1500), (2, "vec", 700), (2, "rows", 64), (4, "rows", 1300),
+                                          (4, "vec", 64)])
+def test_lp_and_grad_fused_maf_backward_vs_oracle(_gpu, D, ctx_kind, B):
     """The NUTS potential's gradient on the fused maf backward (maf_grad.py: the inverse kernel
     with saved states, made_ar_bwd_kernel per layer, batch-reduction dW) at the paper shape (D=2 |
-    C=2, H=[150]x3) vs the fp64 oracle's torch autograd (ref32 = its fp32 run), vs the training
-    walk, graph replay vs eager, and new weights through the replay; ragged row counts."""
+    C=2, H=[150]x3) and the 4-parameter Bayesian MAF (D=4, calibrate_4p.py:75, hmc_maf_exact.py:
+    101-133) vs the fp64 oracle's torch autograd with jnp.clip's gradient (ref32 = its fp32 run),
+    vs the training walk, graph replay vs eager, and new weights through the replay; ragged rows."""
     from naz_amd.flows import bflow_maf as BM
-    spec = dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=3, P=2, B=B, ctx=ctx_kind)
+    spec = dict(flow_type="maf", D=D, C=2, hidden=[150, 150, 150], L=3, P=2, B=B, ctx=ctx_kind, clip_grad="zero")
     layers, draws, x, ctx = _setup(spec, seed=11)
     flow = _flow(spec, layers, x, ctx, "cuda")
     assert flow["grad_fused"], "the paper shape must take the fused maf backward"
@@ -554,12 +566,14 @@ def test_lp_and_grad_fused_maf_backward_vs_oracle(_gpu, ctx_kind, B):
 
 
 @pytest.mark.gpu
-def test_lp_and_grad_fused_full_size_properties(_gpu):
-    """The §8f rank-1 workload (paper shape, L=16, 2^16 training rows, per-row contexts): the fused
-    potential and gradient are finite, the potential bitwise reproducible, the gradient equal up to
-    the dW reductions' summation order, and the potential equals the fused log-density's sum."""
+@pytest.mark.parametrize("D", [2, 4])
+def test_lp_and_grad_fused_full_size_properties(_gpu, D):
+    """The §8f rank-1 workload (paper shape D=2 and the 4-parameter Bayesian MAF D=4, L=16, 2^16
+    training rows, per-row contexts): the fused potential and gradient are finite, the potential
+    bitwise reproducible, the gradient equal up to the dW reductions' summation order, and the
+    potential equals the fused log-density's sum."""
     from naz_amd.flows import bflow_maf as BM
-    spec = dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=16, P=1, B=1 << 16, ctx="rows")
+    spec = dict(flow_type="maf", D=D, C=2, hidden=[150, 150, 150], L=16, P=1, B=1 << 16, ctx="rows")
     layers, draws, x, ctx = _setup(spec, seed=5)
     flow = _flow(spec, layers, x, ctx, "cuda")
     assert flow["grad_fused"]
@@ -577,3 +591,80 @@ def test_lp_and_grad_fused_full_size_properties(_gpu):
     ref = ops.ar_flow_log_prob(mg.desc, ops.ar_flow_pack_batched(mg.desc, p[None], mg.perms, mask=mg.mask)[0],
                                xd, cd)
     assert torch.equal(lp_rows, ref), "the training forward must be the log_prob kernel's arithmetic"
+
+
+def _oracle_grad(spec, layers, d, x, ctx, dtype, clip_grad):
+    """Σ_rows log p and its gradient (ravel order) from the oracle's torch autograd."""
+    st = {}
+    for l, lay in enumerate(d):
+        for i, (W, b) in enumerate(lay):
+            st[f"layers.{l}.nn.layers.{i}.weight"] = torch.tensor(W, dtype=dtype, requires_grad=True)
+            st[f"layers.{l}.nn.layers.{i}.bias"] = torch.tensor(b, dtype=dtype, requires_grad=True)
+        st[f"layers.{l}.nn.permutation"] = torch.tensor(layers[l][1])
+    f = O.build_flow(dict(spec, clip_grad=clip_grad), st, dtype)
+    cc = torch.tensor(ctx, dtype=dtype)
+    cc = cc.expand(len(x), -1) if cc.dim() == 1 else cc
+    lp = f.log_prob(torch.tensor(x, dtype=dtype), cc).sum()
+    lp.backward()
+    g = torch.cat([t.grad.reshape(-1) for l in range(len(d)) for i in range(len(d[0]))
+                   for t in (st[f"layers.{l}.nn.layers.{i}.weight"], st[f"layers.{l}.nn.layers.{i}.bias"])])
+    return lp.item(), g.numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [2, 4])
+def test_lp_and_grad_clip_gradient_is_jnp_clip(_gpu, D):
+    """the reference's JAX MAF clips log_scale with jnp.clip (bflow_jax_maf.py:177,188,
+    192), whose gradient is ZERO outside [-5, 3]; pyro's clamp_preserve_gradients (naz's torch maf)
+    passes it through.  Weights that drive many log_scales past the clip: the NUTS gradient (fused
+    and walk) follows jnp.clip, and differs from the pass-through gradient; NormalizingFlow's maf
+    NLL gradient keeps pyro's semantics."""
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import bflow_maf as BM
+    from naz_amd.flows import io as fio
+    from tests.parity import grad_floor
+    spec = dict(flow_type="maf", D=D, C=2, hidden=[150, 150, 150], L=3, P=1, B=900, ctx="rows")
+    layers, draws, x, ctx = _setup(spec, seed=13)
+    d = [[(W, b) for (W, b) in lay] for lay in draws[0]]
+    for lay in d:  # log_scale rows (D..2D-1) of the output layer: large weights and biases
+        W, b = lay[-1]
+        W, b = W.copy(), b.copy()
+        W[D:] *= 40.0
+        b[D:] += np.where(np.arange(D) % 2 == 0, 4.0, -5.5)
+        lay[-1] = (W, b)
+    flat = BM.ravel([[(torch.tensor(W, dtype=torch.float32, device="cuda"),
+                       torch.tensor(b, dtype=torch.float32, device="cuda")) for (W, b) in lay] for lay in d])
+    flow = _flow(spec, layers, x, ctx, "cuda")
+    assert flow["grad_fused"]
+    total, grad = flow["lp_and_grad"](flat, use_graph=False)
+    walk = _flow(spec, layers, x, ctx, "cuda", fused_grad=False)
+    t_w, g_w = walk["lp_and_grad"](flat, use_graph=False)
+    lp64, g64 = _oracle_grad(spec, layers, d, x, ctx, torch.float64, "zero")
+    lp32, g32 = _oracle_grad(spec, layers, d, x, ctx, torch.float32, "zero")
+    _, gp64 = _oracle_grad(spec, layers, d, x, ctx, torch.float64, "preserve")
+    # the case is exercised: the two clip semantics give visibly different gradients
+    assert np.abs(g64 - gp64).max() > 1e-2 * np.abs(g64).max()
+    assert abs(total.item() - lp64) / abs(lp64) < 1e-5
+    assert_parity(grad.cpu().numpy(), g64, g32, what="fused NUTS gradient (jnp.clip)", floor=grad_floor(g64),
+                  count_factor=None)
+    assert_parity(g_w.cpu().numpy(), g64, g32, what="walk NUTS gradient (jnp.clip)", floor=grad_floor(g64),
+                  count_factor=None)
+    # naz's torch maf (train's loss) keeps clamp_preserve_gradients
+    nf = NormalizingFlow("maf", None, D, 2, [150, 150, 150], spec["L"])
+    st = {}
+    for l, lay in enumerate(d):
+        for i, (W, b) in enumerate(lay):
+            st[f"layers.{l}.nn.layers.{i}.weight"] = W.astype(np.float32)
+            st[f"layers.{l}.nn.layers.{i}.bias"] = b.astype(np.float32)
+        st[f"layers.{l}.nn.permutation"] = np.asarray(layers[l][1])
+    fio.load_state(nf, st)
+    nf = nf.to("cuda")
+    lp = nf.log_prob(torch.tensor(x, device="cuda"), condition=torch.tensor(ctx, device="cuda")).sum()
+    lp.backward()
+    gn = torch.cat([t.grad.reshape(-1) for tr in nf.flow_dist.transforms for lin in tr.nn.layers
+                    for t in (lin.weight, lin.bias)]).cpu().numpy()
+    mask = torch.cat([t.reshape(-1) for tr in nf.flow_dist.transforms for lin in tr.nn.layers
+                      for t in (lin.mask, torch.ones_like(lin.bias))]).cpu().numpy()
+    _, gp32 = _oracle_grad(spec, layers, d, x, ctx, torch.float32, "preserve")
+    assert_parity(gn * mask, gp64, gp32, what="NormalizingFlow maf NLL gradient (pyro clamp)",
+                  floor=grad_floor(gp64), count_factor=None)

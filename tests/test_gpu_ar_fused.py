@@ -24,6 +24,8 @@ CASES = [
     dict(flow_type="nsa", D=4, C=2, hidden=[128, 128], L=3, K=8, n=1200),  # bench --flow nsa
     dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=16, n=3000),  # the maf paper shape
     dict(flow_type="maf", D=16, C=32, hidden=[128, 128], L=4, n=700),
+    # the 4-parameter Bayesian MAF (calibrate_4p.py:75,90-96)
+    dict(flow_type="maf", D=4, C=2, hidden=[150, 150, 150], L=16, n=2500),
 ]
 
 
@@ -107,6 +109,7 @@ SAMPLE_CASES = [
     dict(flow_type="nsa", D=4, C=2, hidden=[128, 128], L=3, K=8),
     dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=16),
     dict(flow_type="maf", D=16, C=32, hidden=[128, 128], L=3),
+    dict(flow_type="maf", D=4, C=2, hidden=[150, 150, 150], L=16),  # the 4-parameter Bayesian MAF
     # naz's 4-parameter MLE MAF (train_mle_all_data_4param.py:87-92): the wide forward-only instance
     dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=18),
 ]
@@ -298,16 +301,25 @@ def test_fused_ar_full_size_properties_nsa16():
         _full_size_properties(fwd, z, c, "nsa16 sample")
 
 
-def test_fused_ar_full_size_properties_maf_paper():
-    """The maf paper shape (D=2 | C=2, H=[150]x3, L=16) at 2^20 rows, log_prob."""
-    spec = dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=16)
+@pytest.mark.parametrize("D", [2, 4])
+def test_fused_ar_full_size_properties_maf_paper(D):
+    """The maf paper shape (D=2 | C=2, H=[150]x3, L=16) and the 4-parameter Bayesian MAF (D=4) at
+    2^20 rows, log_prob and sample."""
+    spec = dict(flow_type="maf", D=D, C=2, hidden=[150, 150, 150], L=16)
     f, _ = _flow(spec)
     assert f.fused
     B = 1 << 20
-    x = torch.as_tensor(O.gaussian_mixture(B, 2, seed=23), device=DEV)
+    x = torch.as_tensor(O.gaussian_mixture(B, D, seed=23), device=DEV)
     c = torch.as_tensor(O.context_normal(B, 2, seed=24), device=DEV)
     with torch.no_grad():
-        _full_size_properties(lambda a, b: f.log_prob(a, condition=b), x, c, "maf log_prob")
+        _full_size_properties(lambda a, b: f.log_prob(a, condition=b), x, c, f"maf D={D} log_prob")
+        if D == 4:
+            z = torch.randn(B, D, device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+
+            def fwd(a, b):
+                y, ld = f._plan.sample(a, b, with_logdet=True)
+                return torch.cat([y, ld[:, None]], 1)
+            _full_size_properties(fwd, z, c, f"maf D={D} sample")
 
 
 def test_wide_maf_forward_only_plan_and_log_prob():

@@ -379,3 +379,25 @@ def test_cnf_dopri5_max_steps_raises():
         f.log_prob(x, condition=c)
     f.transforms[0].strict = False
     assert f.log_prob(x, condition=c).shape == (64,)
+
+
+@pytest.mark.parametrize("mfma", ["auto", "f32"])
+@pytest.mark.parametrize("name", ["cnf_refode_d4c2.npz", "cnf_refode_d16c0.npz"])
+def test_cnf_kernel_vs_reference_odeint(name, mfma):
+    """The HIP FFJORD block solve against the REFERENCE'S OWN solver and trace estimator (naz's
+    neural_odes odeint.py RK4 + cnf.py trace_df_dz_hutchinson, run in the build container by
+    oracle/gen_refode_fixtures.py): 8 RK4 steps t 0 -> 1 (log_prob) and 1 -> 0 (sample), probe
+    fixed per solve; ref32 = the reference run in float32."""
+    from naz_amd import ops
+    fx = load_golden(name)
+    spec, state = _spec_state(fx)
+    f = _product_cnf(spec, state)
+    t = f.transforms[0]
+    t.noise = _cuda(fx["eps"])
+    t._plan.set_mfma(mfma)
+    c = _cuda(fx["ctx"]) if "ctx" in fx else None
+    tt = t.condition(c) if c is not None else t
+    for direction, (t0, t1), v in (("inv", (0.0, 1.0), fx["x"]), ("fwd", (1.0, 0.0), fx["z"])):
+        y, a = tt._solve(_cuda(v), t0, t1, None, ops.LD_ROWSUM)
+        assert_parity(_np(y), fx[f"{direction}_x64"], fx[f"{direction}_x32"], what=f"{name} {direction} x ({mfma})")
+        assert_parity(_np(a), fx[f"{direction}_a64"], fx[f"{direction}_a32"], what=f"{name} {direction} a ({mfma})")

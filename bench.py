@@ -643,7 +643,7 @@ def run_flow_case(args, dev, rank, world, dist):
     fl_row = fl_ref
     plan_ = getattr(f, "_plan", None)
     ar_fused = (ftype in ("nsa", "maf") and plan_ is not None and hasattr(plan_, "executed_flop_per_row") and
-                (args.sample or plan_.inverse))  # the wide MAFs fuse the sampling direction only
+                (args.sample or plan_.inverse))  # (a forward-only instance would take the per-layer inverse)
     if ar_fused and not args.sample:  # the fused autoregressive kernel's executed work (made_ar_r16.h)
         fl_row = f._plan.executed_flop_per_row()
     elif ftype != "nsc":  # executed work of the degree-scheduled inverse (padded blocks included)
@@ -1094,10 +1094,30 @@ def run_log_prob(args, dev, rank, world, dist):
     kern_ms = [a.elapsed_time(b) for a, b in evs]
     avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
 
+    # the same K steps through the Python front end naz callers use (NormalizingFlow.log_prob,
+    # naz flow.py:45-79: condition, distribution, pack-version check, output allocation), timed the
+    # same way after the raw-ABI loop
+    with torch.no_grad():
+        for _ in range(2):
+            flow.log_prob(x, condition=c)
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            lp_api = flow.log_prob(x, condition=c)
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        api_elapsed = time.perf_counter() - t1
+    api_same = bool(torch.equal(lp_api, out))
+
     if dist is not None:
-        t = torch.tensor([elapsed, avg_kern_s], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, avg_kern_s, api_elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, avg_kern_s = float(t[0]), float(t[1])
+        elapsed, avg_kern_s, api_elapsed = float(t[0]), float(t[1]), float(t[2])
 
     if rank == 0:
         total_rows = G * args.steps
@@ -1141,6 +1161,9 @@ def run_log_prob(args, dev, rank, world, dist):
                                    mode, "coupling_x6_kernel") + f"<16,32,8,8,128,lower,inv,{mode}>",
                          "flop_per_row": flops_per_row(), "avg_kernel_ms": avg_kern_s * 1e3,
                          "hbm_alg_GBps": bytes_per_row() * B / avg_kern_s / 1e9},
+            "api_log_prob": {"path": "NormalizingFlow.log_prob(x, condition=ctx) under torch.no_grad (naz flow.py:45-79)",
+                             "ms_per_step": api_elapsed / args.steps * 1e3, "value": total_rows / api_elapsed,
+                             "unit": "samples/s", "same_result_as_abi": api_same},
         }
         if world == 1 and not args.no_cpu_baseline:
             base, parity = cpu_baseline(flow, x_host, c_host)

@@ -247,6 +247,18 @@ int naz_coupling_log_prob(const naz_coupling_desc* d, const void* packed, const 
 int naz_coupling_sample(const naz_coupling_desc* d, const void* packed, const float* z, int64_t ldz,
                         const float* ctx, int64_t ldc, const float* low, const float* high, float* y, int64_t ldy,
                         float* out_ld, int64_t B, void* stream);
+/* ONE layer of the same image (SURVEY §8b naz_coupling_layer_{fwd,inv}; replaces pyro
+ * SplineCoupling._call / ._inverse of one naz transform, transforms.py:113-129,201-236, as the
+ * per-Transform protocol calls it: t(x), t.inv(y)): layer `layer` of the packed flow (mode
+ * NAZ_MFMA_F16X3_R16), fwd: y = T_l(x), inv: y = T_l^{-1}(x); ld [B] receives the layer's FORWARD
+ * log|det J| at the pre-image (pyro's log_abs_det_jacobian) by ld_mode NAZ_LD_ROWSUM (=),
+ * NAZ_LD_ROWSUM_ADD (+=) or NAZ_LD_ROWSUM_SUB (-=).  One launch; no bounding, no base density. */
+int naz_coupling_layer_fwd(const naz_coupling_desc* d, const void* packed, int layer, const float* x, int64_t ldx,
+                           const float* ctx, int64_t ldc, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
+                           void* stream);
+int naz_coupling_layer_inv(const naz_coupling_desc* d, const void* packed, int layer, const float* x, int64_t ldx,
+                           const float* ctx, int64_t ldc, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
+                           void* stream);
 
 /* ---- a10 over a3: the fused NLL training step of the coupling flow ----------------
  * Replaces the autograd walk of train's loss.backward() (naz/trainers/train_flows.py:195,208)
@@ -364,10 +376,12 @@ typedef struct naz_ar_desc {
  * bflow_jax_maf.py:177,188,192, whose potential NUTS differentiates) instead of pyro's
  * clamp_preserve_gradients (identity gradient: naz's torch maf, transforms.py:133-160). */
 #define NAZ_AR_CLIP_ZERO_GRAD 1
-/* 1: both directions fused (log_prob + sample); 2: the forward (sample) direction only — the
- * wide production MAFs (D=4 | C=2, H=[512]x5), whose log_prob keeps the per-layer path and whose
- * inverse-direction entry points (packed_bytes, pack_host, pack, log_prob*) report the shape as
- * unsupported; 0: not instantiated */
+/* 1: both directions fused (log_prob + sample); 2: the forward (sample) direction only (the
+ * inverse-direction entry points report the shape as unsupported; no instance today); 0: not
+ * instantiated.  The wide production MAFs (D=4 | C=2, H=[512]x5) are 1 since ABI 2's round 4:
+ * their log_prob is the persistent-grid wide inverse (one launch; it allocates its per-wave
+ * scratch stream-ordered, 128 KB per resident wave), without the pass-0-constants form
+ * (naz_ar_flow_pass0_floats < 0) and without a fused backward. */
 int naz_ar_flow_supported(const naz_ar_desc* d);
 int64_t naz_ar_flow_packed_bytes(const naz_ar_desc* d);
 /* deg[u] (u < H) = mask index of hidden unit u in every hidden layer (pyro create_mask) */

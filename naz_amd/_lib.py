@@ -81,6 +81,10 @@ SIGNATURES = {
     "naz_coupling_bwd_layer": (C.c_int, [C.POINTER(CouplingDesc), _vp, _vp, _vp, _i, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp, _i64, _vp]),
     "naz_coupling_dp3_columns": (C.c_int, [C.POINTER(CouplingDesc), _vp]),
+    "naz_coupling_layer_fwd": (C.c_int, [C.POINTER(CouplingDesc), _vp, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i,
+                                         _i64, _vp]),
+    "naz_coupling_layer_inv": (C.c_int, [C.POINTER(CouplingDesc), _vp, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i,
+                                         _i64, _vp]),
     "naz_cnf_supported": (C.c_int, [C.POINTER(CnfDesc)]),
     "naz_cnf_param_count": (C.c_int64, [C.POINTER(CnfDesc)]),
     "naz_cnf_packed_bytes": (C.c_int64, [C.POINTER(CnfDesc)]),

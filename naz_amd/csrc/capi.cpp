@@ -300,6 +300,28 @@ int naz_coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const
 
 int naz_coupling_dp3_columns(const naz_coupling_desc* d, int* rows) { return coupling_dp3_columns(d, rows); }
 
+static int coupling_layer_api(const char* what, const naz_coupling_desc* d, int inv, const void* packed, int layer,
+                              const float* x, int64_t ldx, const float* ctx, int64_t ldc, float* y, int64_t ldy,
+                              float* ld, int ld_mode, int64_t B, void* stream) {
+  if (B < 0) return set_error("%s: negative batch", what);
+  if (B > 0 && (packed == nullptr || x == nullptr || y == nullptr || ld == nullptr))
+    return set_error("%s: null pointer", what);
+  if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr) return set_error("%s: conditional flow needs ctx", what);
+  return coupling_layer(d, inv, packed, layer, x, ldx, ctx, ldc, y, ldy, ld, ld_mode, B, as_stream(stream));
+}
+int naz_coupling_layer_fwd(const naz_coupling_desc* d, const void* packed, int layer, const float* x, int64_t ldx,
+                           const float* ctx, int64_t ldc, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
+                           void* stream) {
+  return coupling_layer_api("naz_coupling_layer_fwd", d, 0, packed, layer, x, ldx, ctx, ldc, y, ldy, ld, ld_mode, B,
+                            stream);
+}
+int naz_coupling_layer_inv(const naz_coupling_desc* d, const void* packed, int layer, const float* x, int64_t ldx,
+                           const float* ctx, int64_t ldc, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
+                           void* stream) {
+  return coupling_layer_api("naz_coupling_layer_inv", d, 1, packed, layer, x, ldx, ctx, ldc, y, ldy, ld, ld_mode, B,
+                            stream);
+}
+
 int naz_ar_flow_supported(const naz_ar_desc* d) { return ar_flow_supported(d); }
 int64_t naz_ar_flow_packed_bytes(const naz_ar_desc* d) { return ar_flow_packed_bytes(d); }
 int naz_ar_flow_degrees(const naz_ar_desc* d, int* deg) { return ar_flow_degrees(d, deg); }

@@ -1303,9 +1303,11 @@ __global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_x6_kernel(
 }  // namespace naz
 
 #include "coupling_r16.h"
+#include "coupling_w32.h"
 #include "coupling_train.h"
 #include "made_ar_r16.h"
 #include "made_ar_bwd.h"
+#include "made_ar_wide.h"
 
 namespace naz {
 
@@ -1365,6 +1367,10 @@ struct CouplingOps {
       const int64_t grid = (B + kR16Rows - 1) / kR16Rows;
       hipLaunchKernelGGL((coupling_r16_kernel<G, INV>), dim3((unsigned)grid), dim3(kR16Rows * 4), lds, s, pk, L, x,
                          ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound);
+    } else if constexpr (X6 == 3) {  // f16x3 image: the 32-row-wave kernel (coupling_w32.h)
+      const int64_t grid = (B + kX6Rows - 1) / kX6Rows;
+      hipLaunchKernelGGL((coupling_w32_kernel<G, INV>), dim3((unsigned)grid), dim3(kX6Rows * 2), lds, s, pk, L, x,
+                         ldx, ctx, ldc, low, high, out_lp, y, ldy, B, bound);
     } else if constexpr (X6 == 1) {
       const int64_t grid = (B + kX6Rows - 1) / kX6Rows;
       hipLaunchKernelGGL((coupling_x6_kernel<G, INV>), dim3((unsigned)grid), dim3(kX6Rows * 2), lds, s, pk, L, x,
@@ -1421,6 +1427,28 @@ struct CouplingOps {
       return -2;
     }
   }
+  // naz_coupling_layer_{fwd,inv}: one layer of the r16 image
+  static int layer(bool inv, int mode, const void* packed, int l, int L, const float* x, int64_t ldx, const float* ctx,
+                   int64_t ldc, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B, float bound, hipStream_t s) {
+    if constexpr (R16OK) {
+      if (mode != NAZ_MFMA_F16X3_R16)
+        return set_error("naz_coupling_layer: the packed image must be NAZ_MFMA_F16X3_R16 (mode %d)", mode);
+      if (B == 0) return 0;
+      (void)L;
+      const float* pk = reinterpret_cast<const float*>(packed) + (int64_t)l * CR::LAYER;
+      const int64_t grid = (B + kR16Rows - 1) / kR16Rows;
+      const size_t lds = (size_t)CR::MAXSTAGE * 4;
+      if (inv)
+        hipLaunchKernelGGL((coupling_r16_kernel<CR, true, 2>), dim3((unsigned)grid), dim3(kR16Rows * 4), lds, s, pk,
+                           1, x, ldx, ctx, ldc, nullptr, nullptr, ld, y, ldy, B, bound, nullptr, ld_mode);
+      else
+        hipLaunchKernelGGL((coupling_r16_kernel<CR, false, 2>), dim3((unsigned)grid), dim3(kR16Rows * 4), lds, s, pk,
+                           1, x, ldx, ctx, ldc, nullptr, nullptr, ld, y, ldy, B, bound, nullptr, ld_mode);
+      return check_launch("coupling_r16_kernel<layer>");
+    } else {
+      return set_error("naz_coupling_layer: no 16-row instantiation for this shape");
+    }
+  }
   static int dp3_columns(int* rows) {
     if constexpr (R16OK) {
       using BW = BwdR16<CR>;
@@ -1445,7 +1473,13 @@ struct CouplingOps {
     else if (mode == NAZ_MFMA_F16X3_R16) {
       if constexpr (R16OK) NAZ_RUN(CR, 2);
       else return -2;
-    } else NAZ_RUN(CH, 1);
+    } else {
+#ifdef NAZ_F16X3_X6  // A/B: the round-1 32-row kernel on the same image
+      NAZ_RUN(CH, 1);
+#else
+      NAZ_RUN(CH, 3);
+#endif
+    }
 #undef NAZ_RUN
     return check_launch("coupling_flow_kernel");
   }
@@ -1585,6 +1619,20 @@ int coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const voi
   return rc == -2 ? unsupported(d) : rc;
 }
 
+int coupling_layer(const naz_coupling_desc* d, int inv, const void* packed, int layer, const float* x, int64_t ldx,
+                   const float* ctx, int64_t ldc, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
+                   hipStream_t s) {
+  if (d == nullptr) return set_error("naz_coupling_layer: null descriptor");
+  if (layer < 0 || layer >= d->L) return set_error("naz_coupling_layer: layer %d out of range", layer);
+  if (ld_mode != NAZ_LD_ROWSUM && ld_mode != NAZ_LD_ROWSUM_ADD && ld_mode != NAZ_LD_ROWSUM_SUB)
+    return set_error("naz_coupling_layer: ld_mode must be NAZ_LD_ROWSUM, _ADD or _SUB");
+  int rc = coupling_dispatch(d, [&](auto ops) {
+    return decltype(ops)::layer(inv != 0, d->mfma_mode, packed, layer, d->L, x, ldx, ctx, ldc, y, ldy, ld, ld_mode, B,
+                                d->bound, s);
+  });
+  return rc == -2 ? unsupported(d) : rc;
+}
+
 int coupling_dp3_columns(const naz_coupling_desc* d, int* rows) {
   int rc = coupling_dispatch(d, [&](auto ops) { return decltype(ops)::dp3_columns(rows); });
   return rc == -2 ? unsupported(d) : rc;
@@ -1674,29 +1722,74 @@ struct AROps {
   }
 };
 
-// wide affine MADE, forward (sample) direction only (CfgARW): the inverse-direction entry points
-// report the shape as unsupported, so log_prob keeps the degree-scheduled per-layer path
+// wide affine MADE (CfgARW): the sampler over CfgARF's image, log_prob over CfgARIW's
+// (made_ar_wide.h: the persistent-grid inverse with hidden layers 2.. in per-wave scratch)
+static int device_cu_count() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 template <class CW>
 struct AROpsW {
   using FW = CfgARF<CW>;
-  static int64_t layer_floats() { return -1; }
+  using IW = CfgARIW<CW>;
+  static int64_t layer_floats() { return IW::LAYER; }
   static int degrees(int* deg) {
     for (int u = 0; u < CW::H; ++u) deg[u] = CW::deg(u);
     return 0;
   }
-  static int inverse_unsupported() {
-    return set_error("naz_ar_flow: D=%d C=%d H=%d x %d: fused forward (sample) direction only", CW::D, CW::C, CW::H,
-                     CW::NHID);
+  static constexpr int64_t per() { return ARIWFlat<IW>::per(); }
+  static int pack_host(const float* flat, const int* perm, int L, float* out) {
+    for (int l = 0; l < L; ++l) {
+      bool seen[32] = {};
+      for (int p = 0; p < CW::D; ++p) {
+        const int v = perm[l * CW::D + p];
+        if (v < 0 || v >= CW::D || seen[v]) return set_error("naz_ar_flow_pack: layer %d: bad permutation", l);
+        seen[v] = true;
+      }
+      made_ar_pack_wide_layer<IW>(flat + l * per(), perm + l * CW::D, out + (int64_t)l * IW::LAYER);
+    }
+    return 0;
   }
-  static int pack_host(const float*, const int*, int, float*) { return inverse_unsupported(); }
-  template <class... A>
-  static int log_prob(A...) { return inverse_unsupported(); }
+  static int log_prob(const float* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
+                      const float* low, const float* high, float* out_lp, int64_t B, float, hipStream_t s,
+                      int64_t P = 1, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0, int c0mode = 0,
+                      float* states = nullptr) {
+    if (c0mode) return set_error("naz_ar_flow: D=%d H=%d x %d: no pass-0 constants form", CW::D, CW::H, CW::NHID);
+    if (states != nullptr)
+      return set_error("naz_ar_flow_log_prob_train: D=%d H=%d x %d: no fused backward", CW::D, CW::H, CW::NHID);
+    if (B == 0 || L == 0 || P == 0) return 0;
+    const int64_t tiles = (B + 16 * IW::NW - 1) / (16 * IW::NW) * P;
+    const int64_t grid = std::min<int64_t>(tiles, device_cu_count());
+    const size_t bytes = (size_t)grid * IW::NW * IW::SCRATCH_U4 * sizeof(u32x4);
+    void* scratch = nullptr;
+    if (hipMallocAsync(&scratch, bytes, s) != hipSuccess)
+      return set_error("naz_ar_flow_log_prob: %zu B of per-wave scratch not available", bytes);
+    const size_t lds = (size_t)2 * IW::STG * 4;
+    hipLaunchKernelGGL((made_ar_inv_wide_kernel<IW>), dim3((unsigned)grid), dim3(64 * IW::NW), lds, s, packed, L, x,
+                       ldx, ctx, ldc, low, high, out_lp, B, P, spk, sx, slp, static_cast<u32x4*>(scratch));
+    const int rc = check_launch("made_ar_inv_wide_kernel");
+    (void)hipFreeAsync(scratch, s);
+    return rc;
+  }
   static int64_t pass0_floats() { return -1; }
-  template <class... A>
-  static int pack_device(A...) { return inverse_unsupported(); }
-  static constexpr int64_t per() {
-    return (int64_t)CW::H * (CW::C + CW::D) + CW::H + (int64_t)(CW::NHID - 1) * (CW::H * CW::H + CW::H) +
-           (int64_t)CW::D * CW::P * CW::H + CW::D * CW::P;
+  static int pack_device(const float* flat, int64_t sflat, const int* perm, float* packed, int64_t spk, int L,
+                         int64_t P, hipStream_t s, const float* c0 = nullptr, int64_t = 0,
+                         const float* mask = nullptr) {
+    if (c0 != nullptr) return set_error("naz_ar_flow_pack: D=%d H=%d x %d: no pass-0 constants form", CW::D, CW::H,
+                                        CW::NHID);
+    if (L == 0 || P == 0) return 0;
+    if (P > 65535 || L > 65535) return set_error("naz_ar_flow_pack: at most 65535 draws / layers per call");
+    const dim3 grid((unsigned)((IW::LAYER + 255) / 256), (unsigned)L, (unsigned)P);
+    hipLaunchKernelGGL((made_ar_pack_wide_kernel<IW>), grid, dim3(256), 0, s, flat, sflat, perm, packed, spk, mask);
+    return check_launch("made_ar_pack_wide_kernel");
   }
   static int64_t fwd_layer_floats() { return FW::LAYER; }
   static int64_t flat_floats() { return per(); }
@@ -1728,6 +1821,11 @@ struct AROpsW {
 template <class F>
 static int ar_dispatch(const naz_ar_desc* d, F&& f) {
   if (d == nullptr || d->act != NAZ_ACT_TANH || d->L < 0) return -2;
+#ifdef NAZ_AR_ONLY_WIDE  // resource experiments on the wide instance alone (minutes instead of ten)
+  if (d->kind == NAZ_AR_AFFINE && d->D == 4 && d->C == 2 && d->H == 512 && d->n_hidden == 5)
+    return f(AROpsW<CfgARW<4, 2, 512, 5>>{});
+  return -2;
+#endif
   if (d->kind == NAZ_AR_SPLINE) {
     if (d->K != 8 || d->H != 128 || d->n_hidden != 2 || !(d->bound > 0.f)) return -2;
     if (d->D == 16 && d->C == 32) return f(AROps<CfgAR<16, 32, 128, 8>>{});
@@ -1743,7 +1841,7 @@ static int ar_dispatch(const naz_ar_desc* d, F&& f) {
     // the 4-parameter Bayesian MAF (calibrate_4p.py:75,90-96; hmc_maf_exact.py:101-133)
     if (d->D == 4 && d->C == 2 && d->H == 150 && d->n_hidden == 3) return f(AROps<CfgAR<4, 2, 150, 8, 3, true>>{});
     if (d->D == 16 && d->C == 32 && d->H == 128 && d->n_hidden == 2) return f(AROps<CfgAR<16, 32, 128, 8, 2, true>>{});
-    // naz's production MAFs (4-parameter MLE, POSYDON): forward direction only (AROpsW)
+    // naz's production MAFs (4-parameter MLE, POSYDON; AROpsW: the wide sampler and inverse)
     if (d->D == 4 && d->C == 2 && d->H == 512 && d->n_hidden == 5) return f(AROpsW<CfgARW<4, 2, 512, 5>>{});
     return -2;
   }
@@ -1998,3 +2096,12 @@ int ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* 
 #endif  // part 3
 
 }  // namespace naz
+
+#if NAZ_PART == 9  // register-allocation experiments on one wide-inverse instance (not built by build.py)
+#ifndef NAZ_EXP_NHID
+#define NAZ_EXP_NHID 5
+#endif
+template __global__ void naz::made_ar_inv_wide_kernel<naz::CfgARIW<naz::CfgARW<4, 2, 512, NAZ_EXP_NHID>>>(
+    const float*, int, const float*, int64_t, const float*, int64_t, const float*, const float*, float*, int64_t,
+    int64_t, int64_t, int64_t, int64_t, naz::u32x4*);
+#endif

@@ -354,7 +354,9 @@ __global__ void __launch_bounds__(kR16Rows * 4, NAZ_R16_TRAIN_WAVES_PER_SIMD_SEL
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound,
-    float* __restrict__ states = nullptr) {
+    float* __restrict__ states = nullptr, int layer_ld_mode = NAZ_LD_ROWSUM) {
+  // VAR 2 (naz_coupling_layer_{fwd,inv}): ONE layer (`packed` at its image, L = 1), y to yout and
+  // the layer's FORWARD log|det J| per row to out_lp by layer_ld_mode (=, +=, -=); no base density
   extern __shared__ float4 lds4[];
   float* const slot0 = reinterpret_cast<float*>(lds4);
   float* const slot1 = slot0 + kX6Slot;
@@ -666,7 +668,22 @@ __global__ void __launch_bounds__(kR16Rows * 4, NAZ_R16_TRAIN_WAVES_PER_SIMD_SEL
     }
   }
 
-  if constexpr (DIR_INV) {
+  if constexpr (VAR == 2) {
+    if (valid) {
+#pragma unroll
+      for (int u = 0; u < CF::SQ; ++u) yout[row * ldy + q * CF::SQ + u] = zl[u];
+#pragma unroll
+      for (int u = 0; u < CF::DQ; ++u) yout[row * ldy + CF::S + q * CF::DQ + u] = zu[u];
+    }
+    float v = ldsum;
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (q == 0 && valid) {
+      if (layer_ld_mode == NAZ_LD_ROWSUM_ADD) out_lp[row] += v;
+      else if (layer_ld_mode == NAZ_LD_ROWSUM_SUB) out_lp[row] -= v;
+      else out_lp[row] = v;
+    }
+  } else if constexpr (DIR_INV) {
     constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
     float base = 0.f;
 #pragma unroll

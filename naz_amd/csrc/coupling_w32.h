@@ -1,0 +1,300 @@
+// 32-row-wave fused coupling flow on v_mfma_f32_32x32x16_f16 (NAZ_MFMA_F16X3; included by
+// coupling.hip after the x6 kernel, whose packed image — CfgX6<..., P23 = 2> — it reads).
+//
+// Why (round 4): the 16-row r16 kernel is bound by its SIMDs' VECTOR-ISSUE port, not by the matrix
+// pipe.  Its PMC (profiles/pmc_r03_headline.json) puts SQ_ACTIVE_INST_VALU (one quad-cycle per VALU
+// instruction, two per transcendental) at 70 % of the kernel's cycles on every SIMD, and each
+// v_mfma_f32_16x16x32_f16 holds that port for 8 of its 16 cycles (MI355X_MICROARCH.md, the
+// vector-instruction issue-cost row): 2,304 MFMAs per wave = another 26 %.  A
+// v_mfma_f32_32x32x16_f16 does twice the work for the same 8-cycle hold, so 32-row waves halve
+// the MFMA share of the port (and the A-fragment LDS reads per row) for the same VALU work per row.
+//
+// Layout (the x6 kernel's): lane l owns batch row l & 31 and lane-half h = l >> 5 of that row's
+// dims (lower [h SH, h SH + SH), upper [h DH, h DH + DH)).  Accumulator register i of a 32-feature
+// block on half h = feature acc_row(i, h); the B operand of 16-k step t on half h, element j =
+// feature hid16_feature(t, j, h) = the lane's own registers 8 (t & 1) .. + 7 of block t >> 1, so
+// layers chain in registers.  GEMM3's rows are permuted so half h receives the 3K - 1 parameters
+// of its own DH upper dims (x6_out_row).
+// Versus coupling_x6_kernel on the same image: the context's B fragments are split once per launch
+// (the context is the same for every layer), GEMM2/3 activate and split each k-step's 8 values just
+// before its MFMAs (VALU interleaved with the matrix work instead of a burst at the stage head),
+// the context is loaded before the first barrier, and GEMM stages run at wave priority 1.
+// Precision: f16x3 (the x6 image's f16 pieces); GEMM1 runs the exact-split bf16x6 image for a
+// workgroup whose context or data values reach 2^15 (as the x6 kernel).
+#pragma once
+
+namespace naz {
+
+// k-steps [T0, T0 + KB) of one GEMM over the activated accumulators x (lazy: each k-step's 8
+// values are activated and split right before its MFMAs)
+template <int NB, int KB, int T0, int NX>
+NAZ_DEV void gemm_w32_lazy(floatx16 (&acc)[NB], const float* __restrict__ stage, int lane, floatx16 (&x)[NX]) {
+  const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
+#pragma unroll
+  for (int t = 0; t < KB; ++t) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = NAZ_TANH(x[(T0 + t) >> 1][8 * ((T0 + t) & 1) + j]);
+    const Frag2 b = split8_f16(v);
+#ifdef NAZ_ABL_NOGEMM
+    for (int o = 0; o < NB; ++o) acc[o][0] += (float)b.h[0] * 1e-30f;
+    continue;
+#endif
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const int base = ((o * KB + t) * 2) * 64 + lane;
+      const Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+      acc[o] = mfma3(a, b, acc[o]);
+    }
+  }
+}
+
+template <class CF, bool DIR_INV>
+__global__ void __launch_bounds__(kX6Rows * 2, kX6Waves / 2) coupling_w32_kernel(
+    const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
+    const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
+    float* __restrict__ out_lp, float* __restrict__ yout, int64_t ldy, int64_t B, float bound) {
+  static_assert(CF::F16, "coupling_w32_kernel runs the f16x3 image");
+  extern __shared__ float4 lds4[];
+  float* const slot0 = reinterpret_cast<float*>(lds4);
+  float* const slot1 = slot0 + kX6Slot;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int h = lane >> 5;
+  const int64_t row = (int64_t)blockIdx.x * kX6Rows + wave * 32 + (lane & 31);
+  const bool valid = row < B;
+  const int64_t crow = valid ? row : 0;
+
+  float zl[CF::SH], zu[CF::DH];
+  float ldsum = 0.f, logjac = 0.f;
+#pragma unroll
+  for (int q = 0; q < CF::SH; ++q) zl[q] = valid ? x[crow * ldx + h * CF::SH + q] : 0.f;
+#pragma unroll
+  for (int q = 0; q < CF::DH; ++q) zu[q] = valid ? x[crow * ldx + CF::S + h * CF::DH + q] : 0.f;
+  if (DIR_INV && low != nullptr) {  // naz bounding_transform (transforms.py:20-23)
+    auto bnd = [&](float& v, int dim) {
+      const float lo = low[dim], hi = high[dim];
+      const float u = (v - lo) / (hi - lo);
+      logjac -= logf(u) + log1pf(-u);
+      v = logf(u / (1.f - u));
+    };
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) bnd(zl[q], h * CF::SH + q);
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) bnd(zu[q], CF::S + h * CF::DH + q);
+    if (h == 0) {
+      float sl = 0.f;
+      for (int d = 0; d < CF::D; ++d) sl += logf(high[d] - low[d]);
+      logjac -= sl;
+    }
+  }
+
+  // this lane's context columns of GEMM1's context k-steps: the same for every layer
+  constexpr int CT1 = CF::CT > 0 ? CF::CT : 1;  // (no context: unused)
+  float cv[CT1 * 8];
+#pragma unroll
+  for (int t = 0; t < CF::CT; ++t)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int c = 16 * t + 8 * h + jj;
+      cv[8 * t + jj] = c < CF::C ? ctx[crow * ldc + c] : 0.f;
+    }
+  // GEMM1 precision path of this workgroup (fp16 pieces when every context / data value of its
+  // rows is inside kG1F16Limit; x1 stays inside max(|x|, bound) through the lower splines), ANDed
+  // through ring slot 1 (unused until the first in-loop barrier)
+  bool ok = bound < kG1F16Limit;
+#pragma unroll
+  for (int q = 0; q < CF::SH; ++q) ok = ok && fabsf(zl[q]) < kG1F16Limit;
+#pragma unroll
+  for (int q = 0; q < CF::DH; ++q) ok = ok && fabsf(zu[q]) < kG1F16Limit;
+#pragma unroll
+  for (int k = 0; k < CF::CT * 8; ++k) ok = ok && fabsf(cv[k]) < kG1F16Limit;
+  {
+    int* flags = reinterpret_cast<int*>(slot1);
+    if (lane == 0) flags[wave] = __all(ok) ? 1 : 0;
+    __syncthreads();
+    bool all_ok = true;
+#pragma unroll
+    for (int w = 0; w < kX6Waves; ++w) all_ok = all_ok && flags[w] != 0;
+    ok = all_ok;
+  }
+  const bool g1f16 = ok;
+  const int a_off = g1f16 ? CF::A16_OFF : 0;
+  // the context's f16 B fragments, split once (f16 path)
+  Frag2 cfr[CT1];
+#pragma unroll
+  for (int t = 0; t < CF::CT; ++t) {
+    float v[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) v[jj] = cv[8 * t + jj];
+    cfr[t] = split8_f16(v);
+  }
+
+  stage_issue<CF::A_SIZE, kX6Waves>(slot0, packed + (int64_t)(DIR_INV ? (L - 1) : 0) * CF::LAYER + a_off);
+
+  const RqsConsts<CF::K, DIR_INV> rc(bound);
+  int g = 0;  // global stage counter: stage g lives in slot (g & 1)
+  for (int li = 0; li < L; ++li) {
+    const int l = DIR_INV ? (L - 1 - li) : li;
+    const float* lp = packed + (int64_t)l * CF::LAYER;
+    const float* lnext = packed + (int64_t)(DIR_INV ? (l - 1) : (l + 1)) * CF::LAYER;
+    floatx16 acc1[CF::HB], acc2[CF::HB], acc3[CF::NO];
+
+    static_for<0, CF::NSTG>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      ring_barrier();  // stage j has landed in slot (g & 1); every wave is done with the other slot
+      const float* cur = (g & 1) ? slot1 : slot0;
+      float* nxt = (g & 1) ? slot0 : slot1;
+      if constexpr (j + 1 < CF::NSTG) {
+        stage_issue<CF::stage_size(j + 1), kX6Waves>(nxt, lp + CF::stage_off(j + 1));
+      } else {
+        if (li + 1 < L) stage_issue<CF::A_SIZE, kX6Waves>(nxt, lnext + a_off);
+      }
+      ++g;
+
+      if constexpr (j == 0) {
+        // ---------------- stage A: lower spline (inverse), GEMM1 over [ctx | x1]
+#pragma unroll
+        for (int q = 0; q < CF::SH; ++q) {
+#ifndef NAZ_ABL_NOLOWER
+          if constexpr (DIR_INV && CF::LOWER) {
+            float ld;
+            zl[q] = rqs_table<CF::K, true>(cur + CF::A_TBL + (h * CF::SH + q) * CF::TBL, zl[q], bound, ld);
+            ldsum -= ld;
+          }
+#endif
+        }
+        init_bias<CF::HB>(acc1, cur + CF::A_BIAS, h);
+        if (g1f16) {
+          Frag2 xf[CF::XT];
+#pragma unroll
+          for (int t = 0; t < CF::XT; ++t) {
+            float v[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+              const int q = 8 * t + jj;
+              v[jj] = q < CF::SH ? zl[q < CF::SH ? q : 0] : 0.f;
+            }
+            xf[t] = split8_f16(v);
+          }
+          const u32x4* c4 = reinterpret_cast<const u32x4*>(cur);
+          R16_PRIO(1);
+#pragma unroll
+          for (int t = 0; t < CF::KS0; ++t)
+#pragma unroll
+            for (int o = 0; o < CF::HB; ++o) {
+              const int base = ((o * CF::KS0 + t) * 2) * 64 + lane;
+              const Frag2 a{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
+              acc1[o] = mfma3(a, t < CF::CT ? cfr[t < CF::CT ? t : 0] : xf[t >= CF::CT ? t - CF::CT : 0], acc1[o]);
+            }
+          R16_PRIO(0);
+        } else {
+          // exact-split bf16x6 GEMM1 (the x6 image at offset 0; the context reloaded: a rare path)
+          Frag3 bf[CF::KS0];
+#pragma unroll
+          for (int t = 0; t < CF::KS0; ++t) {
+            float v[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+              if (t < CF::CT) {
+                const int c = 16 * t + 8 * h + jj;
+                v[jj] = c < CF::C ? ctx[crow * ldc + c] : 0.f;
+              } else {
+                const int q = 8 * (t - CF::CT) + jj;
+                v[jj] = q < CF::SH ? zl[q < CF::SH ? q : 0] : 0.f;
+              }
+            }
+            bf[t] = split8(v);
+          }
+          gemm_x6_stage<CF::HB, CF::KS0>(acc1, cur, lane, bf);
+        }
+        if constexpr (!DIR_INV && CF::LOWER) {
+#pragma unroll
+          for (int q = 0; q < CF::SH; ++q) {
+            float ld;
+            zl[q] = rqs_table<CF::K, false>(cur + CF::A_TBL + (h * CF::SH + q) * CF::TBL, zl[q], bound, ld);
+            ldsum += ld;
+          }
+        }
+      } else if constexpr (j <= CF::NB2) {
+        // ---------------- stage B_s: GEMM2 k-steps [T0, T0 + KB2), activation per k-step
+        constexpr int s = j - 1, T0 = s * CF::KB2;
+        if constexpr (s == 0) init_bias<CF::HB>(acc2, cur + CF::B_BIAS, h);
+        R16_PRIO(1);
+        gemm_w32_lazy<CF::HB, CF::KB2, T0>(acc2, cur, lane, acc1);
+        R16_PRIO(0);
+      } else {
+        // ---------------- stage C_s: GEMM3 k-steps [T0, T0 + KB3) -> raw spline parameters
+        constexpr int s = j - 1 - CF::NB2, T0 = s * CF::KB3;
+        if constexpr (s == 0) init_bias<CF::NO>(acc3, cur + CF::C_BIAS, h);
+        R16_PRIO(1);
+        gemm_w32_lazy<CF::NO, CF::KB3, T0>(acc3, cur, lane, acc2);
+        R16_PRIO(0);
+      }
+    });
+
+    // ---------------- upper spline on this lane's DH dims (the next layer's stage A is in flight)
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) {
+      float uw[CF::K], uh[CF::K], ud[CF::K - 1];
+#pragma unroll
+      for (int k = 0; k < CF::K; ++k) {
+        const int sw = q * CF::P + k, sh = q * CF::P + CF::K + k;
+        uw[k] = acc3[sw >> 4][sw & 15];
+        uh[k] = acc3[sh >> 4][sh & 15];
+      }
+#pragma unroll
+      for (int k = 0; k < CF::K - 1; ++k) {
+        const int sd = q * CF::P + 2 * CF::K + k;
+        ud[k] = acc3[sd >> 4][sd & 15];
+      }
+#ifdef NAZ_ABL_NOSPLINE
+      float sacc = 0.f;
+#pragma unroll
+      for (int k = 0; k < CF::K; ++k) sacc += uw[k] + uh[k];
+      zu[q] += 1e-30f * sacc;
+#else
+      float ld;
+      zu[q] = rqs_select<CF::K, DIR_INV>(uw, uh, ud, zu[q], bound, rc, ld);
+      ldsum += DIR_INV ? -ld : ld;
+#endif
+    }
+  }
+
+  if constexpr (DIR_INV) {
+    constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+    float base = 0.f;
+#pragma unroll
+    for (int q = 0; q < CF::SH; ++q) base += -(zl[q] * zl[q]) / 2.f - kLogSqrt2Pi;
+#pragma unroll
+    for (int q = 0; q < CF::DH; ++q) base += -(zu[q] * zu[q]) / 2.f - kLogSqrt2Pi;
+    float v = base - ldsum + logjac;
+    v += __shfl_xor(v, 32);
+    if (h == 0 && valid) out_lp[row] = v;
+  } else {
+    if (low != nullptr) {
+#pragma unroll
+      for (int q = 0; q < CF::SH; ++q) {
+        const int d = h * CF::SH + q;
+        zl[q] = (1.f / (1.f + expf(-zl[q]))) * (high[d] - low[d]) + low[d];
+      }
+#pragma unroll
+      for (int q = 0; q < CF::DH; ++q) {
+        const int d = CF::S + h * CF::DH + q;
+        zu[q] = (1.f / (1.f + expf(-zu[q]))) * (high[d] - low[d]) + low[d];
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int q = 0; q < CF::SH; ++q) yout[row * ldy + h * CF::SH + q] = zl[q];
+#pragma unroll
+      for (int q = 0; q < CF::DH; ++q) yout[row * ldy + CF::S + h * CF::DH + q] = zu[q];
+    }
+    if (out_lp != nullptr) {
+      float v = ldsum + __shfl_xor(ldsum, 32);
+      if (h == 0 && valid) out_lp[row] = v;
+    }
+  }
+}
+
+}  // namespace naz

@@ -44,6 +44,94 @@ constexpr int ar_round_half_even(double v) {
 
 constexpr int kARCap = 20480;  // floats per ring slot at most (2 slots = 160 KB, one workgroup per CU)
 
+// The inverse select-first spline of ONE dim per row, spread over the row's four lanes (quarters q
+// = lane >> 4 of the 16-row MFMA layout) instead of evaluated four times.  The output blocks of
+// the dim's 3K - 1 = 23 parameters leave parameter 16 o + 4 q + i in register i of block o on
+// quarter q: widths 0-3 | 4-7 on quarters 0 | 1, heights 0-3 | 4-7 on quarters 2 | 3 (block 0),
+// slope parameters 0-3 | 4-6 on quarters 0 | 1 (block 1).  Each quarter forms the softmax
+// numerators, prefix sums and knots of ITS half-table (4 exps instead of 16), the bin index is
+// counted on the height quarters (the inverse searches the y knots) and shared, and every quarter
+// assembles the selected bin's knots and slopes through xor-16 (partner half-table) and xor-32
+// (other table) exchanges, then evaluates the bin — the same arithmetic as rqs_select<K, true>
+// (same knot formula, prefix sums in the same order), so the map and log-det agree with it to
+// the rounding of the split prefix sums.  All four lanes of a row return the same value.
+template <int K>
+NAZ_DEV float rqs_select_inv_quad(const floatx4& b0, const floatx4& b1, int q, float y, float bound,
+                                  const RqsConsts<K, true>& rc, float& ld) {
+  static_assert(K == 8, "the quarter layout holds 8 bins: two half-tables of 4 per table");
+  constexpr float kL2E = 1.44269504088896341f;
+  const int qh = q & 1;          // half-table: knots 1-4 (0) or 5-8 (1)
+  const bool hq = q >= 2;        // this quarter holds heights (the searched table)
+  // softmax numerators of this half-table, max over the whole table
+  float m = fmaxf(fmaxf(b0[0], b0[1]), fmaxf(b0[2], b0[3]));
+  m = fmaxf(m, __shfl_xor(m, 16));
+  const float ml = m * kL2E;
+  // E[i] = cumulative numerator through knot 4 qh + i + 1, summed in rqs_select's order (the
+  // upper half-table continues from the lower one's total), so the knots are bit-identical to it
+  float e[4], E[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(b0[i], kL2E, -ml));
+  const float lower_total = __shfl_xor(((e[0] + e[1]) + e[2]) + e[3], 16);  // used by the upper half
+  {
+    float p = qh ? lower_total : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      p = (qh || i > 0) ? p + e[i] : e[i];
+      E[i] = p;
+    }
+  }
+  // (every cross-lane read below runs on all lanes, outside any select: a shuffle in a divergent
+  // branch reads the inactive source lanes' stale values)
+  const float upper_end = __shfl_xor(E[3], 16);
+  const float S = qh ? E[3] : upper_end;  // the table's total E_K (the upper half's end)
+  const float A = rc.cA * Math<true>::rcp(S);
+  // bin index: interior height knots 1..7 with y >= A E_k + key_k (the upper half-table's knot 8 is
+  // the box edge, not searched)
+  int cnt = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = 4 * qh + i + 1;
+    const float key = __builtin_fmaf(A, E[i], __builtin_fmaf(rc.ms, (float)k, rc.nb) + kSearchEps);
+    cnt += (k < K && y >= key) ? 1 : 0;
+  }
+  cnt += __shfl_xor(cnt, 16);
+  const int cnt_h = __shfl_xor(cnt, 32);
+  const int idx = hq ? cnt : cnt_h;  // the height quarters' count, on every quarter
+  const bool first = idx == 0, last = idx == K - 1;
+  // this table's knots of bin idx: E[idx] and E[idx + 1] (E_0 = 0) from their owner half-table
+  auto pick = [&](int n) {  // the table's cumulative numerator through knot n (1 <= n <= 8)
+    const int j = (n - 1) & 3;
+    const float mine = j == 0 ? E[0] : (j == 1 ? E[1] : (j == 2 ? E[2] : E[3]));
+    const float theirs = __shfl_xor(mine, 16);
+    return ((n - 1) >> 2) == qh ? mine : theirs;
+  };
+  const float p0 = pick(first ? 1 : idx), e1 = pick(idx + 1);
+  const float e0 = first ? 0.f : p0;
+  const float fi = (float)idx;
+  const float c0 = __builtin_fmaf(A, e0, __builtin_fmaf(rc.ms, fi, rc.nb));
+  const float c1 = last ? bound : __builtin_fmaf(A, e1, __builtin_fmaf(rc.ms, fi + 1.f, rc.nb));
+  const float c0o = __shfl_xor(c0, 32), c1o = __shfl_xor(c1, 32);
+  const float cs0 = hq ? c0 : c0o, cs1 = hq ? c1 : c1o;  // y (height) knots
+  const float co0 = hq ? c0o : c0, co1 = hq ? c1o : c1;  // x (width) knots
+  // slope parameters ud[idx - 1], ud[idx] from quarters 0 | 1 (block 1)
+  auto pick_ud = [&](int n) {  // 0 <= n <= 6
+    const int j = n & 3;
+    const float mine = j == 0 ? b1[0] : (j == 1 ? b1[1] : (j == 2 ? b1[2] : b1[3]));
+    const float theirs = __shfl_xor(mine, 16);
+    const float pair = ((n >> 2) == qh) ? mine : theirs;
+    const float v = __shfl_xor(pair, 32);
+    return hq ? v : pair;
+  };
+  const float udl = pick_ud(first ? 0 : idx - 1), udh = pick_ud(last ? 0 : idx);
+  const float d0 = first ? 1.f - kMinDerivative : kMinDerivative + softplus<true>(udl);
+  const float d1 = last ? 1.f - kMinDerivative : kMinDerivative + softplus<true>(udh);
+  float lb;
+  const float x = rqs_bin<true>(y, co0, co1 - co0, cs0, cs1 - cs0, d0, d1, lb);
+  const bool inside = y >= -bound && y <= bound;
+  ld = inside ? lb : 0.f;
+  return inside ? x : y;
+}
+
 template <int D_, int C_, int H_, int K_, int NHID_ = 2, bool AFFINE_ = false>
 struct CfgAR {
   static constexpr int D = D_, C = C_, H = H_, K = K_, NHID = NHID_;
@@ -450,6 +538,13 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
             xmax = fmaxf(xmax, fabsf(v[dp]));
             ldsum += ls;
           } else {
+#ifndef NAZ_AR_SPLINE_GATHER
+            // one spline per row spread over its four quarters (rqs_select_inv_quad)
+            float ld;
+            v[dp] = rqs_select_inv_quad<K>(o3[0], o3[CF::NOB > 1 ? 1 : 0], q, y, bound, rc, ld);
+            ldsum -= ld;
+#else
+            // (A/B) every quarter gathers the row's parameters and evaluates the whole spline:
             // parameter pi sits in block pi >> 4, register pi & 3 of quarter (pi & 15) >> 2
             float uw[K], uh[K], ud[K - 1];
 #pragma unroll
@@ -462,6 +557,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
             float ld;
             v[dp] = rqs_select<K, true>(uw, uh, ud, y, bound, rc, ld);
             ldsum -= ld;
+#endif
           }
         }
       });

@@ -81,6 +81,9 @@ int coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const voi
                        const float* g_lp, float* h1, float* h2, float* dp1, float* dp2, float* dp3, float* x0,
                        float* g_out, float* g_low, int64_t B, hipStream_t s);
 int coupling_dp3_columns(const naz_coupling_desc* d, int* rows);
+int coupling_layer(const naz_coupling_desc* d, int inv, const void* packed, int layer, const float* x, int64_t ldx,
+                   const float* ctx, int64_t ldc, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
+                   hipStream_t s);
 
 int ar_flow_supported(const naz_ar_desc* d);
 int64_t ar_flow_packed_bytes(const naz_ar_desc* d);

@@ -296,7 +296,8 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
             # one context vector: the first degree pass (units of mask index 0 see only the
             # context; the first dim's outputs see only them) is a per-draw constant, computed
             # once per draw below and packed in place of that pass's weights
-            if C > 0 and fold_context and int((torch.as_tensor(ops.ar_flow_degrees(ar_desc)) == 0).sum()):
+            if C > 0 and fold_context and ops.ar_flow_pass0_floats(ar_desc) > 0 and \
+                    int((torch.as_tensor(ops.ar_flow_degrees(ar_desc)) == 0).sum()):
                 ar_pass0 = ArPass0(ar_desc, [int(p_[0]) for p_ in pm], act, dev)
 
     def _chunks(P, rows, max_draws=65535):

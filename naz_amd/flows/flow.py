@@ -157,7 +157,7 @@ class _FusedAR:
     checked against them once per parameter change."""
 
     can_sample = True  # sample(): naz_ar_flow_sample (the forward direction, one launch)
-    inverse = True  # log_prob fused too (False for the forward-only wide instances: per-layer log_prob)
+    inverse = True  # log_prob fused too (False for a forward-only instance: per-layer log_prob)
     F16_DATA_LIMIT = 32768.0  # the kernel's f16x3 input split (|x|, |ctx| < 2^15)
 
     def __init__(self, layers: List[nn.Module], kind: str, D: int, C: int, H: int, n_hidden: int, K: int, act: str,
@@ -316,12 +316,18 @@ class _FusedAR:
             self._p0sig = sig
         return self._p0
 
+    def _pass0_form(self) -> bool:
+        """The instance has the pass-0-constants image (the wide H = 512 inverse does not)."""
+        if getattr(self, "_p0form", None) is None:
+            self._p0form = ops.ar_flow_pass0_floats(self.desc) > 0
+        return self._p0form
+
     def log_prob(self, x, context=None, bounds=None, out=None):
         low = high = None
         if bounds is not None:
             low, high = bounds["low"].to(x.device, torch.float32), bounds["high"].to(x.device, torch.float32)
         if (_AR_PASS0 and bounds is None and self.shape[1] > 0 and context is not None and x.dim() == 2 and
-                x.shape[0] >= 4096 and (context.dim() == 1 or context.shape[0] == 1)):
+                x.shape[0] >= 4096 and (context.dim() == 1 or context.shape[0] == 1) and self._pass0_form()):
             # one condition vector (the density grid): the context-only first degree pass once,
             # packed as constants in place of its weights (naz_ar_flow_pack pass0)
             flat, mask, perm, p0 = self._pass0_operands()

@@ -27,6 +27,10 @@ from .. import ops
 from ..nn import (AutoRegressiveNN, ConditionalAutoRegressiveNN, ConditionalDenseNN, DenseNN, cache_epoch)
 from ..utils import device, set_device
 
+# per-Transform spline-coupling calls on the fused one-layer kernel (naz_coupling_layer_{fwd,inv});
+# NAZ_LAYER_FUSED=0 keeps the per-kernel chain (naz_linear_act + naz_rqs)
+_LAYER_FUSED = __import__("os").environ.get("NAZ_LAYER_FUSED", "1") != "0"
+
 __all__ = ["TransformModule", "ConditionalTransformModule", "ComposeTransformModule",
            "ConditionalComposeTransformModule", "Spline", "SplineCoupling", "ConditionalSplineCoupling",
            "SplineAutoregressive", "ConditionalSplineAutoregressive", "AffineAutoregressive",
@@ -212,6 +216,46 @@ class Spline(TransformModule):
         return ld
 
 
+def _fused_coupling_layer(m, v, inverse, context, ld_buf, ld_mode):
+    """One spline-coupling layer as ONE naz_coupling_layer_{fwd,inv} launch for the
+    per-Transform protocol (pyro's t(x) / t.inv(y)): the conditioner, the lower and upper splines and
+    the log-det fused, on the module's own one-layer 16-row f16x3 image (re-packed when a parameter
+    changes).  None where it does not apply (autograd recording, dropout active, a shape without a
+    16-row instantiation, per-dim log-dets): the per-kernel chain runs."""
+    if (v.dim() != 2 or ld_mode not in (ops.LD_ROWSUM, ops.LD_ROWSUM_ADD, ops.LD_ROWSUM_SUB) or v.requires_grad
+            or (torch.is_grad_enabled() and any(p.requires_grad for p in m.parameters()))):
+        return None
+    net = m.nn
+    if not isinstance(net, ConditionalDenseNN) or net.dropout_active() or len(net.hidden_dims) != 2 or \
+            net.hidden_dims[0] != net.hidden_dims[1]:
+        return None
+    C = net.context_dim
+    if C and (context is None or context.dim() > 2 or (context.dim() == 2 and context.shape[0] not in (1, v.shape[0]))):
+        return None
+    plan = m.__dict__.get("_layer_plan")
+    if plan is None:
+        from .flow import _FusedCoupling
+        plan = _FusedCoupling([m], m.input_dim, C, m.split_dim, m.count_bins, net.hidden_dims[0], net.act,
+                              m.lower_spline is not None, m.bound, mfma="f16x3r16")
+        if not ops.coupling_supported(plan.desc):
+            plan = False
+        m.__dict__["_layer_plan"] = plan
+    if plan is False:
+        return None
+    packed = plan.packed()
+    if plan.mode != "f16x3r16":
+        return None
+    # the ABI reports the layer's FORWARD log-det; the per-kernel chain's inverse modes act on the
+    # inverse's (its negation): swap += and -= for the inverse direction
+    mode = ld_mode
+    if inverse and ld_mode != ops.LD_ROWSUM:
+        mode = ops.LD_ROWSUM_SUB if ld_mode == ops.LD_ROWSUM_ADD else ops.LD_ROWSUM_ADD
+    if inverse and ld_mode == ops.LD_ROWSUM:
+        return None
+    ctx = None if not C else (context.reshape(1, -1) if context.dim() == 1 else context)
+    return ops.coupling_layer(plan.desc, packed, 0, v, ctx, inverse, ld_buf, mode)
+
+
 class _ConditionedSplineCoupling(_LDCache, Transform):
     """[pyro] SplineCoupling with the hypernet bound to a context (naz/flows/transforms.py:126-129)."""
 
@@ -230,6 +274,10 @@ class _ConditionedSplineCoupling(_LDCache, Transform):
 
     def _map(self, v, inverse: bool, ld_buf, ld_mode):
         m = self.module
+        if _LAYER_FUSED:
+            y = _fused_coupling_layer(m, v, inverse, self.context, ld_buf, ld_mode)
+            if y is not None:
+                return y
         s = m.split_dim
         out = torch.empty_like(v)
         v1, v2 = v[:, :s], v[:, s:]

@@ -567,6 +567,26 @@ def coupling_log_prob(d: CouplingDesc, packed: Tensor, x: Tensor, context: Optio
     return out
 
 
+def coupling_layer(d: CouplingDesc, packed: Tensor, layer: int, x: Tensor, context: Optional[Tensor], inverse: bool,
+                   ld_out: Tensor, ld_mode: int = LD_ROWSUM, out: Optional[Tensor] = None) -> Tensor:
+    """ONE coupling layer of a packed flow (naz_coupling_layer_{fwd,inv}): y = T_layer(x) or its
+    inverse; ld_out [B] gets the layer's FORWARD log|det J| by ld_mode (=, +=, -=)."""
+    dev = _dev(packed, x, context, ld_out, out)
+    x, ldx = _rows(x)
+    B = x.shape[0]
+    context, ldc = _ctx_arg(context, B)
+    if ld_out.shape != (B,) or not ld_out.is_contiguous() or ld_out.dtype != torch.float32:
+        raise ValueError(f"coupling_layer: ld_out must be a contiguous float32 [{B}] tensor")
+    if out is None:
+        out = torch.empty((B, d.D), device=dev, dtype=torch.float32)
+    if out.dim() != 2 or out.shape != (B, d.D) or out.stride(1) != 1:
+        raise ValueError(f"coupling_layer: out must be [{B}, {d.D}] with unit column stride")
+    fn = lib().naz_coupling_layer_inv if inverse else lib().naz_coupling_layer_fwd
+    check(fn(d, _p(packed), int(layer), _p(x), ldx, _p(context), ldc, _p(out), out.stride(0), _p(ld_out), int(ld_mode),
+             B, _stream(dev)), "coupling_layer")
+    return out
+
+
 # ----------------------------------------------------------------------------- §8b naz_{spline,affine}_ar_inv
 AR_KIND = {"nsa": 0, "maf": 1}  # NAZ_AR_SPLINE, NAZ_AR_AFFINE
 AR_CLIP_ZERO_GRAD = 1  # naz_ar_desc.flags: NAZ_AR_CLIP_ZERO_GRAD
@@ -607,7 +627,8 @@ def ar_executed_flop_per_row(d: ArDesc) -> dict:
 
       inverse  made_ar_r16_kernel (log_prob): per pass p, hidden layer 1's blocks holding units of
                degree p over [ctx | x], the further hidden layers' over the units of degree <= p,
-               and the output blocks of dim p (made_ar_r16.h; f16x3);
+               and the output blocks of dim p (made_ar_r16.h; f16x3); the wide H = 512 instances
+               (made_ar_inv_wide_kernel) recompute ALL of hidden layer 1's degree <= p blocks;
       bwd      made_ar_bwd_kernel, all layers (maf only): one dense MADE pass plus D chains
                (W_out^T g on the VALU in fp32, the W_i^T chain and the input unit on f16x3);
       dw       the batched weight-gradient reductions over the padded operands (bf16x6).
@@ -619,12 +640,14 @@ def ar_executed_flop_per_row(d: ArDesc) -> dict:
     blk = 16 * 32 * 2  # one 16-unit block over one 32-deep k-step, per row
     deg = ar_flow_degrees(d)
     E = [int((deg <= p).sum()) for p in range(D)]
+    wide = HP > 256  # made_ar_wide.h: hidden layer 1 recomputed in full (blocks of degree <= p) every pass
     inv = 0
     for p in range(D):
         e0 = E[p - 1] if p else 0
         nb = ((E[p] - 1) >> 4) - (e0 >> 4) + 1 if E[p] > e0 else 0
+        nb1 = (((E[p] - 1) >> 4) + 1 if E[p] > 0 else 0) if wide else nb
         kt = (E[p] + 31) // 32
-        inv += (nb * (KI + (NH - 1) * kt) + NOB * kt) * blk
+        inv += (nb1 * KI + nb * (NH - 1) * kt + NOB * kt) * blk
     out = {"inverse": inv * L}
     if d.kind == AR_KIND["maf"] and int(lib().naz_ar_flow_bwd_packed_bytes(d)) > 0:
         X0W = ar_flow_bwd_dims(d)["X0W"]

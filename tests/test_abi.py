@@ -34,16 +34,19 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_ar_flow_supported_contract():
-    """naz_ar_flow_supported: 1 = both directions fused, 2 = the sampling direction only (the
-    wide production MAFs), 0 = not instantiated; the inverse entry points of a 2-shape report it."""
+    """naz_ar_flow_supported: 1 = both directions fused, 2 = the sampling direction only (no
+    instance today), 0 = not instantiated.  The wide production MAFs (H = [512] x 5) are fused both
+    ways since round 4 (made_ar_wide.h), without the pass-0-constants form."""
     from naz_amd import _lib, ops
     L = _lib.lib()
     assert L.naz_ar_flow_supported(ops.ar_flow_desc("maf", 2, 2, 150, 16, 3)) == 1
     assert L.naz_ar_flow_supported(ops.ar_flow_desc("maf", 4, 2, 150, 16, 3)) == 1  # the 4-parameter Bayesian MAF
     assert L.naz_ar_flow_supported(ops.ar_flow_desc("nsa", 16, 32, 128, 8, 2)) == 1
     wide = ops.ar_flow_desc("maf", 4, 2, 512, 18, 5)
-    assert L.naz_ar_flow_supported(wide) == 2
-    assert L.naz_ar_flow_packed_bytes(wide) < 0 and L.naz_ar_flow_fwd_packed_bytes(wide) > 0
+    assert L.naz_ar_flow_supported(wide) == 1
+    assert L.naz_ar_flow_packed_bytes(wide) > 0 and L.naz_ar_flow_fwd_packed_bytes(wide) > 0
+    assert L.naz_ar_flow_pass0_floats(wide) < 0
+    assert not ops.ar_flow_bwd_supported(wide)
     assert L.naz_ar_flow_supported(ops.ar_flow_desc("maf", 3, 2, 150, 4, 3)) == 0
     # the fused maf backward exists at both Bayesian shapes
     assert ops.ar_flow_bwd_supported(ops.ar_flow_desc("maf", 4, 2, 150, 16, 3))

@@ -10,7 +10,8 @@ from naz_amd import ops
 
 
 @pytest.mark.parametrize("kind,D,C,H,NH", [("nsa", 16, 32, 128, 2), ("nsa", 16, 0, 128, 2), ("nsa", 8, 0, 128, 2),
-                                           ("nsa", 4, 2, 128, 2), ("maf", 2, 2, 150, 3), ("maf", 16, 32, 128, 2)])
+                                           ("nsa", 4, 2, 128, 2), ("maf", 2, 2, 150, 3), ("maf", 16, 32, 128, 2),
+                                           ("maf", 4, 2, 512, 5)])
 def test_compiled_degrees_match_pyro_create_mask(kind, D, C, H, NH):
     d = ops.ar_flow_desc(kind, D, C, H, 1, NH)
     assert ops.ar_flow_supported(d)
@@ -32,7 +33,7 @@ def test_unsupported_shape_reports():
         ops.ar_flow_degrees(ops.ar_flow_desc("maf", 3, 2, 150, 1, n_hidden=3))
 
 
-@pytest.mark.parametrize("kind,D,C,H,NH", [("nsa", 16, 32, 128, 2), ("maf", 2, 2, 150, 3)])
+@pytest.mark.parametrize("kind,D,C,H,NH", [("nsa", 16, 32, 128, 2), ("maf", 2, 2, 150, 3), ("maf", 4, 2, 512, 5)])
 def test_host_pack_decodes_to_scaled_weights(kind, D, C, H, NH):
     K, L = 8, 2
     P = 2 if kind == "maf" else 3 * K - 1

@@ -26,6 +26,8 @@ CASES = [
     dict(flow_type="maf", D=16, C=32, hidden=[128, 128], L=4, n=700),
     # the 4-parameter Bayesian MAF (calibrate_4p.py:75,90-96)
     dict(flow_type="maf", D=4, C=2, hidden=[150, 150, 150], L=16, n=2500),
+    # naz's 4-parameter MLE MAF (train_mle_all_data_4param.py:87-92): the wide inverse (made_ar_wide.h)
+    dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=18, n=900),
 ]
 
 
@@ -110,7 +112,7 @@ SAMPLE_CASES = [
     dict(flow_type="maf", D=2, C=2, hidden=[150, 150, 150], L=16),
     dict(flow_type="maf", D=16, C=32, hidden=[128, 128], L=3),
     dict(flow_type="maf", D=4, C=2, hidden=[150, 150, 150], L=16),  # the 4-parameter Bayesian MAF
-    # naz's 4-parameter MLE MAF (train_mle_all_data_4param.py:87-92): the wide forward-only instance
+    # naz's 4-parameter MLE MAF (train_mle_all_data_4param.py:87-92): the wide instance
     dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=18),
 ]
 
@@ -322,28 +324,75 @@ def test_fused_ar_full_size_properties_maf_paper(D):
             _full_size_properties(fwd, z, c, f"maf D={D} sample")
 
 
-def test_wide_maf_forward_only_plan_and_log_prob():
-    """The production MAF shapes (D=4 | C=2, H=[512]x5; L=18 MLE, L=16 POSYDON) sample through
-    the fused wide kernel, while log_prob (no fused inverse at H = 512) takes the degree-scheduled
-    per-layer path: parity vs the fp64 oracle on both, and the sampler's y round-trips through
-    log_prob (base(z) - ld(z) == log_prob(y))."""
+def test_wide_maf_fused_both_directions():
+    """The production MAF shapes (D=4 | C=2, H=[512]x5; L=18 MLE, L=16 POSYDON,
+    eposydon/train_maf_mle.py:84-90) take the fused wide inverse (made_ar_inv_wide_kernel) for
+    log_prob and the fused sampler for sample: log_prob parity vs the fp64 oracle and vs the
+    degree-scheduled per-layer path, and the sampler's y round-trips through log_prob
+    (base(z) - ld(z) == log_prob(y))."""
     from naz_amd import ops
     for L in (16, 18):
         spec = dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=L)
         f, state = _flow(spec)
-        assert f.fused and f._plan.inverse is False and ops.ar_flow_fwd_supported(f._plan.desc)
-        assert not ops.ar_flow_supported(f._plan.desc)
+        assert f.fused and f._plan.inverse and ops.ar_flow_supported(f._plan.desc)
         n = 600
         x = torch.as_tensor(O.gaussian_mixture(n, 4, seed=7))
         c = torch.as_tensor(O.context_normal(n, 2, seed=8))
         with torch.no_grad():
             lp = f.log_prob(x.to(DEV), condition=c.to(DEV)).cpu().numpy()
+            f.set_fused(False)
+            lp_walk = f.log_prob(x.to(DEV), condition=c.to(DEV)).cpu().numpy()
+            f.set_fused(True)
         lp64 = O.build_flow(spec, state, torch.float64).log_prob(x.double(), c.double()).numpy()
         lp32 = O.build_flow(spec, state, torch.float32).log_prob(x, c).numpy()
-        assert_parity(lp, lp64, lp32, what=f"wide maf L={L} log_prob (per-layer path)")
+        assert_parity(lp, lp64, lp32, what=f"wide maf L={L} log_prob (fused)")
+        assert_parity(lp_walk, lp64, lp32, what=f"wide maf L={L} log_prob (per-layer path)")
         z = torch.randn(n, 4, generator=torch.Generator().manual_seed(L)).to(DEV)
         y, ld = ops.ar_flow_sample(f._plan.desc, f._plan.packed_fwd(), z, c.to(DEV), with_logdet=True)
         with torch.no_grad():
             lpy = f.log_prob(y, condition=c.to(DEV))
         rt = (lpy - (ops.base_log_prob(z) - ld)).abs() / lpy.abs().clamp_min(1.0)
         assert float(rt.max()) < 1e-4, float(rt.max())
+
+
+def test_wide_maf_persistent_grid_and_draws():
+    """The wide inverse's persistent grid (256 workgroups walking the (draw, 64-row tile) space,
+    hidden layers 2.. through per-wave scratch): a batch of several tiles per workgroup plus a
+    ragged tail against the per-layer path; one broadcast context row; an empty batch; the device
+    packer's image bit-identical to the host packer's; three weight draws in one batched launch
+    equal to three single-draw launches."""
+    from naz_amd import ops
+    spec = dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=3)
+    f, state = _flow(spec)
+    plan = f._plan
+    B = 256 * 64 * 2 + 77
+    x = torch.as_tensor(O.gaussian_mixture(B, 4, seed=31)).to(DEV)
+    c = torch.as_tensor(O.context_normal(B, 2, seed=32)).to(DEV)
+    with torch.no_grad():
+        lp = f.log_prob(x, condition=c)
+        c1 = c[5]
+        lp1 = f.log_prob(x[:3000], condition=c1)
+        empty = f.log_prob(x[:0], condition=c)
+        f.set_fused(False)
+        ref = f.log_prob(x, condition=c)
+        ref1 = f.log_prob(x[:3000], condition=c1)
+        f.set_fused(True)
+    assert empty.shape == (0,)
+    assert torch.isfinite(lp).all()
+    np.testing.assert_allclose(lp.cpu().numpy(), ref.cpu().numpy(), rtol=2e-5, atol=2e-4)
+    np.testing.assert_allclose(lp1.cpu().numpy(), ref1.cpu().numpy(), rtol=2e-5, atol=2e-4)
+    # device packer == host packer, word for word
+    flat = torch.from_numpy(plan._flat()).to(DEV)
+    perm = np.stack([n.permutation.detach().cpu().numpy() for n in plan._nets()]).astype(np.int32)
+    img_dev = ops.ar_flow_pack_batched(plan.desc, flat[None].contiguous(), perm)
+    img_host = plan.packed()
+    assert img_dev.shape[1] == img_host.numel()
+    assert torch.equal(img_dev[0].view(torch.int32), img_host.view(torch.int32))
+    # three draws (scaled weights) in one launch vs one launch each
+    flats = torch.stack([flat * s for s in (1.0, 0.9, 1.1)]).contiguous()
+    imgs = ops.ar_flow_pack_batched(plan.desc, flats, perm)
+    xs = x[:5000]
+    lpb = ops.ar_flow_log_prob_batched(plan.desc, imgs, xs, c1)
+    for p in range(3):
+        one = ops.ar_flow_log_prob(plan.desc, imgs[p].contiguous(), xs, c1)
+        np.testing.assert_array_equal(lpb[p].cpu().numpy(), one.cpu().numpy())

@@ -158,8 +158,14 @@ def _r16_ok(spec):
 
 
 @pytest.mark.parametrize("name", FLOWS)
-@pytest.mark.parametrize("fused", ["auto", "f16x3", "f16x3r16", "bf16x6", "f32", False])
-def test_flow_log_prob_vs_golden(name, fused):
+@pytest.mark.parametrize("fused", ["auto", "f16x3", "f16x3r16", "bf16x6", "f32", False, "chain"])
+def test_flow_log_prob_vs_golden(name, fused, monkeypatch):
+    """fused: the whole-flow kernel in that MFMA mode; False: the per-Transform walk (nsc layers on
+    the one-layer kernel, naz_coupling_layer_inv); "chain": the walk on the per-kernel chain."""
+    from naz_amd.flows import transforms as T
+    if fused == "chain":
+        monkeypatch.setattr(T, "_LAYER_FUSED", False)
+        fused = False
     fx = load_golden(name)
     f, spec, _ = _product_flow(fx)
     if spec["flow_type"] == "nsc":
@@ -375,3 +381,50 @@ def test_full_size_debug_probe_build_clean():
     assert res["debug_build"], res
     for t in res["trials"]:
         assert t["nonfinite_rows"] == 0 and t["record"]["hit"] == 0, res
+
+
+@pytest.mark.parametrize("name", ["nsc_d16c32_l2.npz", "nsc_d8c0_l6.npz"])
+def test_coupling_layer_per_transform_protocol(name, monkeypatch):
+    """naz_coupling_layer_{fwd,inv} through pyro's per-Transform protocol (t(x),
+    t.inv(y), log_abs_det_jacobian): every layer in both directions against the per-kernel chain
+    (naz_linear_act + naz_rqs) and the fp64 oracle's layer, and the round trip."""
+    from naz_amd import ops
+    from naz_amd.flows import transforms as T
+    fx = load_golden(name)
+    f, spec, state = _product_flow(fx)
+    of64 = O.build_flow(spec, state, torch.float64)
+    of32 = O.build_flow(spec, state, torch.float32)
+    c = _cuda(fx["ctx"]) if "ctx" in fx else None
+    pdf = f._pdf(c)
+    x = _cuda(fx["x"])
+    calls = []
+    orig = ops.coupling_layer
+    monkeypatch.setattr(ops, "coupling_layer", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    layers = [t for t in pdf.transforms if hasattr(t, "module")]
+    olayers = [l for l in of64.layers if hasattr(l, "nn")]
+    o32 = [l for l in of32.layers if hasattr(l, "nn")]
+    c64 = None if c is None else torch.as_tensor(fx["ctx"]).double()
+    c32 = None if c is None else torch.as_tensor(fx["ctx"])
+    v = x
+    with torch.no_grad():
+        for t, ol, ol32 in zip(layers, olayers, o32):
+            n0 = len(calls)
+            y = t(v)
+            ld = t.log_abs_det_jacobian(v, y)
+            xi = t._inverse(y)  # (t.inv(y) would return the cached x)
+            ld_i = t._cache_log_detJ  # the inverse call caches the forward log-det at xi
+            assert len(calls) >= n0 + 2, "the per-layer fused kernel was not used"
+            monkeypatch.setattr(T, "_LAYER_FUSED", False)
+            y_c = t._call(v)
+            ld_c = t._cache_log_detJ
+            monkeypatch.setattr(T, "_LAYER_FUSED", True)
+            y64, ld64 = ol.forward(v.double().cpu(), c64)
+            y32, ld32 = ol32.forward(v.cpu(), c32)
+            assert_parity(_np(y), y64.numpy(), y32.numpy(), what=f"{name} layer fwd y")
+            assert_parity(_np(ld), ld64.sum(-1).numpy(), ld32.sum(-1).numpy(), what=f"{name} layer fwd ld",
+                          count_factor=3.0)
+            np.testing.assert_allclose(_np(y), _np(y_c), rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(_np(ld), _np(ld_c), rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(_np(xi), _np(v), rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(_np(ld_i), _np(ld), rtol=1e-4, atol=1e-4)
+            v = y

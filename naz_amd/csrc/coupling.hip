@@ -201,6 +201,27 @@ NAZ_DEV __attribute__((address_space(3))) void* to_lds(const void* p) {
   return (__attribute__((address_space(3))) void*)(uint32_t)(uintptr_t)p;
 }
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// One 16-byte LDS read whose destination hipcc does not track (inline asm): the compiler's waitcnt
+// model treats LDS returns as out of order while an LDS-DMA (global_load_lds) is in flight — i.e.
+// always inside the ring kernels — and so waits lgkmcnt(0) before every use, including on the
+// reads just issued for the NEXT use.  Here the wait is explicit and counted (lds_wait<N>): LDS
+// reads return in order (LGKM also counts SMEM, which returns out of order: the kernels using this
+// issue none across a counted wait — tests/test_isa_ring.py's counted-wait rule — and the DMA
+// counts on vmcnt).  Users: coupling_w32.h (A fragments), made_ar_wide.h.
+template <int OFF>
+NAZ_DEV u32x4_t lds_read_b128_untracked(unsigned addr) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int N>
+NAZ_DEV void lds_wait() {
+  // s_waitcnt lgkmcnt(N), vmcnt / expcnt left at their maxima (gfx9 encoding)
+  __builtin_amdgcn_s_waitcnt(0xC07F | (N << 8));
+}
+
+
 // Asynchronous stage copy HBM/L2 -> LDS with LDS-DMA (global_load_lds_dwordx4): wave w
 // moves 1 KB chunks w, w+4, ...; no VGPRs hold the data.  Completion is published by the
 // next ring_barrier() (naz_device.h: explicit vmcnt(0), then the barrier) — never by a bare
@@ -2104,4 +2125,16 @@ int ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* 
 template __global__ void naz::made_ar_inv_wide_kernel<naz::CfgARIW<naz::CfgARW<4, 2, 512, NAZ_EXP_NHID>>>(
     const float*, int, const float*, int64_t, const float*, int64_t, const float*, const float*, float*, int64_t,
     int64_t, int64_t, int64_t, int64_t, naz::u32x4*);
+#endif
+
+#if NAZ_PART == 8  // schedule experiments on the w32 log_prob kernel alone (not built by build.py)
+template __global__ void naz::coupling_w32_kernel<naz::CfgX6<16, 32, 8, 8, 128, true, 2>, true>(
+    const float*, int, const float*, int64_t, const float*, int64_t, const float*, const float*, float*, float*,
+    int64_t, int64_t, float);
+#endif
+
+#if NAZ_PART == 7  // the wide sampler alone (not built by build.py)
+template __global__ void naz::made_ar_fwd_kernel<naz::CfgARF<naz::CfgARW<4, 2, 512, 5>>>(
+    const float*, int, const float*, int64_t, const float*, int64_t, const float*, const float*, float*, int64_t,
+    float*, int64_t, float, int64_t, int64_t, int64_t, int64_t);
 #endif

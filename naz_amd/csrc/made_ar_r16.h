@@ -43,6 +43,12 @@ constexpr int ar_round_half_even(double v) {
 }
 
 constexpr int kARCap = 20480;  // floats per ring slot at most (2 slots = 160 KB, one workgroup per CU)
+#ifndef NAZ_AR_INV_NW
+#define NAZ_AR_INV_NW 12
+#endif
+#ifndef NAZ_AR_INV_CAP
+#define NAZ_AR_INV_CAP kARCap  // the inverse's per-stage cap (CfgAR::make_layout)
+#endif
 
 // The inverse select-first spline of ONE dim per row, spread over the row's four lanes (quarters q
 // = lane >> 4 of the 16-row MFMA layout) instead of evaluated four times.  The output blocks of
@@ -183,7 +189,7 @@ struct CfgAR {
       int run = 0;
       for (int i = 0; i <= NHID; ++i) {
         const int sz = sub_floats_of(y, p, i);
-        if (i == 0 || run + sz > kARCap) {
+        if (i == 0 || run + sz > NAZ_AR_INV_CAP) {
           ++s;
           run = 0;
         }
@@ -231,11 +237,45 @@ struct CfgAR {
     return (e + 255) / 256;
   }
   static constexpr int LAYER = pad(PERM_OFF + D);
-  // waves per workgroup (one workgroup per CU): 12 (3 per SIMD) when the live set fits 168 VGPRs
-  static constexpr int NW = NHID * KSH <= 8 ? 12 : 8;
+  // waves per SIMD the inverse kernel is compiled for: 3 when the live set fits 168 VGPRs; the
+  // forward kernel's workgroup (CfgARF) keeps one workgroup per CU of 4 x WPE waves
+  static constexpr int WPE = NHID * KSH <= 8 ? 3 : 2;
+  static constexpr int NW_FWD = 4 * WPE;
+  // inverse workgroup: NAZ_AR_INV_NW waves (12: one workgroup per CU; 6 with NAZ_AR_INV_CAP =
+  // 10240: two per CU, each on its own 2 x <= 40 KB ring, so the two do not share barriers)
+  static constexpr int NW = WPE == 3 ? NAZ_AR_INV_NW : NW_FWD;
   static_assert(H <= 256 && D <= 32 && D >= 2 && NHID >= 1 && NHID <= 3, "unsupported fused autoregressive shape");
   static_assert(NOB <= 2 && NSTG <= 128, "output blocks / stages");
 };
+
+// acc += sum over t < N of (A fragment t at LDS byte address ub + 2048 t, hi | lo 1 KB apart) x
+// bset[t] on the f16x3 16-row MFMA.  Fragment t + 1 is read while fragment t's MFMAs run (untracked
+// reads with a counted wait, coupling.hip's lds_read_b128_untracked): for the one-wave-per-SIMD
+// wide MADE kernels, which have no other wave to hide an LDS read behind.
+template <int N, class BS>
+NAZ_DEV floatx4 mfma3_16_chain_lds(unsigned ub, const BS& bset, floatx4 acc) {
+  auto rd = [&](auto tc) {
+    constexpr int o = 2048 * decltype(tc)::value;
+    return Frag2{__builtin_bit_cast(half8, lds_read_b128_untracked<o>(ub)),
+                 __builtin_bit_cast(half8, lds_read_b128_untracked<o + 1024>(ub))};
+  };
+  Frag2 an = rd(std::integral_constant<int, 0>{});
+  static_for<0, N>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    const Frag2 a = an;
+    if constexpr (t + 1 < N) {
+      an = rd(std::integral_constant<int, t + 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+      lds_wait<2>();
+    } else {
+      __builtin_amdgcn_sched_barrier(0);
+      lds_wait<0>();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    acc = mfma3_16(a, bset[t], acc);
+  });
+  return acc;
+}
 
 // ---------------------------------------------------------------- host packer (ar_flow_pack)
 // flat per layer (natural layouts, masks already applied): W0m [H][C + D], b0 [H],
@@ -338,7 +378,7 @@ NAZ_DEV void ar_split4(Frag2& f, const floatx4& a) {
 }
 
 template <class CF>
-__global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_r16_kernel(
+__global__ void __launch_bounds__(64 * CF::NW, CF::WPE) made_ar_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, int64_t B, float bound, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0,
@@ -605,7 +645,7 @@ struct CfgARW {
     return ar_round_half_even(1.0 + (double)u * (double)(D - 2) / (double)(H - 1));
   }
   static constexpr int pad(int n) { return (n + 255) / 256 * 256; }
-  static constexpr int NW = 4;
+  static constexpr int NW = 4, NW_FWD = 4;
   static_assert(H > 256 && H % 32 == 0 && D >= 2 && D <= 8 && NHID >= 1, "wide MADE instances only");
 };
 
@@ -619,7 +659,7 @@ struct CfgARF {
   static constexpr int NG = (D + 3) / 4, NOG = (P + 3) / 4;
   // the forward spline's live set at D = 16 exceeds the 168 VGPRs of 12-wave workgroups (spilled
   // 352-468 B/lane): 8 waves (2 per SIMD) there
-  static constexpr int NW = (G::AFFINE || D <= 8) ? G::NW : 8;
+  static constexpr int NW = (G::AFFINE || D <= 8) ? G::NW_FWD : 8;
   static constexpr bool AFFINE = G::AFFINE;
   static constexpr int NU = NHID * HB + NG;  // units: hidden (i, b) row-major, then one per dim group
   static constexpr int unit_blocks(int u) { return u < NHID * HB ? 1 : NOG; }
@@ -1028,6 +1068,9 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
           const floatx4 ax = mfma3_16(afrag(CF::KC), xf, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(ax[r], us, acc[r]);
+        } else if constexpr (NW == 4) {  // the wide instances (one wave per SIMD): prefetched chain
+          acc = mfma3_16_chain_lds<KSH>((unsigned)(uintptr_t)to_lds(cur) + 16u * lane + 4u * OFF,
+                                        hf[(i - 1) & 1], acc);
         } else {
 #pragma unroll
           for (int t = 0; t < KSH; ++t) acc = mfma3_16(afrag(t), hf[(i - 1) & 1][t], acc);
@@ -1045,10 +1088,15 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
           const float4 bv = bias4[4 * o + q];
           o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
         }
+        if constexpr (NW == 4 && NOG == 1) {
+          o3[0] = mfma3_16_chain_lds<KSH>((unsigned)(uintptr_t)to_lds(cur) + 16u * lane + 4u * OFF,
+                                          hf[(NHID - 1) & 1], o3[0]);
+        } else {
 #pragma unroll
-        for (int t = 0; t < KSH; ++t)
+          for (int t = 0; t < KSH; ++t)
 #pragma unroll
-          for (int o = 0; o < NOG; ++o) o3[o] = mfma3_16(afrag(o * KSH + t), hf[(NHID - 1) & 1][t], o3[o]);
+            for (int o = 0; o < NOG; ++o) o3[o] = mfma3_16(afrag(o * KSH + t), hf[(NHID - 1) & 1][t], o3[o]);
+        }
         float xv = 0.f;  // this quarter's dim
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq)

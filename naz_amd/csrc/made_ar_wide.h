@@ -167,7 +167,7 @@ struct ARIWFlat {  // sub-layer offsets of one layer's flat rows (made_ar_pack_l
   static constexpr int64_t b_off(int i) {
     return w_off(i) + (int64_t)(i < CF::NHID ? CF::H : CF::D * CF::P) * (i == 0 ? CF::C + CF::D : CF::H);
   }
-  static constexpr int64_t per() { return w_off(CF::NHID + 1); }
+  static constexpr int64_t per() { return w_off(CF::NHID) + (int64_t)CF::D * CF::P * (CF::H + 1); }
 };
 
 template <class CF>
@@ -361,6 +361,9 @@ __global__ void __launch_bounds__(64 * CF::NW, 1) made_ar_inv_wide_kernel(
           return Frag2{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
         };
         const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF + CF::unit_kts(u) * CF::OT);
+        // this unit's A fragments (byte address of fragment 0 for this lane), for the prefetched
+        // MFMA chains (mfma3_16_chain_lds: one wave per SIMD has nothing else to hide LDS reads)
+        const unsigned ub = (unsigned)(uintptr_t)to_lds(cur) + 16u * lane + 4u * OFF;
         if constexpr (i == 0 && FIRST_OF_SUB) {
           // the row's values split at a per-row power-of-two scale, |x| sc < 2^14 (the inverse maps
           // grow values by up to e^5 per layer; xmax: max |v| at the layer's start and since)
@@ -401,8 +404,7 @@ __global__ void __launch_bounds__(64 * CF::NW, 1) made_ar_inv_wide_kernel(
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(ax[r], us, acc[r]);
           } else {
-#pragma unroll
-            for (int t = 0; t < KT; ++t) acc = mfma3_16(afrag(t), hf[(i - 1) & 1][t], acc);
+            acc = mfma3_16_chain_lds<KT>(ub, hf[(i - 1) & 1], acc);
           }
           ar_split4<b & 1>(hf[i & 1][b >> 1], acc);
           if constexpr (CF::stores(u) && !CF::deferred(u)) store_half(uc);
@@ -410,8 +412,7 @@ __global__ void __launch_bounds__(64 * CF::NW, 1) made_ar_inv_wide_kernel(
           // the output rows of dim d_p: (mean, log_scale) in registers 0, 1 of quarter 0
           const float4 bv = bias4[q];
           floatx4 o3 = floatx4{bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-          for (int t = 0; t < KT; ++t) o3 = mfma3_16(afrag(t), hf[(NHID - 1) & 1][t], o3);
+          o3 = mfma3_16_chain_lds<KT>(ub, hf[(NHID - 1) & 1], o3);
           const int dp = dps[p];
           const float y = v[dp];
           const float mean = __shfl(o3[0], lane & 15);

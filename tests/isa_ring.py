@@ -81,10 +81,7 @@ def is_dma(ins: str) -> bool:
     return op.startswith("global_load_lds") or (op.startswith("buffer_load") and " lds" in ins.split("//")[0])
 
 
-def ring_violations(start: int, insns: list[tuple[int, str]]) -> list[str]:
-    """Barriers reachable with an LDS-DMA in flight and no vmcnt(0) on some path."""
-    if not any(is_dma(t) for _, t in insns):
-        return []
+def _successors(start: int, insns: list[tuple[int, str]]) -> list[list[int]]:
     index = {a: k for k, (a, _) in enumerate(insns)}
     succ: list[list[int]] = []
     for k, (a, t) in enumerate(insns):
@@ -105,6 +102,13 @@ def ring_violations(start: int, insns: list[tuple[int, str]]) -> list[str]:
             succ.append(tgt if op.startswith("s_branch") else tgt + nxt)
             continue
         succ.append(nxt)
+    return succ
+
+
+def _flagged(start: int, insns: list[tuple[int, str]], sets, clears, flags) -> list[str]:
+    """Instructions `flags(text)` reachable with the state set (`sets`) and not cleared (`clears`)
+    on some path through the control-flow graph (loop back edges included)."""
+    succ = _successors(start, insns)
     pending_in = [None] * len(insns)
     work = [(0, False)]
     bad: dict[int, str] = {}
@@ -115,16 +119,45 @@ def ring_violations(start: int, insns: list[tuple[int, str]]) -> list[str]:
         pending_in[k] = bool(pending_in[k]) or st
         st = pending_in[k]
         a, t = insns[k]
-        op = t.split(None, 1)[0]
-        if op == "s_barrier" and st:
+        if st and flags(t):
             bad[a] = t
-        if op == "s_waitcnt" and "vmcnt(0)" in t:
+        if clears(t):
             st = False
-        elif is_dma(t):
+        elif sets(t):
             st = True
         for s in succ[k]:
             work.append((s, st))
     return [f"+0x{a - start:x}: {t.split('//')[0].strip()}" for a, t in sorted(bad.items())]
+
+
+def ring_violations(start: int, insns: list[tuple[int, str]]) -> list[str]:
+    """Barriers reachable with an LDS-DMA in flight and no vmcnt(0) on some path."""
+    if not any(is_dma(t) for _, t in insns):
+        return []
+    return _flagged(start, insns, sets=is_dma,
+                    clears=lambda t: t.startswith("s_waitcnt") and "vmcnt(0)" in t,
+                    flags=lambda t: t.split(None, 1)[0] == "s_barrier")
+
+
+_LGKM = re.compile(r"lgkmcnt\((\d+)\)")
+
+
+def _is_smem(t: str) -> bool:
+    op = t.split(None, 1)[0]
+    return op.startswith(("s_load", "s_buffer_load", "s_scratch_load", "s_dcache", "s_memtime", "s_memrealtime"))
+
+
+def counted_lgkm_violations(start: int, insns: list[tuple[int, str]]) -> list[str]:
+    """Counted LDS waits (s_waitcnt lgkmcnt(N), N > 0) reachable with a scalar-memory load in flight
+    since the last lgkmcnt(0): LGKM also counts SMEM, which returns out of order, so such a count
+    no longer proves the older LDS reads landed (the hand-counted waits of coupling_w32.h's
+    untracked A-fragment reads rely on this never happening)."""
+    def counted(t):
+        m = _LGKM.search(t.split("//")[0])
+        return t.startswith("s_waitcnt") and m is not None and int(m.group(1)) > 0
+    return _flagged(start, insns, sets=_is_smem,
+                    clears=lambda t: t.startswith("s_waitcnt") and "lgkmcnt(0)" in t.split("//")[0],
+                    flags=counted)
 
 
 def check_library(lib: Path, arch: str = "gfx950") -> tuple[int, dict[str, list[str]]]:

@@ -35,7 +35,7 @@ def test_unsupported_shape_reports():
 
 @pytest.mark.parametrize("kind,D,C,H,NH", [("nsa", 16, 32, 128, 2), ("maf", 2, 2, 150, 3), ("maf", 4, 2, 512, 5)])
 def test_host_pack_decodes_to_scaled_weights(kind, D, C, H, NH):
-    K, L = 8, 2
+    K, L = 8, 3
     P = 2 if kind == "maf" else 3 * K - 1
     d = ops.ar_flow_desc(kind, D, C, H, L, NH, K)
     rng = np.random.default_rng(0)
@@ -47,24 +47,28 @@ def test_host_pack_decodes_to_scaled_weights(kind, D, C, H, NH):
     ops.check(ops.lib().naz_ar_flow_pack_host(d, np.ascontiguousarray(flat).ctypes.data, perm.ctypes.data,
                                                 host.ctypes.data), "pack")
     words = host.view(np.uint32)
-    # layer 0, pass 0, first L1 fragment (block blo(0) = 0, k-step 0 = context): lane (m, kg) pair w
-    # holds W0[m][8 kg + 2w (+1)] * kSigScale as hi | lo f16 pieces
-    W0 = flat[:H * (C + D)].reshape(H, C + D)
-    ks = 2.88539008177792681
-    for lane in (0, 5, 17, 63):
-        m, kg = lane & 15, lane >> 4
-        for pair in range(4):
-            hi = words[(0 * 64 + lane) * 4 + pair]
-            lo = words[(1 * 64 + lane) * 4 + pair]
-            for e in range(2):
-                h16 = np.array([(hi >> (16 * e)) & 0xFFFF], np.uint16).view(np.float16)[0]
-                l16 = np.array([(lo >> (16 * e)) & 0xFFFF], np.uint16).view(np.float16)[0]
-                col = 8 * kg + 2 * pair + e
-                want = np.float32(ks) * W0[m, col] if col < C else np.float32(0)
-                # hi + lo carries ~22 bits; lo below f16's normal range keeps 2^-24 absolute spacing
-                assert abs((np.float32(h16) + np.float32(l16)) - want) <= 2.5e-7 * abs(want) + 3.1e-8
-    # the permutation table rides in the image (last D ints before the layer padding)
     layer_floats = nbytes // 4 // L
+    per = sum(sizes)
+    # every layer l, pass 0, first L1 fragment (block 0, k-step 0 = context): lane (m, kg) pair w
+    # holds W0[m][8 kg + 2w (+1)] * kSigScale as hi | lo f16 pieces (layer l's flat rows at l * per:
+    # a wrong per-layer stride reads another layer's — or no — weights)
+    ks = 2.88539008177792681
+    for layer in range(L):
+        W0 = flat[layer * per:layer * per + H * (C + D)].reshape(H, C + D)
+        base = layer * layer_floats
+        for lane in (0, 5, 17, 63):
+            m, kg = lane & 15, lane >> 4
+            for pair in range(4):
+                hi = words[base + (0 * 64 + lane) * 4 + pair]
+                lo = words[base + (1 * 64 + lane) * 4 + pair]
+                for e in range(2):
+                    h16 = np.array([(hi >> (16 * e)) & 0xFFFF], np.uint16).view(np.float16)[0]
+                    l16 = np.array([(lo >> (16 * e)) & 0xFFFF], np.uint16).view(np.float16)[0]
+                    col = 8 * kg + 2 * pair + e
+                    want = np.float32(ks) * W0[m, col] if col < C else np.float32(0)
+                    # hi + lo carries ~22 bits; lo below f16's normal range keeps 2^-24 absolute spacing
+                    assert abs((np.float32(h16) + np.float32(l16)) - want) <= 2.5e-7 * abs(want) + 3.1e-8
+    # the permutation table rides in the image (last D ints before the layer padding)
     assert layer_floats * 4 * L == nbytes and layer_floats % 256 == 0
     perm_off = None
     for off in range(layer_floats - 512, layer_floats - D + 1):

@@ -2138,3 +2138,9 @@ template __global__ void naz::made_ar_fwd_kernel<naz::CfgARF<naz::CfgARW<4, 2, 5
     const float*, int, const float*, int64_t, const float*, int64_t, const float*, const float*, float*, int64_t,
     float*, int64_t, float, int64_t, int64_t, int64_t, int64_t);
 #endif
+
+#if NAZ_PART == 6  // the config-3 training backward alone (not built by build.py)
+template __global__ void naz::coupling_bwd_r16_kernel<naz::CfgR16<16, 32, 8, 8, 128, true>>(
+    const float*, const float*, const float*, int, const float*, const float*, int64_t, const float*, const float*,
+    naz::BwdOut, int64_t, float);
+#endif

@@ -237,13 +237,53 @@ __global__ void coupling_pack_r16_kernel(const float* __restrict__ flat, float* 
   }
 }
 
-// acc[o] += A(o, t) · B(t) over k-steps [0, KB) with B fragments given
-template <int NB, int KB>
+// acc[o] += A(o, t) · B(t) over k-steps [0, KB), t outer, o inner, with each A fragment read one
+// MFMA triple ahead (untracked LDS reads with counted waits, coupling.hip lds_read_b128_untracked):
+// for kernels with too few waves per SIMD to hide an LDS read behind other waves' work (the
+// training backward: two).  bfn(t) returns k-step t's B fragment (formed inside the loop, so the
+// lazy forms' activation VALU still lands between MFMAs).
+template <int NB, int KB, class BFn>
+NAZ_DEV void gemm_r16_pf(floatx4 (&acc)[NB], const float* __restrict__ stage, int lane, BFn&& bfn) {
+  static_assert(2 * NB * KB * 1024 <= 65536, "A fragment offsets must fit the 16-bit LDS offset");
+  const unsigned ub = (unsigned)(uintptr_t)to_lds(stage) + 16u * lane;
+  auto rd = [&](auto oc, auto tc) {
+    constexpr int off = ((decltype(oc)::value * KB + decltype(tc)::value) * 2) * 1024;
+    return Frag2{__builtin_bit_cast(half8, lds_read_b128_untracked<off>(ub)),
+                 __builtin_bit_cast(half8, lds_read_b128_untracked<off + 1024>(ub))};
+  };
+  Frag2 an = rd(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+  static_for<0, KB>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    const Frag2 b = bfn(tc);
+    static_for<0, NB>([&](auto oc) {
+      constexpr int o = decltype(oc)::value;
+      const Frag2 a = an;
+      if constexpr (o + 1 < NB || t + 1 < KB) {
+        an = rd(std::integral_constant<int, (o + 1 < NB ? o + 1 : 0)>{},
+                std::integral_constant<int, (o + 1 < NB ? t : t + 1)>{});
+        __builtin_amdgcn_sched_barrier(0);
+        lds_wait<2>();
+      } else {
+        __builtin_amdgcn_sched_barrier(0);
+        lds_wait<0>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      acc[o] = mfma3_16(a, b, acc[o]);
+    });
+  });
+}
+
+// acc[o] += A(o, t) · B(t) over k-steps [0, KB) with B fragments given (PF: gemm_r16_pf)
+template <int NB, int KB, bool PF = false>
 NAZ_DEV void gemm_r16_stage(floatx4 (&acc)[NB], const float* __restrict__ stage, int lane, const Frag2 (&bf)[KB]) {
 #ifdef NAZ_ABL_NOGEMM
   for (int o = 0; o < NB; ++o) acc[o][0] += (float)bf[0].h[0] * 1e-30f;
   return;
 #endif
+  if constexpr (PF) {
+    gemm_r16_pf<NB, KB>(acc, stage, lane, [&](auto tc) -> Frag2 { return bf[decltype(tc)::value]; });
+    return;
+  }
   const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
 #pragma unroll
   for (int t = 0; t < KB; ++t)
@@ -258,8 +298,22 @@ NAZ_DEV void gemm_r16_stage(floatx4 (&acc)[NB], const float* __restrict__ stage,
 // k-steps [T0, T0 + KB) with each B fragment split from the activated accumulators just
 // before its MFMAs (blocks 2t, 2t + 1 hold the step's 8 values).  ACT: the step's 8 values are
 // activated here too (sig_fold), so that work can fill the previous step's MFMA shadow.
-template <int NB, int KB, int T0, bool ACT, int NX>
+template <int NB, int KB, int T0, bool ACT, int NX, bool PF = false>
 NAZ_DEV void gemm_r16_lazy(floatx4 (&acc)[NB], const float* __restrict__ stage, int lane, floatx4 (&x)[NX]) {
+  if constexpr (PF) {
+    gemm_r16_pf<NB, KB>(acc, stage, lane, [&](auto tc) -> Frag2 {
+      constexpr int t = decltype(tc)::value;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int blk = 2 * (T0 + t) + (j >> 2);
+        v[j] = blk < NX ? x[blk < NX ? blk : 0][j & 3] : 0.f;
+        if constexpr (ACT) v[j] = sig_fold(v[j]);
+      }
+      return split8_f16(v);
+    });
+    return;
+  }
   const u32x4* c4 = reinterpret_cast<const u32x4*>(stage);
 #pragma unroll
   for (int t = 0; t < KB; ++t) {

@@ -227,6 +227,13 @@ struct BwdOut {
 #define NAZ_BWD_WAVES 4
 #endif
 constexpr int kBwdWaves = NAZ_BWD_WAVES;
+// the backward's GEMMs read their A fragments one MFMA triple ahead (gemm_r16_pf): two waves per
+// SIMD do not hide the LDS latency hipcc's lgkmcnt(0) waits expose (NAZ_BWD_NO_PF: the plain form)
+#ifdef NAZ_BWD_NO_PF
+constexpr bool kBwdPF = false;
+#else
+constexpr bool kBwdPF = true;
+#endif
 
 template <class CF>
 struct BwdSlot {  // LDS ring slot: the largest forward or backward stage
@@ -411,7 +418,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
             for (int jj = 0; jj < 8; ++jj) v[jj] = in[8 * t + jj];
             bf[t] = split8_f16(v);
           }
-          gemm_r16_stage<CF::HB, CF::KS1>(h1, cur, lane, bf);
+          gemm_r16_stage<CF::HB, CF::KS1, kBwdPF>(h1, cur, lane, bf);
         }
         // activation -> natural tanh (stored) ; the next GEMM consumes -tanh/2 (the fold)
 #pragma unroll
@@ -437,7 +444,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
             h2[b] = floatx4{bv.x, bv.y, bv.z, bv.w};
           }
         }
-        gemm_r16_lazy<CF::HB, CF::KB2, T0, false>(h2, cur, lane, h1);
+        gemm_r16_lazy<CF::HB, CF::KB2, T0, false, CF::HB, kBwdPF>(h2, cur, lane, h1);
         if constexpr (s == CF::NB2 - 1) {
 #pragma unroll
           for (int b = 0; b < CF::HB; ++b) {
@@ -501,7 +508,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         }
         if constexpr (kBwdF16) {
           if constexpr (sb == 0) gscale = bwd_row_scale(a3);  // dPre3 already stored unscaled
-          gemm_r16_lazy<CF::HB, BW::KB3, sb * BW::KB3, false>(dacc, cur, lane, a3);
+          gemm_r16_lazy<CF::HB, BW::KB3, sb * BW::KB3, false, CF::NO, kBwdPF>(dacc, cur, lane, a3);
         } else {
           bwd_gemm_stage<CF::HB, BW::U3, sb * BW::U3>(dacc, cur, lane, a3);
         }
@@ -516,7 +523,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
               *reinterpret_cast<float4*>(o.dp2 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
           if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         }
-        if constexpr (kBwdF16) gemm_r16_lazy<CF::HB, BW::KB2, sb * BW::KB2, false>(dacc, cur, lane, dp2);
+        if constexpr (kBwdF16) gemm_r16_lazy<CF::HB, BW::KB2, sb * BW::KB2, false, CF::HB, kBwdPF>(dacc, cur, lane, dp2);
         else bwd_gemm_stage<CF::HB, BW::U2, sb * BW::U2>(dacc, cur, lane, dp2);
         if constexpr (!kEpiEarly && sb == BW::NB2 - 1) epi_dh1();
       } else {
@@ -528,7 +535,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         floatx4 a1[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
         if constexpr (kBwdF16) {
-          gemm_r16_lazy<1, BW::KSH, 0, false>(a1, cur, lane, dp2);
+          gemm_r16_lazy<1, BW::KSH, 0, false, CF::HB, kBwdPF>(a1, cur, lane, dp2);
 #pragma unroll
           for (int r = 0; r < 4; ++r) a1[0][r] *= gscale;
         } else {

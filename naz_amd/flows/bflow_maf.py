@@ -745,8 +745,11 @@ def make_normalizing_flow(transform: MAFSpec, x, masks, mask_skips, perms, bound
         return y[0], lj[0]
 
     def lp_flops_per_row() -> int:
-        """GEMM FLOPs per (draw, row) of lp_batched: the degree schedule's (every MADE unit once; the
-        fused AR kernel executes these plus padding), or with the context folded the per-row part."""
+        """GEMM FLOPs per (draw, row) of lp_batched: on the fused AR kernel the FLOPs it executes
+        (ops.ar_executed_flop_per_row: block rounding and padding included); otherwise the degree
+        schedule's (every MADE unit once), or with the context folded the per-row part."""
+        if ar_perm is not None:
+            return ops.ar_executed_flop_per_row(ar_desc, pass0_const=ar_pass0 is not None)["inverse"]
         tot = 0
         for plan in plans:
             if const_ctx and fold_context and ar_perm is None:

@@ -608,8 +608,8 @@ def ar_flow_supported(d: ArDesc) -> bool:
 
 
 def ar_flow_fwd_supported(d: ArDesc) -> bool:
-    """The sampling direction runs fused (naz_ar_flow_sample*): every fused shape, including the
-    forward-only wide production MAFs (naz_ar_flow_supported == 2)."""
+    """The sampling direction runs fused (naz_ar_flow_sample*): every fused shape, including a
+    forward-only one (naz_ar_flow_supported == 2; none today)."""
     return int(lib().naz_ar_flow_supported(d)) in (1, 2)
 
 
@@ -620,7 +620,7 @@ def ar_flow_degrees(d: ArDesc) -> np.ndarray:
     return out
 
 
-def ar_executed_flop_per_row(d: ArDesc) -> dict:
+def ar_executed_flop_per_row(d: ArDesc, pass0_const: bool = False) -> dict:
     """FP32-equivalent FLOPs per row the fused autoregressive kernels EXECUTE (a split f16x3 /
     bf16x6 product counted once; the 16-unit block recomputation and zero padding included), for
     roofline accounting against the pipe each runs on:
@@ -632,6 +632,7 @@ def ar_executed_flop_per_row(d: ArDesc) -> dict:
       bwd      made_ar_bwd_kernel, all layers (maf only): one dense MADE pass plus D chains
                (W_out^T g on the VALU in fp32, the W_i^T chain and the input unit on f16x3);
       dw       the batched weight-gradient reductions over the padded operands (bf16x6).
+    pass0_const: the images carry the first degree pass as per-draw constants (no MFMAs in pass 0).
     """
     D, C, H, NH, L = d.D, d.C, d.H, d.n_hidden, d.L
     P = 2 if d.kind == AR_KIND["maf"] else 3 * d.K - 1
@@ -642,7 +643,7 @@ def ar_executed_flop_per_row(d: ArDesc) -> dict:
     E = [int((deg <= p).sum()) for p in range(D)]
     wide = HP > 256  # made_ar_wide.h: hidden layer 1 recomputed in full (blocks of degree <= p) every pass
     inv = 0
-    for p in range(D):
+    for p in range(1 if pass0_const else 0, D):  # pass-0 constants: the first pass runs no MFMAs
         e0 = E[p - 1] if p else 0
         nb = ((E[p] - 1) >> 4) - (e0 >> 4) + 1 if E[p] > e0 else 0
         nb1 = (((E[p] - 1) >> 4) + 1 if E[p] > 0 else 0) if wide else nb

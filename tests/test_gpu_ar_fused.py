@@ -372,7 +372,7 @@ def test_wide_maf_persistent_grid_and_draws():
         lp = f.log_prob(x, condition=c)
         c1 = c[5]
         lp1 = f.log_prob(x[:3000], condition=c1)
-        empty = f.log_prob(x[:0], condition=c)
+        empty = f.log_prob(x[:0], condition=c[:0])
         f.set_fused(False)
         ref = f.log_prob(x, condition=c)
         ref1 = f.log_prob(x[:3000], condition=c1)

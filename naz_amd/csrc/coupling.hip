@@ -2144,3 +2144,9 @@ template __global__ void naz::coupling_bwd_r16_kernel<naz::CfgR16<16, 32, 8, 8, 
     const float*, const float*, const float*, int, const float*, const float*, int64_t, const float*, const float*,
     naz::BwdOut, int64_t, float);
 #endif
+
+#if NAZ_PART == 5  // the nsa16 log_prob kernel alone (not built by build.py)
+template __global__ void naz::made_ar_r16_kernel<naz::CfgAR<16, 32, 128, 8>>(
+    const float*, int, const float*, int64_t, const float*, int64_t, const float*, const float*, float*, int64_t,
+    float, int64_t, int64_t, int64_t, int, float*);
+#endif

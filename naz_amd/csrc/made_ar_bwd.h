@@ -274,7 +274,7 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
             for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(ax[r], us, acc[r]);
           } else {
 #pragma unroll
-            for (int t = 0; t < KSH; ++t) acc = mfma3_16(afrag(t), hf[(i - 1) & 1][t], acc);
+            for (int t = 0; t < KT; ++t) acc = mfma3_16(afrag(t), hf[(i - 1) & 1][t], acc);  // FW::hid_kts
           }
           floatx4 v;
 #pragma unroll

@@ -244,6 +244,18 @@ struct CfgAR {
   // inverse workgroup: NAZ_AR_INV_NW waves (12: one workgroup per CU; 6 with NAZ_AR_INV_CAP =
   // 10240: two per CU, each on its own 2 x <= 40 KB ring, so the two do not share barriers)
   static constexpr int NW = WPE == 3 ? NAZ_AR_INV_NW : NW_FWD;
+  // the inverse kernel's waves per SIMD (NAZ_AR_INV_WPE overrides: e.g. 2 with NAZ_AR_INV_NW = 8)
+  // and its prefetched MFMA chains (NAZ_AR_INV_PF: mfma3_16_chain_lds)
+#ifdef NAZ_AR_INV_WPE
+  static constexpr int WPE_INV = WPE == 3 ? NAZ_AR_INV_WPE : WPE;
+#else
+  static constexpr int WPE_INV = WPE;
+#endif
+#ifdef NAZ_AR_INV_PF
+  static constexpr bool PF = true;
+#else
+  static constexpr bool PF = false;
+#endif
   static_assert(H <= 256 && D <= 32 && D >= 2 && NHID >= 1 && NHID <= 3, "unsupported fused autoregressive shape");
   static_assert(NOB <= 2 && NSTG <= 128, "output blocks / stages");
 };
@@ -378,7 +390,7 @@ NAZ_DEV void ar_split4(Frag2& f, const floatx4& a) {
 }
 
 template <class CF>
-__global__ void __launch_bounds__(64 * CF::NW, CF::WPE) made_ar_r16_kernel(
+__global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, int64_t B, float bound, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0,
@@ -483,6 +495,7 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE) made_ar_r16_kernel(
           const int base = (OFF >> 2) + idx * 128 + lane;
           return Frag2{__builtin_bit_cast(half8, c4[base]), __builtin_bit_cast(half8, c4[base + 64])};
         };
+        [[maybe_unused]] const unsigned ub = (unsigned)(uintptr_t)to_lds(cur) + 16u * lane + 4u * OFF;
         const float4* bias4 = reinterpret_cast<const float4*>(cur + OFF_BIAS);
         bool done0 = false;
         if constexpr (p == 0) {
@@ -551,8 +564,12 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE) made_ar_r16_kernel(
             constexpr int bi = decltype(bc)::value, b = BLO + bi;
             const float4 bv = bias4[4 * bi + q];
             floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
+            if constexpr (CF::PF) {
+              acc = mfma3_16_chain_lds<KT>(ub + 2048u * (bi * KT), hf[i - 1], acc);
+            } else {
 #pragma unroll
-            for (int t = 0; t < KT; ++t) acc = mfma3_16(afrag(bi * KT + t), hf[i - 1][t], acc);
+              for (int t = 0; t < KT; ++t) acc = mfma3_16(afrag(bi * KT + t), hf[i - 1][t], acc);
+            }
             ar_split4<b & 1>(hf[i][b >> 1], acc);
           });
         } else if constexpr (i == NHID) {
@@ -563,10 +580,15 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE) made_ar_r16_kernel(
               const float4 bv = bias4[4 * o + q];
               o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
             }
+            if constexpr (CF::PF) {
 #pragma unroll
-            for (int t = 0; t < KT; ++t)
+              for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16_chain_lds<KT>(ub + 2048u * (o * KT), hf[NHID - 1], o3[o]);
+            } else {
 #pragma unroll
-              for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KT + t), hf[NHID - 1][t], o3[o]);
+              for (int t = 0; t < KT; ++t)
+#pragma unroll
+                for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KT + t), hf[NHID - 1][t], o3[o]);
+            }
           }
           const float y = v[dp];
           if constexpr (CF::AFFINE) {
@@ -663,7 +685,28 @@ struct CfgARF {
   static constexpr bool AFFINE = G::AFFINE;
   static constexpr int NU = NHID * HB + NG;  // units: hidden (i, b) row-major, then one per dim group
   static constexpr int unit_blocks(int u) { return u < NHID * HB ? 1 : NOG; }
-  static constexpr int unit_kts(int u) { return u < HB ? KI : KSH; }
+  // k-steps a hidden block b of layers 2.. reads: the units of degree <= the block's largest. The
+  // MADE mask of a hidden layer is deg(u) >= deg(v) and degrees do not decrease along the unit
+  // index, so every later k-step of the block is masked to exact zeros (about a third of each
+  // hidden matrix at D = 4, H = 512): neither streamed nor multiplied — the same values, bit for
+  // bit (adding +0 products changes no fp32 sum)
+  struct KtTab {
+    int kt[64];
+  };
+  static constexpr KtTab make_kt() {
+    KtTab y{};
+    for (int b = 0; b < HB; ++b) {
+      const int last = 16 * b + 15 < H ? 16 * b + 15 : H - 1;
+      const int dmax = G::deg(last);
+      int e = 0;
+      for (int v = 0; v < H; ++v) e += G::deg(v) <= dmax ? 1 : 0;
+      y.kt[b] = (e + 31) / 32;
+    }
+    return y;
+  }
+  static constexpr KtTab KTT = make_kt();
+  static constexpr int hid_kts(int b) { return KTT.kt[b]; }
+  static constexpr int unit_kts(int u) { return u < HB ? KI : (u < NHID * HB ? hid_kts(u % HB) : KSH); }
   static constexpr int unit_floats(int u) { return unit_blocks(u) * (unit_kts(u) * OT + 16); }
   struct Layout {
     int sid[NU], off[NU], sfl[NU];
@@ -1069,11 +1112,11 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::NW / 4) made_ar_fwd_kernel(
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(ax[r], us, acc[r]);
         } else if constexpr (NW == 4) {  // the wide instances (one wave per SIMD): prefetched chain
-          acc = mfma3_16_chain_lds<KSH>((unsigned)(uintptr_t)to_lds(cur) + 16u * lane + 4u * OFF,
-                                        hf[(i - 1) & 1], acc);
+          acc = mfma3_16_chain_lds<KT>((unsigned)(uintptr_t)to_lds(cur) + 16u * lane + 4u * OFF,
+                                       hf[(i - 1) & 1], acc);
         } else {
 #pragma unroll
-          for (int t = 0; t < KSH; ++t) acc = mfma3_16(afrag(t), hf[(i - 1) & 1][t], acc);
+          for (int t = 0; t < KT; ++t) acc = mfma3_16(afrag(t), hf[(i - 1) & 1][t], acc);
         }
         ar_split4<b & 1>(hf[i & 1][b >> 1], acc);
       } else {

@@ -10,6 +10,7 @@ import os
 import shutil
 import subprocess
 import sys
+import time
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -48,9 +49,14 @@ def _compile(src: Path, obj: Path, extra: list) -> str:
     if src.suffix == ".cpp":
         cmd[1:2] = []  # host-only TU
         cmd += ["-x", "c++"] if False else []
+    started = time.time()
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    # date the object at the compile's START: hipcc reads the sources once for the device pass and
+    # again, minutes later, for the host pass, so a header edited meanwhile must make the object
+    # stale (a device image from the old header and a host packer from the new one disagree)
+    os.utime(obj, (started, started))
     return r.stderr
 
 

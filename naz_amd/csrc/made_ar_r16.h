@@ -705,7 +705,11 @@ struct CfgARF {
     return y;
   }
   static constexpr KtTab KTT = make_kt();
+#ifdef NAZ_AR_FWD_DENSE_K  // (A/B: every hidden block reads all KSH k-steps)
+  static constexpr int hid_kts(int) { return KSH; }
+#else
   static constexpr int hid_kts(int b) { return KTT.kt[b]; }
+#endif
   static constexpr int unit_kts(int u) { return u < HB ? KI : (u < NHID * HB ? hid_kts(u % HB) : KSH); }
   static constexpr int unit_floats(int u) { return unit_blocks(u) * (unit_kts(u) * OT + 16); }
   struct Layout {

@@ -2150,3 +2150,7 @@ template __global__ void naz::made_ar_r16_kernel<naz::CfgAR<16, 32, 128, 8>>(
     const float*, int, const float*, int64_t, const float*, int64_t, const float*, const float*, float*, int64_t,
     float, int64_t, int64_t, int64_t, int, float*);
 #endif
+
+#if NAZ_PART == 4  // the 4-parameter Bayesian MAF backward alone (not built by build.py)
+template struct naz::CfgARB<naz::CfgAR<4, 2, 150, 8, 3, true>>;
+#endif

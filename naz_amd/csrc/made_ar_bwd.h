@@ -49,9 +49,33 @@ struct CfgARB {
   // block b) for i = NHID-1 down to 1; last = the input unit W_0[:, C:]ᵀ (one block, rows = dims)
   static constexpr int NUB = 2 + (NHID - 1) * HB;
   static constexpr int TBLF = NO * HP;
-  static constexpr int unit_floats(int j) { return j == 0 ? (TBLF + 255) / 256 * 256 : KSH * OT; }
   static constexpr int hid_i(int j) { return NHID - 1 - (j - 1) / HB; }
   static constexpr int hid_b(int j) { return (j - 1) % HB; }
+  // the transposed products skip their leading k-steps: W_i[v][u] (u: unit of output block b, v:
+  // unit of the layer above, the k index) is masked unless deg(v) >= deg(u), and degrees do not
+  // decrease along the unit index, so k-steps of units all below the block's smallest degree are
+  // exact zeros (bit-identical results, as CfgARF::hid_kts in the forward image)
+  struct T0Tab {
+    int t0[64];
+  };
+  static constexpr T0Tab make_t0() {
+    T0Tab y{};
+    for (int b = 0; b < HB; ++b) {
+      const int first = 16 * b < H ? 16 * b : H - 1;
+      const int dmin = CF::deg(first);
+      int e = 0;
+      for (int v = 0; v < H; ++v) e += CF::deg(v) < dmin ? 1 : 0;
+      y.t0[b] = e >> 5;
+    }
+    return y;
+  }
+  static constexpr T0Tab T0T = make_t0();
+#ifdef NAZ_AR_BWD_DENSE_K  // (A/B: every k-step)
+  static constexpr int kt0(int) { return 0; }
+#else
+  static constexpr int kt0(int j) { return j >= 1 && j < NUB - 1 ? T0T.t0[hid_b(j)] : 0; }
+#endif
+  static constexpr int unit_floats(int j) { return j == 0 ? (TBLF + 255) / 256 * 256 : (KSH - kt0(j)) * OT; }
   struct Layout {
     int sid[NUB], off[NUB], sfl[NUB];
     int nstg, stg;
@@ -123,7 +147,7 @@ __global__ void made_ar_pack_bwd_kernel(const float* __restrict__ flat, const fl
       word = __builtin_bit_cast(unsigned, v);
       return;
     } else {
-      const int t = rel / CB::OT, w = rel % CB::OT;
+      const int t = rel / CB::OT + CB::kt0(j), w = rel % CB::OT;  // (leading masked k-steps not stored)
       const int piece = w / 256, lane = (w % 256) / 4, pair = w % 4;
       const int m = lane & 15, kg = lane >> 4;
 #pragma unroll
@@ -448,8 +472,9 @@ __global__ void __launch_bounds__(64 * CB::NW, CB::NW / 4) made_ar_bwd_kernel(
             }
           }
           floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+          constexpr int T0 = CB::kt0(j);  // leading k-steps masked to zero: not stored, not multiplied
 #pragma unroll
-          for (int t = 0; t < KSH; ++t) acc = mfma3_16(afrag(t), bfr[t], acc);
+          for (int t = T0; t < KSH; ++t) acc = mfma3_16(afrag(t - T0), bfr[t], acc);
           if constexpr (INPUT) {
             // dx of dims m = 4 q + r sits on quarter 0 (D <= 4): every quarter takes the row's values
 #pragma unroll

@@ -311,19 +311,110 @@ def run_train(args, dev, rank, world, dist):
         dist.destroy_process_group()
 
 
-def train_cpu_baseline(flow, rows: int = 1 << 14) -> dict:
+def run_train_flow(args, dev, rank, world, dist):
+    """The NLL step of naz's train (train_flows.py:194-213) on a --flow maf case (naz's MLE MAFs:
+    train_mle_all_data_4param.py:87-92 trains maf4 with batch_frac 0.05), --batch rows per rank
+    (default 2^16), one process per GPU, gradients all-reduced in one flat bucket."""
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import flow as flow_mod
+    from naz_amd.trainers import DataParallel, nll_step
+    from naz_amd.trainers.train_flows import _flow_parameters
+    from naz_amd import ops
+    ftype, Dd, Cd, hid, Ld, extra, _, desc = FLOW_CASES[args.flow]
+    if ftype != "maf":
+        raise SystemExit("--train --flow: the maf cases (the nsc training step is --train alone)")
+    if args.train_walk:
+        flow_mod._TRAIN_FUSED = "0"
+    torch.manual_seed(1234)
+    f = NormalizingFlow(ftype, None, Dd, Cd, hid, Ld, *extra).to(dev)
+    lo, hi, G = shard(args, rank, world, 1 << 16)
+    B = hi - lo
+    x = torch.as_tensor(mixture_rows(lo, hi, Dd, seed=0), device=dev)
+    c = torch.as_tensor(normal_rows(lo, hi, Cd, seed=1), device=dev)
+    dp = DataParallel()
+    params = _flow_parameters(f)
+    dp.broadcast_params(params)
+    opt = torch.optim.Adam(params, lr=1e-4)
+    plan = f._plan
+    path = ("autograd walk (per-layer HIP kernels)" if args.train_walk or not plan.train_ready(x, c) else
+            "fused maf backward (made_ar_bwd.h)" if ops.ar_flow_bwd_supported(plan.desc) else
+            "saved-state wide inverse kernel + GEMM-composed backward (flows/maf_grad_wide.py)")
+
+    def step():
+        return nll_step(f, x, c, opt, params, dp, G, clip_val=1.0, micro_batch=args.micro_batch)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    if rank == 0:
+        step_s = elapsed / args.steps
+        dims = [Dd + Cd] + list(hid) + [2 * Dd]
+        fl_ref = 3 * 2 * Dd * Ld * sum(a * b for a, b in zip(dims[:-1], dims[1:]))  # D-pass fwd + autograd
+        fwd = ops.ar_executed_flop_per_row(plan.desc)["inverse"]
+        bwd = plan.maf_grad().flop_per_row() if "wide" in path else 0  # the blocks the GEMMs execute
+        roof = {"bound": "mfma", "unit": "TFLOP/s", "traffic": None, "kernel": "whole step",
+                "reference_flop_per_row": fl_ref,
+                "reference_tflops": fl_ref * B / step_s / 1e12}
+        if "wide" in path:
+            peak = (fwd + bwd) / (fwd / (BF16_PEAK_TFLOPS / 3) + bwd / FP32_PEAK_TFLOPS)
+            achieved = (fwd + bwd) * B / step_s / 1e12
+            roof.update(achieved=achieved, peak=peak, frac=achieved / peak, flop_per_row=fwd + bwd,
+                        peak_note=f"harmonic FLOP-weighted ceiling: forward {fwd:.3g} FLOP/row on the f16x3 split "
+                                  f"({BF16_PEAK_TFLOPS / 3:.0f} TF), backward {bwd:.3g} FLOP/row on exact FP32 MFMA "
+                                  f"({FP32_PEAK_TFLOPS:.1f} TF)")
+        else:
+            achieved = fl_ref * B / step_s / 1e12
+            roof.update(achieved=achieved, peak=FP32_PEAK_TFLOPS, frac=achieved / FP32_PEAK_TFLOPS,
+                        flop_per_row=fl_ref, peak_note="the reference's FLOPs against the exact FP32 MFMA peak")
+        rec = {
+            "metric": f"samples/sec through the NLL training step (log_prob fwd + backward + grad all-reduce + clip + "
+                      f"Adam), naz {ftype} flow",
+            "value": G / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": args.scaling,
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
+            "config": {"workload": desc + " — NLL step", "batch_per_gpu": B, "global_batch": G,
+                       "micro_batch": args.micro_batch, "path": path,
+                       "parallelism": f"dp{world} (RCCL all-reduce, one flat bucket)"},
+            "roofline": roof, "final_loss": float(loss),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            spec = dict(flow_type=ftype, D=Dd, C=Cd, hidden=list(hid), L=Ld)
+            rec["cpu_baseline"] = train_cpu_baseline(f, rows=1024 if hid[0] >= 512 else 1 << 13, spec=spec)
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def train_cpu_baseline(flow, rows: int = 1 << 14, spec: dict = None) -> dict:
     """The reference's NLL step on the host: the oracle flow (pyro semantics, torch fp32) forward
     + autograd backward + clip + Adam over a bounded sample of the same workload."""
     from naz_amd.flows import io as fio
     from oracle import naz_oracle as O  # baseline only
-    spec = dict(flow_type="nsc", D=D, C=C, hidden=[H, H], L=L, K=K, split=S)
+    spec = dict(flow_type="nsc", D=D, C=C, hidden=[H, H], L=L, K=K, split=S) if spec is None else spec
     state = {k: torch.as_tensor(v).clone() for k, v in fio.export_state(flow).items()}
     of = O.build_flow(spec, state, torch.float32)
     ps = [v.requires_grad_(True) for v in state.values() if v.is_floating_point()]
     cores = host_cores()
     torch.set_num_threads(cores["threads"])
-    xs = torch.as_tensor(mixture_rows(0, rows, D, seed=0))
-    cs = torch.as_tensor(normal_rows(0, rows, C, seed=1))
+    xs = torch.as_tensor(mixture_rows(0, rows, spec["D"], seed=0))
+    cs = torch.as_tensor(normal_rows(0, rows, spec["C"], seed=1))
     opt = torch.optim.Adam(ps, lr=1e-4)
 
     def step():
@@ -341,7 +432,7 @@ def train_cpu_baseline(flow, rows: int = 1 << 14) -> dict:
         runs.append(time.perf_counter() - t0)
     med = statistics.median(runs)
     return {"value": rows / med, "unit": "samples/s", "cores": cores["threads"], "kind": "port",
-            "sample": f"{rows} rows, oracle nsc flow (torch fp32) forward + autograd backward + clip + Adam, "
+            "sample": f"{rows} rows, oracle {spec['flow_type']} flow (torch fp32) forward + autograd backward + clip + Adam, "
                       f"{cores['threads']} threads, median of 5 after 1 warm-up ({med:.2f} s)",
             "host": cores}
 
@@ -1037,6 +1128,8 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
+    if args.train and args.flow:
+        return run_train_flow(args, dev, rank, world, dist)
     if args.train:
         return run_train(args, dev, rank, world, dist)
     if args.cnf_train:

@@ -193,6 +193,17 @@ int naz_wgrad_batched(int64_t M, int N1, int N2, int nbatch, const float* g, int
 int naz_affine_ar_bwd(int mode, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y,
                       int64_t ldy, const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx,
                       float* g_raw, int64_t ldgr, int64_t B, int D, void* stream);
+/* One dim of the maf inverse's VJP, for a maf backward composed of GEMMs (the shapes without the
+ * fused naz_ar_flow_bwd_layer; flows/maf_grad_wide.py).  Replaces, for one dim, the autograd of
+ * pyro AffineAutoregressive._inverse (naz transforms.py:159) + its log-det under naz train's loss
+ * (train_flows.py:195,208).  Layer output s_d = (y_d - m_d) e^{-c(a_d)}, raw = the MADE output
+ * [B, 2D] (mean cols 0..D-1, log_scale cols D..2D-1), g = dL/ds [B, D] (complete for `dim`),
+ * g_lp [B] (NULL: 1).  Writes g_next[:, dim] = dL/dy_dim, tot[:, dim] / tot[:, D + dim] =
+ * dL/d(mean, log_scale), and chain (may be NULL) = a [B, 2D] row zero but for those two columns.
+ * mode: NAZ_AFFINE_CLIP_ZERO_GRAD = jnp.clip's gradient, else pyro's clamp_preserve_gradients. */
+int naz_maf_dim_vjp(int mode, const float* raw, int64_t ldr, const float* s_out, int64_t lds, const float* g,
+                    int64_t ldg, const float* g_lp, float* g_next, int64_t ldgn, float* tot, int64_t ldt, float* chain,
+                    int64_t ldch, int64_t B, int D, int dim, void* stream);
 /* out[n] += sum_m A[m*lda + n]  (atomic; zero `out` first for a plain column sum)         */
 int naz_colsum(const float* A, int64_t lda, int64_t M, int N, float* out, void* stream);
 /* gpre = gy * act'(pre) computed from the post-activation y (tanh, relu, softplus, sigmoid) */
@@ -449,10 +460,13 @@ int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64
  * Replaces jax.grad of bayesian_normalizing_flow's potential Σ_rows flow_lp(unravel(p))
  * (naz/flows/bflow_jax_maf.py:231-235; examples/papers/2506.05657/hmc_maf_exact.py:118-133) and
  * loss.backward() of a maf NLL (naz/trainers/train_flows.py:194-213).  Affine autoregressive flows
- * at the compiled shapes (naz_ar_flow_bwd_packed_bytes < 0 otherwise; today the paper shape
- * D=2 | C=2, H=[150]x3).
+ * at the compiled shapes (naz_ar_flow_bwd_packed_bytes < 0 otherwise; the paper shape
+ * D=2 | C=2, H=[150]x3 and the 4-parameter Bayesian D=4 | C=2, H=[150]x3).
  *   naz_ar_flow_log_prob_train: naz_ar_flow_log_prob (one draw, no bounding) that also writes
  *     states [L][B][D]: states[l] = s_l, layer l's output (layer l maps s_{l+1} -> s_l; s_0 = z).
+ *     Every affine flow whose inverse is fused (naz_ar_flow_supported == 1): at the shapes without
+ *     backward images (the wide MLE MAFs) the backward is composed of naz_linear_act /
+ *     naz_gemm_dact / naz_gemm / naz_maf_dim_vjp (flows/maf_grad_wide.py).
  *   naz_ar_flow_pack_bwd: per-layer backward images (naz_ar_flow_bwd_packed_bytes) from the
  *     naz_ar_flow_pack_host flat layout on the device; mask (nullable, same layout) multiplies.
  *   naz_ar_flow_bwd_dims: dims[6] = {n_hidden, HP, XA, XB, X0W, rows per tile}.

@@ -71,6 +71,8 @@ SIGNATURES = {
                            _i, _vp, _vp]),
     "naz_affine_ar_bwd": (C.c_int, [_i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _i64,
                                     _i, _vp]),
+    "naz_maf_dim_vjp": (C.c_int, [_i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
+                                  _i64, _i, _i, _vp]),
     "naz_colsum": (C.c_int, [_vp, _i64, _i64, _i, _vp, _vp]),
     "naz_act_bwd": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i, _i, _vp]),
     "naz_base_log_prob_bwd": (C.c_int, [_vp, _i64, _vp, _vp, _i64, _i64, _i, _vp]),

@@ -172,6 +172,16 @@ int naz_affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw
                        as_stream(stream));
 }
 
+int naz_maf_dim_vjp(int mode, const float* raw, int64_t ldr, const float* s_out, int64_t lds, const float* g,
+                    int64_t ldg, const float* g_lp, float* g_next, int64_t ldgn, float* tot, int64_t ldt, float* chain,
+                    int64_t ldch, int64_t B, int D, int dim, void* stream) {
+  if (D <= 0 || dim < 0 || dim >= D) return set_error("naz_maf_dim_vjp: dim %d outside [0, %d)", dim, D);
+  if (B > 0 && (raw == nullptr || s_out == nullptr || g == nullptr || g_next == nullptr || tot == nullptr))
+    return set_error("naz_maf_dim_vjp: null pointer");
+  return maf_dim_vjp(mode, raw, ldr, s_out, lds, g, ldg, g_lp, g_next, ldgn, tot, ldt, chain, ldch, B, D, dim,
+                     as_stream(stream));
+}
+
 int naz_colsum(const float* A, int64_t lda, int64_t M, int N, float* out, void* stream) {
   return colsum(A, lda, M, N, out, as_stream(stream));
 }
@@ -394,7 +404,8 @@ int naz_ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const f
     return set_error("naz_ar_flow_log_prob_train: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
     return set_error("naz_ar_flow_log_prob_train: conditional flow needs ctx");
-  if (naz_ar_flow_bwd_packed_bytes(d) < 0) return set_error("naz_ar_flow_log_prob_train: no fused backward for this flow");
+  if (d == nullptr || d->kind != NAZ_AR_AFFINE || naz_ar_flow_supported(d) != 1)
+    return set_error("naz_ar_flow_log_prob_train: no fused affine inverse for this flow");
   return ar_flow_log_prob_train(d, packed, x, ldx, ctx, ldc, out_lp, states, B, as_stream(stream));
 }
 int64_t naz_ar_flow_bwd_packed_bytes(const naz_ar_desc* d) { return ar_flow_bwd_packed_bytes(d); }

@@ -1784,8 +1784,8 @@ struct AROpsW {
                       int64_t P = 1, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0, int c0mode = 0,
                       float* states = nullptr) {
     if (c0mode) return set_error("naz_ar_flow: D=%d H=%d x %d: no pass-0 constants form", CW::D, CW::H, CW::NHID);
-    if (states != nullptr)
-      return set_error("naz_ar_flow_log_prob_train: D=%d H=%d x %d: no fused backward", CW::D, CW::H, CW::NHID);
+    if (states != nullptr && (P != 1 || low != nullptr))
+      return set_error("naz_ar_flow_log_prob_train: one draw, no bounds");
     if (B == 0 || L == 0 || P == 0) return 0;
     const int64_t tiles = (B + 16 * IW::NW - 1) / (16 * IW::NW) * P;
     const int64_t grid = std::min<int64_t>(tiles, device_cu_count());
@@ -1795,7 +1795,7 @@ struct AROpsW {
       return set_error("naz_ar_flow_log_prob: %zu B of per-wave scratch not available", bytes);
     const size_t lds = (size_t)2 * IW::STG * 4;
     hipLaunchKernelGGL((made_ar_inv_wide_kernel<IW>), dim3((unsigned)grid), dim3(64 * IW::NW), lds, s, packed, L, x,
-                       ldx, ctx, ldc, low, high, out_lp, B, P, spk, sx, slp, static_cast<u32x4*>(scratch));
+                       ldx, ctx, ldc, low, high, out_lp, B, P, spk, sx, slp, static_cast<u32x4*>(scratch), states);
     const int rc = check_launch("made_ar_inv_wide_kernel");
     (void)hipFreeAsync(scratch, s);
     return rc;

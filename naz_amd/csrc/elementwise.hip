@@ -118,7 +118,42 @@ __global__ void affine_ar_bwd_kernel(int inverse, const float* __restrict__ x, i
   g_raw[r * ldgr + D + i] = gs;
 }
 
+// One dim of the maf inverse's VJP (the wide maf backward, flows/maf_grad_wide.py).  Layer output
+// s_d = (y_d - m_d) e^{-c(a_d)}, log p += -c(a_d); with g = dL/ds (complete for dim d: every later
+// dim's chain has already added its share) and L = sum_rows g_lp log p:
+//   dL/dy_d = g_d e^{-c},  dL/dm_d = -g_d e^{-c},  dL/da_d = -g_lp - g_d s_d  (x 1[-5 <= a <= 3]: jnp.clip)
+// Writes g_next[:, d]; tot[:, d], tot[:, D + d] (the layer's output gradient, for the dW chain);
+// chain (may be NULL) = the whole row, zero but for those two columns (the dim's own input chain).
+__global__ void maf_dim_vjp_kernel(int mode, const float* __restrict__ raw, int64_t ldr, const float* __restrict__ sv,
+                                   int64_t lds, const float* __restrict__ g, int64_t ldg,
+                                   const float* __restrict__ g_lp, float* __restrict__ g_next, int64_t ldgn,
+                                   float* __restrict__ tot, int64_t ldt, float* __restrict__ chain, int64_t ldch,
+                                   int64_t B, int D, int d) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B) return;
+  const float raw_ls = raw[r * ldr + D + d];
+  const float ls = fminf(fmaxf(raw_ls, -5.f), 3.f);
+  const float gd = g[r * ldg + d];
+  const float gy = gd * expf(-ls);
+  float ga = -(g_lp != nullptr ? g_lp[r] : 1.f) - gd * sv[r * lds + d];
+  if ((mode & NAZ_AFFINE_CLIP_ZERO_GRAD) && !(raw_ls >= -5.f && raw_ls <= 3.f)) ga = 0.f;
+  g_next[r * ldgn + d] = gy;
+  tot[r * ldt + d] = -gy;
+  tot[r * ldt + D + d] = ga;
+  if (chain != nullptr)
+    for (int j = 0; j < 2 * D; ++j) chain[r * ldch + j] = j == d ? -gy : j == D + d ? ga : 0.f;
+}
+
 static unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+int maf_dim_vjp(int mode, const float* raw, int64_t ldr, const float* sv, int64_t lds, const float* g, int64_t ldg,
+                const float* g_lp, float* g_next, int64_t ldgn, float* tot, int64_t ldt, float* chain, int64_t ldch,
+                int64_t B, int D, int d, hipStream_t s) {
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(maf_dim_vjp_kernel, dim3(blocks_for(B)), dim3(256), 0, s, mode, raw, ldr, sv, lds, g, ldg, g_lp,
+                     g_next, ldgn, tot, ldt, chain, ldch, B, D, d);
+  return check_launch("maf_dim_vjp_kernel");
+}
 
 int affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y, int64_t ldy,
                   const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx, float* g_raw,

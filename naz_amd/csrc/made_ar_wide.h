@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(64 * CF::NW, 1) made_ar_inv_wide_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, int64_t B, int64_t ndraw, int64_t spk, int64_t sx, int64_t slp,
-    u32x4* __restrict__ scratch) {
+    u32x4* __restrict__ scratch, float* __restrict__ states) {
   constexpr int D = CF::D, NW = CF::NW, NHID = CF::NHID, KSH = CF::KSH;
   extern __shared__ float4 lds4[];
   float* const slot0 = reinterpret_cast<float*>(lds4);
@@ -422,6 +422,11 @@ __global__ void __launch_bounds__(64 * CF::NW, 1) made_ar_inv_wide_kernel(
           ldsum += ls;
         }
       });
+      // the training forward: layer l's output s_l [L, B, D] (one draw) for the wide maf backward
+      if (states != nullptr && q == 0 && valid) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) states[((int64_t)l * B + row) * D + d] = v[d];
+      }
     }
     constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
     float base = 0.f;

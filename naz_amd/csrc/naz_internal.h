@@ -54,6 +54,9 @@ int gemm_rows_try(int M, int N, int64_t K, const float* A, int64_t sam, int64_t 
 int affine_ar_bwd(int inverse, const float* x, int64_t ldx, const float* raw, int64_t ldr, const float* y, int64_t ldy,
                   const float* g_y, int64_t ldgy, const float* g_ld, float* g_x, int64_t ldgx, float* g_raw,
                   int64_t ldgr, int64_t B, int D, hipStream_t s);
+int maf_dim_vjp(int mode, const float* raw, int64_t ldr, const float* sv, int64_t lds, const float* g, int64_t ldg,
+                const float* g_lp, float* g_next, int64_t ldgn, float* tot, int64_t ldt, float* chain, int64_t ldch,
+                int64_t B, int D, int d, hipStream_t s);
 int colsum(const float* A, int64_t lda, int64_t M, int N, float* out, hipStream_t s);
 int act_bwd(const float* gy, int64_t ldg, const float* y, int64_t ldy, float* gp, int64_t ldp, int64_t M, int N, int act,
             hipStream_t s);

@@ -217,9 +217,17 @@ class _FusedAR:
         at a compiled shape, rows inside the f16 split's range, no gradient wanted for x or the
         context (train's data).  NAZ_TRAIN_FUSED=0 keeps the autograd walk."""
         if self.kind != "maf" or _TRAIN_FUSED == "0" or x.dim() != 2 or x.requires_grad or \
-                (context is not None and context.requires_grad) or not ops.ar_flow_bwd_supported(self.desc):
+                (context is not None and context.requires_grad) or not self._train_kernels():
             return False
         return self.log_prob_ready(x, context)
+
+    def _train_kernels(self) -> bool:
+        """The fused backward kernel (made_ar_bwd.h) at its compiled shapes; elsewhere a fused inverse
+        (naz_ar_flow_log_prob_train) + the GEMM-composed backward (flows/maf_grad_wide.py).
+        NAZ_TRAIN_WIDE=0 keeps the autograd walk at the latter's shapes."""
+        if ops.ar_flow_bwd_supported(self.desc):
+            return True
+        return _TRAIN_WIDE != "0" and self.inverse and ops.ar_flow_supported(self.desc) == 1
 
     def maf_grad(self):
         """MafGrad for the current permutations and masks (rebuilt when one of them changes)."""
@@ -229,10 +237,12 @@ class _FusedAR:
         sig = tuple((t.data_ptr(), t._version) for t in ts) + (cache_epoch(), cz)
         if getattr(self, "_mg", None) is None or self._mg[0] != sig:
             from .maf_grad import MafGrad
+            from .maf_grad_wide import WideMafGrad
             mask = torch.cat([t for n in nets for l in n.layers
                               for t in (l.mask.detach().reshape(-1).float(), torch.ones_like(l.bias.detach()))])
             perm = np.stack([n.permutation.detach().cpu().numpy() for n in nets]).astype(np.int32)
-            self._mg = (sig, MafGrad(self.desc, perm, mask.contiguous(), clip_zero=cz))
+            cls = MafGrad if ops.ar_flow_bwd_supported(self.desc) else WideMafGrad
+            self._mg = (sig, cls(self.desc, perm, mask.contiguous(), clip_zero=cz))
         return self._mg[1]
 
     def train_params(self) -> List[torch.Tensor]:
@@ -345,6 +355,7 @@ class _FusedAR:
 
 
 _TRAIN_FUSED = __import__("os").environ.get("NAZ_TRAIN_FUSED", "1")
+_TRAIN_WIDE = __import__("os").environ.get("NAZ_TRAIN_WIDE", "1")  # the GEMM-composed maf backward
 _AR_FUSED = __import__("os").environ.get("NAZ_AR_FUSED", "1")
 _AR_PASS0 = __import__("os").environ.get("NAZ_AR_PASS0", "1") != "0"  # one-context-vector first-pass folding
 

@@ -351,6 +351,25 @@ def affine_ar_bwd(x: Tensor, raw: Tensor, y: Tensor, inverse: bool, g_y: Tensor,
     return g_x, g_raw
 
 
+def maf_dim_vjp(raw: Tensor, s: Tensor, g: Tensor, g_lp: Optional[Tensor], dim: int, g_next: Tensor, tot: Tensor,
+                chain: Optional[Tensor] = None, clip_zero: bool = False) -> None:
+    """One dim of the maf inverse layer's VJP (naz_maf_dim_vjp): raw [B, 2D] the MADE output, s [B, D]
+    the layer output, g [B, D] = dL/ds; writes g_next[:, dim], tot[:, dim], tot[:, D + dim] and,
+    when given, chain [B, 2D] (zero but for those two columns)."""
+    dev = _dev(raw, s, g, g_lp, g_next, tot, chain)
+    B, D = s.shape
+    ts = [raw, s, g, g_next, tot] + ([] if chain is None else [chain])
+    if any(t.stride(-1) != 1 or t.shape[0] != B for t in ts) or raw.shape[1] != 2 * D or tot.shape[1] != 2 * D or \
+            g.shape[1] != D or g_next.shape[1] != D or (chain is not None and chain.shape[1] != 2 * D):
+        raise ValueError("maf_dim_vjp: raw/tot/chain [B, 2D], s/g/g_next [B, D] with unit column stride")
+    if g_lp is not None and (g_lp.shape != (B,) or not g_lp.is_contiguous()):
+        raise ValueError("maf_dim_vjp: g_lp must be a contiguous [B] tensor")
+    check(lib().naz_maf_dim_vjp(AFFINE_CLIP_ZERO_GRAD if clip_zero else 0, _p(raw), raw.stride(0), _p(s), s.stride(0),
+                                _p(g), g.stride(0), _p(g_lp), _p(g_next), g_next.stride(0), _p(tot), tot.stride(0),
+                                _p(chain), 0 if chain is None else chain.stride(0), B, D, int(dim), _stream(dev)),
+          "maf_dim_vjp")
+
+
 def base_log_prob_bwd(z: Tensor, g_lp: Tensor) -> Tensor:
     dev = _dev(z, g_lp)
     z, ldz = _rows(z)
@@ -590,6 +609,7 @@ def coupling_layer(d: CouplingDesc, packed: Tensor, layer: int, x: Tensor, conte
 # ----------------------------------------------------------------------------- §8b naz_{spline,affine}_ar_inv
 AR_KIND = {"nsa": 0, "maf": 1}  # NAZ_AR_SPLINE, NAZ_AR_AFFINE
 AR_CLIP_ZERO_GRAD = 1  # naz_ar_desc.flags: NAZ_AR_CLIP_ZERO_GRAD
+AFFINE_CLIP_ZERO_GRAD = 2  # naz_affine_ar_bwd / naz_maf_dim_vjp mode bit: NAZ_AFFINE_CLIP_ZERO_GRAD
 
 
 def ar_flow_desc(kind: str, D: int, C: int, H: int, L: int, n_hidden: int = 2, K: int = 8, act: str = "tanh",

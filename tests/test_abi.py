@@ -83,8 +83,19 @@ def test_maf_backward_and_batched_wgrad_host_errors():
     bad = ops.ar_flow_desc("maf", 16, 32, 128, 4, 2)
     rc = L.naz_ar_flow_bwd_layer(bad, 16, 16, 16, 0, 16, 16, 0, 16, None, bufs, 16, 128, None)
     assert rc != 0 and b"no fused backward" in L.naz_last_error()
-    rc = L.naz_ar_flow_log_prob_train(bad, 16, 16, 2, 16, 2, 16, 16, 128, None)
-    assert rc != 0 and b"no fused backward" in L.naz_last_error()
+    # the saved-state forward: any affine flow with a fused inverse (the wide MLE MAFs compose their
+    # backward of GEMMs); a spline flow has none
+    nsa = ops.ar_flow_desc("nsa", 16, 32, 128, 4, 2)
+    rc = L.naz_ar_flow_log_prob_train(nsa, 16, 16, 2, 16, 2, 16, 16, 128, None)
+    assert rc != 0 and b"no fused affine inverse" in L.naz_last_error()
+    wide = ops.ar_flow_desc("maf", 4, 2, 512, 18, 5)
+    assert L.naz_ar_flow_log_prob_train(wide, 16, 16, 4, 16, 2, 16, 16, 0, None) == 0  # no rows: no launch
+    # one dim of the composed backward's VJP: dim range and null checks before any launch
+    rc = L.naz_maf_dim_vjp(0, 16, 8, 16, 4, 16, 4, None, 16, 4, 16, 8, None, 0, 128, 4, 4, None)
+    assert rc != 0 and b"outside" in L.naz_last_error()
+    rc = L.naz_maf_dim_vjp(0, None, 8, 16, 4, 16, 4, None, 16, 4, 16, 8, None, 0, 128, 4, 0, None)
+    assert rc != 0 and b"null pointer" in L.naz_last_error()
+    assert L.naz_maf_dim_vjp(0, None, 8, None, 4, None, 4, None, None, 4, None, 8, None, 0, 0, 4, 0, None) == 0
     # batched dW: widths beyond the bf16x6 instances, misaligned rows
     rc = L.naz_wgrad_batched(1024, 160, 168, 2, 16, 160, 1 << 20, 16, 168, 1 << 20, 16, 168, 0, None, 0, None)
     assert rc != 0 and b"naz_wgrad_batched" in L.naz_last_error()

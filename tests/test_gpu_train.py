@@ -320,17 +320,11 @@ def test_fused_train_full_size_properties():
         assert p.grad is not None and bool(torch.isfinite(p.grad).all()), f"d/d{k} not finite at 2^20 rows"
 
 
-@pytest.mark.parametrize("ctx_rows,B", [(True, 3001), (False, 777)])
-def test_fused_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
-    """The maf NLL step on the fused maf backward (flows/maf_grad.py: saved-state inverse kernel,
-    made_ar_bwd_kernel per layer, batched bf16x6 dW) at the paper shape (D=2 | C=2, H=[150]x3)
-    against the oracle's float64 autograd (tests/parity.py gradient criterion) and the per-node
-    walk; ragged batches, per-row and broadcast contexts."""
+def _maf_train_vs_oracle_and_walk(monkeypatch, D, C, hidden, L, B, ctx_rows, what):
     from naz_amd.flows import NormalizingFlow
     from naz_amd.flows import flow as flow_mod
     from naz_amd.flows import io as fio
-    D, C, L = 2, 2, 4
-    spec = dict(flow_type="maf", D=D, C=C, hidden=[150, 150, 150], L=L)
+    spec = dict(flow_type="maf", D=D, C=C, hidden=list(hidden), L=L)
     state = {k: v.numpy() for k, v in O.random_state(spec, seed=23).items()}
     xh = O.gaussian_mixture(B, D, seed=4)
     ch = O.context_normal(B if ctx_rows else 1, C, seed=5)
@@ -339,7 +333,7 @@ def test_fused_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
     res = {}
     for fused in ("1", "0"):
         monkeypatch.setattr(flow_mod, "_TRAIN_FUSED", fused)
-        f = NormalizingFlow("maf", None, D, C, [150, 150, 150], L)
+        f = NormalizingFlow("maf", None, D, C, list(hidden), L)
         fio.load_state(f, state)
         assert f.fused and f._plan.train_ready(x, c) == (fused == "1")
         lp = f.log_prob(x, condition=c)
@@ -355,10 +349,28 @@ def test_fused_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
         keys = [k for k in sd if sd[k].requires_grad]
         out.update(zip(keys, torch.autograd.grad(-lpo.mean(), [sd[k] for k in keys])))
         out["lp"] = lpo.detach()
-    assert_parity(_np(res["1"][0]), _np(g64["lp"]), _np(g32["lp"]), what="fused maf train log_prob")
+    assert_parity(_np(res["1"][0]), _np(g64["lp"]), _np(g32["lp"]), what=f"{what} train log_prob")
     for k, g in res["0"][1].items():
         a = res["1"][1][k]
         ref = _np(g64[k])
-        assert_parity(_np(a), ref, _np(g32[k]), what=f"fused maf d/d{k}", floor=grad_floor(ref), count_factor=None)
+        assert_parity(_np(a), ref, _np(g32[k]), what=f"{what} d/d{k}", floor=grad_floor(ref), count_factor=None)
         rel = float((a - g).norm() / g.norm().clamp_min(1e-30))
-        assert rel < 5e-3, f"{k}: fused vs walk {rel:.2e}"
+        assert rel < 5e-3, f"{k}: {what} vs walk {rel:.2e}"
+
+
+@pytest.mark.parametrize("ctx_rows,B", [(True, 3001), (False, 777)])
+def test_fused_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
+    """The maf NLL step on the fused maf backward (flows/maf_grad.py: saved-state inverse kernel,
+    made_ar_bwd_kernel per layer, batched bf16x6 dW) at the paper shape (D=2 | C=2, H=[150]x3)
+    against the oracle's float64 autograd (tests/parity.py gradient criterion) and the per-node
+    walk; ragged batches, per-row and broadcast contexts."""
+    _maf_train_vs_oracle_and_walk(monkeypatch, 2, 2, [150] * 3, 4, B, ctx_rows, "fused maf")
+
+
+@pytest.mark.parametrize("ctx_rows,B", [(True, 1027), (False, 300)])
+def test_wide_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
+    """The MLE maf's NLL step (train_mle_all_data_4param.py:87-92: D=4 | C=2, H=[512]x5) on the
+    saved-state wide inverse kernel + the GEMM-composed backward (flows/maf_grad_wide.py: one dense
+    MADE pass, D - 1 input chains and one dW chain per layer) against the oracle's float64 autograd
+    and the per-node walk, at L=3; ragged batches, per-row and broadcast contexts."""
+    _maf_train_vs_oracle_and_walk(monkeypatch, 4, 2, [512] * 5, 3, B, ctx_rows, "wide maf")

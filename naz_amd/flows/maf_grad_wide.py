@@ -46,6 +46,10 @@ from torch import Tensor
 
 from .. import ops
 
+# dW: one strided GEMM per block (measured faster than the batch-reduction kernel on these strided
+# views: 222 vs 254 ms per 2^16-row maf4 step, profiles/r04_s10_*); NAZ_MAF_WIDE_WGRAD=1 = the latter
+_ONE_DW_GEMM = os.environ.get("NAZ_MAF_WIDE_WGRAD", "0") != "1"
+
 
 class WideMafGrad:
     """Same interface as ``maf_grad.MafGrad`` (images / forward / backward / __call__) for an affine
@@ -176,6 +180,23 @@ class WideMafGrad:
         ops.ar_flow_log_prob_train(self.desc, imgs[0], x, ctx, b["states"], out=b["lp"])
         return b["lp"], b["states"]
 
+    @staticmethod
+    def _wgrad(gv: Tensor, xv: Tensor, out: Tensor, rowsum: Optional[Tensor]) -> None:
+        """out += gvᵀ xv (+ rowsum += Σ_rows gv) in pieces of <= 256 x 256 outputs (the bias column
+        rides with the last column piece): the batch-reduction kernel's shape limits (gemm_rows.hip
+        wgrad: N1 <= 256, N2 + 1 <= 256), which take strided row views."""
+        n1, n2 = gv.shape[1], xv.shape[1]
+        if _ONE_DW_GEMM:  # one strided GEMM per block (the generic 64 x 64 tile kernel)
+            ops.gemm(gv.t(), xv, out=out, accumulate=True, rowsum=rowsum)
+            return
+        for r0 in range(0, n1, 256):
+            r1 = min(n1, r0 + 256)
+            cuts = list(range(0, n2, 255)) + [n2]
+            for j, (c0, c1) in enumerate(zip(cuts[:-1], cuts[1:])):
+                last = j == len(cuts) - 2
+                ops.gemm(gv[:, r0:r1].t(), xv[:, c0:c1], out=out[r0:r1, c0:c1], accumulate=True,
+                         rowsum=rowsum[r0:r1] if (last and rowsum is not None) else None)
+
     def _chain(self, a: Tensor, W, h, P: int, b: dict, dw=None) -> Tensor:
         """The transposed products of one chain, output layer first, over the units [0, P): a = dL/d
         (MADE output) [B, 2D] -> dL/d(first hidden pre-activation) [B, :P].  ``dw``: the layer's dW
@@ -186,8 +207,7 @@ class WideMafGrad:
         for i in range(NH - 1, 0, -1):
             if dw is not None:
                 for (a0, b0, fk, _) in blks:
-                    ops.gemm(dl[:, a0:b0].t(), h[i - 1][:, :fk], out=dw[i][0][a0:b0, :fk], accumulate=True,
-                             rowsum=dw[i][1][a0:b0])
+                    self._wgrad(dl[:, a0:b0], h[i - 1][:, :fk], dw[i][0][a0:b0, :fk], dw[i][1][a0:b0])
             nxt = b["db"] if dl.data_ptr() == b["da"].data_ptr() else b["da"]
             for (a0, b0, _, k0) in blks:
                 ops.gemm_dact(dl[:, k0:P], W[i][0][k0:P, a0:b0], h[i - 1][:, a0:b0], "tanh", out=nxt[:, a0:b0])
@@ -238,11 +258,11 @@ class WideMafGrad:
             ops.maf_dim_vjp(raw, s, g, g_lp, int(self.perms[l, 0]), g_next, tot, chain=None,
                             clip_zero=self.clip_zero)
             # 3. the total δ's and this layer's dW / db
-            ops.gemm(tot.t(), h[NH - 1][:, :A], out=G[NH][0][:, :A], accumulate=True, rowsum=G[NH][1])
+            self._wgrad(tot, h[NH - 1][:, :A], G[NH][0][:, :A], G[NH][1])
             dl = self._chain(tot, W, h, A, b, dw=G)
             if cb is not None:
-                ops.gemm(dl.t(), cb, out=G[0][0][:A, :C], accumulate=True)
-            ops.gemm(dl.t(), s, out=G[0][0][:A, C:], accumulate=True, rowsum=G[0][1][:A])
+                self._wgrad(dl, cb, G[0][0][:A, :C], None)
+            self._wgrad(dl, s, G[0][0][:A, C:], G[0][1][:A])
             g, g_next = g_next, g
         return self.ws * self.mask, g
 

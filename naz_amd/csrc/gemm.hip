@@ -77,6 +77,96 @@ __global__ void __launch_bounds__(256) gemm_kernel(int M, int N, int64_t K, cons
   }
 }
 
+// gemm_tn128_kernel: the same contract for the batch-reduction shape with wide outputs —
+//   C[m, n] (+)= Σ_k A[k·sak + m] · B[k·sbk + n] [· mask(m, n)]   (A = Gᵀ, B = X, unit m / n strides)
+// dW = mask ⊙ (δᵀ·h) of a 512-wide MADE's degree blocks (flows/maf_grad_wide.py), whose outputs
+// exceed the batch-reduction kernel's 256 x 256 (gemm_rows.hip wgrad).  128 x 128 tiles per 256-thread
+// workgroup (4 waves x 64 x 64 = 2 x 2 v_mfma_f32_32x32x2_f32 blocks), BK = 16 through a
+// double-buffered LDS pair with the next chunk's global loads (coalesced along m / n) in flight
+// during this chunk's MFMAs: twice the generic tile's FLOPs per loaded byte.
+constexpr int TB = 128, TPAD = 4;
+__global__ void __launch_bounds__(256) gemm_tn128_kernel(int M, int N, int64_t K, const float* __restrict__ A,
+                                                         int64_t sak, const float* __restrict__ Bm, int64_t sbk,
+                                                         float* __restrict__ Cm, int64_t scm, int64_t scn,
+                                                         const float* __restrict__ mask, int64_t smm, int64_t smn,
+                                                         int accumulate, int atomic, int64_t k_per_split,
+                                                         float* __restrict__ rowsum) {
+  __shared__ float As[2][GBK][TB + TPAD];
+  __shared__ float Bs[2][GBK][TB + TPAD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * TB, n0 = blockIdx.y * TB;
+  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
+  const int64_t kend = (kbeg + k_per_split) < K ? (kbeg + k_per_split) : K;
+  const int NE = rowsum != nullptr ? N + 1 : N;  // column N: an all-ones B column -> rowsum
+  const int mm = tid & (TB - 1), kq = tid >> 7;  // loader: column mm, k rows kq + 2u
+  const int am = m0 + mm, bn = n0 + mm;
+  float ra[8], rb[8];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = k0 + kq + 2 * u;
+      const bool kin = k < kend;
+      ra[u] = (kin && am < M) ? A[k * sak + am] : 0.f;
+      rb[u] = (kin && bn < N) ? Bm[k * sbk + bn] : ((kin && bn == N && bn < NE) ? 1.f : 0.f);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      As[buf][kq + 2 * u][mm] = ra[u];
+      Bs[buf][kq + 2 * u][mm] = rb[u];
+    }
+  };
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int64_t nk = (kend - kbeg + GBK - 1) / GBK;
+  if (nk > 0) {
+    load(kbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int64_t c = 0; c < nk; ++c) {
+    const int buf = (int)(c & 1);
+    if (c + 1 < nk) load(kbeg + (c + 1) * GBK);  // in flight during this chunk's MFMAs
+#pragma unroll
+    for (int kk = 0; kk < GBK; kk += 2) {
+      const int kr = kk + (lane >> 5), cl = lane & 31;
+      const float a0 = As[buf][kr][wm * 64 + cl], a1 = As[buf][kr][wm * 64 + 32 + cl];
+      const float b0 = Bs[buf][kr][wn * 64 + cl], b1 = Bs[buf][kr][wn * 64 + 32 + cl];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (c + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+    if (n >= NE) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= M) continue;
+        float v = acc[i][j][r];
+        if (mask != nullptr && n < N) v *= mask[(int64_t)m * smm + (int64_t)n * smn];
+        float* dst = n < N ? Cm + (int64_t)m * scm + (int64_t)n * scn : rowsum + m;
+        if (atomic) atomicAdd(dst, v);
+        else *dst = accumulate ? *dst + v : v;
+      }
+    }
+  }
+}
+
 // out[n] (+)= Σ_m A[m, n]   (A row-major with row stride lda).  A block is `cw` adjacent columns
 // (a power of two <= 64, >= N when N is narrow) x 256 / cw row lanes, so a wave reads whole
 // 256-byte row pieces (the [B, 16] bias gradients of the CNF walk: 16 x 16), walking
@@ -111,6 +201,14 @@ __global__ void act_bwd_kernel(const float* __restrict__ gy, int64_t ldg, const 
   gp[m * ldp + n] = gy[m * ldg + n] * activate_grad_from_out(act, y[m * ldy + n]);
 }
 
+static bool gemm_tn128_enabled() {  // NAZ_GEMM_TN128=0: the generic 64 x 64 tile kernel (A/B)
+  static const bool on = [] {
+    const char* e = getenv("NAZ_GEMM_TN128");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
 int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
          float* C, int64_t scm, int64_t scn, const float* mask, int64_t smm, int64_t smn, int mask_b, int accumulate,
          int split_k, float* rowsum, hipStream_t s) {
@@ -119,7 +217,11 @@ int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, cons
     if (!accumulate && split_k <= 1) return set_error("naz_gemm: K = 0 with overwrite is not supported");
     return 0;
   }
-  {  // batch-row fast paths (gemm_rows.hip)
+  // the batch reduction over strided column views with outputs >= 64 x 64 (a wide MADE's degree
+  // blocks): the 128 x 128 tiles below; gemm_rows.hip's reductions are built for contiguous rows
+  const bool tn = sam == 1 && sbn == 1 && !(mask_b && mask != nullptr) && M >= 64 &&
+                  N + (rowsum != nullptr ? 1 : 0) >= 64 && K >= 2048 && gemm_tn128_enabled();
+  if (!(tn && (sak != M || sbk != N))) {  // batch-row fast paths (gemm_rows.hip)
     int rc = 0;
     if (gemm_rows_try(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, mask, smm, smn, mask_b, accumulate, rowsum, s,
                       &rc) == 0)
@@ -130,9 +232,15 @@ int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, cons
   kps = (kps + GBK - 1) / GBK * GBK;
   const int64_t splits = (K + kps - 1) / kps;
   const int NE = rowsum != nullptr ? N + 1 : N;
-  dim3 grid((unsigned)((M + GBM - 1) / GBM), (unsigned)((NE + GBN - 1) / GBN), (unsigned)splits);
   // split-K always accumulates atomically into C (the caller zeroes C for an overwrite)
   const int atomic = splits > 1 ? 1 : 0;
+  if (tn) {  // the batch reduction with wide outputs: 128 x 128 tiles
+    dim3 g128((unsigned)((M + TB - 1) / TB), (unsigned)((NE + TB - 1) / TB), (unsigned)splits);
+    hipLaunchKernelGGL(gemm_tn128_kernel, g128, dim3(256), 0, s, M, N, K, A, sak, B, sbk, C, scm, scn, mask, smm, smn,
+                       accumulate, atomic, kps, rowsum);
+    return check_launch("gemm_tn128_kernel");
+  }
+  dim3 grid((unsigned)((M + GBM - 1) / GBM), (unsigned)((NE + GBN - 1) / GBN), (unsigned)splits);
   hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, s, M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, mask, smm,
                      smn, mask_b && mask != nullptr, accumulate, atomic, kps, rowsum);
   return check_launch("gemm_kernel");

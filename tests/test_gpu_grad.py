@@ -184,6 +184,32 @@ def test_gemm_strided_split_k(M, N, K, split):
     _check(rs, a.double().sum(0), a.sum(0), f"gemm {M}x{N}x{K} fused row sums (bias gradient)")
 
 
+@pytest.mark.parametrize("M,N,K,masked,acc", [(512, 432, 65573, True, False), (172, 512, 70001, False, True),
+                                                (428, 300, 2048, False, False), (100, 97, 9000, True, True),
+                                                (88, 512, 65536, False, True), (84, 88, 4096, True, False)])
+def test_gemm_tn128_wide_reductions(M, N, K, masked, acc):
+    """The 128 x 128-tile batch reduction (gemm_tn128_kernel: dW of a 512-wide MADE's degree blocks,
+    flows/maf_grad_wide.py) on strided column views of wider row-major buffers, ragged tiles and
+    chunks, split-K atomics, the fused row sums, an output mask and accumulation, vs fp64."""
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(M * 3 + N)
+    ga = torch.randn(K, M + 9, generator=g)  # G = ga[:, 5:5+M] (row stride M + 9)
+    xb = torch.randn(K, N + 3, generator=g)
+    a, b = ga[:, 5:5 + M], xb[:, 1:1 + N]
+    mask = (torch.rand(M, N, generator=g) > 0.3).float() if masked else None
+    c0 = torch.randn(M, N, generator=g) if acc else torch.zeros(M, N)
+    r0 = torch.randn(M, generator=g) if acc else torch.zeros(M)
+    out, rs = _cuda(c0).clone(), _cuda(r0).clone()
+    ops.gemm(_cuda(ga)[:, 5:5 + M].t(), _cuda(xb)[:, 1:1 + N], out=out, mask=None if mask is None else _cuda(mask),
+             accumulate=acc, rowsum=rs)
+    p64 = a.double().t() @ b.double()
+    p32 = a.t() @ b
+    if mask is not None:
+        p64, p32 = p64 * mask.double(), p32 * mask
+    _check(out, p64 + c0.double(), p32 + c0, f"gemm_tn128 {M}x{N}x{K}")
+    _check(rs, a.double().sum(0) + r0.double(), a.sum(0) + r0, f"gemm_tn128 {M}x{N}x{K} row sums")
+
+
 @pytest.mark.parametrize("N1,N2,M", [(192, 128, 70001), (128, 128, 4096), (128, 40, 33333), (184, 128, 517),
                                      (60, 20, 1000), (256, 96, 20000), (100, 52, 16), (4, 4, 9), (128, 8, 1 << 18),
                                      # the deep-ring (3-4 slot) instances: fewer chunks than slots,

@@ -215,7 +215,7 @@ def load_traffic(mode: str, rows: int = None):
     (profiles/traffic_config3_<mode>.json, written by scripts/pmc_summary.py /
     scripts/pmc_step_traffic.py), if present.  A file that records the rows it was measured on
     (``rows_per_launch``) is scaled linearly to ``rows`` (the traffic of a step is per row)."""
-    p = ROOT / "profiles" / f"traffic_config3_{mode}.json"
+    p = ROOT / "profiles" / (mode if mode.endswith(".json") else f"traffic_config3_{mode}.json")
     if p.exists():
         try:
             d = json.loads(p.read_text())
@@ -367,7 +367,9 @@ def run_train_flow(args, dev, rank, world, dist):
         fl_ref = 3 * 2 * Dd * Ld * sum(a * b for a, b in zip(dims[:-1], dims[1:]))  # D-pass fwd + autograd
         fwd = ops.ar_executed_flop_per_row(plan.desc)["inverse"]
         bwd = plan.maf_grad().flop_per_row() if "wide" in path else 0  # the blocks the GEMMs execute
-        roof = {"bound": "mfma", "unit": "TFLOP/s", "traffic": None, "kernel": "whole step",
+        traffic, traffic_src = load_traffic(f"traffic_{args.flow}_train.json", rows=B)
+        roof = {"bound": "mfma", "unit": "TFLOP/s", "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": "whole step",
                 "reference_flop_per_row": fl_ref,
                 "reference_tflops": fl_ref * B / step_s / 1e12}
         if "wide" in path:

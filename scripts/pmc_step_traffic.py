@@ -2,7 +2,10 @@
 1, WRITE_SIZE in pass 2): sum over every dispatch, FETCH_SIZE x 2 (gfx950 wide-read counting,
 MI355X_MICROARCH.md §HBM) + WRITE_SIZE, divided by the number of steps the profiled command ran.
 
-    python scripts/pmc_step_traffic.py gpurun_out/pmc_<TAG> <steps> profiles/traffic_config3_train.json
+    python scripts/pmc_step_traffic.py gpurun_out/pmc_<TAG> <steps> profiles/traffic_config3_train.json [rows]
+
+``rows`` (optional): the rows one step processed, recorded as ``rows_per_launch`` so bench.py scales
+the figure to its own batch.
 """
 import csv
 import json
@@ -29,6 +32,8 @@ def main():
            "steps_profiled": steps, "source": str(src),
            "top_kernels_bytes_per_step": {k: v / steps for k, v in top},
            "correction": "FETCH_SIZE x2 (gfx950 wide-read counting, MI355X_MICROARCH.md §HBM)"}
+    if len(sys.argv) > 4:
+        out["rows_per_launch"] = int(sys.argv[4])
     dst.write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
 

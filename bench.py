@@ -379,10 +379,21 @@ def run_train_flow(args, dev, rank, world, dist):
                         peak_note=f"harmonic FLOP-weighted ceiling: forward {fwd:.3g} FLOP/row on the f16x3 split "
                                   f"({BF16_PEAK_TFLOPS / 3:.0f} TF), backward {bwd:.3g} FLOP/row on exact FP32 MFMA "
                                   f"({FP32_PEAK_TFLOPS:.1f} TF)")
+        elif "made_ar_bwd" in path:  # the fused maf backward: executed FLOPs, each on its pipe (§4.10)
+            ex = ops.ar_executed_flop_per_row(plan.desc)
+            f16 = ex["inverse"] + ex["bwd"]
+            tot = f16 + ex["dw"]
+            peak = tot / (f16 / (BF16_PEAK_TFLOPS / 3) + ex["dw"] / (BF16_PEAK_TFLOPS / X6_PRODUCTS))
+            achieved = tot * B / step_s / 1e12
+            roof.update(achieved=achieved, peak=peak, frac=achieved / peak, flop_per_row=tot,
+                        peak_note=f"harmonic FLOP-weighted ceiling: inverse + backward {f16:.3g} FLOP/row on the "
+                                  f"f16x3 split ({BF16_PEAK_TFLOPS / 3:.0f} TF), dW {ex['dw']:.3g} on bf16x6 "
+                                  f"({BF16_PEAK_TFLOPS / X6_PRODUCTS:.0f} TF)")
         else:
             achieved = fl_ref * B / step_s / 1e12
             roof.update(achieved=achieved, peak=FP32_PEAK_TFLOPS, frac=achieved / FP32_PEAK_TFLOPS,
-                        flop_per_row=fl_ref, peak_note="the reference's FLOPs against the exact FP32 MFMA peak")
+                        flop_per_row=fl_ref, peak_note="the reference's FLOPs against the exact FP32 MFMA peak "
+                                                       "(the walk's degree-scheduled GEMMs execute fewer)")
         rec = {
             "metric": f"samples/sec through the NLL training step (log_prob fwd + backward + grad all-reduce + clip + "
                       f"Adam), naz {ftype} flow",

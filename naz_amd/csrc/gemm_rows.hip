@@ -316,11 +316,15 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
     p.vst = p.vst && p.zc % 4 == 0;
   }
   int nb = (p.N + 31) / 32;
+  // outputs of more than 4 column blocks in half-width panels (<= 4 x 32 for up to 8 blocks: 4 waves /
+  // SIMD instead of 2):
+  // the wide maf's 168-172-unit degree blocks, 200.0 -> 184.6 ms per NLL step (profiles/r04_s14_*);
+  // NAZ_RG_SPLIT=0 keeps one panel
   static const int split = [] {
     const char* e = getenv("NAZ_RG_SPLIT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
-  if (split && nb > 4) nb = (nb + 1) / 2;  // two column blocks of <= 4 x 32: 4 waves / SIMD
+  if (split && nb > 4) nb = (nb + 1) / 2;
   switch (nb > 8 ? 8 : nb) {
     case 1: rowgemm_launch<1>(p, nz, s); break;
     case 2: rowgemm_launch<2>(p, nz, s); break;

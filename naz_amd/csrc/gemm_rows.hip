@@ -215,12 +215,13 @@ __global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel
       constexpr int F4R = 8 * EG, RPI = 64 / F4R;
       const int rr = lane / F4R, c4 = lane % F4R;
       const int col = n0 + 32 * o0 + 4 * c4;
+      const bool inpanel = 32 * o0 + 4 * c4 < 32 * NB;  // odd NB, EG = 2: the pair's second block is absent
       if (p.jvp != nullptr) {  // naz_gemm_jvp_bwd: RPI (value, tangent) row pairs per wave-instruction
 #pragma unroll
         for (int it = 0; it < 16 / RPI; ++it) {
           const int pr = it * RPI + rr;
           const int64_t m = m0 + wave * 32 + 2 * pr;  // value row; m + 1 = its tangent row (M is even)
-          if (m >= p.M || col >= p.N) continue;
+          if (m >= p.M || col >= p.N || !inpanel) continue;
           const float* ev = E + (2 * pr) * EP + 4 * c4;
           const float* sv = p.jvp + m * p.ldjvp + col;
           float* cv = p.c + m * p.ldc + col;
@@ -241,7 +242,7 @@ __global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel
       for (int it = 0; it < 32 / RPI; ++it) {
         const int row = it * RPI + rr;
         const int64_t m = m0 + wave * 32 + row;
-        if (m >= p.M || col >= p.N) continue;
+        if (m >= p.M || col >= p.N || !inpanel) continue;
         float4 v = *reinterpret_cast<const float4*>(E + row * EP + 4 * c4);
         if (p.dy != nullptr) {  // chained act' (naz_gemm_dact), applied on the 16-byte row piece
           const float* dyr = p.dy + m * p.lddy + col;
@@ -316,13 +317,13 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
     p.vst = p.vst && p.zc % 4 == 0;
   }
   int nb = (p.N + 31) / 32;
-  // outputs of more than 4 column blocks in half-width panels (<= 4 x 32 for up to 8 blocks: 4 waves /
-  // SIMD instead of 2):
-  // the wide maf's 168-172-unit degree blocks, 200.0 -> 184.6 ms per NLL step (profiles/r04_s14_*);
-  // NAZ_RG_SPLIT=0 keeps one panel
+  // NAZ_RG_SPLIT=1: outputs of more than 4 column blocks in half-width panels (<= 4 x 32 for up to 8
+  // blocks: 4 waves / SIMD instead of 2): the wide maf's 168-172-unit degree blocks, 200.0 -> 184.6 ms
+  // per NLL step (profiles/r04_s14_*).  Off by default until the full suite has run with it (an odd
+  // NB's paired epilogue wrote past its panel: fixed below, not yet re-validated on the GPU)
   static const int split = [] {
     const char* e = getenv("NAZ_RG_SPLIT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   if (split && nb > 4) nb = (nb + 1) / 2;
   switch (nb > 8 ? 8 : nb) {

@@ -2124,7 +2124,7 @@ int ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* 
 #endif
 template __global__ void naz::made_ar_inv_wide_kernel<naz::CfgARIW<naz::CfgARW<4, 2, 512, NAZ_EXP_NHID>>>(
     const float*, int, const float*, int64_t, const float*, int64_t, const float*, const float*, float*, int64_t,
-    int64_t, int64_t, int64_t, int64_t, naz::u32x4*);
+    int64_t, int64_t, int64_t, int64_t, naz::u32x4*, float*);
 #endif
 
 #if NAZ_PART == 8  // schedule experiments on the w32 log_prob kernel alone (not built by build.py)

@@ -367,10 +367,20 @@ def test_fused_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
     _maf_train_vs_oracle_and_walk(monkeypatch, 2, 2, [150] * 3, 4, B, ctx_rows, "fused maf")
 
 
-@pytest.mark.parametrize("ctx_rows,B", [(True, 1027), (False, 300)])
+@pytest.mark.parametrize("ctx_rows,B", [(True, 1027), (False, 300), (True, 2311)])
 def test_wide_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
     """The MLE maf's NLL step (train_mle_all_data_4param.py:87-92: D=4 | C=2, H=[512]x5) on the
     saved-state wide inverse kernel + the GEMM-composed backward (flows/maf_grad_wide.py: one dense
     MADE pass, D - 1 input chains and one dW chain per layer) against the oracle's float64 autograd
-    and the per-node walk, at L=3; ragged batches, per-row and broadcast contexts."""
+    and the per-node walk, at L=3; ragged batches, per-row and broadcast contexts.  B = 2311 puts the
+    dW reductions (K = B >= 2048) on gemm_tn128_kernel."""
     _maf_train_vs_oracle_and_walk(monkeypatch, 4, 2, [512] * 5, 3, B, ctx_rows, "wide maf")
+
+
+@pytest.mark.parametrize("ctx_rows,B", [(True, 1500), (False, 333)])
+def test_config3_ar_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
+    """SURVEY §8d's config-3 AR variant as a maf (D=16 | C=32, H=[128,128]): its inverse is fused but
+    made_ar_bwd is not compiled for it, so its NLL step takes the GEMM-composed backward
+    (flows/maf_grad_wide.py: 15 input chains per layer, a 32-wide context in the dW of W_0) -- checked
+    here against the oracle's float64 autograd and the per-node walk."""
+    _maf_train_vs_oracle_and_walk(monkeypatch, 16, 32, [128, 128], 3, B, ctx_rows, "composed maf D16C32")

@@ -317,7 +317,7 @@ def run_train_flow(args, dev, rank, world, dist):
     (default 2^16), one process per GPU, gradients all-reduced in one flat bucket."""
     from naz_amd.flows import NormalizingFlow
     from naz_amd.flows import flow as flow_mod
-    from naz_amd.trainers import DataParallel, nll_step
+    from naz_amd.trainers import DataParallel, GraphedNllStep, nll_step
     from naz_amd.trainers.train_flows import _flow_parameters
     from naz_amd import ops
     ftype, Dd, Cd, hid, Ld, extra, _, desc = FLOW_CASES[args.flow]
@@ -334,13 +334,17 @@ def run_train_flow(args, dev, rank, world, dist):
     dp = DataParallel()
     params = _flow_parameters(f)
     dp.broadcast_params(params)
-    opt = torch.optim.Adam(params, lr=1e-4)
+    opt = torch.optim.Adam(params, lr=1e-4, capturable=bool(args.graph))
     plan = f._plan
     path = ("autograd walk (per-layer HIP kernels)" if args.train_walk or not plan.train_ready(x, c) else
             "fused maf backward (made_ar_bwd.h)" if ops.ar_flow_bwd_supported(plan.desc) else
             "saved-state wide inverse kernel + GEMM-composed backward (flows/maf_grad_wide.py)")
 
+    graphed = GraphedNllStep(f, opt, params, dp, G, clip_val=1.0, micro_batch=args.micro_batch) if args.graph else None
+
     def step():
+        if graphed is not None:  # the whole step as one captured HIP graph (trainers.GraphedNllStep)
+            return graphed(x, c)
         return nll_step(f, x, c, opt, params, dp, G, clip_val=1.0, micro_batch=args.micro_batch)
 
     for _ in range(args.warmup):
@@ -403,6 +407,7 @@ def run_train_flow(args, dev, rank, world, dist):
             "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
             "config": {"workload": desc + " — NLL step", "batch_per_gpu": B, "global_batch": G,
                        "micro_batch": args.micro_batch, "path": path,
+                       "hip_graph": bool(args.graph) and graphed.replays >= args.steps,
                        "parallelism": f"dp{world} (RCCL all-reduce, one flat bucket)"},
             "roofline": roof, "final_loss": float(loss),
         }
@@ -1092,6 +1097,8 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=1 << 20,
                     help="--train: rows per forward+backward chunk (gradients accumulate before the all-reduce)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="--train --flow: replay the whole NLL step as one captured HIP graph (trainers.GraphedNllStep)")
     ap.add_argument("--train-walk", action="store_true",
                     help="--train: run the per-node autograd walk instead of the fused NLL step (A/B)")
     ap.add_argument("--train", action="store_true",

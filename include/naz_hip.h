@@ -53,7 +53,30 @@ extern "C" {
 /* ---- library ------------------------------------------------------------ */
 const char* naz_last_error(void);
 int naz_abi_version(void); /* bumps on any signature or contract change (2: naz_ar_desc.flags, affine clip modes,
-                             * naz_ar_flow_supported = 2 for forward-only shapes) */
+                             * naz_ar_flow_supported = 2 for forward-only shapes; 3: packed-image headers and
+                             * registry, caller-owned workspace for the autoregressive log_prob entries) */
+
+/* ---- Packed images (ABI 3) -----------------------------------------------
+ * Every packed weight image (naz_coupling_pack, naz_coupling_pack_bwd, naz_ar_flow_pack[_host],
+ * naz_ar_flow_pack_fwd[_host], naz_ar_flow_pack_bwd, naz_cnf_pack) starts with a 256-byte header:
+ * magic "NAZI", layout version, image kind, a layout tag hashed from the descriptor fields the layout
+ * depends on, layers, flags (pass-0 constants), body bytes.  The *_packed_bytes functions include
+ * it.  The device packers register each image they write (base address, header, draw stride,
+ * draws) with the library; a host-packed image, once copied to the device, is registered by
+ * naz_image_attach (reads its header back once, synchronising `stream`; `bytes` = the device
+ * buffer's size).  Every launch entry resolves its image argument through the registry before it
+ * launches and refuses, with an error, an address that holds no registered image (or is not a draw
+ * of one), an image of another kind, descriptor or layout version, a different layer count or body
+ * size, or a draw range outside the packed set.  The registry trusts the last packer or attach at an
+ * address: memory overwritten by other means is not detected.  naz_image_release forgets one.
+ * Python-assembled images of the per-layer MADE kernels (naz_made_*) carry no header.          */
+int naz_image_attach(const void* image, int64_t bytes, void* stream);
+/* Library-wide launch choices that change no result.  "rowgemm_split": the batch-row GEMM (naz_linear_act,
+ * naz_gemm_dact, naz_gemm_jvp_bwd, naz_gemm's dX shape) runs outputs wider than 128 columns as two
+ * half-width panels (1, default; NAZ_RG_SPLIT in the environment sets the initial value) or as one (0).
+ * value >= 0 sets it; returns the value before the call (-1 and an error for an unknown key). */
+int naz_tuning(const char* key, int value);
+int naz_image_release(const void* image);
 /* Diagnostics (no reference counterpart): the first non-finite row state a fused log_prob
  * kernel met, as {1, workgroup, layer, stage counter, row} ({0, ...} = none), optionally
  * cleared.  Fails unless the library was built with -DNAZ_DEBUG_NONFINITE.               */
@@ -390,11 +413,16 @@ typedef struct naz_ar_desc {
 /* 1: both directions fused (log_prob + sample); 2: the forward (sample) direction only (the
  * inverse-direction entry points report the shape as unsupported; no instance today); 0: not
  * instantiated.  The wide production MAFs (D=4 | C=2, H=[512]x5) are 1 since ABI 2's round 4:
- * their log_prob is the persistent-grid wide inverse (one launch; it allocates its per-wave
- * scratch stream-ordered, 128 KB per resident wave), without the pass-0-constants form
- * (naz_ar_flow_pass0_floats < 0) and without a fused backward. */
+ * their log_prob is the persistent-grid wide inverse (one launch; its hidden layers 2.. persist in
+ * caller-owned WORKSPACE, 128 KB per resident wave: naz_ar_flow_workspace_bytes), without the
+ * pass-0-constants form (naz_ar_flow_pass0_floats < 0) and without a fused backward. */
 int naz_ar_flow_supported(const naz_ar_desc* d);
 int64_t naz_ar_flow_packed_bytes(const naz_ar_desc* d);
+/* Device workspace (bytes, 16-byte aligned) that naz_ar_flow_log_prob[_batched|_train] need for B rows
+ * x P draws on the current device: 0 for every shape but the wide MAFs (one 4-wave workgroup per CU,
+ * 128 KB per wave); -1 for an unsupported descriptor.  Pass it as (workspace, workspace_bytes): a call
+ * given less returns an error; no entry allocates.  One workspace per stream. */
+int64_t naz_ar_flow_workspace_bytes(const naz_ar_desc* d, int64_t B, int64_t P);
 /* deg[u] (u < H) = mask index of hidden unit u in every hidden layer (pyro create_mask) */
 int naz_ar_flow_degrees(const naz_ar_desc* d, int* deg);
 /* HOST memory in and out.  flat: per layer W0 (x) mask0 [H][C + D] | b0 [H] | {Wi (x) maski [H][H] | bi [H]}
@@ -405,7 +433,8 @@ int naz_ar_flow_pack_host(const naz_ar_desc* d, const float* flat, const int* pe
 /* out_lp[r] = log p(x_r | ctx_r) (+ naz bounding map when low/high are set); ldc = 0 broadcasts one
  * context row.  |x|, |ctx| must stay below 2^15 (the f16x3 input split); the caller checks. */
 int naz_ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                         int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream);
+                         int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* workspace,
+                         int64_t workspace_bytes, void* stream);
 
 /* The sampling direction of the same flows (pyro *Autoregressive._call, flow.py:94-129): one launch
  * for all L layers in forward order, each layer ONE MADE pass over its input followed by every dim's
@@ -454,7 +483,7 @@ int naz_ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, con
                      int64_t P, const float* pass0, int64_t sp0, const float* mask, void* stream);
 int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                                  int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B,
-                                 int64_t P, int pass0_const, void* stream);
+                                 int64_t P, int pass0_const, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ---- fused maf backward: the NUTS potential's gradient ------------------
  * Replaces jax.grad of bayesian_normalizing_flow's potential Σ_rows flow_lp(unravel(p))
@@ -479,7 +508,8 @@ int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64
  *     (pi D + d), zero padded.  dW_0 = dp_1ᵀ x0, dW_i = dp_{i+1}ᵀ h_i, dW_out = goutᵀ h_n,
  *     biases = column sums of dp_i / gout (naz_gemm), then times the masks. */
 int naz_ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                               int64_t ldc, float* out_lp, float* states, int64_t B, void* stream);
+                               int64_t ldc, float* out_lp, float* states, int64_t B, void* workspace,
+                               int64_t workspace_bytes, void* stream);
 int64_t naz_ar_flow_bwd_packed_bytes(const naz_ar_desc* d);
 int naz_ar_flow_bwd_dims(const naz_ar_desc* d, int* dims);
 int naz_ar_flow_pack_bwd(const naz_ar_desc* d, const float* flat, const float* mask, void* packed, void* stream);
@@ -492,8 +522,9 @@ int naz_ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const vo
  * "nsc": naz_coupling_*) and the autoregressive flows (naz "nsa" / "maf": naz_ar_flow_*).  The
  * packed image is the kind's own (naz_coupling_pack on the device, naz_ar_flow_pack_host on the
  * host); these entries only dispatch.  Replaces NormalizingFlow.log_prob / .sample
- * (naz/flows/flow.py:45-79, 94-129).  naz_workspace_bytes is 0: the fused kernels keep every
- * intermediate on chip.  naz_flow_sample of an AR flow takes its forward image (naz_ar_flow_pack_fwd_host). */
+ * (naz/flows/flow.py:45-79, 94-129).  naz_workspace_bytes(d, B) = the workspace naz_flow_log_prob
+ * needs for B rows: 0 for the coupling kernels and the narrow AR kernels (every intermediate stays
+ * on chip), naz_ar_flow_workspace_bytes for the wide MAFs.  naz_flow_sample of an AR flow takes its forward image (naz_ar_flow_pack_fwd_host). */
 #define NAZ_FLOW_COUPLING 1
 #define NAZ_FLOW_AR 2
 typedef struct naz_flow_desc {
@@ -505,7 +536,8 @@ typedef struct naz_flow_desc {
 int64_t naz_flow_packed_bytes(const naz_flow_desc* d);
 int64_t naz_workspace_bytes(const naz_flow_desc* d, int64_t B);
 int naz_flow_log_prob(const naz_flow_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                      int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream);
+                      int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* workspace,
+                      int64_t workspace_bytes, void* stream);
 int naz_flow_sample(const naz_flow_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx,
                     int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld, int64_t B,
                     void* stream);

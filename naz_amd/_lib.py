@@ -47,6 +47,9 @@ FLOW_COUPLING, FLOW_AR = 1, 2
 SIGNATURES = {
     "naz_last_error": (C.c_char_p, []),
     "naz_abi_version": (C.c_int, []),
+    "naz_image_attach": (C.c_int, [_vp, _i64, _vp]),
+    "naz_image_release": (C.c_int, [_vp]),
+    "naz_tuning": (C.c_int, [C.c_char_p, _i]),
     "naz_debug_nonfinite": (C.c_int, [C.POINTER(C.c_int64), _i]),
     "naz_rqs_fwd": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _i64, _i, _i, _i, C.c_float, _vp]),
     "naz_rqs_inv": (C.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i, _i64, _i, _i, _i, C.c_float, _vp]),
@@ -104,19 +107,22 @@ SIGNATURES = {
     "naz_ar_flow_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),
     "naz_ar_flow_degrees": (C.c_int, [C.POINTER(ArDesc), _vp]),
     "naz_ar_flow_pack_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _vp]),
-    "naz_ar_flow_log_prob": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
+    "naz_ar_flow_workspace_bytes": (C.c_int64, [C.POINTER(ArDesc), _i64, _i64]),
+    "naz_ar_flow_log_prob": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64,
+                                       _vp]),
     "naz_ar_flow_fwd_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),
     "naz_ar_flow_pass0_floats": (C.c_int64, [C.POINTER(ArDesc)]),
     "naz_ar_flow_pack": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
     "naz_ar_flow_log_prob_batched": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
-                                               _i64, _i64, _i, _vp]),
+                                               _i64, _i64, _i, _vp, _i64, _vp]),
     "naz_ar_flow_pack_fwd": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _i64, _i64, _vp, _vp]),
     "naz_ar_flow_sample_batched": (C.c_int, [C.POINTER(ArDesc), _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
                                              _i64, _vp, _i64, _i64, _i64, _vp]),
     "naz_ar_flow_pack_fwd_host": (C.c_int, [C.POINTER(ArDesc), _vp, _vp]),
     "naz_wgrad_batched": (C.c_int, [_i64, _i, _i, _i, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64,
                                     _vp]),
-    "naz_ar_flow_log_prob_train": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
+    "naz_ar_flow_log_prob_train": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64,
+                                             _vp]),
     "naz_ar_flow_bwd_packed_bytes": (C.c_int64, [C.POINTER(ArDesc)]),
     "naz_ar_flow_bwd_dims": (C.c_int, [C.POINTER(ArDesc), _vp]),
     "naz_ar_flow_pack_bwd": (C.c_int, [C.POINTER(ArDesc), _vp, _vp, _vp, _vp]),
@@ -126,7 +132,8 @@ SIGNATURES = {
                                      _vp]),
     "naz_flow_packed_bytes": (C.c_int64, [C.POINTER(FlowDesc)]),
     "naz_workspace_bytes": (C.c_int64, [C.POINTER(FlowDesc), _i64]),
-    "naz_flow_log_prob": (C.c_int, [C.POINTER(FlowDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp]),
+    "naz_flow_log_prob": (C.c_int, [C.POINTER(FlowDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64,
+                                    _vp]),
     "naz_flow_sample": (C.c_int, [C.POINTER(FlowDesc), _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _i64,
                                   _vp]),
     "naz_coupling_supported": (C.c_int, [C.POINTER(CouplingDesc)]),

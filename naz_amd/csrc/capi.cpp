@@ -2,6 +2,11 @@
 // Thin argument validation + dispatch into the HIP translation units.
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
+
+#include <initializer_list>
+#include <map>
+#include <mutex>
 
 #include "naz_internal.h"
 
@@ -34,6 +39,162 @@ static int check_spline_args(const char* fn, const float* x, const float* y, int
   return 0;
 }
 
+// ---- packed weight images: header + registry (include/naz_hip.h "Packed images") -------------
+// Every image a packer writes starts with a 256-byte header (the body stays 256-byte aligned for the
+// kernels' LDS-DMA rings): magic, layout version, image kind, a layout tag hashed from the
+// descriptor fields the layout depends on, layers, flags, body bytes.  The device packers record
+// (base, header, draw stride, draws) in a host-side registry; host-packed images enter it through
+// naz_image_attach, which reads the header back once.  Every launch entry resolves its image
+// pointer through the registry BEFORE launching, so an image that is foreign, truncated, packed for
+// another descriptor, kind or layer count, or by another layout version is refused with an error
+// instead of being streamed into LDS out of bounds.
+constexpr int64_t kImgHdr = 256;
+constexpr uint32_t kImgMagic = 0x495a414eu;  // "NAZI"
+constexpr uint32_t kImgVersion = 3;          // bump whenever any packed layout changes
+enum : uint32_t { IMG_COUPLING = 1, IMG_COUPLING_BWD = 2, IMG_AR_INV = 3, IMG_AR_FWD = 4, IMG_AR_BWD = 5, IMG_CNF = 6 };
+enum : uint32_t { IMG_FLAG_PASS0 = 1 };
+static const char* const kImgKindName[] = {"?", "coupling", "coupling backward", "autoregressive inverse",
+                                           "autoregressive forward", "autoregressive backward", "cnf"};
+
+struct ImgSpec {  // what a descriptor expects of an image
+  uint32_t kind, tag;
+  int L;
+  int64_t body;  // bytes after the header (-1: unsupported descriptor)
+};
+struct ImgRec {
+  uint32_t kind, tag, L, flags;
+  int64_t body, stride, draws;
+};
+static std::mutex g_img_mu;
+static std::map<uintptr_t, ImgRec> g_img;  // image base -> record
+
+static uint32_t fnv(uint32_t h, uint32_t v) {
+  for (int i = 0; i < 4; ++i) {
+    h ^= (v >> (8 * i)) & 0xffu;
+    h *= 16777619u;
+  }
+  return h;
+}
+static uint32_t fbits(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+static uint32_t layout_tag(uint32_t kind, std::initializer_list<uint32_t> fields) {
+  uint32_t h = fnv(fnv(2166136261u, kImgVersion), kind);
+  for (uint32_t v : fields) h = fnv(h, v);
+  return h;
+}
+static ImgSpec spec_coupling(const naz_coupling_desc* d, uint32_t kind) {
+  if (d == nullptr) return {kind, 0, 0, -1};
+  const int64_t b = kind == IMG_COUPLING ? coupling_packed_bytes(d) : coupling_bwd_packed_bytes(d);
+  return {kind,
+          layout_tag(kind, {(uint32_t)d->D, (uint32_t)d->C, (uint32_t)d->S, (uint32_t)d->K, (uint32_t)d->H,
+                            (uint32_t)d->act, (uint32_t)d->has_lower, fbits(d->bound), (uint32_t)d->mfma_mode}),
+          d->L, b};
+}
+static ImgSpec spec_ar(const naz_ar_desc* d, uint32_t kind) {
+  if (d == nullptr) return {kind, 0, 0, -1};
+  const int64_t b = kind == IMG_AR_INV ? ar_flow_packed_bytes(d)
+                    : kind == IMG_AR_FWD ? ar_flow_fwd_packed_bytes(d)
+                                         : ar_flow_bwd_packed_bytes(d);
+  return {kind,
+          layout_tag(kind, {(uint32_t)d->D, (uint32_t)d->C, (uint32_t)d->H, (uint32_t)d->K, (uint32_t)d->act,
+                            d->kind == NAZ_AR_SPLINE ? fbits(d->bound) : 0u, (uint32_t)d->n_hidden,
+                            (uint32_t)d->kind}),
+          d->L, b};
+}
+static ImgSpec spec_cnf(const naz_cnf_desc* d) {
+  if (d == nullptr) return {IMG_CNF, 0, 0, -1};
+  uint32_t hs[4] = {};
+  for (int i = 0; i < 4 && i < d->n_hidden; ++i) hs[i] = (uint32_t)d->H[i];
+  return {IMG_CNF,
+          layout_tag(IMG_CNF, {(uint32_t)d->D, (uint32_t)d->C, (uint32_t)d->n_hidden, hs[0], hs[1], hs[2], hs[3],
+                               (uint32_t)d->act, (uint32_t)d->mfma_mode}),
+          1, cnf_packed_bytes(d)};
+}
+static int64_t img_bytes(int64_t body) { return body < 0 ? body : body + kImgHdr; }
+static void img_words(const ImgSpec& sp, uint32_t flags, uint32_t* w) {
+  w[0] = kImgMagic;
+  w[1] = kImgVersion;
+  w[2] = sp.kind;
+  w[3] = sp.tag;
+  w[4] = (uint32_t)sp.L;
+  w[5] = flags;
+  w[6] = (uint32_t)((uint64_t)sp.body & 0xffffffffu);
+  w[7] = (uint32_t)((uint64_t)sp.body >> 32);
+}
+static void img_record(const void* base, const ImgRec& r) {
+  std::lock_guard<std::mutex> lk(g_img_mu);
+  const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+  // a new image over the span of older ones replaces them
+  auto it = g_img.lower_bound(b);
+  while (it != g_img.end() && it->first < b + (uintptr_t)(r.stride * r.draws)) it = g_img.erase(it);
+  it = g_img.lower_bound(b);
+  if (it != g_img.begin()) {
+    auto pv = std::prev(it);
+    if (pv->first + (uintptr_t)(pv->second.stride * pv->second.draws) > b) g_img.erase(pv);
+  }
+  g_img[b] = r;
+}
+// the device packers: headers for P images at `stride` bytes, then the registry record
+static int img_publish(const char* fn, const ImgSpec& sp, void* base, int64_t stride, int64_t P, uint32_t flags,
+                       hipStream_t s) {
+  if (P <= 0) return 0;
+  uint32_t w[8];
+  img_words(sp, flags, w);
+  if (int rc = write_image_headers(base, stride, P, w, 8, s)) return rc;
+  (void)fn;
+  img_record(base, ImgRec{sp.kind, sp.tag, (uint32_t)sp.L, flags, sp.body, stride, P});
+  return 0;
+}
+// resolve an image pointer (a registered base, or draw p of a registered multi-draw buffer) for a
+// launch over P draws at spk floats per draw (P = 1: spk unused); returns the body pointer
+static int img_resolve(const char* fn, const ImgSpec& sp, const void* image, int64_t P, int64_t spk, uint32_t flags,
+                       const void** body) {
+  if (sp.body < 0) {  // no instance: the dispatch behind the entry reports the descriptor (nothing launches)
+    *body = image;
+    return 0;
+  }
+  if (image == nullptr) return set_error("%s: null packed image", fn);
+  const uintptr_t p = reinterpret_cast<uintptr_t>(image);
+  ImgRec r{};
+  int64_t draw = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_img_mu);
+    auto it = g_img.upper_bound(p);
+    if (it == g_img.begin())
+      return set_error("%s: %p is not a packed image (pack it with a naz_*_pack entry, or naz_image_attach a "
+                       "host-packed copy)", fn, image);
+    --it;
+    r = it->second;
+    const uintptr_t off = p - it->first;
+    if (off % (uintptr_t)r.stride != 0 || off / (uintptr_t)r.stride >= (uintptr_t)r.draws)
+      return set_error("%s: %p is not a packed image (inside one at %p)", fn, image, (const void*)it->first);
+    draw = (int64_t)(off / (uintptr_t)r.stride);
+  }
+  if (r.kind != sp.kind)
+    return set_error("%s: image %p is a %s image, expected a %s image", fn, image,
+                     kImgKindName[r.kind < 7 ? r.kind : 0], kImgKindName[sp.kind]);
+  if (r.tag != sp.tag)
+    return set_error("%s: image %p was packed for another descriptor or layout (tag %08x, expected %08x)", fn, image,
+                     r.tag, sp.tag);
+  if ((int)r.L != sp.L || r.body != sp.body)
+    return set_error("%s: image %p holds %u layers / %lld B, the descriptor needs %d layers / %lld B", fn, image, r.L,
+                     (long long)r.body, sp.L, (long long)sp.body);
+  if ((r.flags & IMG_FLAG_PASS0) != (flags & IMG_FLAG_PASS0))
+    return set_error("%s: image %p %s pass-0 constants, the call %s them", fn, image,
+                     (r.flags & IMG_FLAG_PASS0) ? "carries" : "has no", (flags & IMG_FLAG_PASS0) ? "expects" : "does not expect");
+  if (P > 1 && (spk * 4 != r.stride || draw + P > r.draws))
+    return set_error("%s: %lld draws at %lld floats per draw from draw %lld of an image set of %lld draws at %lld B",
+                     fn, (long long)P, (long long)spk, (long long)draw, (long long)r.draws, (long long)r.stride);
+  *body = static_cast<const char*>(image) + kImgHdr;
+  return 0;
+}
+#define NAZ_IMG(fn, spec, image, P, spk, flags, body) \
+  const void* body = nullptr;                           \
+  if (int rc_ = img_resolve(fn, spec, image, P, spk, flags, &body)) return rc_
+
 }  // namespace naz
 
 using namespace naz;
@@ -41,7 +202,36 @@ using namespace naz;
 extern "C" {
 
 const char* naz_last_error(void) { return g_err; }
-int naz_abi_version(void) { return 2; }
+int naz_abi_version(void) { return 3; }
+
+int naz_image_attach(const void* image, int64_t bytes, void* stream) {
+  if (image == nullptr || bytes < kImgHdr) return set_error("naz_image_attach: null image or fewer than 256 bytes");
+  uint32_t w[8];
+  hipStream_t s = as_stream(stream);
+  if (hipMemcpyAsync(w, image, sizeof(w), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return set_error("naz_image_attach: cannot read the header of %p", image);
+  if (w[0] != kImgMagic) return set_error("naz_image_attach: %p holds no packed-image header", image);
+  if (w[1] != kImgVersion)
+    return set_error("naz_image_attach: %p was packed by layout version %u, this library reads %u", image, w[1],
+                     kImgVersion);
+  if (w[2] < IMG_COUPLING || w[2] > IMG_CNF) return set_error("naz_image_attach: %p: unknown image kind %u", image, w[2]);
+  const int64_t body = (int64_t)((uint64_t)w[6] | ((uint64_t)w[7] << 32));
+  if (body <= 0 || body > bytes - kImgHdr)
+    return set_error("naz_image_attach: %p: the header announces %lld B of weights, the buffer holds %lld B", image,
+                     (long long)body, (long long)(bytes - kImgHdr));
+  img_record(image, ImgRec{w[2], w[3], w[4], w[5], body, body + kImgHdr, 1});
+  return 0;
+}
+
+int naz_tuning(const char* key, int value) {
+  if (key != nullptr && strcmp(key, "rowgemm_split") == 0) return rowgemm_split_setting(value);
+  return set_error("naz_tuning: unknown key '%s'", key ? key : "(null)");
+}
+
+int naz_image_release(const void* image) {
+  std::lock_guard<std::mutex> lk(g_img_mu);
+  return g_img.erase(reinterpret_cast<uintptr_t>(image)) ? 0 : set_error("naz_image_release: %p is not registered", image);
+}
 
 int naz_rqs_fwd(const float* x, int64_t ldx, const float* raw, int64_t ldr, float* y, int64_t ldy, float* ld,
                 int ld_mode, int64_t B, int Dt, int K, int layout, float bound, void* stream) {
@@ -206,10 +396,12 @@ int naz_base_log_prob_bwd(const float* z, int64_t ldz, const float* g_lp, float*
 
 int naz_cnf_supported(const naz_cnf_desc* d) { return cnf_supported(d); }
 int64_t naz_cnf_param_count(const naz_cnf_desc* d) { return cnf_param_count(d); }
-int64_t naz_cnf_packed_bytes(const naz_cnf_desc* d) { return cnf_packed_bytes(d); }
+int64_t naz_cnf_packed_bytes(const naz_cnf_desc* d) { return img_bytes(cnf_packed_bytes(d)); }
 int naz_cnf_pack(const naz_cnf_desc* d, const float* flat, void* packed, void* stream) {
   if (flat == nullptr || packed == nullptr) return set_error("naz_cnf_pack: null pointer");
-  return cnf_pack(d, flat, packed, as_stream(stream));
+  const ImgSpec sp = spec_cnf(d);
+  if (int rc = cnf_pack(d, flat, static_cast<char*>(packed) + kImgHdr, as_stream(stream))) return rc;
+  return img_publish("naz_cnf_pack", sp, packed, img_bytes(sp.body), 1, 0, as_stream(stream));
 }
 int naz_cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
                       int64_t ldc, const float* eps, int64_t lde, float t0, float t1, int steps, float* y,
@@ -218,7 +410,9 @@ int naz_cnf_integrate(const naz_cnf_desc* d, const void* packed, const float* x,
   if (B > 0 && (packed == nullptr || x == nullptr || eps == nullptr || y == nullptr))
     return set_error("naz_cnf_integrate: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr) return set_error("naz_cnf_integrate: context required");
-  return cnf_integrate(d, packed, x, ldx, ctx, ldc, eps, lde, t0, t1, steps, y, ldy, ld, ld_mode, B,
+  if (B == 0) return 0;
+  NAZ_IMG("naz_cnf_integrate", spec_cnf(d), packed, 1, 0, 0, body);
+  return cnf_integrate(d, body, x, ldx, ctx, ldc, eps, lde, t0, t1, steps, y, ldy, ld, ld_mode, B,
                        as_stream(stream));
 }
 
@@ -231,7 +425,9 @@ int naz_cnf_integrate_dopri5(const naz_cnf_desc* d, const void* packed, const fl
     return set_error("naz_cnf_integrate_dopri5: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
     return set_error("naz_cnf_integrate_dopri5: context required");
-  return cnf_integrate_dopri5(d, packed, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy, ld,
+  if (B == 0) return 0;
+  NAZ_IMG("naz_cnf_integrate_dopri5", spec_cnf(d), packed, 1, 0, 0, body);
+  return cnf_integrate_dopri5(d, body, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy, ld,
                               ld_mode, nfe, B, as_stream(stream));
 }
 
@@ -249,7 +445,9 @@ int naz_cnf_integrate_dopri5_global(const naz_cnf_desc* d, const void* packed, c
     return set_error("naz_cnf_integrate_dopri5_global: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
     return set_error("naz_cnf_integrate_dopri5_global: context required");
-  return cnf_integrate_dopri5_global(d, packed, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy,
+  if (B == 0) return 0;
+  NAZ_IMG("naz_cnf_integrate_dopri5_global", spec_cnf(d), packed, 1, 0, 0, body);
+  return cnf_integrate_dopri5_global(d, body, x, ldx, ctx, ldc, eps, lde, t0, t1, atol, rtol, max_steps, y, ldy,
                                      ld, ld_mode, nfe, workspace, B, as_stream(stream));
 }
 
@@ -266,37 +464,51 @@ int naz_gemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t
 
 int naz_coupling_supported(const naz_coupling_desc* d) { return coupling_supported(d); }
 int64_t naz_coupling_param_count(const naz_coupling_desc* d) { return coupling_param_count(d); }
-int64_t naz_coupling_packed_bytes(const naz_coupling_desc* d) { return coupling_packed_bytes(d); }
+int64_t naz_coupling_packed_bytes(const naz_coupling_desc* d) { return img_bytes(coupling_packed_bytes(d)); }
 
 int naz_coupling_pack(const naz_coupling_desc* d, const float* flat_params, void* packed, void* stream) {
-  return coupling_pack(d, flat_params, packed, as_stream(stream));
+  const ImgSpec sp = spec_coupling(d, IMG_COUPLING);
+  if (sp.body < 0) return set_error("naz_coupling_pack: no fused instantiation for this descriptor");
+  if (packed == nullptr) return set_error("naz_coupling_pack: null image");
+  if (int rc = coupling_pack(d, flat_params, static_cast<char*>(packed) + kImgHdr, as_stream(stream))) return rc;
+  return img_publish("naz_coupling_pack", sp, packed, img_bytes(sp.body), 1, 0, as_stream(stream));
 }
 
 int naz_coupling_log_prob(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx,
                           const float* ctx, int64_t ldc, const float* low, const float* high, float* out_lp,
                           int64_t B, void* stream) {
   if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_log_prob: conditional flow needs ctx");
-  return coupling_log_prob(d, packed, x, ldx, ctx, ldc, low, high, out_lp, B, as_stream(stream));
+  if (B == 0) return 0;
+  NAZ_IMG("naz_coupling_log_prob", spec_coupling(d, IMG_COUPLING), packed, 1, 0, 0, body);
+  return coupling_log_prob(d, body, x, ldx, ctx, ldc, low, high, out_lp, B, as_stream(stream));
 }
 
 int naz_coupling_sample(const naz_coupling_desc* d, const void* packed, const float* z, int64_t ldz,
                         const float* ctx, int64_t ldc, const float* low, const float* high, float* y, int64_t ldy,
                         float* out_ld, int64_t B, void* stream) {
   if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_sample: conditional flow needs ctx");
-  return coupling_sample(d, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, as_stream(stream));
+  if (B == 0) return 0;
+  NAZ_IMG("naz_coupling_sample", spec_coupling(d, IMG_COUPLING), packed, 1, 0, 0, body);
+  return coupling_sample(d, body, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, as_stream(stream));
 }
 
-int64_t naz_coupling_bwd_packed_bytes(const naz_coupling_desc* d) { return coupling_bwd_packed_bytes(d); }
+int64_t naz_coupling_bwd_packed_bytes(const naz_coupling_desc* d) { return img_bytes(coupling_bwd_packed_bytes(d)); }
 
 int naz_coupling_pack_bwd(const naz_coupling_desc* d, const float* flat_params, void* packed_bwd, void* stream) {
-  return coupling_pack_bwd(d, flat_params, packed_bwd, as_stream(stream));
+  const ImgSpec sp = spec_coupling(d, IMG_COUPLING_BWD);
+  if (sp.body < 0) return set_error("naz_coupling_pack_bwd: no fused instantiation for this descriptor");
+  if (packed_bwd == nullptr) return set_error("naz_coupling_pack_bwd: null image");
+  if (int rc = coupling_pack_bwd(d, flat_params, static_cast<char*>(packed_bwd) + kImgHdr, as_stream(stream))) return rc;
+  return img_publish("naz_coupling_pack_bwd", sp, packed_bwd, img_bytes(sp.body), 1, 0, as_stream(stream));
 }
 
 int naz_coupling_log_prob_train(const naz_coupling_desc* d, const void* packed, const float* x, int64_t ldx,
                                 const float* ctx, int64_t ldc, const float* low, const float* high, float* out_lp,
                                 float* states, int64_t B, void* stream) {
   if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_log_prob_train: conditional flow needs ctx");
-  return coupling_log_prob_train(d, packed, x, ldx, ctx, ldc, low, high, out_lp, states, B, as_stream(stream));
+  if (B == 0) return 0;
+  NAZ_IMG("naz_coupling_log_prob_train", spec_coupling(d, IMG_COUPLING), packed, 1, 0, 0, body);
+  return coupling_log_prob_train(d, body, x, ldx, ctx, ldc, low, high, out_lp, states, B, as_stream(stream));
 }
 
 int naz_coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const void* packed_bwd, const float* flat,
@@ -304,7 +516,9 @@ int naz_coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const
                            const float* g_lp, float* h1, float* h2, float* dp1, float* dp2, float* dp3, float* x0,
                            float* g_out, float* g_low, int64_t B, void* stream) {
   if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_bwd_layer: conditional flow needs ctx");
-  return coupling_bwd_layer(d, packed, packed_bwd, flat, layer, state, ctx, ldc, g_in, g_lp, h1, h2, dp1, dp2, dp3,
+  NAZ_IMG("naz_coupling_bwd_layer", spec_coupling(d, IMG_COUPLING), packed, 1, 0, 0, body);
+  NAZ_IMG("naz_coupling_bwd_layer", spec_coupling(d, IMG_COUPLING_BWD), packed_bwd, 1, 0, 0, body_bwd);
+  return coupling_bwd_layer(d, body, body_bwd, flat, layer, state, ctx, ldc, g_in, g_lp, h1, h2, dp1, dp2, dp3,
                             x0, g_out, g_low, B, as_stream(stream));
 }
 
@@ -317,7 +531,8 @@ static int coupling_layer_api(const char* what, const naz_coupling_desc* d, int 
   if (B > 0 && (packed == nullptr || x == nullptr || y == nullptr || ld == nullptr))
     return set_error("%s: null pointer", what);
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr) return set_error("%s: conditional flow needs ctx", what);
-  return coupling_layer(d, inv, packed, layer, x, ldx, ctx, ldc, y, ldy, ld, ld_mode, B, as_stream(stream));
+  NAZ_IMG(what, spec_coupling(d, IMG_COUPLING), packed, 1, 0, 0, body);
+  return coupling_layer(d, inv, body, layer, x, ldx, ctx, ldc, y, ldy, ld, ld_mode, B, as_stream(stream));
 }
 int naz_coupling_layer_fwd(const naz_coupling_desc* d, const void* packed, int layer, const float* x, int64_t ldx,
                            const float* ctx, int64_t ldc, float* y, int64_t ldy, float* ld, int ld_mode, int64_t B,
@@ -333,24 +548,44 @@ int naz_coupling_layer_inv(const naz_coupling_desc* d, const void* packed, int l
 }
 
 int naz_ar_flow_supported(const naz_ar_desc* d) { return ar_flow_supported(d); }
-int64_t naz_ar_flow_packed_bytes(const naz_ar_desc* d) { return ar_flow_packed_bytes(d); }
+int64_t naz_ar_flow_packed_bytes(const naz_ar_desc* d) { return img_bytes(ar_flow_packed_bytes(d)); }
+int64_t naz_ar_flow_workspace_bytes(const naz_ar_desc* d, int64_t B, int64_t P) {
+  if (B < 0 || P < 0) return -1;
+  return ar_flow_workspace_bytes(d, B, P);
+}
 int naz_ar_flow_degrees(const naz_ar_desc* d, int* deg) { return ar_flow_degrees(d, deg); }
+// host packers: the header goes into the host buffer; the caller uploads it and naz_image_attach-es it
+static int host_image(const ImgSpec& sp, void* packed) {
+  uint32_t w[8];
+  img_words(sp, 0, w);
+  memset(packed, 0, kImgHdr);
+  memcpy(packed, w, sizeof(w));
+  return 0;
+}
 int naz_ar_flow_pack_host(const naz_ar_desc* d, const float* flat, const int* perm, void* packed) {
-  return ar_flow_pack_host(d, flat, perm, packed);
+  if (packed == nullptr) return set_error("naz_ar_flow_pack_host: null image");
+  if (int rc = ar_flow_pack_host(d, flat, perm, static_cast<char*>(packed) + kImgHdr)) return rc;
+  return host_image(spec_ar(d, IMG_AR_INV), packed);
 }
 int naz_ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                           int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream) {
+                         int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* workspace,
+                         int64_t workspace_bytes, void* stream) {
   if (B < 0) return set_error("naz_ar_flow_log_prob: negative batch");
   if (B > 0 && (packed == nullptr || x == nullptr || out_lp == nullptr))
     return set_error("naz_ar_flow_log_prob: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
     return set_error("naz_ar_flow_log_prob: conditional flow needs ctx");
-  return ar_flow_log_prob(d, packed, x, ldx, ctx, ldc, low, high, out_lp, B, as_stream(stream));
+  if (B == 0) return 0;
+  NAZ_IMG("naz_ar_flow_log_prob", spec_ar(d, IMG_AR_INV), packed, 1, 0, 0, body);
+  return ar_flow_log_prob(d, body, x, ldx, ctx, ldc, low, high, out_lp, B, workspace, workspace_bytes,
+                          as_stream(stream));
 }
 
-int64_t naz_ar_flow_fwd_packed_bytes(const naz_ar_desc* d) { return ar_flow_fwd_packed_bytes(d); }
+int64_t naz_ar_flow_fwd_packed_bytes(const naz_ar_desc* d) { return img_bytes(ar_flow_fwd_packed_bytes(d)); }
 int naz_ar_flow_pack_fwd_host(const naz_ar_desc* d, const float* flat, void* packed) {
-  return ar_flow_pack_fwd_host(d, flat, packed);
+  if (packed == nullptr) return set_error("naz_ar_flow_pack_fwd_host: null image");
+  if (int rc = ar_flow_pack_fwd_host(d, flat, static_cast<char*>(packed) + kImgHdr)) return rc;
+  return host_image(spec_ar(d, IMG_AR_FWD), packed);
 }
 int naz_ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z, int64_t ldz, const float* ctx,
                        int64_t ldc, const float* low, const float* high, float* y, int64_t ldy, float* out_ld,
@@ -359,13 +594,23 @@ int naz_ar_flow_sample(const naz_ar_desc* d, const void* packed, const float* z,
   if (B > 0 && (packed == nullptr || z == nullptr || y == nullptr)) return set_error("naz_ar_flow_sample: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
     return set_error("naz_ar_flow_sample: conditional flow needs ctx");
-  return ar_flow_sample(d, packed, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, as_stream(stream));
+  if (B == 0) return 0;
+  NAZ_IMG("naz_ar_flow_sample", spec_ar(d, IMG_AR_FWD), packed, 1, 0, 0, body);
+  return ar_flow_sample(d, body, z, ldz, ctx, ldc, low, high, y, ldy, out_ld, B, as_stream(stream));
 }
 
 int naz_ar_flow_pack_fwd(const naz_ar_desc* d, const float* flat, int64_t sflat, void* packed, int64_t spk, int64_t P,
                          const float* mask, void* stream) {
   if (P < 0) return set_error("naz_ar_flow_pack_fwd: negative draw count");
-  return ar_flow_pack_fwd(d, flat, sflat, packed, spk, P, mask, as_stream(stream));
+  const ImgSpec sp = spec_ar(d, IMG_AR_FWD);
+  if (sp.body < 0) return set_error("naz_ar_flow_pack_fwd: no fused instantiation for this descriptor");
+  if (packed == nullptr) return set_error("naz_ar_flow_pack_fwd: null image");
+  if (sp.body >= 0 && P > 1 && spk * 4 < img_bytes(sp.body))
+    return set_error("naz_ar_flow_pack_fwd: draw stride %lld floats shorter than one image", (long long)spk);
+  if (int rc = ar_flow_pack_fwd(d, flat, sflat, static_cast<char*>(packed) + kImgHdr, P > 1 ? spk : sp.body / 4 + 64, P,
+                                mask, as_stream(stream)))
+    return rc;
+  return img_publish("naz_ar_flow_pack_fwd", sp, packed, P > 1 ? spk * 4 : img_bytes(sp.body), P, 0, as_stream(stream));
 }
 int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* z, int64_t ldz,
                                int64_t sz, const float* ctx, int64_t ldc, float* y, int64_t ldy, int64_t sy,
@@ -375,30 +620,44 @@ int naz_ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t
     return set_error("naz_ar_flow_sample_batched: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && P > 0 && ctx == nullptr)
     return set_error("naz_ar_flow_sample_batched: conditional flow needs ctx");
-  return ar_flow_sample_batched(d, packed, spk, z, ldz, sz, ctx, ldc, y, ldy, sy, out_ld, sld, B, P, as_stream(stream));
+  if (B == 0 || P == 0) return 0;
+  NAZ_IMG("naz_ar_flow_sample_batched", spec_ar(d, IMG_AR_FWD), packed, P, spk, 0, body);
+  return ar_flow_sample_batched(d, body, spk, z, ldz, sz, ctx, ldc, y, ldy, sy, out_ld, sld, B, P, as_stream(stream));
 }
 
 int64_t naz_ar_flow_pass0_floats(const naz_ar_desc* d) { return ar_flow_pass0_floats(d); }
 int naz_ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
                      int64_t P, const float* pass0, int64_t sp0, const float* mask, void* stream) {
   if (P < 0) return set_error("naz_ar_flow_pack: negative draw count");
-  return ar_flow_pack(d, flat, sflat, perm, packed, spk, P, pass0, sp0, mask, as_stream(stream));
+  const ImgSpec sp = spec_ar(d, IMG_AR_INV);
+  if (sp.body < 0) return set_error("naz_ar_flow_pack: no fused instantiation for this descriptor");
+  if (packed == nullptr) return set_error("naz_ar_flow_pack: null image");
+  if (sp.body >= 0 && P > 1 && spk * 4 < img_bytes(sp.body))
+    return set_error("naz_ar_flow_pack: draw stride %lld floats shorter than one image", (long long)spk);
+  if (int rc = ar_flow_pack(d, flat, sflat, perm, static_cast<char*>(packed) + kImgHdr, P > 1 ? spk : sp.body / 4 + 64,
+                            P, pass0, sp0, mask, as_stream(stream)))
+    return rc;
+  return img_publish("naz_ar_flow_pack", sp, packed, P > 1 ? spk * 4 : img_bytes(sp.body), P,
+                     pass0 != nullptr ? IMG_FLAG_PASS0 : 0u, as_stream(stream));
 }
 int naz_ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                                  int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B,
-                                 int64_t P, int pass0_const, void* stream) {
+                                 int64_t P, int pass0_const, void* workspace, int64_t workspace_bytes, void* stream) {
   if (B < 0 || P < 0) return set_error("naz_ar_flow_log_prob_batched: negative size");
   if (B > 0 && P > 0 && (packed == nullptr || x == nullptr || out_lp == nullptr))
     return set_error("naz_ar_flow_log_prob_batched: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && P > 0 && ctx == nullptr)
     return set_error("naz_ar_flow_log_prob_batched: conditional flow needs ctx");
-  return ar_flow_log_prob_batched(d, packed, spk, x, ldx, sx, ctx, ldc, out_lp, slp, B, P, pass0_const,
-                                  as_stream(stream));
+  if (B == 0 || P == 0) return 0;
+  NAZ_IMG("naz_ar_flow_log_prob_batched", spec_ar(d, IMG_AR_INV), packed, P, spk, pass0_const ? IMG_FLAG_PASS0 : 0u, body);
+  return ar_flow_log_prob_batched(d, body, spk, x, ldx, sx, ctx, ldc, out_lp, slp, B, P, pass0_const, workspace,
+                                  workspace_bytes, as_stream(stream));
 }
 
 // ---- fused maf backward (made_ar_bwd.h): NUTS potential gradient / maf NLL step ----------
 int naz_ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                               int64_t ldc, float* out_lp, float* states, int64_t B, void* stream) {
+                               int64_t ldc, float* out_lp, float* states, int64_t B, void* workspace,
+                               int64_t workspace_bytes, void* stream) {
   if (B < 0) return set_error("naz_ar_flow_log_prob_train: negative batch");
   if (B > 0 && (packed == nullptr || x == nullptr || out_lp == nullptr))
     return set_error("naz_ar_flow_log_prob_train: null pointer");
@@ -406,12 +665,19 @@ int naz_ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const f
     return set_error("naz_ar_flow_log_prob_train: conditional flow needs ctx");
   if (d == nullptr || d->kind != NAZ_AR_AFFINE || naz_ar_flow_supported(d) != 1)
     return set_error("naz_ar_flow_log_prob_train: no fused affine inverse for this flow");
-  return ar_flow_log_prob_train(d, packed, x, ldx, ctx, ldc, out_lp, states, B, as_stream(stream));
+  if (B == 0) return 0;
+  NAZ_IMG("naz_ar_flow_log_prob_train", spec_ar(d, IMG_AR_INV), packed, 1, 0, 0, body);
+  return ar_flow_log_prob_train(d, body, x, ldx, ctx, ldc, out_lp, states, B, workspace, workspace_bytes,
+                                as_stream(stream));
 }
-int64_t naz_ar_flow_bwd_packed_bytes(const naz_ar_desc* d) { return ar_flow_bwd_packed_bytes(d); }
+int64_t naz_ar_flow_bwd_packed_bytes(const naz_ar_desc* d) { return img_bytes(ar_flow_bwd_packed_bytes(d)); }
 int naz_ar_flow_bwd_dims(const naz_ar_desc* d, int* dims) { return ar_flow_bwd_dims(d, dims); }
 int naz_ar_flow_pack_bwd(const naz_ar_desc* d, const float* flat, const float* mask, void* packed, void* stream) {
-  return ar_flow_pack_bwd(d, flat, mask, packed, as_stream(stream));
+  const ImgSpec sp = spec_ar(d, IMG_AR_BWD);
+  if (sp.body < 0) return set_error("naz_ar_flow_pack_bwd: no fused instantiation for this descriptor");
+  if (packed == nullptr) return set_error("naz_ar_flow_pack_bwd: null image");
+  if (int rc = ar_flow_pack_bwd(d, flat, mask, static_cast<char*>(packed) + kImgHdr, as_stream(stream))) return rc;
+  return img_publish("naz_ar_flow_pack_bwd", sp, packed, img_bytes(sp.body), 1, 0, as_stream(stream));
 }
 int naz_ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const void* packed_bwd, const int* perm,
                           int layer, const float* state, const float* ctx, int64_t ldc, const float* g_in,
@@ -422,29 +688,42 @@ int naz_ar_flow_bwd_layer(const naz_ar_desc* d, const void* packed_fwd, const vo
     return set_error("naz_ar_flow_bwd_layer: null pointer");
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr)
     return set_error("naz_ar_flow_bwd_layer: conditional flow needs ctx");
-  return ar_flow_bwd_layer(d, packed_fwd, packed_bwd, perm, layer, state, ctx, ldc, g_in, g_lp, bufs, g_out, B,
+  if (d == nullptr || layer < 0 || layer >= d->L) return set_error("naz_ar_flow_bwd_layer: layer out of range");
+  if (ar_flow_bwd_packed_bytes(d) < 0) {  // no backward instance: report the descriptor
+    int dims[6];
+    return ar_flow_bwd_dims(d, dims);
+  }
+  if (B == 0) return 0;
+  NAZ_IMG("naz_ar_flow_bwd_layer", spec_ar(d, IMG_AR_FWD), packed_fwd, 1, 0, 0, body_fwd);
+  NAZ_IMG("naz_ar_flow_bwd_layer", spec_ar(d, IMG_AR_BWD), packed_bwd, 1, 0, 0, body_bwd);
+  return ar_flow_bwd_layer(d, body_fwd, body_bwd, perm, layer, state, ctx, ldc, g_in, g_lp, bufs, g_out, B,
                            as_stream(stream));
 }
 
 // ---- §8b whole-flow entries over the fused kinds ----------------------------------------
 int64_t naz_flow_packed_bytes(const naz_flow_desc* d) {
   if (d == nullptr) return -1;
-  if (d->kind == NAZ_FLOW_COUPLING) return coupling_packed_bytes(&d->coupling);
-  if (d->kind == NAZ_FLOW_AR) return ar_flow_packed_bytes(&d->ar);
+  if (d->kind == NAZ_FLOW_COUPLING) return naz_coupling_packed_bytes(&d->coupling);
+  if (d->kind == NAZ_FLOW_AR) return naz_ar_flow_packed_bytes(&d->ar);
   return -1;
 }
 
 int64_t naz_workspace_bytes(const naz_flow_desc* d, int64_t B) {
-  (void)B;  // the fused kernels keep every intermediate on chip
-  return naz_flow_packed_bytes(d) < 0 ? -1 : 0;
+  if (naz_flow_packed_bytes(d) < 0 || B < 0) return -1;
+  // the coupling kernels keep every intermediate on chip; the wide autoregressive inverse keeps its
+  // hidden layers 2.. in per-wave workspace
+  return d->kind == NAZ_FLOW_AR ? ar_flow_workspace_bytes(&d->ar, B, 1) : 0;
 }
 
 int naz_flow_log_prob(const naz_flow_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                      int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* stream) {
+                      int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* workspace,
+                      int64_t workspace_bytes, void* stream) {
   if (d == nullptr) return set_error("naz_flow_log_prob: null descriptor");
   if (d->kind == NAZ_FLOW_COUPLING)
     return naz_coupling_log_prob(&d->coupling, packed, x, ldx, ctx, ldc, low, high, out_lp, B, stream);
-  if (d->kind == NAZ_FLOW_AR) return naz_ar_flow_log_prob(&d->ar, packed, x, ldx, ctx, ldc, low, high, out_lp, B, stream);
+  if (d->kind == NAZ_FLOW_AR)
+    return naz_ar_flow_log_prob(&d->ar, packed, x, ldx, ctx, ldc, low, high, out_lp, B, workspace, workspace_bytes,
+                                stream);
   return set_error("naz_flow_log_prob: unknown flow kind %d", d->kind);
 }
 

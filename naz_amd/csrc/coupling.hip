@@ -1688,7 +1688,7 @@ struct AROps {
   static int log_prob(const float* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
                       const float* low, const float* high, float* out_lp, int64_t B, float bound, hipStream_t s,
                       int64_t P = 1, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0, int c0mode = 0,
-                      float* states = nullptr) {
+                      float* states = nullptr, void* = nullptr, int64_t = 0) {
     static_assert(2 * CF::STG * 4 <= 160 * 1024, "two weight stages exceed the LDS");
     if (B == 0 || L == 0 || P == 0) return 0;
     if (P > 65535) return set_error("naz_ar_flow_log_prob_batched: at most 65535 draws per call");
@@ -1698,6 +1698,7 @@ struct AROps {
                        L, x, ldx, ctx, ldc, low, high, out_lp, B, bound, spk, sx, slp, c0mode, states);
     return check_launch("made_ar_r16_kernel");
   }
+  static int64_t workspace_bytes(int64_t, int64_t) { return 0; }  // every intermediate stays on chip
   static int64_t pass0_floats() { return CF::C0; }
   static int pack_device(const float* flat, int64_t sflat, const int* perm, float* packed, int64_t spk, int L,
                          int64_t P, hipStream_t s, const float* c0 = nullptr, int64_t sc0 = 0,
@@ -1782,23 +1783,32 @@ struct AROpsW {
   static int log_prob(const float* packed, int L, const float* x, int64_t ldx, const float* ctx, int64_t ldc,
                       const float* low, const float* high, float* out_lp, int64_t B, float, hipStream_t s,
                       int64_t P = 1, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0, int c0mode = 0,
-                      float* states = nullptr) {
+                      float* states = nullptr, void* ws = nullptr, int64_t ws_bytes = 0) {
     if (c0mode) return set_error("naz_ar_flow: D=%d H=%d x %d: no pass-0 constants form", CW::D, CW::H, CW::NHID);
     if (states != nullptr && (P != 1 || low != nullptr))
       return set_error("naz_ar_flow_log_prob_train: one draw, no bounds");
     if (B == 0 || L == 0 || P == 0) return 0;
-    const int64_t tiles = (B + 16 * IW::NW - 1) / (16 * IW::NW) * P;
-    const int64_t grid = std::min<int64_t>(tiles, device_cu_count());
-    const size_t bytes = (size_t)grid * IW::NW * IW::SCRATCH_U4 * sizeof(u32x4);
-    void* scratch = nullptr;
-    if (hipMallocAsync(&scratch, bytes, s) != hipSuccess)
-      return set_error("naz_ar_flow_log_prob: %zu B of per-wave scratch not available", bytes);
+    const int64_t grid = grid_size(B, P);
+    // the hidden layers 2.. of every resident wave persist in caller-owned workspace (no allocation
+    // inside a call: a captured HIP graph replays one fixed address)
+    const int64_t need = workspace_bytes(B, P);
+    if (ws == nullptr || ws_bytes < need || (reinterpret_cast<uintptr_t>(ws) & 15) != 0)
+      return set_error("naz_ar_flow_log_prob: D=%d H=%d x %d needs %lld B of 16-byte aligned workspace "
+                       "(naz_ar_flow_workspace_bytes), got %lld B at %p", CW::D, CW::H, CW::NHID, (long long)need,
+                       (long long)ws_bytes, ws);
     const size_t lds = (size_t)2 * IW::STG * 4;
     hipLaunchKernelGGL((made_ar_inv_wide_kernel<IW>), dim3((unsigned)grid), dim3(64 * IW::NW), lds, s, packed, L, x,
-                       ldx, ctx, ldc, low, high, out_lp, B, P, spk, sx, slp, static_cast<u32x4*>(scratch), states);
-    const int rc = check_launch("made_ar_inv_wide_kernel");
-    (void)hipFreeAsync(scratch, s);
-    return rc;
+                       ldx, ctx, ldc, low, high, out_lp, B, P, spk, sx, slp, static_cast<u32x4*>(ws), states);
+    return check_launch("made_ar_inv_wide_kernel");
+  }
+  // the persistent grid: one 4-wave workgroup per CU (at most one per (draw, row tile))
+  static int64_t grid_size(int64_t B, int64_t P) {
+    const int64_t tiles = (B + 16 * IW::NW - 1) / (16 * IW::NW) * P;
+    return std::min<int64_t>(tiles, device_cu_count());
+  }
+  static int64_t workspace_bytes(int64_t B, int64_t P) {
+    if (B <= 0 || P <= 0) return 0;
+    return grid_size(B, P) * IW::NW * IW::SCRATCH_U4 * (int64_t)sizeof(u32x4);
   }
   static int64_t pass0_floats() { return -1; }
   static int pack_device(const float* flat, int64_t sflat, const int* perm, float* packed, int64_t spk, int L,
@@ -1978,34 +1988,45 @@ int ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const i
   return rc == -2 ? ar_unsupported(d) : rc;
 }
 
+int64_t ar_flow_workspace_bytes(const naz_ar_desc* d, int64_t B, int64_t P) {
+  int64_t v = -1;
+  ar_dispatch(d, [&](auto ops) {
+    v = decltype(ops)::workspace_bytes(B, P);
+    return 0;
+  });
+  return v;
+}
+
 int ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                              int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B, int64_t P,
-                             int pass0_const, hipStream_t s) {
+                             int pass0_const, void* ws, int64_t ws_bytes, hipStream_t s) {
   if (pass0_const && (d == nullptr || d->C <= 0 || ldc != 0))
     return set_error("naz_ar_flow_log_prob_batched: pass-0 constants need one context vector (ldc = 0)");
   const int rc = ar_dispatch(d, [&](auto ops) {
     return decltype(ops)::log_prob(static_cast<const float*>(packed), d->L, x, ldx, ctx, ldc, nullptr, nullptr, out_lp,
-                                   B, d->bound, s, P, spk, sx, slp, pass0_const ? 1 : 0);
+                                   B, d->bound, s, P, spk, sx, slp, pass0_const ? 1 : 0, nullptr, ws, ws_bytes);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }
 
 int ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                     int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s) {
+                     int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* ws,
+                     int64_t ws_bytes, hipStream_t s) {
   if ((low == nullptr) != (high == nullptr)) return set_error("naz_ar_flow_log_prob: low/high must both be set");
   const int rc = ar_dispatch(d, [&](auto ops) {
     return decltype(ops)::log_prob(static_cast<const float*>(packed), d->L, x, ldx, ctx, ldc, low, high, out_lp, B,
-                                   d->bound, s);
+                                   d->bound, s, 1, 0, 0, 0, 0, nullptr, ws, ws_bytes);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }
 
 int ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                           int64_t ldc, float* out_lp, float* states, int64_t B, hipStream_t s) {
+                           int64_t ldc, float* out_lp, float* states, int64_t B, void* ws, int64_t ws_bytes,
+                           hipStream_t s) {
   if (states == nullptr) return set_error("naz_ar_flow_log_prob_train: null states");
   const int rc = ar_dispatch(d, [&](auto ops) {
     return decltype(ops)::log_prob(static_cast<const float*>(packed), d->L, x, ldx, ctx, ldc, nullptr, nullptr, out_lp,
-                                   B, d->bound, s, 1, 0, 0, 0, 0, states);
+                                   B, d->bound, s, 1, 0, 0, 0, 0, states, ws, ws_bytes);
   });
   return rc == -2 ? ar_unsupported(d) : rc;
 }

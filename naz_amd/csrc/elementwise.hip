@@ -237,4 +237,27 @@ int bounding_inv(const float* y, int64_t ldy, const float* low, const float* hig
   return check_launch("bounding_inv_kernel");
 }
 
+// The 256-byte header in front of every packed weight image (capi.cpp: magic, image kind, layout tag,
+// layers, body bytes; include/naz_hip.h "Packed images").  Written by a kernel, not a host copy, so
+// that a packer call captured in a HIP graph replays it without a host pointer.
+struct ImageHeaderWords {
+  uint32_t w[16];
+};
+
+__global__ void image_header_kernel(uint32_t* __restrict__ base, int64_t stride_words, ImageHeaderWords h, int nwords) {
+  const int i = threadIdx.x;  // 64 threads: one 32-bit header word each (the words past nwords are 0)
+  base[(int64_t)blockIdx.x * stride_words + i] = i < nwords ? h.w[i] : 0u;
+}
+
+int write_image_headers(void* base, int64_t stride_bytes, int64_t P, const uint32_t* words, int nwords, hipStream_t s) {
+  if (P <= 0) return 0;
+  if (P > 65535) return set_error("packed image headers: at most 65535 images per call");
+  if (nwords < 0 || nwords > 16 || (stride_bytes & 3) != 0) return set_error("packed image headers: bad layout");
+  ImageHeaderWords h{};
+  for (int i = 0; i < nwords; ++i) h.w[i] = words[i];
+  hipLaunchKernelGGL(image_header_kernel, dim3((unsigned)P), dim3(64), 0, s, static_cast<uint32_t*>(base),
+                     stride_bytes / 4, h, nwords);
+  return check_launch("image_header_kernel");
+}
+
 }  // namespace naz

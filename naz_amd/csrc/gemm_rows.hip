@@ -18,6 +18,8 @@
 //   * wgrad: a workgroup reduces a contiguous slice of rows into the full (small) output in
 //     registers — each wave owns a set of 32×32 output blocks — and adds it to C with one fp32
 //     atomic per element at the end (split-K over workgroups, no partial buffers).
+#include <atomic>
+
 #include "naz_device.h"
 #include "naz_internal.h"
 
@@ -80,6 +82,9 @@ struct RowGemmArgs {
   const float* jvp;
   int64_t ldjvp;
   int jact;
+  // host-side launch choice (rowgemm()): outputs of more than 4 column blocks in half-width panels
+  // (1), in one panel (0), or the library's setting (-1: naz_tuning "rowgemm_split")
+  int split = -1;
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -301,6 +306,21 @@ void rowgemm_launch(const RowGemmArgs& p, int nz, hipStream_t s) {
 
 static bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
+}  // namespace
+
+// the library-wide panel-split setting (naz_tuning "rowgemm_split"): NAZ_RG_SPLIT at first use, else
+// on (round 5 same-box A/B of the wide maf NLL step); v >= 0 sets it; returns the
+// setting before the call
+int rowgemm_split_setting(int v) {
+  static std::atomic<int> cur{[] {
+    const char* e = getenv("NAZ_RG_SPLIT");
+    return e ? (atoi(e) != 0 ? 1 : 0) : 1;
+  }()};
+  return v >= 0 ? cur.exchange(v != 0 ? 1 : 0) : cur.load();
+}
+
+namespace {
+
 int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   if (p.M <= 0 || p.N <= 0 || nz <= 0) return 0;
   const int64_t K = p.ka0 + p.ka1;
@@ -317,14 +337,12 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
     p.vst = p.vst && p.zc % 4 == 0;
   }
   int nb = (p.N + 31) / 32;
-  // NAZ_RG_SPLIT=1: outputs of more than 4 column blocks in half-width panels (<= 4 x 32 for up to 8
-  // blocks: 4 waves / SIMD instead of 2): the wide maf's 168-172-unit degree blocks, 200.0 -> 184.6 ms
-  // per NLL step (profiles/r04_s14_*).  Off by default until the full suite has run with it (an odd
-  // NB's paired epilogue wrote past its panel: fixed below, not yet re-validated on the GPU)
-  static const int split = [] {
-    const char* e = getenv("NAZ_RG_SPLIT");
-    return e ? atoi(e) : 0;
-  }();
+  // panel split: outputs of more than 4 column blocks in half-width panels (<= 4 x 32 for up to 8
+  // blocks: 4 waves / SIMD instead of 2; the wide maf's 168-172-unit degree blocks, 200.0 -> 184.6 ms
+  // per NLL step, profiles/r04_s14_*).  An odd NB's paired epilogue (EG = 2) stores only inside its
+  // panel (`inpanel` above); tests/test_gpu_grad.py::test_rowgemm_panel_split runs every epilogue at
+  // N = 168 / 172 / 300 with the split on and off against fp64.
+  const int split = p.split >= 0 ? p.split : rowgemm_split_setting(-1);
   if (split && nb > 4) nb = (nb + 1) / 2;
   switch (nb > 8 ? 8 : nb) {
     case 1: rowgemm_launch<1>(p, nz, s); break;

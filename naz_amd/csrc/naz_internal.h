@@ -104,13 +104,16 @@ int ar_flow_sample_batched(const naz_ar_desc* d, const void* packed, int64_t spk
 int64_t ar_flow_pass0_floats(const naz_ar_desc* d);
 int ar_flow_pack(const naz_ar_desc* d, const float* flat, int64_t sflat, const int* perm, void* packed, int64_t spk,
                  int64_t P, const float* pass0, int64_t sp0, const float* mask, hipStream_t s);
+int64_t ar_flow_workspace_bytes(const naz_ar_desc* d, int64_t B, int64_t P);
 int ar_flow_log_prob_batched(const naz_ar_desc* d, const void* packed, int64_t spk, const float* x, int64_t ldx,
                              int64_t sx, const float* ctx, int64_t ldc, float* out_lp, int64_t slp, int64_t B, int64_t P,
-                             int pass0_const, hipStream_t s);
+                             int pass0_const, void* ws, int64_t ws_bytes, hipStream_t s);
 int ar_flow_log_prob(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                       int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, hipStream_t s);
+                     int64_t ldc, const float* low, const float* high, float* out_lp, int64_t B, void* ws,
+                     int64_t ws_bytes, hipStream_t s);
 int ar_flow_log_prob_train(const naz_ar_desc* d, const void* packed, const float* x, int64_t ldx, const float* ctx,
-                           int64_t ldc, float* out_lp, float* states, int64_t B, hipStream_t s);
+                           int64_t ldc, float* out_lp, float* states, int64_t B, void* ws, int64_t ws_bytes,
+                           hipStream_t s);
 int64_t ar_flow_bwd_packed_bytes(const naz_ar_desc* d);
 int ar_flow_bwd_dims(const naz_ar_desc* d, int* dims);
 int ar_flow_pack_bwd(const naz_ar_desc* d, const float* flat, const float* mask, void* packed, hipStream_t s);
@@ -137,6 +140,10 @@ int cnf_integrate_dopri5_global(const naz_cnf_desc* d, const void* packed, const
 int wgrad_batched(int64_t M, int N1, int N2, int nbatch, const float* g, int64_t sgm, int64_t bg, const float* x,
                   int64_t sxm, int64_t bx, float* c, int64_t scm, int64_t bc, float* rowsum, int64_t br,
                   hipStream_t s);
+// elementwise.hip: the 256-byte header in front of each of P packed images (image p at base + p * stride)
+int write_image_headers(void* base, int64_t stride_bytes, int64_t P, const uint32_t* words, int nwords, hipStream_t s);
+// gemm_rows.hip: the batch-row GEMM's panel-split setting (v >= 0 sets; returns the previous value)
+int rowgemm_split_setting(int v);
 int rowgemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
                     const float* S, int64_t lds, int act, int64_t M, int N, hipStream_t s);
 

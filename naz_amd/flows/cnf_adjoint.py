@@ -124,6 +124,101 @@ class CnfWalk:
         return g_z
 
 
+# ----------------------------------------------------------------------------- the per-layer solve
+# The fused solve kernels (csrc/cnf.hip) hold the whole vector field in one CU's LDS; naz's POSYDON
+# CNF (examples/papers/eposydon/train_cnf_mle.py:91, train_cnf_mle_q.py:92: D = 4, H = [128] x 4) does
+# not fit (~200 KB of weights).  Every other shape integrates through the walk's RHS instead: per
+# RHS one batch-row GEMM launch per layer for the values and one for the Hutchinson tangents (the
+# same kernels as the backward), torch only for the [B, D] stage combinations.
+
+def walk_rk4(walk: CnfWalk, x: torch.Tensor, ctx, eps: torch.Tensor, t0: float, t1: float, steps: int,
+             checkpoints: Optional[list] = None):
+    """Classical RK4 on the augmented state [x, a] (naz odeint.py:46-52, the config-5 pin) with the
+    walk's RHS: returns (x(t1), a(t1) = int -eps^T J eps dt).  ``checkpoints`` receives each step's
+    start state (the discrete adjoint's, as the fused forward keeps them)."""
+    x = x.contiguous()
+    a = torch.zeros(x.shape[0], device=x.device, dtype=torch.float32)
+    h = (t1 - t0) / steps
+    for _ in range(steps):
+        if checkpoints is not None:
+            checkpoints.append(x)
+        f1, g1, _ = walk.rhs(x, ctx, eps)
+        f2, g2, _ = walk.rhs(x + (0.5 * h) * f1, ctx, eps)
+        f3, g3, _ = walk.rhs(x + (0.5 * h) * f2, ctx, eps)
+        f4, g4, _ = walk.rhs(x + h * f3, ctx, eps)
+        x = x + (h / 6.0) * (f1 + 2.0 * f2 + 2.0 * f3 + f4)
+        a = a + (h / 6.0) * (g1 + 2.0 * g2 + 2.0 * g3 + g4)
+    return x, a
+
+
+# Dormand-Prince 5(4): naz's in-tree tableau (neural_nets/__deprecated__/neural_odes/odeint.py:136-160;
+# rows a_ij, 5th-order weights b, error weights b - b*)
+_DP5_A = [[1 / 5], [3 / 40, 9 / 40], [44 / 45, -56 / 15, 32 / 9], [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729],
+          [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656]]
+_DP5_B = [35 / 384, 0.0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84]
+_DP5_E = [35 / 384 - 5179 / 57600, 0.0, 500 / 1113 - 7571 / 16695, 125 / 192 - 393 / 640, -2187 / 6784 + 92097 / 339200,
+          11 / 84 - 187 / 2100, -1 / 40]
+
+
+def walk_dopri5(walk: CnfWalk, x: torch.Tensor, ctx, eps: torch.Tensor, t0: float, t1: float, atol: float,
+                rtol: float, max_steps: int):
+    """Adaptive Dormand-Prince 5(4) with torchdyn's batch-global control (naz FFJORDTransform
+    solver='dopri5', continuous_transforms.py:73-81), the controller of
+    naz_cnf_integrate_dopri5_global on the walk's RHS: ONE step size for the batch, error ratio =
+    RMS over every element of [B, D + 1] of err / (atol + rtol max(|y0|, |y1|)), accept at <= 1,
+    h *= clamp(0.9 r^(-1/5), 0.2 (1 on accept), 10), Hairer's initial step, FSAL, the last step
+    clipped to t1.  The controller reads one scalar per attempt back to the host (torchdyn's is
+    host-driven too).  Returns (x(t1), a(t1), nfe) with nfe < 0 when max_steps ran out."""
+    y = x.contiguous()
+    B = y.shape[0]
+    a = torch.zeros(B, device=y.device, dtype=torch.float32)
+    n_el = float(B * (y.shape[1] + 1))
+    direction = 1.0 if t1 > t0 else -1.0
+
+    def f(v):
+        k, g, _ = walk.rhs(v, ctx, eps)
+        return k, g
+
+    def rms(u, ua):
+        return float(torch.sqrt(((u.double() ** 2).sum() + (ua.double() ** 2).sum()) / n_el))
+
+    k0, k0a = f(y)
+    sc, sca = atol + rtol * y.abs(), atol + rtol * a.abs()
+    d0, d1 = rms(y / sc, a / sca), rms(k0 / sc, k0a / sca)
+    h0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
+    f1, f1a = f(y + (direction * h0) * k0)
+    d2 = rms((f1 - k0) / sc, (f1a - k0a) / sca) / h0
+    h1 = max(1e-6, h0 * 1e-3) if max(d1, d2) <= 1e-15 else (0.01 / max(d1, d2)) ** (1.0 / 6.0)
+    h = min(100 * h0, h1)
+    nfe, t, steps = 2, t0, 0
+    while steps < max_steps and t != t1:
+        rem = abs(t1 - t)
+        last = h >= rem
+        hh = direction * (rem if last else h)
+        ks, kas = [k0], [k0a]
+        for row in _DP5_A:
+            ki, kia = f(y + hh * sum(c * k for c, k in zip(row, ks)))
+            ks.append(ki)
+            kas.append(kia)
+        y5 = y + hh * sum(c * k for c, k in zip(_DP5_B, ks) if c != 0.0)
+        a5 = a + hh * sum(c * k for c, k in zip(_DP5_B, kas) if c != 0.0)
+        k6, k6a = f(y5)
+        ks.append(k6)
+        kas.append(k6a)
+        err = hh * sum(c * k for c, k in zip(_DP5_E, ks) if c != 0.0)
+        erra = hh * sum(c * k for c, k in zip(_DP5_E, kas) if c != 0.0)
+        en = rms(err / (atol + rtol * torch.maximum(y.abs(), y5.abs())),
+                 erra / (atol + rtol * torch.maximum(a.abs(), a5.abs())))
+        nfe += 6
+        if en <= 1.0:
+            y, a, k0, k0a = y5, a5, k6, k6a
+            t = t1 if last else t + hh
+        factor = 10.0 if en == 0 else min(10.0, max(0.9 / en ** 0.2, 1.0 if en <= 1.0 else 0.2))
+        h = abs(hh) * factor
+        steps += 1
+    return y, a, (nfe if t == t1 else -nfe)
+
+
 def _rk4_step_adjoint(walk, x, ctx, eps, h, lam, mu, gW, gb, g_ctx):
     """Discrete adjoint of one classical RK4 step from checkpoint x (naz odeint.py:46-52)."""
     k1, _, s1 = walk.rhs(x, ctx, eps)
@@ -171,9 +266,21 @@ class CnfSolveFn(Function):
     @staticmethod
     def forward(ctx, v, context, eps, core, t0: float, t1: float, *params):
         plan = core._plan
+        v = v.detach().contiguous()
+        if not plan.fused:  # the per-layer solve (no fused kernel at this shape)
+            if core.solver == "dopri5":
+                y, ld = core._solve_walk(v, eps, t0, t1, None, ops.LD_ROWSUM)
+                ctx.checkpoints = None
+                ctx.save_for_backward(y, eps, context)
+            else:
+                xs: list = []
+                y, ld = walk_rk4(plan.walk(), v, context, eps, t0, t1, core.steps, checkpoints=xs)
+                ctx.checkpoints = len(xs)
+                ctx.save_for_backward(eps, context, *xs)
+            ctx.core, ctx.t0, ctx.t1 = core, t0, t1
+            return y, ld
         packed = plan.packed()
         desc = plan.desc
-        v = v.detach().contiguous()
         if core.solver == "dopri5":
             y, ld = core._dopri5(desc, packed, v, eps, t0, t1, None, ops.LD_ROWSUM)
             ctx.checkpoints = None

@@ -83,11 +83,16 @@ class _CnfPlan:
         self.net = net
         self.mfma = mfma
         self.mode = None
-        self.desc = ops.cnf_desc(net.input_dim, net.context_dim, net.hidden_dims, net.act)
-        if not ops.cnf_supported(self.desc):
-            from .._lib import lib
-            raise NotImplementedError(f"naz_amd CNF: {lib().naz_last_error().decode()}")
+        # fused: the whole solve in one launch (csrc/cnf.hip, the vector field resident in one CU's
+        # LDS); otherwise (e.g. naz's POSYDON CNF, D = 4, H = [128] x 4: ~200 KB of weights) the
+        # per-layer solve over the walk's RHS (flows/cnf_adjoint.py walk_rk4 / walk_dopri5)
+        try:
+            self.desc = ops.cnf_desc(net.input_dim, net.context_dim, net.hidden_dims, net.act)
+            self.fused = bool(ops.cnf_supported(self.desc))
+        except ValueError:  # more hidden layers than the fused kernels take
+            self.desc, self.fused = None, False
         self._sig, self._packed = None, None
+        self._wsig, self._walk = None, None
 
     def set_mfma(self, mfma: str) -> None:
         self.mfma = mfma
@@ -103,7 +108,18 @@ class _CnfPlan:
         big = max(float(lin.weight.detach().abs().max()) for lin in lins[1:])
         return "f16x3" if big < self.F16_WEIGHT_LIMIT else "f32"
 
+    def walk(self):
+        """The per-layer RHS over the current parameters (rebuilt when one changes)."""
+        from .cnf_adjoint import CnfWalk
+        ps = [t for lin in self.net.linears() for t in (lin.weight, lin.bias)]
+        sig = tuple((p.data_ptr(), p._version) for p in ps) + (cache_epoch(),)
+        if sig != self._wsig or self._walk is None:
+            self._walk, self._wsig = CnfWalk(self.net), sig
+        return self._walk
+
     def packed(self):
+        if not self.fused:
+            raise RuntimeError("naz_amd CNF: no fused solve kernel at this shape (the per-layer solve runs instead)")
         ps = [t for lin in self.net.linears() for t in (lin.weight, lin.bias)]
         sig = tuple((p.data_ptr(), p._version) for p in ps) + (cache_epoch(),)
         if sig != self._sig or self._packed is None:
@@ -145,6 +161,34 @@ class _FFJORDCore:
                                "raise max_steps, loosen atol/rtol, or set strict=False to accept partial solves")
         return y, ld
 
+    def _solve_walk(self, v, noise, t0, t1, ld_buf, ld_mode):
+        """The per-layer solve (no fused kernel at this shape): rk4 or dopri5 with torchdyn's
+        batch-global control over the walk's RHS (flows/cnf_adjoint.py)."""
+        from .cnf_adjoint import walk_dopri5, walk_rk4
+        walk = self._plan.walk()
+        v = v.detach().contiguous()
+        if self.solver == "dopri5":
+            if self.step_control != "global":
+                raise NotImplementedError("naz_amd CNF: step_control='group' needs the fused solve kernel; this "
+                                          "shape runs the per-layer solve with torchdyn's batch-global control")
+            y, ld, nfe = walk_dopri5(walk, v, self._context, noise, t0, t1, self.atol, self.rtol, self.max_steps)
+            self.last_nfe = torch.tensor([nfe], device=v.device, dtype=torch.int32)
+            if self.strict and nfe < 0:
+                raise RuntimeError(f"naz_amd CNF dopri5: the batch reached max_steps={self.max_steps} before t1 "
+                                   "(step size collapsed or non-finite state); raise max_steps, loosen atol/rtol, "
+                                   "or set strict=False to accept partial solves")
+        else:
+            y, ld = walk_rk4(walk, v, self._context, noise, t0, t1, self.steps)
+        if ld_buf is None:
+            return y, ld
+        if ld_mode == ops.LD_ROWSUM_ADD:
+            ld_buf.add_(ld)
+        elif ld_mode == ops.LD_ROWSUM_SUB:
+            ld_buf.sub_(ld)
+        else:
+            ld_buf.copy_(ld)
+        return y, ld_buf
+
     def _solve(self, v, t0, t1, ld_buf, ld_mode):
         if ld_buf is None and self._needs_graph(v):
             # (the in-place accumulating forms, _inverse_acc / _call_acc, serve the no-grad walk and
@@ -153,6 +197,8 @@ class _FFJORDCore:
             ps = [t for lin in self._net.linears() for t in (lin.weight, lin.bias)]
             return CnfSolveFn.apply(v, self._context, self._noise(v), self, float(t0), float(t1), *ps)
         noise = self._noise(v)
+        if not self._plan.fused:
+            return self._solve_walk(v, noise, t0, t1, ld_buf, ld_mode)
         packed = self._plan.packed()  # may re-resolve the mode: read desc only after it
         if self.solver == "dopri5":
             return self._dopri5(self._plan.desc, packed, v, noise, t0, t1, ld_buf, ld_mode)

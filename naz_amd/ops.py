@@ -8,6 +8,7 @@ without copies.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -58,6 +59,51 @@ def _rows(t: Tensor) -> Tuple[Tensor, int]:
 
 def _p(t: Optional[Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
+
+
+_WS: dict = {}
+
+
+def workspace(dev: torch.device, nbytes: int) -> Tuple[Optional[int], int]:
+    """Caller-owned device workspace of the autoregressive log_prob entries (include/naz_hip.h
+    naz_ar_flow_workspace_bytes: the wide MAF inverse's per-wave hidden layers; no entry allocates):
+    one buffer per (device, stream), grown on demand and kept, so a captured HIP graph replays one
+    fixed address.  Returns (pointer, bytes) for the call."""
+    if nbytes <= 0:
+        return None, 0
+    key = (str(dev), _stream(dev))
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = _WS[key] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    return buf.data_ptr(), buf.numel()
+
+
+def rowgemm_split(value: Optional[bool] = None) -> bool:
+    """The batch-row GEMM's panel split (naz_tuning "rowgemm_split": outputs wider than 128 columns
+    as two half-width panels; no result changes).  ``value`` sets it; returns the setting before."""
+    r = int(lib().naz_tuning(b"rowgemm_split", -1 if value is None else int(bool(value))))
+    if r < 0:
+        check(r, "rowgemm_split")
+    return bool(r)
+
+
+def _release_image(ptr: int) -> None:
+    lib().naz_image_release(ptr)  # (an image packed over it since has replaced the record: no-op)
+
+
+def track_image(img: Tensor) -> Tensor:
+    """Forget the library's registry record of a packed image when its tensor is freed: the caching
+    allocator hands the memory to the next tensor, which must not pass for an image."""
+    if not getattr(img, "_naz_tracked", False):
+        weakref.finalize(img, _release_image, img.data_ptr()).atexit = False
+        img._naz_tracked = True
+    return img
+
+
+def attach_image(img: Tensor, what: str) -> Tensor:
+    """Register a host-packed image copied to the device (naz_image_attach reads its header once)."""
+    check(lib().naz_image_attach(_p(img), img.numel() * img.element_size(), _stream(img.device)), what)
+    return track_image(img)
 
 
 # ----------------------------------------------------------------------------- a1 + a2
@@ -558,7 +604,7 @@ def coupling_pack(d: CouplingDesc, flat: Tensor, packed: Optional[Tensor] = None
     if packed is None or packed.numel() * 4 != nbytes:
         packed = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
     check(lib().naz_coupling_pack(d, _p(flat), _p(packed), _stream(dev)), "coupling_pack")
-    return packed
+    return track_image(packed)
 
 
 def _ctx_arg(context: Optional[Tensor], B: int):
@@ -690,7 +736,7 @@ def ar_flow_pack(d: ArDesc, flat: np.ndarray, perm: np.ndarray, device) -> Tenso
         raise RuntimeError("naz_amd ar_flow_pack: unsupported descriptor")
     host = np.empty(nbytes // 4, dtype=np.float32)
     check(lib().naz_ar_flow_pack_host(d, flat.ctypes.data, perm.ctypes.data, host.ctypes.data), "ar_flow_pack")
-    return torch.from_numpy(host).to(device)
+    return attach_image(torch.from_numpy(host).to(device), "ar_flow_pack")
 
 
 def ar_flow_pack_fwd(d: ArDesc, flat: np.ndarray, device) -> Tensor:
@@ -702,7 +748,7 @@ def ar_flow_pack_fwd(d: ArDesc, flat: np.ndarray, device) -> Tensor:
         raise RuntimeError("naz_amd ar_flow_pack_fwd: unsupported descriptor")
     host = np.empty(nbytes // 4, dtype=np.float32)
     check(lib().naz_ar_flow_pack_fwd_host(d, flat.ctypes.data, host.ctypes.data), "ar_flow_pack_fwd")
-    return torch.from_numpy(host).to(device)
+    return attach_image(torch.from_numpy(host).to(device), "ar_flow_pack_fwd")
 
 
 def ar_flow_sample(d: ArDesc, packed_fwd: Tensor, z: Tensor, context: Optional[Tensor] = None,
@@ -743,7 +789,7 @@ def ar_flow_pack_fwd_batched(d: ArDesc, flat: Tensor, mask: Optional[Tensor] = N
     if mask is not None and (mask.numel() != flat.shape[1] or not mask.is_contiguous()):
         raise ValueError("ar_flow_pack_fwd_batched: mask must be a contiguous [L * per] tensor")
     check(lib().naz_ar_flow_pack_fwd(d, _p(flat), sflat, _p(out), n, P, _p(mask), _stream(dev)), "ar_flow_pack_fwd")
-    return out
+    return track_image(out)
 
 
 def ar_flow_sample_batched(d: ArDesc, packed: Tensor, z: Tensor, context: Optional[Tensor] = None,
@@ -802,7 +848,7 @@ def ar_flow_pack_batched(d: ArDesc, flat: Tensor, perm, pass0: Optional[Tensor] 
     out = torch.empty((P, n), device=dev, dtype=torch.float32)
     check(lib().naz_ar_flow_pack(d, _p(flat), sflat, _p(pmd), _p(out), n, P, _p(pass0), sp0, _p(mask),
                                  _stream(dev)), "ar_flow_pack")
-    return out
+    return track_image(out)
 
 
 def ar_flow_log_prob_batched(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor] = None,
@@ -823,8 +869,9 @@ def ar_flow_log_prob_batched(d: ArDesc, packed: Tensor, x: Tensor, context: Opti
         raise ValueError("ar_flow_log_prob_batched: x must be [B, D] or [P, B, D]")
     ctx = None if context is None else context.reshape(1, -1).contiguous()
     out = torch.empty((P, B), device=dev, dtype=torch.float32)
+    ws, wsb = workspace(dev, int(lib().naz_ar_flow_workspace_bytes(d, B, P)))
     check(lib().naz_ar_flow_log_prob_batched(d, _p(packed), packed.stride(0), _p(x), x.shape[-1], sx, _p(ctx), 0,
-                                             _p(out), B, B, P, int(pass0_const), _stream(dev)),
+                                             _p(out), B, B, P, int(pass0_const), ws, wsb, _stream(dev)),
           "ar_flow_log_prob_batched")
     return out
 
@@ -838,8 +885,9 @@ def ar_flow_log_prob(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Ten
     context, ldc = _ctx_arg(context, B)
     if out is None:
         out = torch.empty((B,), device=dev, dtype=torch.float32)
+    ws, wsb = workspace(dev, int(lib().naz_ar_flow_workspace_bytes(d, B, 1)))
     check(lib().naz_ar_flow_log_prob(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out), B,
-                                     _stream(dev)), "ar_flow_log_prob")
+                                     ws, wsb, _stream(dev)), "ar_flow_log_prob")
     return out
 
 
@@ -867,7 +915,7 @@ def ar_flow_pack_bwd(d: ArDesc, flat: Tensor, mask: Optional[Tensor] = None) -> 
         raise ValueError("ar_flow_pack_bwd: mask must be a contiguous tensor shaped like flat")
     out = torch.empty(n, device=dev, dtype=torch.float32)
     check(lib().naz_ar_flow_pack_bwd(d, _p(flat), _p(mask), _p(out), _stream(dev)), "ar_flow_pack_bwd")
-    return out
+    return track_image(out)
 
 
 def ar_flow_log_prob_train(d: ArDesc, packed: Tensor, x: Tensor, context: Optional[Tensor], states: Tensor,
@@ -882,8 +930,9 @@ def ar_flow_log_prob_train(d: ArDesc, packed: Tensor, x: Tensor, context: Option
         raise ValueError(f"ar_flow_log_prob_train: states must be contiguous {(d.L, B, d.D)}")
     if out is None:
         out = torch.empty((B,), device=dev, dtype=torch.float32)
+    ws, wsb = workspace(dev, int(lib().naz_ar_flow_workspace_bytes(d, B, 1)))
     check(lib().naz_ar_flow_log_prob_train(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(out), _p(states), B,
-                                           _stream(dev)), "ar_flow_log_prob_train")
+                                           ws, wsb, _stream(dev)), "ar_flow_log_prob_train")
     return out
 
 
@@ -951,8 +1000,9 @@ def flow_log_prob(d: FlowDesc, packed: Tensor, x: Tensor, context: Optional[Tens
     context, ldc = _ctx_arg(context, B)
     if out is None:
         out = torch.empty((B,), device=dev, dtype=torch.float32)
+    ws, wsb = workspace(dev, int(lib().naz_workspace_bytes(d, B)))
     check(lib().naz_flow_log_prob(d, _p(packed), _p(x), ldx, _p(context), ldc, _p(low), _p(high), _p(out), B,
-                                  _stream(dev)), "flow_log_prob")
+                                  ws, wsb, _stream(dev)), "flow_log_prob")
     return out
 
 
@@ -979,7 +1029,7 @@ def coupling_pack_bwd(d: CouplingDesc, flat: Tensor, out: Optional[Tensor] = Non
     if out is None or out.numel() * 4 != n:
         out = torch.empty(n // 4, device=dev, dtype=torch.float32)
     check(lib().naz_coupling_pack_bwd(d, _p(flat.contiguous()), _p(out), _stream(dev)), "coupling_pack_bwd")
-    return out
+    return track_image(out)
 
 
 def coupling_log_prob_train(d: CouplingDesc, packed: Tensor, x: Tensor, context: Optional[Tensor],
@@ -1077,7 +1127,7 @@ def cnf_pack(d: CnfDesc, flat: Tensor, packed: Optional[Tensor] = None) -> Tenso
     if packed is None or packed.numel() * 4 != nbytes:
         packed = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
     check(lib().naz_cnf_pack(d, _p(flat), _p(packed), _stream(dev)), "cnf_pack")
-    return packed
+    return track_image(packed)
 
 
 def cnf_integrate(d: CnfDesc, packed: Tensor, x: Tensor, eps: Tensor, t0: float, t1: float, steps: int,

@@ -1,3 +1,3 @@
-from .train_flows import DataParallel, get_params, nll_step, predict, set_params, train, train_lightning
+from .train_flows import DataParallel, GraphedNllStep, get_params, nll_step, predict, set_params, train, train_lightning
 
-__all__ = ["DataParallel", "get_params", "nll_step", "predict", "set_params", "train", "train_lightning"]
+__all__ = ["DataParallel", "GraphedNllStep", "get_params", "nll_step", "predict", "set_params", "train", "train_lightning"]

@@ -23,7 +23,8 @@ import torch
 import torch.optim as optim
 from torch import nn
 
-__all__ = ["DataParallel", "get_params", "set_params", "nll_step", "train", "train_lightning", "predict"]
+__all__ = ["DataParallel", "GraphedNllStep", "get_params", "set_params", "nll_step", "train", "train_lightning",
+           "predict"]
 
 
 def _transforms(flow):
@@ -161,6 +162,76 @@ def nll_step(flow, x_b: torch.Tensor, y_b: Optional[torch.Tensor], optimizer, pa
         nn.utils.clip_grad_norm_(params, clip_val)
     optimizer.step()
     return dp.all_reduce_sum(loss)
+
+
+class GraphedNllStep:
+    """``nll_step`` replayed as ONE captured HIP graph (forward kernels, the composed or fused
+    backward, the gradient all-reduce, clip and Adam) for a fixed minibatch shape: naz's ``train``
+    runs the same ``batch_frac`` minibatch shape every step (train_flows.py:194-213), and at naz's
+    batch sizes (e.g. 10.7 k rows for the 4-parameter MLE MAF, train_mle_all_data_4param.py:95) the
+    composed wide-MAF backward is hundreds of small launches per layer.
+
+    The rows are copied into static buffers and the graph replays; the first call for a shape is
+    an eager step on a side stream (it creates the gradients, the optimizer state and the paths'
+    caches: schedules, packs, buffers) after which one step is captured without running, so every
+    call is exactly one optimizer step.  The optimizer must be
+    capturable (``torch.optim.Adam(..., capturable=True)``; set here before its first step).  The
+    fused autoregressive paths check that the rows fit their f16 input split (|x|, |ctx| < 2^15)
+    with a host read-back, which a capture cannot do: the check runs eagerly before every replay,
+    and an out-of-range minibatch takes the eager step instead."""
+
+    def __init__(self, flow, optimizer, params: List[torch.Tensor], dp: "DataParallel", global_batch: int,
+                 clip_val: Optional[float] = 1.0, micro_batch: Optional[int] = None):
+        self.flow, self.opt, self.params, self.dp = flow, optimizer, params, dp
+        self.global_batch, self.clip_val, self.micro_batch = global_batch, clip_val, micro_batch
+        for g in optimizer.param_groups:
+            if "capturable" in g:
+                g["capturable"] = True
+        self._key, self._graph = None, None
+        self.replays = 0
+        self.eager_steps = 0
+
+    def _eager(self, x_b, y_b):
+        self.eager_steps += 1
+        return nll_step(self.flow, x_b, y_b, self.opt, self.params, self.dp, self.global_batch, self.clip_val,
+                        micro_batch=self.micro_batch)
+
+    def _in_range(self, x_b, y_b) -> bool:
+        m = x_b.detach().abs().amax() if x_b.numel() else torch.zeros((), device=x_b.device)
+        if y_b is not None and y_b.numel():
+            m = torch.maximum(m, y_b.detach().abs().amax())
+        return float(m) < 32768.0
+
+    def __call__(self, x_b: torch.Tensor, y_b: Optional[torch.Tensor]) -> torch.Tensor:
+        from ..flows import flow as flow_mod
+        key = (tuple(x_b.shape), None if y_b is None else tuple(y_b.shape), x_b.device)
+        if not self._in_range(x_b, y_b):
+            return self._eager(x_b, y_b)
+        if key != self._key:
+            dev = x_b.device
+            self._x = x_b.detach().clone()
+            self._y = None if y_b is None else y_b.detach().clone()
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                loss = self._eager(self._x, self._y).clone()  # this call's step
+            torch.cuda.current_stream(dev).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            flow_mod._RANGE_CHECKED = True
+            try:
+                with torch.cuda.graph(graph):  # recorded, not run
+                    self._loss = nll_step(self.flow, self._x, self._y, self.opt, self.params, self.dp,
+                                          self.global_batch, self.clip_val, micro_batch=self.micro_batch)
+            finally:
+                flow_mod._RANGE_CHECKED = False
+            self._graph, self._key = graph, key
+            return loss
+        self._x.copy_(x_b)
+        if y_b is not None:
+            self._y.copy_(y_b)
+        self._graph.replay()
+        self.replays += 1
+        return self._loss
 
 
 def train(flow, x, y, opt=optim.Adam, lr=0.001, num_epochs=1024, train_frac=0.7, batch_frac=0.005,

@@ -127,6 +127,10 @@ def main():
     # config 5's block shape (D=16, H=[128]*3, unconditional)
     _fixture("cnf_refode_d16c0.npz", dict(flow_type="cnf", D=16, C=0, hidden=[128, 128, 128], L=1,
                                           activation="softplus", steps=8), 160)
+    # naz's POSYDON CNF (examples/papers/eposydon/train_cnf_mle.py:91, train_cnf_mle_q.py:92: 4 parameters,
+    # H = [128] x 4, one block; the lambda width comes from the data file: 4 here)
+    _fixture("cnf_refode_d4c4_h128x4.npz", dict(flow_type="cnf", D=4, C=4, hidden=[128] * 4, L=1,
+                                                activation="softplus", steps=8), 128)
 
 
 if __name__ == "__main__":

@@ -160,6 +160,102 @@ def counted_lgkm_violations(start: int, insns: list[tuple[int, str]]) -> list[st
                     flags=counted)
 
 
+_REG = re.compile(r"\b([va])(?:\[(\d+):(\d+)\]|(\d+)\b)")
+_NODEST = ("ds_write", "ds_store", "global_store", "buffer_store", "flat_store", "scratch_store", "s_", "ds_add_u32",
+           "ds_add_f32", "ds_max", "ds_min")
+
+
+def _regs(operands: str) -> list[tuple[str, int]]:
+    out = []
+    for m in _REG.finditer(operands):
+        kind = m.group(1)
+        if m.group(4) is not None:
+            out.append((kind, int(m.group(4))))
+        else:
+            out.extend((kind, r) for r in range(int(m.group(2)), int(m.group(3)) + 1))
+    return out
+
+
+def _operands(t: str) -> tuple[str, list[str]]:
+    body = t.split("//")[0].strip()
+    parts = body.split(None, 1)
+    if len(parts) < 2:
+        return parts[0] if parts else "", []
+    return parts[0], [o.strip() for o in parts[1].split(",")]
+
+
+def _dst_src(op: str, ops: list[str]) -> tuple[set, set]:
+    """(destination, source) vector registers of one instruction (v and a registers)."""
+    if not ops:
+        return set(), set()
+    if op.startswith(_NODEST):
+        return set(), set(_regs(", ".join(ops)))
+    dst, src = set(_regs(ops[0])), set(_regs(", ".join(ops[1:])))
+    if "mac" in op or "fmac" in op or op.startswith(("v_dot2c", "v_pk_fmac")):
+        src |= dst  # accumulates into its destination
+    return dst, src
+
+
+def _is_lgkm_op(op: str) -> bool:
+    return op.startswith(("ds_", "s_load", "s_buffer_load", "s_scratch_load", "s_dcache", "s_memtime", "flat_",
+                          "s_sendmsg"))
+
+
+def pending_lds_read_uses(start: int, insns: list[tuple[int, str]], cap: int = 24) -> list[str]:
+    """Instructions that read or overwrite a destination VGPR of an LDS read which an s_waitcnt
+    lgkmcnt has not yet retired on some path (loop back edges included).
+
+    The untracked A-fragment reads (naz_device.h lds_read_b128_untracked: inline asm, so the
+    compiler's waitcnt pass does not see their destinations) are safe only if nothing touches those
+    registers before the hand-counted lds_wait<N> that retires them: a v_mov copy or spill of a
+    prefetched fragment placed before the wait would read stale data without any error.  The
+    analysis tracks the LGKM queue in issue order (LDS returns in order; `s_waitcnt lgkmcnt(N)` keeps
+    the newest N entries) as a may-pending set per queue position, merging paths aligned at the
+    newest entry; SMEM entries are counted as queue entries without vector destinations (a counted
+    wait with SMEM in flight is counted_lgkm_violations' finding)."""
+    succ = _successors(start, insns)
+    state_in: list = [None] * len(insns)
+    work = [(0, ())]
+    bad: dict[int, str] = {}
+
+    def merge(a, b):
+        if a is None:
+            return b
+        n = max(len(a), len(b))
+        a2 = (frozenset(),) * (n - len(a)) + a
+        b2 = (frozenset(),) * (n - len(b)) + b
+        return tuple(x | y for x, y in zip(a2, b2))
+
+    while work:
+        k, st = work.pop()
+        new = merge(state_in[k], st)
+        if new == state_in[k]:
+            continue
+        state_in[k] = new
+        st = new
+        a, t = insns[k]
+        op, ops = _operands(t)
+        dst, src = _dst_src(op, ops)
+        pend = frozenset().union(*st) if st else frozenset()
+        lds_read = op.startswith(("ds_read", "ds_load", "ds_bpermute", "ds_permute", "ds_swizzle"))
+        # (a later LDS read into a pending read's registers is fine: LDS returns in issue order)
+        if pend and ((src | (set() if lds_read else dst)) & pend) and not op.startswith("s_waitcnt"):
+            bad[a] = t
+        if op.startswith("s_waitcnt"):
+            m = _LGKM.search(t.split("//")[0])
+            if m is not None:
+                keep = int(m.group(1))
+                st = st[len(st) - keep:] if keep < len(st) else st
+                if keep == 0:
+                    st = ()
+        elif _is_lgkm_op(op):
+            st = (st + (frozenset(dst) if op.startswith(("ds_read", "ds_load", "ds_bpermute", "ds_permute",
+                                                         "ds_swizzle", "flat_load")) else frozenset(),))[-cap:]
+        for s2 in succ[k]:
+            work.append((s2, st))
+    return [f"+0x{a - start:x}: {t.split('//')[0].strip()}" for a, t in sorted(bad.items())]
+
+
 def check_library(lib: Path, arch: str = "gfx950") -> tuple[int, dict[str, list[str]]]:
     """(number of DMA kernels checked, {kernel: violations})."""
     checked = 0

@@ -29,8 +29,9 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     assert set(declared_functions()) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
     # 2: naz_ar_desc.flags (NAZ_AR_CLIP_ZERO_GRAD), naz_affine_ar_bwd's mode bits, and
-    # naz_ar_flow_supported's 0 / 1 / 2 contract (2 = forward direction only)
-    assert L.naz_abi_version() == 2
+    # naz_ar_flow_supported's 0 / 1 / 2 contract (2 = forward direction only); 3: packed-image
+    # headers + registry, caller-owned workspace of the autoregressive log_prob entries
+    assert L.naz_abi_version() == 3
 
 
 def test_ar_flow_supported_contract():
@@ -86,10 +87,10 @@ def test_maf_backward_and_batched_wgrad_host_errors():
     # the saved-state forward: any affine flow with a fused inverse (the wide MLE MAFs compose their
     # backward of GEMMs); a spline flow has none
     nsa = ops.ar_flow_desc("nsa", 16, 32, 128, 4, 2)
-    rc = L.naz_ar_flow_log_prob_train(nsa, 16, 16, 2, 16, 2, 16, 16, 128, None)
+    rc = L.naz_ar_flow_log_prob_train(nsa, 16, 16, 2, 16, 2, 16, 16, 128, None, 0, None)
     assert rc != 0 and b"no fused affine inverse" in L.naz_last_error()
     wide = ops.ar_flow_desc("maf", 4, 2, 512, 18, 5)
-    assert L.naz_ar_flow_log_prob_train(wide, 16, 16, 4, 16, 2, 16, 16, 0, None) == 0  # no rows: no launch
+    assert L.naz_ar_flow_log_prob_train(wide, 16, 16, 4, 16, 2, 16, 16, 0, None, 0, None) == 0  # no rows: no launch
     # one dim of the composed backward's VJP: dim range and null checks before any launch
     rc = L.naz_maf_dim_vjp(0, 16, 8, 16, 4, 16, 4, None, 16, 4, 16, 8, None, 0, 128, 4, 4, None)
     assert rc != 0 and b"outside" in L.naz_last_error()
@@ -139,9 +140,82 @@ def test_generic_flow_entries_dispatch_without_compute():
     bad = _lib.FlowDesc()
     bad.kind = 7
     assert L.naz_flow_packed_bytes(bad) == -1
-    assert L.naz_flow_log_prob(bad, None, None, 0, None, 0, None, None, None, 0, None) != 0
+    assert L.naz_flow_log_prob(bad, None, None, 0, None, 0, None, None, None, 0, None, 0, None) != 0
     assert b"unknown flow kind" in L.naz_last_error()
     assert L.naz_flow_sample(fa, None, None, 0, None, 0, None, None, None, 0, None, 0, None) == 0  # B = 0
     assert L.naz_flow_sample(fa, None, None, 0, None, 0, None, None, None, 0, None, 1, None) != 0
     assert b"null pointer" in L.naz_last_error()
     assert L.naz_ar_flow_fwd_packed_bytes(a) > 0
+
+
+def test_workspace_sizes_are_the_wide_inverse_scratch():
+    """naz_ar_flow_workspace_bytes / naz_workspace_bytes (ABI 3): 0 wherever every intermediate stays
+    on chip; for the wide MLE MAF (made_ar_wide.h) one 4-wave workgroup per CU (at most one per
+    64-row tile and draw), 128 KiB of hidden-layer fragments per wave.  Without a GPU the CU count
+    reads as 256.  No log_prob entry allocates: too little workspace is an error before any launch."""
+    from naz_amd import _lib, ops
+    L = _lib.lib()
+    wide = ops.ar_flow_desc("maf", 4, 2, 512, 18, 5)
+    per_wg = 4 * 128 * 1024
+    assert L.naz_ar_flow_workspace_bytes(wide, 100, 1) == 2 * per_wg  # 2 tiles of 64 rows
+    assert L.naz_ar_flow_workspace_bytes(wide, 64, 3) == 3 * per_wg  # one tile per draw
+    assert L.naz_ar_flow_workspace_bytes(wide, 1 << 18, 1) == 256 * per_wg  # 128 MiB: the persistent grid
+    assert L.naz_workspace_bytes(ops.flow_desc(wide), 1 << 18) == 256 * per_wg
+    assert L.naz_ar_flow_workspace_bytes(wide, 0, 1) == 0 and L.naz_ar_flow_workspace_bytes(wide, -1, 1) == -1
+    for narrow in (ops.ar_flow_desc("maf", 2, 2, 150, 16, 3), ops.ar_flow_desc("nsa", 16, 32, 128, 8, 2)):
+        assert L.naz_ar_flow_workspace_bytes(narrow, 1 << 20, 4) == 0
+    assert L.naz_ar_flow_workspace_bytes(ops.ar_flow_desc("maf", 3, 2, 150, 4, 3), 128, 1) == -1
+
+
+def test_image_registry_refuses_unregistered_images():
+    """Every launch entry resolves its packed image through the registry before launching (ABI 3):
+    an address no packer wrote (or attached) is an error, not a launch -- checked here without a GPU
+    (the registry lookup precedes every device call)."""
+    from naz_amd import _lib, ops
+    L = _lib.lib()
+    c = ops.coupling_desc(16, 32, 8, 8, 8, 128)
+    fake = 1 << 40
+    rc = L.naz_coupling_log_prob(c, fake, fake, 16, fake, 32, None, None, fake, 128, None)
+    assert rc != 0 and b"is not a packed image" in L.naz_last_error()
+    a = ops.ar_flow_desc("nsa", 16, 32, 128, 8, 2)
+    rc = L.naz_ar_flow_log_prob(a, fake, fake, 16, fake, 32, None, None, fake, 128, None, 0, None)
+    assert rc != 0 and b"is not a packed image" in L.naz_last_error()
+    rc = L.naz_ar_flow_sample(a, None, fake, 16, fake, 32, None, None, fake, 16, None, 128, None)
+    assert rc != 0 and b"null" in L.naz_last_error()
+    assert L.naz_image_release(fake) != 0
+    assert L.naz_image_attach(None, 4096, None) != 0
+
+
+def test_host_packed_image_headers():
+    """The host packers write the 256-byte header the registry reads back (naz_image_attach): magic,
+    layout version, kind (3 inverse / 4 forward), a tag that depends on the descriptor's layout fields
+    only, layers, body bytes."""
+    import ctypes
+    import numpy as np
+    from naz_amd import _lib, ops
+    L = _lib.lib()
+
+    def header(d, fwd):
+        n = int((L.naz_ar_flow_fwd_packed_bytes if fwd else L.naz_ar_flow_packed_bytes)(d))
+        per = (4 * 2 + 2) * 150 + 2 * (150 * 150 + 150) + 2 * 2 * 150 + 4  # D=2 | C=2, H=[150]x3 maf
+        flat = np.zeros(d.L * per, np.float32)
+        perm = np.tile(np.arange(2, dtype=np.int32), (d.L, 1))
+        host = np.zeros(n // 4, np.float32)
+        if fwd:
+            ops.check(L.naz_ar_flow_pack_fwd_host(d, flat.ctypes.data, host.ctypes.data), "fwd")
+        else:
+            ops.check(L.naz_ar_flow_pack_host(d, flat.ctypes.data, perm.ctypes.data, host.ctypes.data), "inv")
+        return n, host[:64].view(np.uint32).copy()
+
+    d = ops.ar_flow_desc("maf", 2, 2, 150, 4, 3)
+    n, h = header(d, False)
+    assert (h[0], h[1], h[2], h[4], h[5]) == (0x495A414E, 3, 3, 4, 0)
+    assert int(h[6]) | (int(h[7]) << 32) == n - 256
+    _, hf = header(d, True)
+    assert hf[2] == 4 and hf[3] != h[3]
+    d2 = ops.ar_flow_desc("maf", 2, 2, 150, 7, 3)  # more layers: same layout tag, more bytes
+    n2, h2 = header(d2, False)
+    assert h2[3] == h[3] and h2[4] == 7 and n2 - 256 == (n - 256) // 4 * 7
+    d3 = ops.ar_flow_desc("maf", 2, 2, 150, 4, 3)
+    d3.flags = 1  # the backward's clip semantics do not change the layout
+    assert header(d3, False)[1][3] == h[3]

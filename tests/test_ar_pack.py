@@ -46,8 +46,13 @@ def test_host_pack_decodes_to_scaled_weights(kind, D, C, H, NH):
     host = np.empty(nbytes // 4, dtype=np.float32)
     ops.check(ops.lib().naz_ar_flow_pack_host(d, np.ascontiguousarray(flat).ctypes.data, perm.ctypes.data,
                                                 host.ctypes.data), "pack")
+    # the 256-byte image header (include/naz_hip.h "Packed images"), then the layers
+    hdr = host[:64].view(np.uint32)
+    assert hdr[0] == 0x495A414E and hdr[2] == 3 and hdr[4] == L and hdr[5] == 0
+    assert int(hdr[6]) | (int(hdr[7]) << 32) == nbytes - 256 and not hdr[8:].any()
+    host = host[64:]
     words = host.view(np.uint32)
-    layer_floats = nbytes // 4 // L
+    layer_floats = host.size // L
     per = sum(sizes)
     # every layer l, pass 0, first L1 fragment (block 0, k-step 0 = context): lane (m, kg) pair w
     # holds W0[m][8 kg + 2w (+1)] * kSigScale as hi | lo f16 pieces (layer l's flat rows at l * per:
@@ -69,7 +74,7 @@ def test_host_pack_decodes_to_scaled_weights(kind, D, C, H, NH):
                     # hi + lo carries ~22 bits; lo below f16's normal range keeps 2^-24 absolute spacing
                     assert abs((np.float32(h16) + np.float32(l16)) - want) <= 2.5e-7 * abs(want) + 3.1e-8
     # the permutation table rides in the image (last D ints before the layer padding)
-    assert layer_floats * 4 * L == nbytes and layer_floats % 256 == 0
+    assert layer_floats * 4 * L + 256 == nbytes and layer_floats % 256 == 0
     perm_off = None
     for off in range(layer_floats - 512, layer_floats - D + 1):
         if np.array_equal(host[off:off + D].view(np.int32), perm[0]):
@@ -85,7 +90,7 @@ def test_fused_maf_backward_host_queries():
     assert ops.ar_flow_bwd_supported(d)
     assert ops.ar_flow_bwd_dims(d) == dict(n_hidden=3, HP=160, XA=160, XB=0, X0W=8, rows=128)
     per_layer = int(ops.lib().naz_ar_flow_bwd_packed_bytes(ops.ar_flow_desc("maf", 2, 2, 150, 1, 3)))
-    assert per_layer > 0 and int(ops.lib().naz_ar_flow_bwd_packed_bytes(d)) == 16 * per_layer
+    assert per_layer > 256 and int(ops.lib().naz_ar_flow_bwd_packed_bytes(d)) - 256 == 16 * (per_layer - 256)
     for bad in (ops.ar_flow_desc("nsa", 16, 32, 128, 1), ops.ar_flow_desc("maf", 16, 32, 128, 1, 2),
                 ops.ar_flow_desc("maf", 2, 2, 150, 1, 3, act="relu"), ops.ar_flow_desc("maf", 4, 2, 512, 1, 5)):
         assert not ops.ar_flow_bwd_supported(bad)

@@ -90,8 +90,10 @@ def _product_grads(f, x, c, eps, w):
     return lp, g
 
 
+# the last two: naz's POSYDON CNF (eposydon/train_cnf_mle.py:91, D = 4, H = [128] x 4, the lambda width from the
+# data) on the per-layer solve (no fused kernel fits its weights)
 CASES = [(4, 2, [32, 32], 2, "softplus"), (4, 2, [32, 32], 1, "tanh"), (5, 3, [48, 32, 16, 16], 1, "softplus"),
-         (16, 0, [128, 128, 128], 1, "softplus")]
+         (16, 0, [128, 128, 128], 1, "softplus"), (4, 4, [128] * 4, 1, "softplus"), (4, 6, [128] * 4, 1, "tanh")]
 
 
 @pytest.mark.parametrize("D,C,hidden,L,act", CASES, ids=lambda v: str(v))
@@ -122,7 +124,7 @@ def test_cnf_broadcast_context_gradient():
     assert_parity(_np(g["ctx"]), r64, r32, what="broadcast ctx grad", floor=grad_floor(r64), count_factor=None)
 
 
-@pytest.mark.parametrize("D,C,hidden", [(4, 2, [32, 32]), (16, 0, [128, 128, 128])])
+@pytest.mark.parametrize("D,C,hidden", [(4, 2, [32, 32]), (16, 0, [128, 128, 128]), (4, 4, [128] * 4)])
 def test_cnf_dopri5_adjoint_gradient_vs_converged(D, C, hidden):
     spec, state, f, x, c, eps, w = _setup(D, C, hidden, 1, "softplus", B=192, seed=3, solver="dopri5")
     lp, g = _product_grads(f, x, c, eps, w)

@@ -167,6 +167,51 @@ def test_rowgemm_config3_shapes():
     _check(dx, G.double() @ (W.double() * mask.double()), G @ (W * mask), "rowgemm dX masked")
 
 
+@pytest.mark.parametrize("N", [168, 172, 300])
+@pytest.mark.parametrize("split", [False, True])
+def test_rowgemm_panel_split(N, split):
+    """The batch-row kernel with the panel split on and off (naz_tuning "rowgemm_split"; default on):
+    widths of 6 / 6 / 10 column blocks (an odd half-panel at 168 / 172 runs the paired epilogue's
+    guard) through every epilogue -- bias + activation (linear_act), the masked dX GEMM, the chained
+    act' (gemm_dact), the CNF pair VJP (gemm_jvp_bwd) -- on a ragged row count, against fp64."""
+    from naz_amd import ops
+    prev = ops.rowgemm_split(split)
+    try:
+        g = torch.Generator().manual_seed(N + 11 * split)
+        M = 4098
+        ctx, x = torch.randn(M, 13, generator=g), torch.randn(M, 40, generator=g)
+        W = torch.randn(N, 53, generator=g) / 53 ** 0.5
+        b = torch.randn(N, generator=g) * 0.1
+        y = ops.linear_act(_cuda(x), _cuda(W), _cuda(b), "tanh", context=_cuda(ctx))
+        inp = torch.cat([ctx, x], 1)
+        _check(y, torch.tanh(inp.double() @ W.double().t() + b.double()), torch.tanh(inp @ W.t() + b),
+               f"fwd N={N} split={split}")
+        G = torch.randn(M, 184, generator=g)
+        W2 = torch.randn(184, N, generator=g) / 13.0
+        mask = (torch.rand(184, N, generator=g) > 0.3).float()
+        dx = ops.gemm(_cuda(G), _cuda(W2), mask=_cuda(mask), mask_b=True)
+        _check(dx, G.double() @ (W2.double() * mask.double()), G @ (W2 * mask), f"dX N={N} split={split}")
+        h = torch.tanh(torch.randn(M, N, generator=g))
+        da = ops.gemm_dact(_cuda(G), _cuda(W2), _cuda(h), "tanh", mask=_cuda(mask))
+        ref64 = (G.double() @ (W2.double() * mask.double())) * (1 - h.double() ** 2)
+        _check(da, ref64, (G @ (W2 * mask)) * (1 - h * h), f"dact N={N} split={split}")
+        S = torch.tanh(torch.randn(M, N, generator=g))
+        S[1::2] = torch.randn(M // 2, N, generator=g)  # tangent rows
+        jv = ops.gemm_jvp_bwd(_cuda(G), _cuda(W2), _cuda(S), "tanh")
+        P64 = G.double() @ W2.double()
+        hv, dt = S[0::2].double(), S[1::2].double()
+        r64 = torch.empty(M, N, dtype=torch.float64)
+        r64[0::2] = P64[0::2] * (1 - hv ** 2) + P64[1::2] * dt * (-2 * hv)
+        r64[1::2] = P64[1::2] * (1 - hv ** 2)
+        P32 = G @ W2
+        r32 = torch.empty(M, N)
+        r32[0::2] = P32[0::2] * (1 - S[0::2] ** 2) + P32[1::2] * S[1::2] * (-2 * S[0::2])
+        r32[1::2] = P32[1::2] * (1 - S[0::2] ** 2)
+        _check(jv, r64, r32, f"jvp N={N} split={split}")
+    finally:
+        ops.rowgemm_split(prev)
+
+
 @pytest.mark.parametrize("M,N,K,split", [(128, 40, 50000, None), (184, 128, 4097, 7), (3, 5, 1, None),
                                          (1000, 24, 70, None), (65, 130, 200000, None)])
 def test_gemm_strided_split_k(M, N, K, split):

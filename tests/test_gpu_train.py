@@ -384,3 +384,46 @@ def test_config3_ar_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
     (flows/maf_grad_wide.py: 15 input chains per layer, a 32-wide context in the dW of W_0) -- checked
     here against the oracle's float64 autograd and the per-node walk."""
     _maf_train_vs_oracle_and_walk(monkeypatch, 16, 32, [128, 128], 3, B, ctx_rows, "composed maf D16C32")
+
+
+def test_graphed_nll_step_matches_eager_steps():
+    """trainers.GraphedNllStep (the whole NLL step -- wide maf forward kernel, the GEMM-composed
+    backward, clip, capturable Adam -- replayed as one captured HIP graph) takes the same steps as
+    eager nll_step calls: same losses and parameters after 4 steps (to the split-K reductions'
+    atomic ordering), new minibatch rows through the static buffers, and an out-of-range
+    minibatch runs eagerly."""
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    from naz_amd.trainers import DataParallel, GraphedNllStep, nll_step
+    from naz_amd.trainers.train_flows import _flow_parameters
+    spec = dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=2)
+    state = {k: v.numpy() for k, v in O.random_state(spec, seed=31).items()}
+    B = 2048
+    xs = [torch.as_tensor(O.gaussian_mixture(B, 4, seed=40 + i), device=DEV) for i in range(4)]
+    cs = [torch.as_tensor(O.context_normal(B, 2, seed=50 + i), device=DEV) for i in range(4)]
+    runs = {}
+    for graphed in (False, True):
+        f = NormalizingFlow("maf", None, 4, 2, [512] * 5, 2)
+        fio.load_state(f, state)
+        f = f.to(DEV)
+        params = _flow_parameters(f)
+        dp = DataParallel()
+        opt = torch.optim.Adam(params, lr=1e-3, capturable=graphed)
+        g = GraphedNllStep(f, opt, params, dp, B) if graphed else None
+        losses = []
+        for x, c in zip(xs, cs):
+            loss = g(x, c) if graphed else nll_step(f, x, c, opt, params, dp, B)
+            losses.append(float(loss))
+        runs[graphed] = (losses, [p.detach().clone() for p in params])
+        if graphed:
+            assert g.replays == 3 and g.eager_steps == 1
+            big = xs[0].clone()
+            big[0, 0] = 1e6  # outside the fused kernel's f16 input split: the eager walk
+            assert torch.isfinite(g(big, cs[0]))
+            assert g.eager_steps == 2 and g.replays == 3
+    le, pe = runs[False]
+    lg, pg = runs[True]
+    assert np.allclose(le, lg, rtol=1e-5, atol=1e-5), (le, lg)
+    for a, b in zip(pe, pg):
+        rel = float((a - b).norm() / a.norm().clamp_min(1e-30))
+        assert rel < 1e-5, rel

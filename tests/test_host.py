@@ -80,5 +80,11 @@ def test_pickle_whole_model():
 def test_unsupported_options_fail_loudly():
     with pytest.raises(NotImplementedError):
         NormalizingFlow("nsc", None, 4, 2, [16, 16], 2, 8, 2, use_batchnorm=True)
-    with pytest.raises(NotImplementedError):
-        NormalizingFlow("cnf", None, 4, 2, [16, 16], 2)
+    with pytest.raises(NotImplementedError):  # MC dropout in the CNF vector field
+        NormalizingFlow("cnf", None, 4, 2, [16, 16], 2, dropout_p=0.1)
+    # a CNF shape without a fused solve kernel runs the per-layer solve (flows/cnf_adjoint.py), e.g.
+    # naz's POSYDON CNF (eposydon/train_cnf_mle.py:91): it constructs, it does not fall back silently
+    f = NormalizingFlow("cnf", None, 4, 2, [16, 16], 2)
+    assert not any(t._plan.fused for t in f.transforms)
+    f = NormalizingFlow("cnf", None, 4, 5, [128] * 4, 1)
+    assert not f.transforms[0]._plan.fused

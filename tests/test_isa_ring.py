@@ -5,7 +5,7 @@ from pathlib import Path
 import pytest
 
 from tests.isa_ring import (check_library, code_objects, counted_lgkm_violations, disassemble, functions, is_dma,
-                            ring_violations)
+                            pending_lds_read_uses, ring_violations)
 
 LIB = Path(__file__).resolve().parents[1] / "naz_amd" / "lib" / "libnazhip.so"
 # the config-3 log_prob kernels (name prefixes: the parameter lists' mangling follows the signature)
@@ -83,3 +83,74 @@ def test_checker_flags_a_back_edge_without_wait():
     assert ring_violations(s, prog) == ["+0x4: s_barrier"]
     fixed = prog[:4] + [(s + 0x10, "s_waitcnt vmcnt(0) lgkmcnt(0) // 1010:")] + prog[5:]
     assert ring_violations(s, fixed) == []
+
+
+# kernels whose A-fragment reads are untracked inline asm with hand-counted waits
+UNTRACKED = ("_ZN3naz19coupling_w32_kernel", "_ZN3naz23coupling_bwd_r16_kernel", "_ZN3naz23made_ar_inv_wide_kernel",
+             "_ZN3naz18made_ar_fwd_kernel")
+
+
+def test_no_instruction_touches_a_pending_lds_read(lib):
+    """No instruction of any kernel reads or overwrites a destination register of an LDS read that an
+    s_waitcnt lgkmcnt has not retired on some path (loop back edges included): the hazard the
+    untracked reads of lds_read_b128_untracked (naz_device.h) would hit if the compiler copied,
+    spilled or re-used a prefetched fragment before its counted lds_wait.  Every kernel with LDS
+    reads is checked; the ones built on the untracked reads must be among them."""
+    bad, seen = {}, set()
+    for co in code_objects(lib):
+        for name, (start, insns) in functions(disassemble(co)).items():
+            if not any(t.startswith("ds_read") for _, t in insns):
+                continue
+            for pre in UNTRACKED:
+                if name.startswith(pre):
+                    seen.add(pre)
+            v = pending_lds_read_uses(start, insns)
+            if v:
+                bad[name] = v
+    assert seen == set(UNTRACKED), f"untracked-read kernels missing: {set(UNTRACKED) - seen}"
+    assert not bad, "registers used before their LDS read retired:\n" + "\n".join(
+        f"{k}: {v[:4]}" for k, v in bad.items())
+
+
+def test_pending_read_checker_flags_early_uses():
+    s = 0x3000
+    prog = [
+        (s + 0x0, "ds_read_b128 v[0:3], v10 // 3000:"),
+        (s + 0x4, "ds_read_b128 v[4:7], v10 offset:16 // 3004:"),
+        (s + 0x8, "s_waitcnt lgkmcnt(1) // 3008:"),
+        (s + 0xc, "v_mov_b32_e32 v20, v1 // 300C:"),  # first read retired: fine
+        (s + 0x10, "v_mfma_f32_16x16x32_f16 a[0:3], v[4:7], v[4:7], a[0:3] // 3010:"),  # second still pending
+        (s + 0x14, "s_waitcnt lgkmcnt(0) // 3014:"),
+        (s + 0x18, "v_mov_b32_e32 v21, v5 // 3018:"),
+        (s + 0x1c, "s_endpgm // 301C:"),
+    ]
+    assert pending_lds_read_uses(s, prog) == ["+0x10: v_mfma_f32_16x16x32_f16 a[0:3], v[4:7], v[4:7], a[0:3]"]
+    # an overwrite of a pending destination (the LDS return would land after it) is flagged too
+    waw = prog[:2] + [(s + 0x8, "v_mov_b32_e32 v2, 0 // 3008:")] + prog[5:]
+    assert pending_lds_read_uses(s, waw) == ["+0x8: v_mov_b32_e32 v2, 0"]
+    # a read issued at a loop's tail and used at its head through the back edge, no wait between
+    loop = [
+        (s + 0x0, "v_add_f32_e32 v8, v0, v8 // 3000:"),
+        (s + 0x4, "ds_read_b32 v0, v10 // 3004:"),
+        (s + 0x8, "s_cbranch_scc1 65533 // 3008: <k+0x0>"),
+        (s + 0xc, "s_endpgm // 300C:"),
+    ]
+    assert pending_lds_read_uses(s, loop) == ["+0x0: v_add_f32_e32 v8, v0, v8"]
+
+
+def test_pending_read_checker_catches_a_copy_in_the_w32_kernel(lib):
+    """Mutation check on the real w32 kernel: a v_mov of the newest untracked A-fragment read's
+    destination inserted just before its counted wait is flagged."""
+    for co in code_objects(lib):
+        for name, (start, insns) in functions(disassemble(co)).items():
+            if not name.startswith(UNTRACKED[0]):
+                continue
+            for k, (a, t) in enumerate(insns):
+                if t.startswith("s_waitcnt") and "lgkmcnt(2)" in t:
+                    j = max(i for i in range(k) if insns[i][1].startswith("ds_read_b128"))
+                    reg = insns[j][1].split()[1].split(",")[0]  # v[n:m]
+                    first = int(reg[2:].split(":")[0])
+                    mutated = insns[:k] + [(a - 2, f"v_mov_b32_e32 v255, v{first} // {a - 2:X}:")] + insns[k:]
+                    assert any("v255" in x for x in pending_lds_read_uses(start, mutated))
+                    return
+    pytest.fail("no counted lgkmcnt(2) wait found in the w32 kernel")

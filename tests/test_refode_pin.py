@@ -14,7 +14,7 @@ import torch
 from oracle import naz_oracle as O
 from tests.conftest import load_golden, spec_state
 
-NAMES = ["cnf_refode_d4c2.npz", "cnf_refode_d16c0.npz"]
+NAMES = ["cnf_refode_d4c2.npz", "cnf_refode_d16c0.npz", "cnf_refode_d4c4_h128x4.npz"]
 
 
 def _net_inputs(fx):

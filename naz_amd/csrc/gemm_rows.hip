@@ -85,12 +85,123 @@ struct RowGemmArgs {
   // host-side launch choice (rowgemm()): outputs of more than 4 column blocks in half-width panels
   // (1), in one panel (0), or the library's setting (-1: naz_tuning "rowgemm_split")
   int split = -1;
+  // arithmetic (rowgemm()): exact FP32 MFMA (0), bf16x6 (1: rowgemm_x6_kernel), or the library's
+  // setting (-1: naz_tuning "rowgemm_x6")
+  int x6 = -1;
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
 NAZ_DEV float rg_a(const RowGemmArgs& p, int64_t m, int k) {
   if (k < p.ka0) return p.a0[m * p.lda0 + k];
   return p.a1[m * p.lda1 + (k - p.ka0)];
+}
+
+// The batch-row GEMM's epilogue (shared by rowgemm_kernel and rowgemm_x6_kernel): accumulator
+// (block o, reg r) = C[row, col] with row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) of the wave's 32 rows
+// and col = 32 o + (lane & 31) of the panel; bias + activation, the chained act' (dy), the CNF pair
+// VJP (jvp) or accumulation, staged through SHARE floats of LDS per wave into 16-byte row pieces
+template <int NB, int SHARE>
+NAZ_DEV void rowgemm_epilogue(const RowGemmArgs& p, floatx16 (&acc)[NB], float* smem, int64_t m0, int n0, int wave,
+                              int lane) {
+  if (p.vst) {
+    // staged through this wave's share of the (now free) LDS: EG blocks at a time are written
+    // [32 rows][32 EG cols] and stored back as whole 16-byte row pieces
+    constexpr int EG = SHARE >= 32 * (64 + 4) ? 2 : 1;
+    constexpr int EP = 32 * EG + 4;  // pitch
+    float* E = smem + wave * SHARE;
+#pragma unroll
+    for (int o0 = 0; o0 < NB; o0 += EG) {
+#pragma unroll
+      for (int oo = 0; oo < EG; ++oo) {
+        if (o0 + oo >= NB) continue;
+        const int n = n0 + 32 * (o0 + oo) + (lane & 31);
+        const float bn = (p.bias != nullptr && n < p.N) ? p.bias[n] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          E[row * EP + 32 * oo + (lane & 31)] = activate_rt(p.act, acc[o0 + oo][r] + bn);
+        }
+      }
+      // 8 EG float4 per row; 64 / (8 EG) rows per wave-instruction
+      constexpr int F4R = 8 * EG, RPI = 64 / F4R;
+      const int rr = lane / F4R, c4 = lane % F4R;
+      const int col = n0 + 32 * o0 + 4 * c4;
+      const bool inpanel = 32 * o0 + 4 * c4 < 32 * NB;  // odd NB, EG = 2: the pair's second block is absent
+      if (p.jvp != nullptr) {  // naz_gemm_jvp_bwd: RPI (value, tangent) row pairs per wave-instruction
+#pragma unroll
+        for (int it = 0; it < 16 / RPI; ++it) {
+          const int pr = it * RPI + rr;
+          const int64_t m = m0 + wave * 32 + 2 * pr;  // value row; m + 1 = its tangent row (M is even)
+          if (m >= p.M || col >= p.N || !inpanel) continue;
+          const float* ev = E + (2 * pr) * EP + 4 * c4;
+          const float* sv = p.jvp + m * p.ldjvp + col;
+          float* cv = p.c + m * p.ldc + col;
+          const int nt = p.N - col < 4 ? p.N - col : 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (j >= nt) continue;
+            float d1, rat;
+            act_d1_ratio(p.jact, sv[j], d1, rat);
+            const float gv = ev[j], gt = ev[EP + j];
+            cv[j] = gv * d1 + gt * sv[p.ldjvp + j] * rat;
+            cv[p.ldc + j] = gt * d1;
+          }
+        }
+        continue;
+      }
+#pragma unroll
+      for (int it = 0; it < 32 / RPI; ++it) {
+        const int row = it * RPI + rr;
+        const int64_t m = m0 + wave * 32 + row;
+        if (m >= p.M || col >= p.N || !inpanel) continue;
+        float4 v = *reinterpret_cast<const float4*>(E + row * EP + 4 * c4);
+        if (p.dy != nullptr) {  // chained act' (naz_gemm_dact), applied on the 16-byte row piece
+          const float* dyr = p.dy + m * p.lddy + col;
+          if (p.dyvec && col + 4 <= p.N) {  // one 16-byte load of the row piece
+            const float4 d4 = *reinterpret_cast<const float4*>(dyr);
+            v.x *= activate_grad_from_out(p.dact, d4.x);
+            v.y *= activate_grad_from_out(p.dact, d4.y);
+            v.z *= activate_grad_from_out(p.dact, d4.z);
+            v.w *= activate_grad_from_out(p.dact, d4.w);
+          } else {
+            v.x *= activate_grad_from_out(p.dact, dyr[0]);
+            if (col + 1 < p.N) v.y *= activate_grad_from_out(p.dact, dyr[1]);
+            if (col + 2 < p.N) v.z *= activate_grad_from_out(p.dact, dyr[2]);
+            if (col + 3 < p.N) v.w *= activate_grad_from_out(p.dact, dyr[3]);
+          }
+        }
+        if (col + 4 <= p.N) {
+          float4* dst = reinterpret_cast<float4*>(p.c + m * p.ldc + col);
+          if (p.accumulate) {
+            const float4 o = *dst;
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *dst = v;
+        } else {  // row tail (N % 4 != 0): only the real columns (static indices: no scratch)
+          float* d1 = p.c + m * p.ldc + col;
+          const int nt = p.N - col;
+          d1[0] = p.accumulate ? d1[0] + v.x : v.x;
+          if (nt > 1) d1[1] = p.accumulate ? d1[1] + v.y : v.y;
+          if (nt > 2) d1[2] = p.accumulate ? d1[2] + v.z : v.z;
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int o = 0; o < NB; ++o) {
+    const int n = n0 + 32 * o + (lane & 31);
+    if (n >= p.N) continue;
+    const float bn = p.bias != nullptr ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m >= p.M) continue;
+      float* dst = p.c + m * p.ldc + n;
+      const float v = activate_rt(p.act, acc[o][r] + bn);  // (dy: vst path only, see rowgemm_dact)
+      *dst = p.accumulate ? *dst + v : v;
+    }
+  }
 }
 
 #ifndef NAZ_RG_OCC
@@ -195,107 +306,7 @@ __global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel
     __syncthreads();
   }
 
-  // epilogue: accumulator (block o, reg r) = C[row, col]
-  if (p.vst) {
-    // staged through this wave's share of the (now free) LDS: EG blocks at a time are written
-    // [32 rows][32 EG cols] and stored back as whole 16-byte row pieces
-    constexpr int SHARE = (AS_F + BS_F) / (RG_T / 64);
-    constexpr int EG = SHARE >= 32 * (64 + 4) ? 2 : 1;
-    constexpr int EP = 32 * EG + 4;  // pitch
-    float* E = smem + wave * SHARE;
-#pragma unroll
-    for (int o0 = 0; o0 < NB; o0 += EG) {
-#pragma unroll
-      for (int oo = 0; oo < EG; ++oo) {
-        if (o0 + oo >= NB) continue;
-        const int n = n0 + 32 * (o0 + oo) + (lane & 31);
-        const float bn = (p.bias != nullptr && n < p.N) ? p.bias[n] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          E[row * EP + 32 * oo + (lane & 31)] = activate_rt(p.act, acc[o0 + oo][r] + bn);
-        }
-      }
-      // 8 EG float4 per row; 64 / (8 EG) rows per wave-instruction
-      constexpr int F4R = 8 * EG, RPI = 64 / F4R;
-      const int rr = lane / F4R, c4 = lane % F4R;
-      const int col = n0 + 32 * o0 + 4 * c4;
-      const bool inpanel = 32 * o0 + 4 * c4 < 32 * NB;  // odd NB, EG = 2: the pair's second block is absent
-      if (p.jvp != nullptr) {  // naz_gemm_jvp_bwd: RPI (value, tangent) row pairs per wave-instruction
-#pragma unroll
-        for (int it = 0; it < 16 / RPI; ++it) {
-          const int pr = it * RPI + rr;
-          const int64_t m = m0 + wave * 32 + 2 * pr;  // value row; m + 1 = its tangent row (M is even)
-          if (m >= p.M || col >= p.N || !inpanel) continue;
-          const float* ev = E + (2 * pr) * EP + 4 * c4;
-          const float* sv = p.jvp + m * p.ldjvp + col;
-          float* cv = p.c + m * p.ldc + col;
-          const int nt = p.N - col < 4 ? p.N - col : 4;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (j >= nt) continue;
-            float d1, rat;
-            act_d1_ratio(p.jact, sv[j], d1, rat);
-            const float gv = ev[j], gt = ev[EP + j];
-            cv[j] = gv * d1 + gt * sv[p.ldjvp + j] * rat;
-            cv[p.ldc + j] = gt * d1;
-          }
-        }
-        continue;
-      }
-#pragma unroll
-      for (int it = 0; it < 32 / RPI; ++it) {
-        const int row = it * RPI + rr;
-        const int64_t m = m0 + wave * 32 + row;
-        if (m >= p.M || col >= p.N || !inpanel) continue;
-        float4 v = *reinterpret_cast<const float4*>(E + row * EP + 4 * c4);
-        if (p.dy != nullptr) {  // chained act' (naz_gemm_dact), applied on the 16-byte row piece
-          const float* dyr = p.dy + m * p.lddy + col;
-          if (p.dyvec && col + 4 <= p.N) {  // one 16-byte load of the row piece
-            const float4 d4 = *reinterpret_cast<const float4*>(dyr);
-            v.x *= activate_grad_from_out(p.dact, d4.x);
-            v.y *= activate_grad_from_out(p.dact, d4.y);
-            v.z *= activate_grad_from_out(p.dact, d4.z);
-            v.w *= activate_grad_from_out(p.dact, d4.w);
-          } else {
-            v.x *= activate_grad_from_out(p.dact, dyr[0]);
-            if (col + 1 < p.N) v.y *= activate_grad_from_out(p.dact, dyr[1]);
-            if (col + 2 < p.N) v.z *= activate_grad_from_out(p.dact, dyr[2]);
-            if (col + 3 < p.N) v.w *= activate_grad_from_out(p.dact, dyr[3]);
-          }
-        }
-        if (col + 4 <= p.N) {
-          float4* dst = reinterpret_cast<float4*>(p.c + m * p.ldc + col);
-          if (p.accumulate) {
-            const float4 o = *dst;
-            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
-          }
-          *dst = v;
-        } else {  // row tail (N % 4 != 0): only the real columns (static indices: no scratch)
-          float* d1 = p.c + m * p.ldc + col;
-          const int nt = p.N - col;
-          d1[0] = p.accumulate ? d1[0] + v.x : v.x;
-          if (nt > 1) d1[1] = p.accumulate ? d1[1] + v.y : v.y;
-          if (nt > 2) d1[2] = p.accumulate ? d1[2] + v.z : v.z;
-        }
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int o = 0; o < NB; ++o) {
-    const int n = n0 + 32 * o + (lane & 31);
-    if (n >= p.N) continue;
-    const float bn = p.bias != nullptr ? p.bias[n] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (m >= p.M) continue;
-      float* dst = p.c + m * p.ldc + n;
-      const float v = activate_rt(p.act, acc[o][r] + bn);  // (dy: vst path only, see rowgemm_dact)
-      *dst = p.accumulate ? *dst + v : v;
-    }
-  }
+  rowgemm_epilogue<NB, (AS_F + BS_F) / (RG_T / 64)>(p, acc, smem, m0, n0, wave, lane);
 }
 
 template <int NB>
@@ -311,6 +322,15 @@ static bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) =
 // the library-wide panel-split setting (naz_tuning "rowgemm_split"): NAZ_RG_SPLIT at first use, else
 // on (round 5 same-box A/B of the wide maf NLL step); v >= 0 sets it; returns the
 // setting before the call
+int rowgemm_x6_setting(int v) {
+  // NAZ_RG_X6 at first use, else off until a same-box A/B sets the default
+  static std::atomic<int> cur{[] {
+    const char* e = getenv("NAZ_RG_X6");
+    return e ? (atoi(e) != 0 ? 1 : 0) : 0;
+  }()};
+  return v >= 0 ? cur.exchange(v != 0 ? 1 : 0) : cur.load();
+}
+
 int rowgemm_split_setting(int v) {
   static std::atomic<int> cur{[] {
     const char* e = getenv("NAZ_RG_SPLIT");
@@ -320,6 +340,8 @@ int rowgemm_split_setting(int v) {
 }
 
 namespace {
+
+int rowgemm_x6_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s);  // below
 
 int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   if (p.M <= 0 || p.N <= 0 || nz <= 0) return 0;
@@ -344,6 +366,9 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   // N = 168 / 172 / 300 with the split on and off against fp64.
   const int split = p.split >= 0 ? p.split : rowgemm_split_setting(-1);
   if (split && nb > 4) nb = (nb + 1) / 2;
+  // the bf16x6 form where the batch is long enough to fill the chip and k deep enough to pay the split
+  const int x6 = p.x6 >= 0 ? p.x6 : rowgemm_x6_setting(-1);
+  if (x6 && K >= 32 && p.M >= 2048) return rowgemm_x6_dispatch(p, nz, nb, s);
   switch (nb > 8 ? 8 : nb) {
     case 1: rowgemm_launch<1>(p, nz, s); break;
     case 2: rowgemm_launch<2>(p, nz, s); break;
@@ -826,6 +851,161 @@ NAZ_DEV floatx4w wg_mfma6(const WgFrag3& a, const WgFrag3& b, floatx4w c) {
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.h, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.m, c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// rowgemm_x6_kernel: the batch-row GEMM on the bf16 matrix pipe (naz_tuning "rowgemm_x6").  The same
+// C = epi(A · B) as rowgemm_kernel, with every A and B value split EXACTLY into three bf16 pieces by
+// truncation (wg_split8) and C += the six largest piece products on v_mfma_f32_32x32x16_bf16 (fp32
+// accumulate; the dropped ml, lm, ll terms are <= 2^-24 relative, no range limit: fp32-grade at
+// 2.67x the FP32 MFMA rate).  16-k chunks.  Wave w of the 128-row panel owns rows 32 w .. 32 w + 31
+// and reads its A values straight into registers, one chunk ahead (lane (i, kh): row i, k 8 kh ..
+// 8 kh + 7 of the chunk — the MFMA's A layout).  The workgroup splits each B chunk once into LDS in
+// the MFMA's B layout ([32-column block][piece][lane][8 bf16], one 16-byte read per piece), double
+// buffered, one barrier per chunk; the epilogue is rowgemm_kernel's.
+NAZ_DEV floatx16 rg_mfma6(const WgFrag3& a, const WgFrag3& b, floatx16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);  // small terms first
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, c, 0, 0, 0);
+}
+
+constexpr int RX_SHARE = 32 * (64 + 4);  // epilogue staging per wave (two 32-column blocks at a time)
+
+template <int NB>
+__global__ void __launch_bounds__(RG_T, NB <= 2 ? 4 : (NB <= 4 ? 3 : 2)) rowgemm_x6_kernel(RowGemmArgs p) {
+  {  // problem of this z slice (uniform: stays in SGPRs)
+    const int64_t z = blockIdx.z;
+    p.a0 += z * p.za0;
+    p.a1 += z * p.za1;
+    p.b += z * p.zb;
+    if (p.bias != nullptr) p.bias += z * p.zbias;
+    p.c += z * p.zc;
+  }
+  constexpr int BN = 32 * NB;
+  constexpr int BSLOT = NB * 3 * 64 * 4;  // u32 words of one B chunk: [NB][piece][64 lanes][4]
+  constexpr int SMEM = 2 * BSLOT > 4 * RX_SHARE ? 2 * BSLOT : 4 * RX_SHARE;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  unsigned* const bsm = reinterpret_cast<unsigned*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kh = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * RG_BM;
+  const int n0 = blockIdx.y * BN;
+  const int K = p.ka0 + p.ka1;
+  const int nk = (K + 15) / 16;
+  const int64_t am = m0 + wave * 32 + (lane & 31);
+  const bool arow = am < p.M;
+
+  // A: this lane's 8 k values of the chunk (one segment: ka0 % 8 == 0 or the group inside one)
+  auto load_a = [&](int kc, float (&v)[8]) {
+    const int kb = 16 * kc + 8 * kh;
+    if (p.vec && arow && kb + 8 <= K && (kb >= p.ka0 || kb + 8 <= p.ka0)) {
+      const float* src = kb < p.ka0 ? p.a0 + am * p.lda0 + kb : p.a1 + am * p.lda1 + (kb - p.ka0);
+      const float4 v0 = *reinterpret_cast<const float4*>(src);
+      const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+      v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+      v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (arow && kb + e < K) ? rg_a(p, am, kb + e) : 0.f;
+    }
+  };
+  // B: thread -> fragment fr = (column block fr >> 6, lane fr & 63: column lane & 31, k-half lane >> 5)
+  const auto bsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), (short)0, 0x7fffffff, 0x00020000);
+  const auto msrd =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.mask ? p.mask : p.b), (short)0, 0x7fffffff, 0x00020000);
+  const int sbk = (int)p.sbk, sbn = (int)p.sbn, smk = (int)p.smk, smn = (int)p.smn;
+  constexpr int FR = 64 * NB;  // B fragments per chunk
+  constexpr int FPT = (FR + RG_T - 1) / RG_T;
+  float rb[FPT][8];
+  auto load_b = [&](int kc) {
+#pragma unroll
+    for (int f = 0; f < FPT; ++f) {
+      const int fr = tid + RG_T * f, fl = fr & 63, n = n0 + 32 * (fr >> 6) + (fl & 31);
+      const int kb = 16 * kc + 8 * (fl >> 5);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = 0.f;
+        if (fr < FR && kb + e < K && n < p.N) {
+          v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bsrd, 4 * ((kb + e) * sbk + n * sbn), 0, 0));
+          if (p.mask != nullptr)
+            v *= __builtin_bit_cast(float,
+                                    __builtin_amdgcn_raw_buffer_load_b32(msrd, 4 * ((kb + e) * smk + n * smn), 0, 0));
+        }
+        rb[f][e] = v;
+      }
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int f = 0; f < FPT; ++f) {
+      const int fr = tid + RG_T * f;
+      if (fr < FR) {
+        const WgFrag3 q = wg_split8(rb[f]);
+        wg_u32x4* d = reinterpret_cast<wg_u32x4*>(bsm + buf * BSLOT) + (fr >> 6) * 3 * 64 + (fr & 63);
+        d[0] = __builtin_bit_cast(wg_u32x4, q.h);
+        d[64] = __builtin_bit_cast(wg_u32x4, q.m);
+        d[128] = __builtin_bit_cast(wg_u32x4, q.l);
+      }
+    }
+  };
+
+  floatx16 acc[NB];
+#pragma unroll
+  for (int o = 0; o < NB; ++o)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[o][r] = 0.f;
+
+  float va[8];
+  load_a(0, va);
+  load_b(0);
+  store_b(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    float vn[8];
+    if (kc + 1 < nk) {  // in flight during this chunk's MFMAs
+      load_a(kc + 1, vn);
+      load_b(kc + 1);
+    }
+    const WgFrag3 a = wg_split8(va);
+    const wg_u32x4* bp = reinterpret_cast<const wg_u32x4*>(bsm + buf * BSLOT) + lane;
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const WgFrag3 b{__builtin_bit_cast(wg_bf16x8, bp[(o * 3 + 0) * 64]),
+                      __builtin_bit_cast(wg_bf16x8, bp[(o * 3 + 1) * 64]),
+                      __builtin_bit_cast(wg_bf16x8, bp[(o * 3 + 2) * 64])};
+      acc[o] = rg_mfma6(a, b, acc[o]);
+    }
+    if (kc + 1 < nk) {
+      store_b(buf ^ 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) va[e] = vn[e];
+    }
+    __syncthreads();
+  }
+  rowgemm_epilogue<NB, RX_SHARE>(p, acc, smem, m0, n0, wave, lane);
+}
+
+template <int NB>
+void rowgemm_x6_launch(const RowGemmArgs& p, int nz, hipStream_t s) {
+  dim3 grid((unsigned)((p.M + RG_BM - 1) / RG_BM), (unsigned)((p.N + 32 * NB - 1) / (32 * NB)), (unsigned)nz);
+  hipLaunchKernelGGL(rowgemm_x6_kernel<NB>, grid, dim3(RG_T), 0, s, p);
+}
+
+int rowgemm_x6_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s) {
+  switch (nb > 8 ? 8 : nb) {
+    case 1: rowgemm_x6_launch<1>(p, nz, s); break;
+    case 2: rowgemm_x6_launch<2>(p, nz, s); break;
+    case 3: rowgemm_x6_launch<3>(p, nz, s); break;
+    case 4: rowgemm_x6_launch<4>(p, nz, s); break;
+    case 5: rowgemm_x6_launch<5>(p, nz, s); break;
+    case 6: rowgemm_x6_launch<6>(p, nz, s); break;
+    case 7: rowgemm_x6_launch<7>(p, nz, s); break;
+    default: rowgemm_x6_launch<8>(p, nz, s); break;
+  }
+  return check_launch("rowgemm_x6_kernel");
 }
 
 template <int NOW, int NB2, int JS>

@@ -144,6 +144,8 @@ int wgrad_batched(int64_t M, int N1, int N2, int nbatch, const float* g, int64_t
 int write_image_headers(void* base, int64_t stride_bytes, int64_t P, const uint32_t* words, int nwords, hipStream_t s);
 // gemm_rows.hip: the batch-row GEMM's panel-split setting (v >= 0 sets; returns the previous value)
 int rowgemm_split_setting(int v);
+// ... and its arithmetic: exact FP32 MFMA (0) or the bf16x6 split (1, rowgemm_x6_kernel)
+int rowgemm_x6_setting(int v);
 int rowgemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
                     const float* S, int64_t lds, int act, int64_t M, int N, hipStream_t s);
 

@@ -100,6 +100,16 @@ def track_image(img: Tensor) -> Tensor:
     return img
 
 
+def rowgemm_x6(value: Optional[bool] = None) -> bool:
+    """The batch-row GEMM's arithmetic (naz_tuning "rowgemm_x6"): exact FP32 MFMA (False) or the
+    exact bf16x6 split on the bf16 matrix pipe (True; fp32-grade, 2.67x the FP32 MFMA rate).
+    ``value`` sets it; returns the setting before."""
+    r = int(lib().naz_tuning(b"rowgemm_x6", -1 if value is None else int(bool(value))))
+    if r < 0:
+        check(r, "rowgemm_x6")
+    return bool(r)
+
+
 def attach_image(img: Tensor, what: str) -> Tensor:
     """Register a host-packed image copied to the device (naz_image_attach reads its header once)."""
     check(lib().naz_image_attach(_p(img), img.numel() * img.element_size(), _stream(img.device)), what)

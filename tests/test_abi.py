@@ -219,3 +219,16 @@ def test_host_packed_image_headers():
     d3 = ops.ar_flow_desc("maf", 2, 2, 150, 4, 3)
     d3.flags = 1  # the backward's clip semantics do not change the layout
     assert header(d3, False)[1][3] == h[3]
+
+
+def test_tuning_keys():
+    """naz_tuning: the batch-row GEMM's panel split (default on) and arithmetic (default exact FP32),
+    set and read back; an unknown key is an error."""
+    from naz_amd import _lib
+    L = _lib.lib()
+    for key, default in ((b"rowgemm_split", 1), (b"rowgemm_x6", 0)):
+        cur = L.naz_tuning(key, -1)
+        assert cur in (0, 1)
+        assert L.naz_tuning(key, 1 - cur) == cur and L.naz_tuning(key, -1) == 1 - cur
+        assert L.naz_tuning(key, cur) == 1 - cur and L.naz_tuning(key, -1) == cur
+    assert L.naz_tuning(b"no_such_key", 1) == -1 and b"unknown key" in L.naz_last_error()

@@ -169,13 +169,16 @@ def test_rowgemm_config3_shapes():
 
 @pytest.mark.parametrize("N", [168, 172, 300])
 @pytest.mark.parametrize("split", [False, True])
-def test_rowgemm_panel_split(N, split):
+@pytest.mark.parametrize("x6", [False, True])
+def test_rowgemm_panel_split(N, split, x6):
     """The batch-row kernel with the panel split on and off (naz_tuning "rowgemm_split"; default on):
     widths of 6 / 6 / 10 column blocks (an odd half-panel at 168 / 172 runs the paired epilogue's
     guard) through every epilogue -- bias + activation (linear_act), the masked dX GEMM, the chained
-    act' (gemm_dact), the CNF pair VJP (gemm_jvp_bwd) -- on a ragged row count, against fp64."""
+    act' (gemm_dact), the CNF pair VJP (gemm_jvp_bwd) -- on a ragged row count, against fp64; on both
+    arithmetics (naz_tuning "rowgemm_x6": exact FP32 MFMA, or the bf16x6 split)."""
     from naz_amd import ops
     prev = ops.rowgemm_split(split)
+    prev6 = ops.rowgemm_x6(x6)
     try:
         g = torch.Generator().manual_seed(N + 11 * split)
         M = 4098
@@ -210,6 +213,7 @@ def test_rowgemm_panel_split(N, split):
         _check(jv, r64, r32, f"jvp N={N} split={split}")
     finally:
         ops.rowgemm_split(prev)
+        ops.rowgemm_x6(prev6)
 
 
 @pytest.mark.parametrize("M,N,K,split", [(128, 40, 50000, None), (184, 128, 4097, 7), (3, 5, 1, None),

@@ -1,4 +1,6 @@
 // Small row-wise kernels on the flow path.
+#include <atomic>
+
 #include "naz_device.h"
 #include "naz_internal.h"
 
@@ -258,6 +260,18 @@ int write_image_headers(void* base, int64_t stride_bytes, int64_t P, const uint3
   hipLaunchKernelGGL(image_header_kernel, dim3((unsigned)P), dim3(64), 0, s, static_cast<uint32_t*>(base),
                      stride_bytes / 4, h, nwords);
   return check_launch("image_header_kernel");
+}
+
+int device_cus() {
+  static std::atomic<int> cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = cached[dev].load();
+  if (n == 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev].store(n);
+  }
+  return n;
 }
 
 }  // namespace naz

@@ -88,6 +88,9 @@ struct RowGemmArgs {
   // arithmetic (rowgemm()): exact FP32 MFMA (0), bf16x6 (1: rowgemm_x6_kernel), or the library's
   // setting (-1: naz_tuning "rowgemm_x6")
   int x6 = -1;
+  // small batches: narrow the column panels until the grid holds this many workgroups per CU
+  // (0: off, -1: the library's setting, naz_tuning "rowgemm_fill")
+  int fill = -1;
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -331,6 +334,16 @@ int rowgemm_x6_setting(int v) {
   return v >= 0 ? cur.exchange(v != 0 ? 1 : 0) : cur.load();
 }
 
+int rowgemm_fill_setting(int v) {
+  // NAZ_RG_FILL at first use, else 2 workgroups (= waves per SIMD) per CU
+  static std::atomic<int> cur{[] {
+    const char* e = getenv("NAZ_RG_FILL");
+    const int f = e ? atoi(e) : 2;
+    return f < 0 ? 0 : (f > 16 ? 16 : f);
+  }()};
+  return v >= 0 ? cur.exchange(v > 16 ? 16 : v) : cur.load();
+}
+
 int rowgemm_split_setting(int v) {
   static std::atomic<int> cur{[] {
     const char* e = getenv("NAZ_RG_SPLIT");
@@ -366,6 +379,16 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   // N = 168 / 172 / 300 with the split on and off against fp64.
   const int split = p.split >= 0 ? p.split : rowgemm_split_setting(-1);
   if (split && nb > 4) nb = (nb + 1) / 2;
+  // grid fill: at naz's 10,752-row minibatch a 128-row panel grid is 84 workgroups tall, so the wide
+  // maf's 512-unit layers ran 168 workgroups (one wave on two of three SIMDs).  Narrower column
+  // panels (nb halved, down to one 32-column block) until the grid holds `fill` workgroups per CU:
+  // A panels are re-read once per column panel, from L2.
+  const int fill = p.fill >= 0 ? p.fill : rowgemm_fill_setting(-1);
+  if (fill > 0) {
+    const int64_t target = (int64_t)fill * device_cus();
+    const int64_t gx = (p.M + RG_BM - 1) / RG_BM * nz;
+    while (nb > 1 && gx * ((p.N + 32 * (nb > 8 ? 8 : nb) - 1) / (32 * (nb > 8 ? 8 : nb))) < target) nb = (nb + 1) / 2;
+  }
   // the bf16x6 form where the batch is long enough to fill the chip and k deep enough to pay the split
   const int x6 = p.x6 >= 0 ? p.x6 : rowgemm_x6_setting(-1);
   if (x6 && K >= 32 && p.M >= 2048) return rowgemm_x6_dispatch(p, nz, nb, s);

@@ -146,6 +146,10 @@ int write_image_headers(void* base, int64_t stride_bytes, int64_t P, const uint3
 int rowgemm_split_setting(int v);
 // ... and its arithmetic: exact FP32 MFMA (0) or the bf16x6 split (1, rowgemm_x6_kernel)
 int rowgemm_x6_setting(int v);
+// ... and its small-batch grid fill: column panels narrowed to reach v workgroups per CU (0 = off)
+int rowgemm_fill_setting(int v);
+// elementwise.hip: compute units of the current device (cached per device)
+int device_cus();
 int rowgemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,
                     const float* S, int64_t lds, int act, int64_t M, int N, hipStream_t s);
 

@@ -87,6 +87,16 @@ def rowgemm_split(value: Optional[bool] = None) -> bool:
     return bool(r)
 
 
+def rowgemm_fill(value: Optional[int] = None) -> int:
+    """The batch-row GEMM's small-batch grid fill (naz_tuning "rowgemm_fill": column panels narrowed
+    until the grid holds ``value`` workgroups per CU, 0 = off; no result changes).  Returns the
+    setting before."""
+    r = int(lib().naz_tuning(b"rowgemm_fill", -1 if value is None else int(value)))
+    if r < 0:
+        check(r, "rowgemm_fill")
+    return r
+
+
 def _release_image(ptr: int) -> None:
     lib().naz_image_release(ptr)  # (an image packed over it since has replaced the record: no-op)
 

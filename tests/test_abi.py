@@ -222,8 +222,8 @@ def test_host_packed_image_headers():
 
 
 def test_tuning_keys():
-    """naz_tuning: the batch-row GEMM's panel split (default on) and arithmetic (default exact FP32),
-    set and read back; an unknown key is an error."""
+    """naz_tuning: the batch-row GEMM's panel split (default on), arithmetic (default exact FP32) and
+    small-batch grid fill (clamped to 16), set and read back; an unknown key is an error."""
     from naz_amd import _lib
     L = _lib.lib()
     for key, default in ((b"rowgemm_split", 1), (b"rowgemm_x6", 0)):
@@ -231,4 +231,8 @@ def test_tuning_keys():
         assert cur in (0, 1)
         assert L.naz_tuning(key, 1 - cur) == cur and L.naz_tuning(key, -1) == 1 - cur
         assert L.naz_tuning(key, cur) == 1 - cur and L.naz_tuning(key, -1) == cur
+    cur = L.naz_tuning(b"rowgemm_fill", -1)  # workgroups per CU the small-batch narrowing aims for
+    assert 0 <= cur <= 16
+    assert L.naz_tuning(b"rowgemm_fill", 4) == cur and L.naz_tuning(b"rowgemm_fill", 99) == 4
+    assert L.naz_tuning(b"rowgemm_fill", cur) == 16 and L.naz_tuning(b"rowgemm_fill", -1) == cur
     assert L.naz_tuning(b"no_such_key", 1) == -1 and b"unknown key" in L.naz_last_error()

@@ -179,6 +179,7 @@ def test_rowgemm_panel_split(N, split, x6):
     from naz_amd import ops
     prev = ops.rowgemm_split(split)
     prev6 = ops.rowgemm_x6(x6)
+    prevf = ops.rowgemm_fill(0)  # the panels as the split sets them (4098 rows would be narrowed)
     try:
         g = torch.Generator().manual_seed(N + 11 * split)
         M = 4098
@@ -214,6 +215,41 @@ def test_rowgemm_panel_split(N, split, x6):
     finally:
         ops.rowgemm_split(prev)
         ops.rowgemm_x6(prev6)
+        ops.rowgemm_fill(prevf)
+
+
+@pytest.mark.parametrize("M,N", [(10752, 512), (10752, 172), (1000, 300), (70000, 512)])
+def test_rowgemm_fill_changes_no_bit(M, N):
+    """The small-batch grid fill (naz_tuning "rowgemm_fill": column panels narrowed until the grid
+    holds that many workgroups per CU) only regroups output columns into workgroups; each output's
+    k-order is the same, so every epilogue -- bias + activation, the masked dX GEMM, the chained act',
+    the CNF pair VJP -- is bit-identical with it off, at the default and at 16.  The first shape is the
+    wide maf at naz's 10,752-row minibatch."""
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(M + N)
+    ctx, x = torch.randn(M, 2, generator=g), torch.randn(M, 40, generator=g)
+    W = torch.randn(N, 42, generator=g) / 42 ** 0.5
+    b = torch.randn(N, generator=g) * 0.1
+    G = torch.randn(M, 184, generator=g)
+    W2 = torch.randn(184, N, generator=g) / 13.0
+    mask = (torch.rand(184, N, generator=g) > 0.3).float()
+    h = torch.tanh(torch.randn(M, N, generator=g))
+    outs = {}
+    prev = ops.rowgemm_fill()
+    try:
+        for fill in (0, prev, 16):
+            ops.rowgemm_fill(fill)
+            outs[fill] = (ops.linear_act(_cuda(x), _cuda(W), _cuda(b), "tanh", context=_cuda(ctx)),
+                          ops.gemm(_cuda(G), _cuda(W2), mask=_cuda(mask), mask_b=True),
+                          ops.gemm_dact(_cuda(G), _cuda(W2), _cuda(h), "tanh", mask=_cuda(mask)),
+                          ops.gemm_jvp_bwd(_cuda(G), _cuda(W2), _cuda(h), "tanh"))
+    finally:
+        ops.rowgemm_fill(prev)
+    ref64 = torch.tanh(torch.cat([ctx, x], 1).double() @ W.double().t() + b.double())
+    _check(outs[0][0], ref64, torch.tanh(torch.cat([ctx, x], 1) @ W.t() + b), f"fwd M={M} N={N}")
+    for fill in (prev, 16):
+        for name, a, c in zip(("fwd", "dX", "dact", "jvp"), outs[0], outs[fill]):
+            assert torch.equal(a, c), f"{name} M={M} N={N}: fill {fill} changed bits"
 
 
 @pytest.mark.parametrize("M,N,K,split", [(128, 40, 50000, None), (184, 128, 4097, 7), (3, 5, 1, None),

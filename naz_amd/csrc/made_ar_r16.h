@@ -163,6 +163,11 @@ struct CfgAR {
     int sfl[128];      // floats of stage s (padded)
     int nstg, stg;
   };
+#ifdef NAZ_AR_INV_SPAN
+  static constexpr bool SPAN = true;
+#else
+  static constexpr bool SPAN = false;
+#endif
   static constexpr int E_of(const Layout& y, int p) { return p < 0 ? 0 : y.E[p]; }
   static constexpr int blo_of(const Layout& y, int p) { return E_of(y, p - 1) >> 4; }
   static constexpr int bhi_of(const Layout& y, int p) {
@@ -183,13 +188,15 @@ struct CfgAR {
     int cnt[32] = {};
     for (int u = 0; u < H; ++u) ++cnt[deg(u) < 0 ? 0 : deg(u)];
     for (int p = 0, run = 0; p < D; ++p) y.E[p] = run += cnt[p];
-    // greedy grouping of each pass's sub-layers into stages of <= kARCap floats
-    int s = -1;
+    // greedy grouping of the sub-layers into stages of <= kARCap floats: per pass, or (SPAN) across
+    // passes from pass 1 on — fewer ring barriers, and the waves of a workgroup drift apart by up to
+    // a stage's passes, so one wave's spline overlaps another's MFMA chain (pass 0 keeps stages of
+    // its own: the pass-0-constant images stream only their constants)
+    int s = -1, run = 0;
     for (int p = 0; p < D; ++p) {
-      int run = 0;
       for (int i = 0; i <= NHID; ++i) {
         const int sz = sub_floats_of(y, p, i);
-        if (i == 0 || run + sz > NAZ_AR_INV_CAP) {
+        if ((i == 0 && (!SPAN || p <= 1)) || run + sz > NAZ_AR_INV_CAP) {
           ++s;
           run = 0;
         }
@@ -514,6 +521,9 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
       // pass constants bound to constexpr locals (a constexpr function in a loop bound or argument
       // is not folded reliably: the loops then stay rolled and the fragments go to scratch)
       constexpr int NBP = CF::nb(p), BLO = CF::blo(p), KT = CF::kt(p);
+      // (no instruction moves across a pass boundary: with stages spanning passes the scheduler
+      // otherwise hoists the next pass's fragment reads over the spline and spills)
+      if constexpr (CF::SPAN) __builtin_amdgcn_sched_barrier(0);
       const int dp = dps[p];
       const int oq = D <= 8 ? 0 : dp >> 3, jj = D <= 8 ? dp : dp & 7;  // owner quarter, slot
       floatx4 o3[NT][CF::NOB];
@@ -521,10 +531,10 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
         constexpr int i = decltype(ic)::value;
         constexpr int SID = CF::stage_id(p, i), OFF = CF::sub_off(p, i);
         constexpr int OFF_BIAS = OFF + CF::frags(p, i) * CF::OT;
-        // a stage starts at sub-layer 0 of every pass and wherever the grouping opened a new one
-        // (not at OFF == 0: empty sub-layers — no units of degree p, e.g. pass 0 without a
-        // context — also sit at offset 0 of their pass's stage)
-        constexpr bool NEW_STAGE = i == 0 || SID != CF::stage_id(p, i > 0 ? i - 1 : 0);
+        // a stage starts wherever the grouping opened a new one (not at OFF == 0: empty sub-layers
+        // — no units of degree p, e.g. pass 0 without a context — also sit at offset 0 of a stage)
+        constexpr int SID_PREV = i > 0 ? CF::stage_id(p, i - 1) : (p > 0 ? CF::stage_id(p > 0 ? p - 1 : 0, NHID) : -1);
+        constexpr bool NEW_STAGE = SID != SID_PREV;
         if constexpr (NEW_STAGE) {  // it has landed in slot (g & 1)
           constexpr int SF_NEXT = SID + 1 < CF::NSTG ? CF::stage_floats(SID + 1) : CF::stage_floats(0);
           ring_barrier();  // ... and every wave is done with the other slot

@@ -1,7 +1,8 @@
 """Time the wide maf NLL step's GEMM shapes alone (H = 512 degree blocks) at naz's 10,752-row minibatch
 and at 2^16 rows: the batch-row GEMM (linear_act, masked dX, chained act') over the rowgemm_fill
 setting, and the dW batch reduction (naz_gemm over transposed views) over split-K.
-    python scripts/rg_wide_probe.py"""
+    python scripts/rg_wide_probe.py
+torch.mm of the same product (the platform's fp32 GEMM library) is timed beside it for reference."""
 import sys
 from pathlib import Path
 
@@ -21,6 +22,8 @@ for M in (10752, 65536):
     mask = (torch.rand(512, 512, device=dev) > 0.3).float()
     for K, N in ((512, 512), (512, 172), (426, 512), (86, 170)):
         Xk, Wk, bk = X[:, :K], W[:N, :K].contiguous(), b[:N].contiguous()
+        t0 = timeit(lambda: torch.mm(Xk, Wk.t()))
+        print(f"M={M} K={K} N={N}: torch.mm (library fp32) {t0:7.1f} us {2.0 * M * N * K / t0 / 1e6:6.1f} TF", flush=True)
         for fill in (0, 1, 2, 4, 8):
             ops.rowgemm_fill(fill)
             t = timeit(lambda: ops.linear_act(Xk, Wk, bk, "tanh"))

@@ -1692,7 +1692,7 @@ struct AROps {
     static_assert(2 * CF::STG * 4 <= 160 * 1024, "two weight stages exceed the LDS");
     if (B == 0 || L == 0 || P == 0) return 0;
     if (P > 65535) return set_error("naz_ar_flow_log_prob_batched: at most 65535 draws per call");
-    const int64_t rows = CF::ROWS_INV, grid = (B + rows - 1) / rows;
+    const int64_t rows = 16 * CF::NW, grid = (B + rows - 1) / rows;
     const size_t lds = (size_t)2 * CF::STG * 4;
     hipLaunchKernelGGL((made_ar_r16_kernel<CF>), dim3((unsigned)grid, (unsigned)P), dim3(64 * CF::NW), lds, s, packed,
                        L, x, ldx, ctx, ldc, low, high, out_lp, B, bound, spk, sx, slp, c0mode, states);

@@ -335,10 +335,10 @@ int rowgemm_x6_setting(int v) {
 }
 
 int rowgemm_fill_setting(int v) {
-  // NAZ_RG_FILL at first use, else 2 workgroups (= waves per SIMD) per CU
+  // NAZ_RG_FILL at first use, else 4 workgroups (= waves per SIMD) per CU
   static std::atomic<int> cur{[] {
     const char* e = getenv("NAZ_RG_FILL");
-    const int f = e ? atoi(e) : 2;
+    const int f = e ? atoi(e) : 4;
     return f < 0 ? 0 : (f > 16 ? 16 : f);
   }()};
   return v >= 0 ? cur.exchange(v > 16 ? 16 : v) : cur.load();
@@ -372,13 +372,17 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
     p.vst = p.vst && p.zc % 4 == 0;
   }
   int nb = (p.N + 31) / 32;
-  // panel split: outputs of more than 4 column blocks in half-width panels (<= 4 x 32 for up to 8
-  // blocks: 4 waves / SIMD instead of 2; the wide maf's 168-172-unit degree blocks, 200.0 -> 184.6 ms
-  // per NLL step, profiles/r04_s14_*).  An odd NB's paired epilogue (EG = 2) stores only inside its
-  // panel (`inpanel` above); tests/test_gpu_grad.py::test_rowgemm_panel_split runs every epilogue at
-  // N = 168 / 172 / 300 with the split on and off against fp64.
+  // panel split: outputs of more than 4 column blocks in balanced panels of at most 4 blocks (4 waves
+  // per SIMD instead of 2: the wide maf's 168-172-unit degree blocks as 2 x 3, its 512-unit layers as
+  // 4 x 4 instead of 2 x 8 — 42 -> 100 TF at 2^16 rows, profiles/r05_g8_rg_probe.txt).  An odd NB's
+  // paired epilogue (EG = 2) stores only inside its panel (`inpanel` above);
+  // tests/test_gpu_grad.py::test_rowgemm_panel_split runs every epilogue at N = 168 / 172 / 300 with
+  // the split on and off against fp64.
   const int split = p.split >= 0 ? p.split : rowgemm_split_setting(-1);
-  if (split && nb > 4) nb = (nb + 1) / 2;
+  if (split && nb > 4) {
+    const int panels = (nb + 3) / 4;
+    nb = (nb + panels - 1) / panels;
+  }
   // grid fill: at naz's 10,752-row minibatch a 128-row panel grid is 84 workgroups tall, so the wide
   // maf's 512-unit layers ran 168 workgroups (one wave on two of three SIMDs).  Narrower column
   // panels (nb halved, down to one 32-column block) until the grid holds `fill` workgroups per CU:

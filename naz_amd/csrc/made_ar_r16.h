@@ -70,14 +70,14 @@ NAZ_DEV float rqs_select_inv_quad(const floatx4& b0, const floatx4& b1, int q, f
   const bool hq = q >= 2;        // this quarter holds heights (the searched table)
   // softmax numerators of this half-table, max over the whole table
   float m = fmaxf(fmaxf(b0[0], b0[1]), fmaxf(b0[2], b0[3]));
-  m = fmaxf(m, lane_xor16(m));
+  m = fmaxf(m, __shfl_xor(m, 16));
   const float ml = m * kL2E;
   // E[i] = cumulative numerator through knot 4 qh + i + 1, summed in rqs_select's order (the
   // upper half-table continues from the lower one's total), so the knots are bit-identical to it
   float e[4], E[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(b0[i], kL2E, -ml));
-  const float lower_total = lane_xor16(((e[0] + e[1]) + e[2]) + e[3]);  // used by the upper half
+  const float lower_total = __shfl_xor(((e[0] + e[1]) + e[2]) + e[3], 16);  // used by the upper half
   {
     float p = qh ? lower_total : 0.f;
 #pragma unroll
@@ -88,7 +88,7 @@ NAZ_DEV float rqs_select_inv_quad(const floatx4& b0, const floatx4& b1, int q, f
   }
   // (every cross-lane read below runs on all lanes, outside any select: a shuffle in a divergent
   // branch reads the inactive source lanes' stale values)
-  const float upper_end = lane_xor16(E[3]);
+  const float upper_end = __shfl_xor(E[3], 16);
   const float S = qh ? E[3] : upper_end;  // the table's total E_K (the upper half's end)
   const float A = rc.cA * Math<true>::rcp(S);
   // bin index: interior height knots 1..7 with y >= A E_k + key_k (the upper half-table's knot 8 is
@@ -100,15 +100,15 @@ NAZ_DEV float rqs_select_inv_quad(const floatx4& b0, const floatx4& b1, int q, f
     const float key = __builtin_fmaf(A, E[i], __builtin_fmaf(rc.ms, (float)k, rc.nb) + kSearchEps);
     cnt += (k < K && y >= key) ? 1 : 0;
   }
-  cnt += lane_xor16(cnt);
-  const int cnt_h = lane_xor32(cnt);
+  cnt += __shfl_xor(cnt, 16);
+  const int cnt_h = __shfl_xor(cnt, 32);
   const int idx = hq ? cnt : cnt_h;  // the height quarters' count, on every quarter
   const bool first = idx == 0, last = idx == K - 1;
   // this table's knots of bin idx: E[idx] and E[idx + 1] (E_0 = 0) from their owner half-table
   auto pick = [&](int n) {  // the table's cumulative numerator through knot n (1 <= n <= 8)
-    const int j = (n - 1) & 3;  // (a select tree on j's bits: a compare chain became branches)
-    const float mine = (j & 2) ? ((j & 1) ? E[3] : E[2]) : ((j & 1) ? E[1] : E[0]);
-    const float theirs = lane_xor16(mine);
+    const int j = (n - 1) & 3;
+    const float mine = j == 0 ? E[0] : (j == 1 ? E[1] : (j == 2 ? E[2] : E[3]));
+    const float theirs = __shfl_xor(mine, 16);
     return ((n - 1) >> 2) == qh ? mine : theirs;
   };
   const float p0 = pick(first ? 1 : idx), e1 = pick(idx + 1);
@@ -116,16 +116,16 @@ NAZ_DEV float rqs_select_inv_quad(const floatx4& b0, const floatx4& b1, int q, f
   const float fi = (float)idx;
   const float c0 = __builtin_fmaf(A, e0, __builtin_fmaf(rc.ms, fi, rc.nb));
   const float c1 = last ? bound : __builtin_fmaf(A, e1, __builtin_fmaf(rc.ms, fi + 1.f, rc.nb));
-  const float c0o = lane_xor32(c0), c1o = lane_xor32(c1);
+  const float c0o = __shfl_xor(c0, 32), c1o = __shfl_xor(c1, 32);
   const float cs0 = hq ? c0 : c0o, cs1 = hq ? c1 : c1o;  // y (height) knots
   const float co0 = hq ? c0o : c0, co1 = hq ? c1o : c1;  // x (width) knots
   // slope parameters ud[idx - 1], ud[idx] from quarters 0 | 1 (block 1)
   auto pick_ud = [&](int n) {  // 0 <= n <= 6
     const int j = n & 3;
-    const float mine = (j & 2) ? ((j & 1) ? b1[3] : b1[2]) : ((j & 1) ? b1[1] : b1[0]);
-    const float theirs = lane_xor16(mine);
+    const float mine = j == 0 ? b1[0] : (j == 1 ? b1[1] : (j == 2 ? b1[2] : b1[3]));
+    const float theirs = __shfl_xor(mine, 16);
     const float pair = ((n >> 2) == qh) ? mine : theirs;
-    const float v = lane_xor32(pair);
+    const float v = __shfl_xor(pair, 32);
     return hq ? v : pair;
   };
   const float udl = pick_ud(first ? 0 : idx - 1), udh = pick_ud(last ? 0 : idx);
@@ -163,11 +163,6 @@ struct CfgAR {
     int sfl[128];      // floats of stage s (padded)
     int nstg, stg;
   };
-#ifdef NAZ_AR_INV_SPAN
-  static constexpr bool SPAN = true;
-#else
-  static constexpr bool SPAN = false;
-#endif
   static constexpr int E_of(const Layout& y, int p) { return p < 0 ? 0 : y.E[p]; }
   static constexpr int blo_of(const Layout& y, int p) { return E_of(y, p - 1) >> 4; }
   static constexpr int bhi_of(const Layout& y, int p) {
@@ -188,15 +183,13 @@ struct CfgAR {
     int cnt[32] = {};
     for (int u = 0; u < H; ++u) ++cnt[deg(u) < 0 ? 0 : deg(u)];
     for (int p = 0, run = 0; p < D; ++p) y.E[p] = run += cnt[p];
-    // greedy grouping of the sub-layers into stages of <= kARCap floats: per pass, or (SPAN) across
-    // passes from pass 1 on — fewer ring barriers, and the waves of a workgroup drift apart by up to
-    // a stage's passes, so one wave's spline overlaps another's MFMA chain (pass 0 keeps stages of
-    // its own: the pass-0-constant images stream only their constants)
-    int s = -1, run = 0;
+    // greedy grouping of each pass's sub-layers into stages of <= kARCap floats
+    int s = -1;
     for (int p = 0; p < D; ++p) {
+      int run = 0;
       for (int i = 0; i <= NHID; ++i) {
         const int sz = sub_floats_of(y, p, i);
-        if ((i == 0 && (!SPAN || p <= 1)) || run + sz > NAZ_AR_INV_CAP) {
+        if (i == 0 || run + sz > NAZ_AR_INV_CAP) {
           ++s;
           run = 0;
         }
@@ -248,29 +241,21 @@ struct CfgAR {
   // forward kernel's workgroup (CfgARF) keeps one workgroup per CU of 4 x WPE waves
   static constexpr int WPE = NHID * KSH <= 8 ? 3 : 2;
   static constexpr int NW_FWD = 4 * WPE;
-  // 16-row tiles per inverse wave (NAZ_AR_INV_NT: two tiles interleaved pass by pass in 8-wave
-  // workgroups, two waves per SIMD for the doubled register set; spline instances with D >= 8)
-#ifdef NAZ_AR_INV_NT
-  static constexpr int NT = (!AFFINE && D >= 8 && WPE == 3) ? NAZ_AR_INV_NT : 1;
-#else
-  static constexpr int NT = 1;
-#endif
   // inverse workgroup: NAZ_AR_INV_NW waves (12: one workgroup per CU; 6 with NAZ_AR_INV_CAP =
   // 10240: two per CU, each on its own 2 x <= 40 KB ring, so the two do not share barriers)
-  static constexpr int NW = NT > 1 ? 8 : (WPE == 3 ? NAZ_AR_INV_NW : NW_FWD);
+  static constexpr int NW = WPE == 3 ? NAZ_AR_INV_NW : NW_FWD;
   // the inverse kernel's waves per SIMD (NAZ_AR_INV_WPE overrides: e.g. 2 with NAZ_AR_INV_NW = 8)
   // and its prefetched MFMA chains (NAZ_AR_INV_PF: mfma3_16_chain_lds)
 #ifdef NAZ_AR_INV_WPE
-  static constexpr int WPE_INV = NT > 1 ? 2 : (WPE == 3 ? NAZ_AR_INV_WPE : WPE);
+  static constexpr int WPE_INV = WPE == 3 ? NAZ_AR_INV_WPE : WPE;
 #else
-  static constexpr int WPE_INV = NT > 1 ? 2 : WPE;
+  static constexpr int WPE_INV = WPE;
 #endif
 #ifdef NAZ_AR_INV_PF
-  static constexpr bool PF = NT == 1;
+  static constexpr bool PF = true;
 #else
   static constexpr bool PF = false;
 #endif
-  static constexpr int ROWS_INV = 16 * NT * NW;  // rows per inverse workgroup
   static_assert(H <= 256 && D <= 32 && D >= 2 && NHID >= 1 && NHID <= 3, "unsupported fused autoregressive shape");
   static_assert(NOB <= 2 && NSTG <= 128, "output blocks / stages");
 };
@@ -404,25 +389,13 @@ NAZ_DEV void ar_split4(Frag2& f, const floatx4& a) {
   f.l = __builtin_bit_cast(half8, Lo);
 }
 
-// t of quarter oq (wave-uniform) of the lane's row, on every quarter
-NAZ_DEV float from_quarter(float t, int q, int oq) {
-#ifndef NAZ_XOR_PERMLANE
-  return __shfl(t, (int)(threadIdx.x & 15) + 16 * oq);
-#endif
-  const float a = lane_xor16(t);
-  const float u = ((q ^ oq) & 1) ? a : t;
-  const float b = lane_xor32(u);
-  return ((q ^ oq) & 2) ? b : u;
-}
-
 template <class CF>
 __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
     const float* __restrict__ packed, int L, const float* __restrict__ x, int64_t ldx,
     const float* __restrict__ ctx, int64_t ldc, const float* __restrict__ low, const float* __restrict__ high,
     float* __restrict__ out_lp, int64_t B, float bound, int64_t spk = 0, int64_t sx = 0, int64_t slp = 0,
     int c0mode = 0, float* __restrict__ states = nullptr) {
-  constexpr int D = CF::D, K = CF::K, P = CF::P, NW = CF::NW, NHID = CF::NHID, NT = CF::NT;
-  static_assert(NT == 1 || !CF::PF, "the prefetched chains hold one tile's B fragments");
+  constexpr int D = CF::D, K = CF::K, P = CF::P, NW = CF::NW, NHID = CF::NHID;
   {  // blockIdx.y = draw (naz_ar_flow_log_prob_batched): image packed + draw spk, rows x + draw sx
     const int64_t dz = blockIdx.y;
     packed += dz * spk;
@@ -435,56 +408,38 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int q = lane >> 4;
-  // NT independent 16-row tiles per wave (CfgAR::NT): every A fragment read from the ring feeds
-  // all of them, and one tile's elementwise work (activation split, spline) has the other's MFMA
-  // chain to overlap with instead of waiting out its own
-  int64_t row[NT];
-  bool valid[NT];
-  // the row's values: quarter q holds dims 8 q .. 8 q + 7 (zero past D) — exactly its slice of the
-  // x k-step's B fragment, so hidden layer 1 splits them as they are; pass p's dim is read from (and
-  // written back to) its owner quarter only (lane_xor16 / lane_xor32 broadcasts)
-  float xq[NT][8];
-  float logjac[NT];  // this quarter's dims' share (summed over the quarters at the end)
+  const int64_t row = (int64_t)blockIdx.x * (16 * NW) + wave * 16 + (lane & 15);
+  const bool valid = row < B;
+  const int64_t crow = valid ? row : 0;
+
+  float v[D];  // the row's values in natural dim order (every quarter holds all of them)
+  float logjac = 0.f;
 #pragma unroll
-  for (int tt = 0; tt < NT; ++tt) {
-    row[tt] = (int64_t)blockIdx.x * (16 * NW * NT) + (wave * NT + tt) * 16 + (lane & 15);
-    valid[tt] = row[tt] < B;
-    const int64_t crow = valid[tt] ? row[tt] : 0;
-    logjac[tt] = 0.f;
+  for (int d = 0; d < D; ++d) v[d] = valid ? x[crow * ldx + d] : 0.f;
+  if (low != nullptr) {  // naz bounding_transform (transforms.py:20-23), as the coupling kernel
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int d = 8 * q + j;
-      const bool in = d < D;
-      xq[tt][j] = (valid[tt] && in) ? x[crow * ldx + (in ? d : 0)] : 0.f;
-      if (low != nullptr && in) {  // naz bounding_transform (transforms.py:20-23), as the coupling kernel
-        const float lo = low[d], hi = high[d];
-        const float u = (xq[tt][j] - lo) / (hi - lo);
-        logjac[tt] -= logf(u) + log1pf(-u) + logf(hi - lo);
-        xq[tt][j] = logf(u / (1.f - u));
-      }
+    for (int d = 0; d < D; ++d) {
+      const float lo = low[d], hi = high[d];
+      const float u = (v[d] - lo) / (hi - lo);
+      logjac -= logf(u) + log1pf(-u) + logf(hi - lo);
+      v[d] = logf(u / (1.f - u));
     }
   }
   // context B fragments: the same for every pass and layer
-  Frag2 cf[NT][CF::KC > 0 ? CF::KC : 1];
+  Frag2 cf[CF::KC > 0 ? CF::KC : 1];
 #pragma unroll
-  for (int tt = 0; tt < NT; ++tt) {
-    const int64_t crow = valid[tt] ? row[tt] : 0;
+  for (int t = 0; t < CF::KC; ++t) {
+    float c8[8];
 #pragma unroll
-    for (int t = 0; t < CF::KC; ++t) {
-      float c8[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = 32 * t + 8 * q + j;
-        c8[j] = col < CF::C ? ctx[crow * ldc + col] : 0.f;
-      }
-      cf[tt][t] = split8_f16(c8);
+    for (int j = 0; j < 8; ++j) {
+      const int col = 32 * t + 8 * q + j;
+      c8[j] = col < CF::C ? ctx[crow * ldc + col] : 0.f;
     }
+    cf[t] = split8_f16(c8);
   }
 
   const RqsConsts<K, true> rc(bound);
-  float ldsum[NT];  // the layers' forward log-dets (log p = base - ldsum + logjac)
-#pragma unroll
-  for (int tt = 0; tt < NT; ++tt) ldsum[tt] = 0.f;
+  float ldsum = 0.f;  // the layers' forward log-dets (log p = base - ldsum + logjac)
   const int ch0 = c0mode ? CF::c0_chunks(0) : CF::stage_floats(0) / 256;  // stage 0's KB to stream
   stage_issue_lim<CF::stage_floats(0), NW>(slot0, packed + (int64_t)(L - 1) * CF::LAYER, ch0);
   int g = 0;
@@ -496,24 +451,15 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
     int dps[D];  // dim of order p, wave-uniform (SGPRs)
 #pragma unroll
     for (int p = 0; p < D; ++p) dps[p] = __builtin_amdgcn_readfirstlane(perm[p]);
-    Frag2 hf[NT][NHID][CF::KSH];  // hidden layers as B fragments; zero = nothing computed yet
+    Frag2 hf[NHID][CF::KSH];  // hidden layers as B fragments; zero = nothing computed yet
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt)
+    for (int i = 0; i < NHID; ++i)
 #pragma unroll
-      for (int i = 0; i < NHID; ++i)
+      for (int t = 0; t < CF::KSH; ++t) hf[i][t] = Frag2{half8{}, half8{}};
+    float xmax = 0.f;
+    if constexpr (CF::AFFINE) {
 #pragma unroll
-        for (int t = 0; t < CF::KSH; ++t) hf[tt][i][t] = Frag2{half8{}, half8{}};
-    float xmax[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) {
-      xmax[tt] = 0.f;
-      if constexpr (CF::AFFINE) {
-        float m = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(xq[tt][j]));
-        m = fmaxf(m, lane_xor16(m));
-        xmax[tt] = fmaxf(m, lane_xor32(m));
-      }
+      for (int d = 0; d < D; ++d) xmax = fmaxf(xmax, fabsf(v[d]));
     }
     const float* cur = slot0;
     static_for<0, D>([&](auto pc) {
@@ -521,20 +467,16 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
       // pass constants bound to constexpr locals (a constexpr function in a loop bound or argument
       // is not folded reliably: the loops then stay rolled and the fragments go to scratch)
       constexpr int NBP = CF::nb(p), BLO = CF::blo(p), KT = CF::kt(p);
-      // (no instruction moves across a pass boundary: with stages spanning passes the scheduler
-      // otherwise hoists the next pass's fragment reads over the spline and spills)
-      if constexpr (CF::SPAN) __builtin_amdgcn_sched_barrier(0);
       const int dp = dps[p];
-      const int oq = D <= 8 ? 0 : dp >> 3, jj = D <= 8 ? dp : dp & 7;  // owner quarter, slot
-      floatx4 o3[NT][CF::NOB];
+      floatx4 o3[CF::NOB];
       static_for<0, NHID + 1>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         constexpr int SID = CF::stage_id(p, i), OFF = CF::sub_off(p, i);
         constexpr int OFF_BIAS = OFF + CF::frags(p, i) * CF::OT;
-        // a stage starts wherever the grouping opened a new one (not at OFF == 0: empty sub-layers
-        // — no units of degree p, e.g. pass 0 without a context — also sit at offset 0 of a stage)
-        constexpr int SID_PREV = i > 0 ? CF::stage_id(p, i - 1) : (p > 0 ? CF::stage_id(p > 0 ? p - 1 : 0, NHID) : -1);
-        constexpr bool NEW_STAGE = SID != SID_PREV;
+        // a stage starts at sub-layer 0 of every pass and wherever the grouping opened a new one
+        // (not at OFF == 0: empty sub-layers — no units of degree p, e.g. pass 0 without a
+        // context — also sit at offset 0 of their pass's stage)
+        constexpr bool NEW_STAGE = i == 0 || SID != CF::stage_id(p, i > 0 ? i - 1 : 0);
         if constexpr (NEW_STAGE) {  // it has landed in slot (g & 1)
           constexpr int SF_NEXT = SID + 1 < CF::NSTG ? CF::stage_floats(SID + 1) : CF::stage_floats(0);
           ring_barrier();  // ... and every wave is done with the other slot
@@ -566,15 +508,13 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
               static_for<0, NBP>([&](auto bc) {
                 constexpr int bi = decltype(bc)::value, b = BLO + bi;
                 const float4 c = cv[4 * bi + q];
-#pragma unroll
-                for (int tt = 0; tt < NT; ++tt) ar_split4<b & 1>(hf[tt][i][b >> 1], floatx4{c.x, c.y, c.z, c.w});
+                ar_split4<b & 1>(hf[i][b >> 1], floatx4{c.x, c.y, c.z, c.w});
               });
             } else {
 #pragma unroll
               for (int o = 0; o < CF::NOB; ++o) {
                 const float4 c = cv[4 * o + q];
-#pragma unroll
-                for (int tt = 0; tt < NT; ++tt) o3[tt][o] = floatx4{c.x, c.y, c.z, c.w};
+                o3[o] = floatx4{c.x, c.y, c.z, c.w};
               }
             }
             done0 = true;
@@ -589,44 +529,33 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
           // (xmax: a running bound, max |v| at the layer's start and every value written since).
           // Affine flows only: a spline maps [-B, B] into itself and is the identity outside, so an
           // nsa row never exceeds max(|input|, B) and the launch-time input check covers it.
-          Frag2 xf[NT];
-          float us[NT];
+          int e = 0;
+          if constexpr (CF::AFFINE) e = xmax >= 16384.f ? __builtin_amdgcn_frexp_expf(xmax) - 14 : 0;
+          const float sc = __builtin_amdgcn_ldexpf(1.f, -e), us = __builtin_amdgcn_ldexpf(1.f, e);
+          float x8[8];
 #pragma unroll
-          for (int tt = 0; tt < NT; ++tt) {
-            int e = 0;
-            if constexpr (CF::AFFINE) e = xmax[tt] >= 16384.f ? __builtin_amdgcn_frexp_expf(xmax[tt]) - 14 : 0;
-            const float sc = __builtin_amdgcn_ldexpf(1.f, -e);
-            us[tt] = __builtin_amdgcn_ldexpf(1.f, e);
-            float x8[8];
+          for (int j = 0; j < 8; ++j) {
+            float s = 0.f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) x8[j] = xq[tt][j] * sc;
-            xf[tt] = split8_f16(x8);
+            for (int qq = 0; qq < 4; ++qq)
+              if (8 * qq + j < D) s = q == qq ? v[8 * qq + j] : s;
+            x8[j] = s * sc;
           }
+          const Frag2 xf = split8_f16(x8);
           static_for<0, NBP>([&](auto bc) {
             constexpr int bi = decltype(bc)::value, b = BLO + bi;
             const float4 bv = bias4[4 * bi + q];
-            floatx4 acc[NT];
+            floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
-            for (int tt = 0; tt < NT; ++tt) acc[tt] = floatx4{bv.x, bv.y, bv.z, bv.w};
+            for (int t = 0; t < CF::KC; ++t) acc = mfma3_16(afrag(bi * CF::KI + t), cf[t], acc);
+            if constexpr (CF::AFFINE) {
+              const floatx4 ax = mfma3_16(afrag(bi * CF::KI + CF::KC), xf, floatx4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-            for (int t = 0; t < CF::KC; ++t) {
-              const Frag2 a = afrag(bi * CF::KI + t);
-#pragma unroll
-              for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma3_16(a, cf[tt][t], acc[tt]);
+              for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(ax[r], us, acc[r]);
+            } else {
+              acc = mfma3_16(afrag(bi * CF::KI + CF::KC), xf, acc);
             }
-            const Frag2 a = afrag(bi * CF::KI + CF::KC);
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt) {
-              if constexpr (CF::AFFINE) {
-                const floatx4 ax = mfma3_16(a, xf[tt], floatx4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[tt][r] = __builtin_fmaf(ax[r], us[tt], acc[tt][r]);
-              } else {
-                acc[tt] = mfma3_16(a, xf[tt], acc[tt]);
-              }
-            }
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt) ar_split4<b & 1>(hf[tt][0][b >> 1], acc[tt]);
+            ar_split4<b & 1>(hf[0][b >> 1], acc);
           });
          }
         } else if constexpr (i > 0 && i < NHID && NBP > 0) {
@@ -634,21 +563,14 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
           if (!done0) static_for<0, NBP>([&](auto bc) {
             constexpr int bi = decltype(bc)::value, b = BLO + bi;
             const float4 bv = bias4[4 * bi + q];
-            floatx4 acc[NT];
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt) acc[tt] = floatx4{bv.x, bv.y, bv.z, bv.w};
+            floatx4 acc = floatx4{bv.x, bv.y, bv.z, bv.w};
             if constexpr (CF::PF) {
-              acc[0] = mfma3_16_chain_lds<KT>(ub + 2048u * (bi * KT), hf[0][i - 1], acc[0]);
+              acc = mfma3_16_chain_lds<KT>(ub + 2048u * (bi * KT), hf[i - 1], acc);
             } else {
 #pragma unroll
-              for (int t = 0; t < KT; ++t) {
-                const Frag2 a = afrag(bi * KT + t);
-#pragma unroll
-                for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma3_16(a, hf[tt][i - 1][t], acc[tt]);
-              }
+              for (int t = 0; t < KT; ++t) acc = mfma3_16(afrag(bi * KT + t), hf[i - 1][t], acc);
             }
-#pragma unroll
-            for (int tt = 0; tt < NT; ++tt) ar_split4<b & 1>(hf[tt][i][b >> 1], acc[tt]);
+            ar_split4<b & 1>(hf[i][b >> 1], acc);
           });
         } else if constexpr (i == NHID) {
           // ---- the output rows of dim d_p, then the elementwise inverse on x[d_p]
@@ -656,87 +578,64 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
 #pragma unroll
             for (int o = 0; o < CF::NOB; ++o) {
               const float4 bv = bias4[4 * o + q];
-#pragma unroll
-              for (int tt = 0; tt < NT; ++tt) o3[tt][o] = floatx4{bv.x, bv.y, bv.z, bv.w};
+              o3[o] = floatx4{bv.x, bv.y, bv.z, bv.w};
             }
             if constexpr (CF::PF) {
 #pragma unroll
-              for (int o = 0; o < CF::NOB; ++o)
-                o3[0][o] = mfma3_16_chain_lds<KT>(ub + 2048u * (o * KT), hf[0][NHID - 1], o3[0][o]);
+              for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16_chain_lds<KT>(ub + 2048u * (o * KT), hf[NHID - 1], o3[o]);
             } else {
 #pragma unroll
               for (int t = 0; t < KT; ++t)
 #pragma unroll
-                for (int o = 0; o < CF::NOB; ++o) {
-                  const Frag2 a = afrag(o * KT + t);
-#pragma unroll
-                  for (int tt = 0; tt < NT; ++tt) o3[tt][o] = mfma3_16(a, hf[tt][NHID - 1][t], o3[tt][o]);
-                }
+                for (int o = 0; o < CF::NOB; ++o) o3[o] = mfma3_16(afrag(o * KT + t), hf[NHID - 1][t], o3[o]);
             }
           }
-#pragma unroll
-          for (int tt = 0; tt < NT; ++tt) {
-            const float y = from_quarter(xq[tt][jj], q, oq);
-            float vn;
-            if constexpr (CF::AFFINE) {
-              // pyro AffineAutoregressive._inverse: rows 0, 1 = (mean, log_scale) of dim d_p, held by
-              // quarter 0 registers 0, 1; log_scale clamped to [-5, 3]; log|det| = the clamped ls
-              const float mean = __shfl(o3[tt][0][0], lane & 15);
-              const float ls = fminf(fmaxf(__shfl(o3[tt][0][1], lane & 15), -5.f), 3.f);
-              vn = (y - mean) * __expf(-ls);
-              xmax[tt] = fmaxf(xmax[tt], fabsf(vn));
-              ldsum[tt] += ls;
-            } else {
+          const float y = v[dp];
+          if constexpr (CF::AFFINE) {
+            // pyro AffineAutoregressive._inverse: rows 0, 1 = (mean, log_scale) of dim d_p, held by
+            // quarter 0 registers 0, 1; log_scale clamped to [-5, 3]; log|det| = the clamped ls
+            const float mean = __shfl(o3[0][0], lane & 15);
+            const float ls = fminf(fmaxf(__shfl(o3[0][1], lane & 15), -5.f), 3.f);
+            v[dp] = (y - mean) * __expf(-ls);
+            xmax = fmaxf(xmax, fabsf(v[dp]));
+            ldsum += ls;
+          } else {
 #ifndef NAZ_AR_SPLINE_GATHER
-              // one spline per row spread over its four quarters (rqs_select_inv_quad)
-              float ld;
-              vn = rqs_select_inv_quad<K>(o3[tt][0], o3[tt][CF::NOB > 1 ? 1 : 0], q, y, bound, rc, ld);
-              ldsum[tt] -= ld;
+            // one spline per row spread over its four quarters (rqs_select_inv_quad)
+            float ld;
+            v[dp] = rqs_select_inv_quad<K>(o3[0], o3[CF::NOB > 1 ? 1 : 0], q, y, bound, rc, ld);
+            ldsum -= ld;
 #else
-              // (A/B) every quarter gathers the row's parameters and evaluates the whole spline:
-              // parameter pi sits in block pi >> 4, register pi & 3 of quarter (pi & 15) >> 2
-              float uw[K], uh[K], ud[K - 1];
+            // (A/B) every quarter gathers the row's parameters and evaluates the whole spline:
+            // parameter pi sits in block pi >> 4, register pi & 3 of quarter (pi & 15) >> 2
+            float uw[K], uh[K], ud[K - 1];
 #pragma unroll
-              for (int pi = 0; pi < P; ++pi) {
-                const float val = __shfl(o3[tt][pi >> 4][pi & 3], (lane & 15) + 16 * ((pi & 15) >> 2));
-                if (pi < K) uw[pi] = val;
-                else if (pi < 2 * K) uh[pi - K] = val;
-                else ud[pi - 2 * K] = val;
-              }
-              float ld;
-              vn = rqs_select<K, true>(uw, uh, ud, y, bound, rc, ld);
-              ldsum[tt] -= ld;
-#endif
+            for (int pi = 0; pi < P; ++pi) {
+              const float val = __shfl(o3[pi >> 4][pi & 3], (lane & 15) + 16 * ((pi & 15) >> 2));
+              if (pi < K) uw[pi] = val;
+              else if (pi < 2 * K) uh[pi - K] = val;
+              else ud[pi - 2 * K] = val;
             }
-            const float old = xq[tt][jj];  // (every quarter formed vn; only the owner keeps it)
-            xq[tt][jj] = q == oq ? vn : old;
+            float ld;
+            v[dp] = rqs_select<K, true>(uw, uh, ud, y, bound, rc, ld);
+            ldsum -= ld;
+#endif
           }
         }
       });
     });
     // the training forward (naz_ar_flow_log_prob_train, one draw): layer l's output s_l for the
     // backward (made_ar_bwd.h)
-    if (states != nullptr) {
+    if (states != nullptr && q == 0 && valid) {
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt)
-        if (valid[tt]) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (8 * q + j < D) states[((int64_t)l * B + row[tt]) * D + 8 * q + j] = xq[tt][j];
-        }
+      for (int d = 0; d < D; ++d) states[((int64_t)l * B + row) * D + d] = v[d];
     }
   }
   constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+  float base = 0.f;
 #pragma unroll
-  for (int tt = 0; tt < NT; ++tt) {
-    float part = logjac[tt];  // this quarter's dims: base density and bounding log-det
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (8 * q + j < D) part += -(xq[tt][j] * xq[tt][j]) / 2.f - kLogSqrt2Pi;
-    part += lane_xor16(part);
-    part += lane_xor32(part);
-    if (q == 0 && valid[tt]) out_lp[row[tt]] = part - ldsum[tt];
-  }
+  for (int d = 0; d < D; ++d) base += -(v[d] * v[d]) / 2.f - kLogSqrt2Pi;
+  if (q == 0 && valid) out_lp[row] = base - ldsum + logjac;
 }
 
 // ================================================================ forward (sample) direction

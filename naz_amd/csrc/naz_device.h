@@ -22,32 +22,6 @@ constexpr float kMinBinHeight = 1e-3f;
 constexpr float kMinDerivative = 1e-3f;
 constexpr float kSearchEps = 1e-6f;
 
-// The value of lane l ^ 16 / l ^ 32 of the wave, through gfx950's v_permlane16_swap /
-// v_permlane32_swap (VALU: odd 16-lane rows of the first operand trade places with even rows of
-// the second; 32-lane halves likewise).  A __shfl_xor is a ds_bpermute: a round trip through the
-// LDS pipe, and inside a ring kernel hipcc waits lgkmcnt(0) behind every LDS read in flight before
-// using its result.
-template <class T>
-NAZ_DEV T lane_xor16(T x) {
-  static_assert(sizeof(T) == 4, "32-bit lanes");
-#ifndef NAZ_XOR_PERMLANE  // the LDS-pipe exchange unless built for the A/B
-  return __builtin_bit_cast(T, __shfl_xor(__builtin_bit_cast(int, x), 16));
-#endif
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-  return __builtin_bit_cast(T, (threadIdx.x & 16) ? r[0] : r[1]);
-}
-template <class T>
-NAZ_DEV T lane_xor32(T x) {
-  static_assert(sizeof(T) == 4, "32-bit lanes");
-#ifndef NAZ_XOR_PERMLANE
-  return __builtin_bit_cast(T, __shfl_xor(__builtin_bit_cast(int, x), 32));
-#endif
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return __builtin_bit_cast(T, (threadIdx.x & 32) ? r[0] : r[1]);
-}
-
 // Publish an LDS-DMA ring slot.  A global_load_lds write is pending on the issuing wave's
 // vmcnt until it lands in LDS; __syncthreads() alone does NOT reliably drain it: on a loop
 // back edge hipcc (ROCm 7.2) emitted only lgkmcnt(0) before the barrier, so a wave could read
@@ -111,8 +85,6 @@ struct Math<true> {
 template <bool FAST = false>
 NAZ_DEV float softplus(float x) {
   if constexpr (FAST) {
-    // both sides evaluated and selected (an early return became a divergent branch in the spline
-    // kernels: exec-mask bookkeeping around ~12 VALU, once per knot slope)
     if (x > 20.f) return x;
     return fmaxf(x, 0.f) + Math<true>::log1p(Math<true>::exp(-fabsf(x)));
   } else {

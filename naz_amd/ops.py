@@ -80,7 +80,8 @@ def workspace(dev: torch.device, nbytes: int) -> Tuple[Optional[int], int]:
 
 def rowgemm_split(value: Optional[bool] = None) -> bool:
     """The batch-row GEMM's panel split (naz_tuning "rowgemm_split": outputs wider than 128 columns
-    as two half-width panels; no result changes).  ``value`` sets it; returns the setting before."""
+    as balanced panels of at most 128; no result changes).  ``value`` sets it; returns the setting
+    before."""
     r = int(lib().naz_tuning(b"rowgemm_split", -1 if value is None else int(bool(value))))
     if r < 0:
         check(r, "rowgemm_split")
@@ -447,9 +448,12 @@ def base_log_prob_bwd(z: Tensor, g_lp: Tensor) -> Tensor:
 
 
 def _split_k(M: int, N: int, K: int) -> int:
+    # about 2048 64 x 64 tiles over the grid, each split at least 192 batch rows deep (at naz's
+    # 10,752-row minibatch a 512-row floor held the wide maf's dW at 21 splits: 58 vs 70 TF at 32,
+    # profiles/r05_g8_rg_probe.txt)
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     want = max(1, 2048 // tiles)
-    return int(max(1, min(want, K // 512)))
+    return int(max(1, min(want, K // 192)))
 
 
 def gemm(a: Tensor, b: Tensor, out: Optional[Tensor] = None, mask: Optional[Tensor] = None, mask_b: bool = False,

@@ -75,6 +75,7 @@ struct RowGemmArgs {
   int64_t lddy;
   int dact;
   int dyvec;  // dy rows allow 16-byte loads (set by rowgemm())
+  int bn1;    // B's n index has unit stride: the B chunk is loaded along n (set by rowgemm())
   // optional VJP epilogue of a CNF vector-field layer under the Hutchinson JVP (naz_gemm_jvp_bwd):
   // rows come in (value, tangent) pairs 2i, 2i + 1 and jvp = the layer's stacked output S with the
   // same pairing; C[2i] = G[2i] act' + G[2i+1] (act''/act') S[2i+1], C[2i+1] = G[2i+1] act',
@@ -237,10 +238,18 @@ __global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel
   const int ar = tid >> 1, ak = (tid & 1) * APT;
   const int64_t am = m0 + ar;
   const bool arow = am < p.M;
-  // B chunk: RG_BK k x BN n: thread -> (k = tid % RG_BK, n = tid / RG_BK + (256 / RG_BK) j)
+  // B chunk: RG_BK k x BN n, BPT values per thread.  k-major (B = Wᵀ, unit k stride): thread ->
+  // (k = tid % RG_BK, n = tid / RG_BK + (256 / RG_BK) j); n-major (p.bn1: B = W, unit n stride, the
+  // dX products): 32 lanes along n, value j = (block j % NB, row half j / NB) -> (k = tid / 32 +
+  // 8 (j / NB), n = tid % 32 + 32 (j % NB)).  A k-major load of a row-major W put each lane on another
+  // row: 64 cache lines per wave instruction (gemm_dact at half linear_act's rate, r05_g8 probe).
   constexpr int BKS = RG_T / RG_BK;
-  const int bk = tid % RG_BK, bn0 = tid / RG_BK;
+  static_assert(RG_BK == 16 && RG_T == 256, "the n-major B mapping assumes 16-deep chunks of 256 threads");
+  const bool bn1 = p.bn1 != 0;
+  const int bk = bn1 ? (tid >> 5) : tid % RG_BK, bn0 = bn1 ? (tid & 31) : tid / RG_BK;
   constexpr int BPT = BN / BKS;
+  auto bkj = [&](int j) { return bn1 ? bk + 8 * (j / NB) : bk; };
+  auto bnj = [&](int j) { return bn1 ? bn0 + 32 * (j % NB) : bn0 + BKS * j; };
 
   const auto bsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), (short)0, 0x7fffffff, 0x00020000);
   const auto msrd =
@@ -270,7 +279,7 @@ __global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       // weights / masks are small: 32-bit buffer offsets (no 64-bit address registers)
-      const int k = kc0 + bk, n = n0 + bn0 + BKS * j;
+      const int k = kc0 + bkj(j), n = n0 + bnj(j);
       float v = 0.f;
       if (k < K && n < p.N) {
         v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bsrd, 4 * (k * sbk + n * sbn), 0, 0));
@@ -284,7 +293,7 @@ __global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel
 #pragma unroll
     for (int i = 0; i < APT; ++i) As[buf][ak + i][ar] = ra[i];
 #pragma unroll
-    for (int j = 0; j < BPT; ++j) Bs[buf][bk][bn0 + BKS * j] = rb[j];
+    for (int j = 0; j < BPT; ++j) Bs[buf][bkj(j)][bnj(j)] = rb[j];
   };
 
   floatx16 acc[NB];
@@ -367,6 +376,7 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
           (p.ka1 == 0 || (al16(p.a1) && p.lda1 % 4 == 0));
   p.vst = p.ldc % 4 == 0 && al16(p.c);  // 16-byte row pieces; a ragged row tail is stored per column
   p.dyvec = p.dy != nullptr && p.lddy % 4 == 0 && al16(p.dy);
+  p.bn1 = p.sbn == 1 && p.sbk != 1;  // the dX products' B = W (row-major [k][n]): lanes along n
   if (nz > 1) {  // every problem's base keeps the alignment
     p.vec = p.vec && p.za0 % 4 == 0 && p.za1 % 4 == 0;
     p.vst = p.vst && p.zc % 4 == 0;

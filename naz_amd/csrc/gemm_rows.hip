@@ -76,6 +76,7 @@ struct RowGemmArgs {
   int dact;
   int dyvec;  // dy rows allow 16-byte loads (set by rowgemm())
   int bn1;    // B's n index has unit stride: the B chunk is loaded along n (set by rowgemm())
+  int bbytes, mbytes;  // byte spans of B / the mask (buffer range: out-of-range loads return 0)
   // optional VJP epilogue of a CNF vector-field layer under the Hutchinson JVP (naz_gemm_jvp_bwd):
   // rows come in (value, tangent) pairs 2i, 2i + 1 and jvp = the layer's stacked output S with the
   // same pairing; C[2i] = G[2i] act' + G[2i+1] (act''/act') S[2i+1], C[2i+1] = G[2i+1] act',
@@ -89,6 +90,9 @@ struct RowGemmArgs {
   // arithmetic (rowgemm()): exact FP32 MFMA (0), bf16x6 (1: rowgemm_x6_kernel), or the library's
   // setting (-1: naz_tuning "rowgemm_x6")
   int x6 = -1;
+  // ... or the f16x3 split (1: rowgemm_h3_kernel, |B| < 2^9), or the library's setting (-1:
+  // naz_tuning "rowgemm_h3"); x6 wins when both are on
+  int h3 = -1;
   // small batches: narrow the column panels until the grid holds this many workgroups per CU
   // (0: off, -1: the library's setting, naz_tuning "rowgemm_fill")
   int fill = -1;
@@ -251,11 +255,15 @@ __global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel
   auto bkj = [&](int j) { return bn1 ? bk + 8 * (j / NB) : bk; };
   auto bnj = [&](int j) { return bn1 ? bn0 + 32 * (j % NB) : bn0 + BKS * j; };
 
-  const auto bsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), (short)0, 0x7fffffff, 0x00020000);
+  // B and mask reads are buffer loads over their exact byte spans: an element outside the k x n box
+  // reads at offset `span` and returns 0, so the loads are branch-free, and the mask factors are
+  // applied at the LDS store (after this chunk's MFMAs), not right behind their loads
+  const auto bsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), (short)0, p.bbytes, 0x00020000);
   const auto msrd =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.mask ? p.mask : p.b), (short)0, 0x7fffffff, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.mask ? p.mask : p.b), (short)0, p.mbytes, 0x00020000);
   const int sbk = (int)p.sbk, sbn = (int)p.sbn, smk = (int)p.smk, smn = (int)p.smn;
-  float ra[APT], rb[BPT];
+  const bool masked = p.mask != nullptr;
+  float ra[APT], rb[BPT], rm[BPT];
   auto load = [&](int kc) {
     const int kc0 = kc * RG_BK;
 #pragma unroll
@@ -280,20 +288,19 @@ __global__ void __launch_bounds__(RG_T, NB <= 4 ? NAZ_RG_OCC : 2) rowgemm_kernel
     for (int j = 0; j < BPT; ++j) {
       // weights / masks are small: 32-bit buffer offsets (no 64-bit address registers)
       const int k = kc0 + bkj(j), n = n0 + bnj(j);
-      float v = 0.f;
-      if (k < K && n < p.N) {
-        v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bsrd, 4 * (k * sbk + n * sbn), 0, 0));
-        if (p.mask != nullptr)
-          v *= __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(msrd, 4 * (k * smk + n * smn), 0, 0));
-      }
-      rb[j] = v;
+      const bool in = k < K && n < p.N;
+      rb[j] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(bsrd, in ? 4 * (k * sbk + n * sbn) : p.bbytes, 0, 0));
+      if (masked)
+        rm[j] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(msrd, in ? 4 * (k * smk + n * smn) : p.mbytes, 0, 0));
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < APT; ++i) As[buf][ak + i][ar] = ra[i];
 #pragma unroll
-    for (int j = 0; j < BPT; ++j) Bs[buf][bkj(j)][bnj(j)] = rb[j];
+    for (int j = 0; j < BPT; ++j) Bs[buf][bkj(j)][bnj(j)] = masked ? rb[j] * rm[j] : rb[j];
   };
 
   floatx16 acc[NB];
@@ -343,6 +350,15 @@ int rowgemm_x6_setting(int v) {
   return v >= 0 ? cur.exchange(v != 0 ? 1 : 0) : cur.load();
 }
 
+int rowgemm_h3_setting(int v) {
+  // NAZ_RG_H3 at first use, else off until a same-box A/B sets the default
+  static std::atomic<int> cur{[] {
+    const char* e = getenv("NAZ_RG_H3");
+    return e ? (atoi(e) != 0 ? 1 : 0) : 0;
+  }()};
+  return v >= 0 ? cur.exchange(v != 0 ? 1 : 0) : cur.load();
+}
+
 int rowgemm_fill_setting(int v) {
   // NAZ_RG_FILL at first use, else 4 workgroups (= waves per SIMD) per CU
   static std::atomic<int> cur{[] {
@@ -364,6 +380,7 @@ int rowgemm_split_setting(int v) {
 namespace {
 
 int rowgemm_x6_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s);  // below
+int rowgemm_h3_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s);
 
 int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   if (p.M <= 0 || p.N <= 0 || nz <= 0) return 0;
@@ -377,6 +394,8 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   p.vst = p.ldc % 4 == 0 && al16(p.c);  // 16-byte row pieces; a ragged row tail is stored per column
   p.dyvec = p.dy != nullptr && p.lddy % 4 == 0 && al16(p.dy);
   p.bn1 = p.sbn == 1 && p.sbk != 1;  // the dX products' B = W (row-major [k][n]): lanes along n
+  p.bbytes = (int)(4 * (bspan + 1));
+  p.mbytes = (int)(4 * (mspan + 1));
   if (nz > 1) {  // every problem's base keeps the alignment
     p.vec = p.vec && p.za0 % 4 == 0 && p.za1 % 4 == 0;
     p.vst = p.vst && p.zc % 4 == 0;
@@ -406,6 +425,9 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   // the bf16x6 form where the batch is long enough to fill the chip and k deep enough to pay the split
   const int x6 = p.x6 >= 0 ? p.x6 : rowgemm_x6_setting(-1);
   if (x6 && K >= 32 && p.M >= 2048) return rowgemm_x6_dispatch(p, nz, nb, s);
+  // the f16x3 form (the caller's |B| < 2^9: naz_tuning "rowgemm_h3")
+  const int h3 = p.h3 >= 0 ? p.h3 : rowgemm_h3_setting(-1);
+  if (h3 && K >= 32 && p.M >= 2048) return rowgemm_h3_dispatch(p, nz, nb, s);
   switch (nb > 8 ? 8 : nb) {
     case 1: rowgemm_launch<1>(p, nz, s); break;
     case 2: rowgemm_launch<2>(p, nz, s); break;
@@ -1043,6 +1065,196 @@ int rowgemm_x6_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s) {
     default: rowgemm_x6_launch<8>(p, nz, s); break;
   }
   return check_launch("rowgemm_x6_kernel");
+}
+
+// ---------------------------------------------------------------------------------------------
+// rowgemm_h3_kernel: the batch-row GEMM on the f16 matrix pipe (naz_tuning "rowgemm_h3").  The same
+// C = epi(A · B) as rowgemm_kernel with A and B split into f16 hi / lo pieces (hi = f16(v), lo =
+// f16(v - hi); v - hi is exact) and C += Ah·Bh + Ah·Bl + Al·Bh on v_mfma_f32_32x32x16_f16 — the
+// fused kernels' f16x3 form (§4.1): 5.3x the FP32 MFMA rate per product set, the dropped Al·Bl term
+// <= 2^-22 relative.  f16 has 5 exponent bits, so every A row is split at a power-of-two scale that
+// puts its largest |value| in [2^13, 2^14) (a pre-pass over the wave's 32 rows; the lo pieces stay
+// clear of f16's subnormals, the gradients' range is unbounded), and B at 2^6 (weights: the caller
+// guarantees |B| < 2^9); the accumulators are unscaled exactly before the shared epilogue.  16-k
+// chunks; a wave reads its A values straight into registers two chunks ahead; the workgroup splits
+// each B chunk once into LDS in the MFMA's B layout ([block][piece][lane][8 f16]), double buffered.
+typedef _Float16 rg_half8 __attribute__((ext_vector_type(8)));
+typedef unsigned rg_u32x4 __attribute__((ext_vector_type(4)));
+struct RgH2 {
+  rg_half8 h, l;
+};
+constexpr float kRgH3BScale = 64.f;
+
+NAZ_DEV RgH2 rg_split8_f16(const float (&v)[8], float sc) {
+  RgH2 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = v[e] * sc;  // (a power of two: exact)
+    const _Float16 hh = (_Float16)x;
+    r.h[e] = hh;
+    r.l[e] = (_Float16)(x - (float)hh);
+  }
+  return r;
+}
+NAZ_DEV floatx16 rg_mfma3(const RgH2& a, const RgH2& b, floatx16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.l, b.h, c, 0, 0, 0);  // small terms first
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.h, b.l, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a.h, b.h, c, 0, 0, 0);
+}
+
+template <int NB>
+__global__ void __launch_bounds__(RG_T, NB <= 2 ? 4 : (NB <= 4 ? 3 : 2)) rowgemm_h3_kernel(RowGemmArgs p) {
+  {  // problem of this z slice (uniform: stays in SGPRs)
+    const int64_t z = blockIdx.z;
+    p.a0 += z * p.za0;
+    p.a1 += z * p.za1;
+    p.b += z * p.zb;
+    if (p.bias != nullptr) p.bias += z * p.zbias;
+    p.c += z * p.zc;
+  }
+  constexpr int BSLOT = NB * 2 * 64 * 4;  // u32 words of one B chunk: [NB][piece][64 lanes][4]
+  constexpr int SMEM = 2 * BSLOT > 4 * RX_SHARE ? 2 * BSLOT : 4 * RX_SHARE;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  __shared__ float rinv[4][32];  // per row: 1 / (row scale x B scale)
+  unsigned* const bsm = reinterpret_cast<unsigned*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kh = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * RG_BM;
+  const int n0 = blockIdx.y * 32 * NB;
+  const int K = p.ka0 + p.ka1;
+  const int nk = (K + 15) / 16;
+  const int64_t am = m0 + wave * 32 + (lane & 31);
+  const bool arow = am < p.M;
+
+  // A: this lane's 8 k values of the chunk (lane (row i, k-half kh): the MFMA's A layout)
+  auto load_a = [&](int kc, float (&v)[8]) {
+    const int kb = 16 * kc + 8 * kh;
+    if (p.vec && arow && kb + 8 <= K && (kb >= p.ka0 || kb + 8 <= p.ka0)) {
+      const float* src = kb < p.ka0 ? p.a0 + am * p.lda0 + kb : p.a1 + am * p.lda1 + (kb - p.ka0);
+      const float4 v0 = *reinterpret_cast<const float4*>(src);
+      const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+      v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+      v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (arow && kb + e < K) ? rg_a(p, am, kb + e) : 0.f;
+    }
+  };
+  // the row's scale: its largest |A| into [2^13, 2^14) (both lanes of a row agree); all-zero rows 1
+  float sc;
+  {
+    float mx = 0.f;
+    for (int kc = 0; kc < nk; ++kc) {
+      float v[8];
+      load_a(kc, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(v[e]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    int ex = mx > 0.f ? __builtin_amdgcn_frexp_expf(mx) : 14;  // mx < 2^ex (a non-finite row: 0)
+    ex = ex < -100 ? -100 : ex;
+    sc = __builtin_amdgcn_ldexpf(1.f, 14 - ex);
+    if (kh == 0) rinv[wave][lane & 31] = __builtin_amdgcn_ldexpf(1.f, ex - 14) * (1.f / kRgH3BScale);
+  }
+  // B: thread -> fragment fr = (column block fr >> 6, lane fr & 63: column lane & 31, k-half lane >> 5)
+  const auto bsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), (short)0, 0x7fffffff, 0x00020000);
+  const auto msrd =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.mask ? p.mask : p.b), (short)0, 0x7fffffff, 0x00020000);
+  const int sbk = (int)p.sbk, sbn = (int)p.sbn, smk = (int)p.smk, smn = (int)p.smn;
+  constexpr int FR = 64 * NB;  // B fragments per chunk
+  constexpr int FPT = (FR + RG_T - 1) / RG_T;
+  float rb[FPT][8];
+  auto load_b = [&](int kc) {
+#pragma unroll
+    for (int f = 0; f < FPT; ++f) {
+      const int fr = tid + RG_T * f, fl = fr & 63, n = n0 + 32 * (fr >> 6) + (fl & 31);
+      const int kb = 16 * kc + 8 * (fl >> 5);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = 0.f;
+        if (fr < FR && kb + e < K && n < p.N) {
+          v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bsrd, 4 * ((kb + e) * sbk + n * sbn), 0, 0));
+          if (p.mask != nullptr)
+            v *= __builtin_bit_cast(float,
+                                    __builtin_amdgcn_raw_buffer_load_b32(msrd, 4 * ((kb + e) * smk + n * smn), 0, 0));
+        }
+        rb[f][e] = v;
+      }
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int f = 0; f < FPT; ++f) {
+      const int fr = tid + RG_T * f;
+      if (fr < FR) {
+        const RgH2 q = rg_split8_f16(rb[f], kRgH3BScale);
+        rg_u32x4* d = reinterpret_cast<rg_u32x4*>(bsm + buf * BSLOT) + (fr >> 6) * 2 * 64 + (fr & 63);
+        d[0] = __builtin_bit_cast(rg_u32x4, q.h);
+        d[64] = __builtin_bit_cast(rg_u32x4, q.l);
+      }
+    }
+  };
+
+  floatx16 acc[NB];
+#pragma unroll
+  for (int o = 0; o < NB; ++o)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[o][r] = 0.f;
+
+  float va[8], vb[8];
+  load_a(0, va);
+  if (nk > 1) load_a(1, vb);
+  load_b(0);
+  store_b(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    float vc[8];
+    if (kc + 2 < nk) load_a(kc + 2, vc);  // two chunks ahead: in flight during two chunks' MFMAs
+    if (kc + 1 < nk) load_b(kc + 1);
+    const RgH2 a = rg_split8_f16(va, sc);
+    const rg_u32x4* bp = reinterpret_cast<const rg_u32x4*>(bsm + buf * BSLOT) + lane;
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const RgH2 b{__builtin_bit_cast(rg_half8, bp[(o * 2 + 0) * 64]), __builtin_bit_cast(rg_half8, bp[(o * 2 + 1) * 64])};
+      acc[o] = rg_mfma3(a, b, acc[o]);
+    }
+    if (kc + 1 < nk) store_b(buf ^ 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      va[e] = vb[e];
+      vb[e] = vc[e];
+    }
+    __syncthreads();
+  }
+  // unscale: accumulator register r of a block holds row (r & 3) + 8 (r >> 2) + 4 kh of the wave's 32
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float u = rinv[wave][(r & 3) + 8 * (r >> 2) + 4 * kh];
+#pragma unroll
+    for (int o = 0; o < NB; ++o) acc[o][r] *= u;
+  }
+  __syncthreads();  // (the epilogue stages through the B ring's LDS)
+  rowgemm_epilogue<NB, RX_SHARE>(p, acc, smem, m0, n0, wave, lane);
+}
+
+template <int NB>
+void rowgemm_h3_launch(const RowGemmArgs& p, int nz, hipStream_t s) {
+  dim3 grid((unsigned)((p.M + RG_BM - 1) / RG_BM), (unsigned)((p.N + 32 * NB - 1) / (32 * NB)), (unsigned)nz);
+  hipLaunchKernelGGL(rowgemm_h3_kernel<NB>, grid, dim3(RG_T), 0, s, p);
+}
+
+int rowgemm_h3_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s) {
+  switch (nb > 8 ? 8 : nb) {
+    case 1: rowgemm_h3_launch<1>(p, nz, s); break;
+    case 2: rowgemm_h3_launch<2>(p, nz, s); break;
+    case 3: rowgemm_h3_launch<3>(p, nz, s); break;
+    case 4: rowgemm_h3_launch<4>(p, nz, s); break;
+    case 5: rowgemm_h3_launch<5>(p, nz, s); break;
+    case 6: rowgemm_h3_launch<6>(p, nz, s); break;
+    case 7: rowgemm_h3_launch<7>(p, nz, s); break;
+    default: rowgemm_h3_launch<8>(p, nz, s); break;
+  }
+  return check_launch("rowgemm_h3_kernel");
 }
 
 template <int NOW, int NB2, int JS>

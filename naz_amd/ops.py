@@ -88,6 +88,16 @@ def rowgemm_split(value: Optional[bool] = None) -> bool:
     return bool(r)
 
 
+def rowgemm_h3(value: Optional[bool] = None) -> bool:
+    """The batch-row GEMM's f16x3 form (naz_tuning "rowgemm_h3": A rows split at a per-row
+    power-of-two scale, B at 2^6, three products on the f16 matrix pipe; fp32-grade, other rounding).
+    The caller keeps |B| < 2^9 while it is on.  ``value`` sets it; returns the setting before."""
+    r = int(lib().naz_tuning(b"rowgemm_h3", -1 if value is None else int(bool(value))))
+    if r < 0:
+        check(r, "rowgemm_h3")
+    return bool(r)
+
+
 def rowgemm_fill(value: Optional[int] = None) -> int:
     """The batch-row GEMM's small-batch grid fill (naz_tuning "rowgemm_fill": column panels narrowed
     until the grid holds ``value`` workgroups per CU, 0 = off; no result changes).  Returns the

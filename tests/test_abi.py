@@ -226,7 +226,7 @@ def test_tuning_keys():
     small-batch grid fill (clamped to 16), set and read back; an unknown key is an error."""
     from naz_amd import _lib
     L = _lib.lib()
-    for key, default in ((b"rowgemm_split", 1), (b"rowgemm_x6", 0)):
+    for key, default in ((b"rowgemm_split", 1), (b"rowgemm_x6", 0), (b"rowgemm_h3", 0)):
         cur = L.naz_tuning(key, -1)
         assert cur in (0, 1)
         assert L.naz_tuning(key, 1 - cur) == cur and L.naz_tuning(key, -1) == 1 - cur

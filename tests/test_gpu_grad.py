@@ -169,16 +169,18 @@ def test_rowgemm_config3_shapes():
 
 @pytest.mark.parametrize("N", [168, 172, 300])
 @pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("x6", [False, True])
-def test_rowgemm_panel_split(N, split, x6):
+@pytest.mark.parametrize("arith", ["fp32", "x6", "h3"])
+def test_rowgemm_panel_split(N, split, arith):
     """The batch-row kernel with the panel split on and off (naz_tuning "rowgemm_split"; default on):
     widths of 6 / 6 / 10 column blocks (an odd half-panel at 168 / 172 runs the paired epilogue's
     guard) through every epilogue -- bias + activation (linear_act), the masked dX GEMM, the chained
     act' (gemm_dact), the CNF pair VJP (gemm_jvp_bwd) -- on a ragged row count, against fp64; on both
-    arithmetics (naz_tuning "rowgemm_x6": exact FP32 MFMA, or the bf16x6 split)."""
+    arithmetics (naz_tuning "rowgemm_x6" / "rowgemm_h3": exact FP32 MFMA, the bf16x6 split, or the
+    f16x3 split with per-row power-of-two scales)."""
     from naz_amd import ops
     prev = ops.rowgemm_split(split)
-    prev6 = ops.rowgemm_x6(x6)
+    prev6 = ops.rowgemm_x6(arith == "x6")
+    prevh = ops.rowgemm_h3(arith == "h3")
     prevf = ops.rowgemm_fill(0)  # the panels as the split sets them (4098 rows would be narrowed)
     try:
         g = torch.Generator().manual_seed(N + 11 * split)
@@ -215,7 +217,35 @@ def test_rowgemm_panel_split(N, split, x6):
     finally:
         ops.rowgemm_split(prev)
         ops.rowgemm_x6(prev6)
+        ops.rowgemm_h3(prevh)
         ops.rowgemm_fill(prevf)
+
+
+@pytest.mark.parametrize("N", [64, 172])
+def test_rowgemm_h3_row_scales(N):
+    """The f16x3 batch-row GEMM splits every A row at its own power-of-two scale: rows spanning 10^-30
+    .. 10^30 (gradients have no range), an all-zero row and a ragged row count keep fp32-grade relative
+    accuracy per row in every epilogue's product, against fp64."""
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(N)
+    M, K = 4099, 200
+    A = torch.randn(M, K, generator=g) * torch.pow(10.0, torch.empty(M, 1).uniform_(-30, 30, generator=g))
+    A[5] = 0.0
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    prev = ops.rowgemm_h3(True)
+    try:
+        y = ops.linear_act(_cuda(A), _cuda(W), None, "identity")
+        dx = ops.gemm(_cuda(A), _cuda(W.t().contiguous()))
+    finally:
+        ops.rowgemm_h3(prev)
+    ref = A.double() @ W.double().t()
+    for out, what in ((y, "linear_act"), (dx, "dX")):
+        o = out.double().cpu()
+        scale = ref.abs().amax(1, keepdim=True).clamp_min(1e-300)
+        rel = ((o - ref).abs() / scale).amax(1)
+        assert torch.isfinite(o).all(), what
+        assert float(rel.max()) < 2e-6, (what, float(rel.max()))
+        assert float(o[5].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("M,N", [(10752, 512), (10752, 172), (1000, 300), (70000, 512)])

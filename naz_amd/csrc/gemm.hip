@@ -90,9 +90,9 @@ __global__ void __launch_bounds__(256) gemm_tn128_kernel(int M, int N, int64_t K
                                                          float* __restrict__ Cm, int64_t scm, int64_t scn,
                                                          const float* __restrict__ mask, int64_t smm, int64_t smn,
                                                          int accumulate, int atomic, int64_t k_per_split,
-                                                         float* __restrict__ rowsum) {
-  __shared__ float As[2][GBK][TB + TPAD];
-  __shared__ float Bs[2][GBK][TB + TPAD];
+                                                         float* __restrict__ rowsum, int vec) {
+  __shared__ __attribute__((aligned(16))) float As[2][GBK][TB + TPAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][GBK][TB + TPAD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.x * TB, n0 = blockIdx.y * TB;
@@ -101,8 +101,37 @@ __global__ void __launch_bounds__(256) gemm_tn128_kernel(int M, int N, int64_t K
   const int NE = rowsum != nullptr ? N + 1 : N;  // column N: an all-ones B column -> rowsum
   const int mm = tid & (TB - 1), kq = tid >> 7;  // loader: column mm, k rows kq + 2u
   const int am = m0 + mm, bn = n0 + mm;
+  // vec (16-byte aligned rows of A and B, m / n strides 1): 16-byte loads, thread -> (4 columns
+  // 4 m4 .. 4 m4 + 3, k rows kr and kr + 8): a quarter of the load instructions and address math of
+  // the scalar form (PMC r05: 4.7 VALU per MFMA, two thirds of the wave-cycles issue-stalled)
+  const int m4 = tid & 31, kr = tid >> 5;
   float ra[8], rb[8];
+  auto ld4 = [&](const float* __restrict__ base, int64_t sk, int64_t k, int c0, int lim, bool ones) {
+    float4 v = {0.f, 0.f, 0.f, 0.f};
+    if (k < kend) {
+      if (c0 + 3 < lim) {
+        v = *reinterpret_cast<const float4*>(base + k * sk + c0);
+      } else {  // the ragged last group (and the rowsum's all-ones column N)
+        float t[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[e] = c0 + e < lim ? base[k * sk + c0 + e] : ((ones && c0 + e == N) ? 1.f : 0.f);
+        v = {t[0], t[1], t[2], t[3]};
+      }
+    }
+    return v;
+  };
   auto load = [&](int64_t k0) {
+    if (vec) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t k = k0 + kr + 8 * u;
+        const float4 a = ld4(A, sak, k, m0 + 4 * m4, M, false);
+        const float4 b = ld4(Bm, sbk, k, n0 + 4 * m4, N, NE > N);
+        ra[4 * u] = a.x; ra[4 * u + 1] = a.y; ra[4 * u + 2] = a.z; ra[4 * u + 3] = a.w;
+        rb[4 * u] = b.x; rb[4 * u + 1] = b.y; rb[4 * u + 2] = b.z; rb[4 * u + 3] = b.w;
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int64_t k = k0 + kq + 2 * u;
@@ -112,6 +141,14 @@ __global__ void __launch_bounds__(256) gemm_tn128_kernel(int M, int N, int64_t K
     }
   };
   auto store = [&](int buf) {
+    if (vec) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        *reinterpret_cast<float4*>(&As[buf][kr + 8 * u][4 * m4]) = {ra[4 * u], ra[4 * u + 1], ra[4 * u + 2], ra[4 * u + 3]};
+        *reinterpret_cast<float4*>(&Bs[buf][kr + 8 * u][4 * m4]) = {rb[4 * u], rb[4 * u + 1], rb[4 * u + 2], rb[4 * u + 3]};
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       As[buf][kq + 2 * u][mm] = ra[u];
@@ -236,8 +273,10 @@ int gemm(int M, int N, int64_t K, const float* A, int64_t sam, int64_t sak, cons
   const int atomic = splits > 1 ? 1 : 0;
   if (tn) {  // the batch reduction with wide outputs: 128 x 128 tiles
     dim3 g128((unsigned)((M + TB - 1) / TB), (unsigned)((NE + TB - 1) / TB), (unsigned)splits);
+    const auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    const int vec = a16(A) && a16(B) && sak % 4 == 0 && sbk % 4 == 0;
     hipLaunchKernelGGL(gemm_tn128_kernel, g128, dim3(256), 0, s, M, N, K, A, sak, B, sbk, C, scm, scn, mask, smm, smn,
-                       accumulate, atomic, kps, rowsum);
+                       accumulate, atomic, kps, rowsum, vec);
     return check_launch("gemm_tn128_kernel");
   }
   dim3 grid((unsigned)((M + GBM - 1) / GBM), (unsigned)((NE + GBN - 1) / GBN), (unsigned)splits);

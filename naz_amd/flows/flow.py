@@ -11,6 +11,7 @@ kernels through the Transform objects.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -395,6 +396,24 @@ class _MafTrainFn(torch.autograd.Function):
         return (None, None, None, *outs)
 
 
+# layer l's dW reductions on a side stream while layer l + 1's backward kernel runs (default on:
+# 164.4 / 165.5 -> 156.6 / 158.6 ms per 2^23-row step, profiles/r05_g17_*; NAZ_TRAIN_DW_STREAM=0 off)
+_DW_STREAM = os.environ.get("NAZ_TRAIN_DW_STREAM", "1") == "1"
+_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _SIDE:
+        _SIDE[i] = torch.cuda.Stream(dev)
+    return _SIDE[i]
+
+
+def _nullcontext():
+    import contextlib
+    return contextlib.nullcontext()
+
+
 class _CouplingTrainFn(torch.autograd.Function):
     """NormalizingFlow.log_prob of an nsc flow under autograd (naz train's loss, train_flows.py:
     195, 208).  forward: naz_coupling_log_prob_train (all layers, one launch, layer inputs
@@ -439,32 +458,62 @@ class _CouplingTrainFn(torch.autograd.Function):
         valid = rows >= 0
         cols, orow = torch.nonzero(valid).flatten(), rows[valid]
         f32 = dict(device=dev, dtype=torch.float32)
-        bufs = {"h1": torch.empty((B, H), **f32), "h2": torch.empty((B, H), **f32),
-                "dp1": torch.empty((B, H), **f32), "dp2": torch.empty((B, H), **f32),
-                "dp3": torch.empty((B, rows.numel()), **f32), "x0": torch.empty((B, C + S), **f32)}
+
+        def operand_set():
+            return {"h1": torch.empty((B, H), **f32), "h2": torch.empty((B, H), **f32),
+                    "dp1": torch.empty((B, H), **f32), "dp2": torch.empty((B, H), **f32),
+                    "dp3": torch.empty((B, rows.numel()), **f32), "x0": torch.empty((B, C + S), **f32)}
+
+        # layer l's dW reductions on a side stream, overlapping layer l + 1's backward kernel (two
+        # operand sets; fork / join by events, capture-safe; NAZ_TRAIN_DW_STREAM=0: one stream)
+        overlap = _DW_STREAM and dev.type == "cuda"
+        sets = [operand_set(), operand_set()] if overlap else [operand_set()]
+        main = torch.cuda.current_stream(dev) if overlap else None
+        side = _side_stream(dev) if overlap else None
+        done = [None, None]  # the side stream's event after the dW of the last layer that used set i
         n_low = S * (3 * K - 1) if lower else 0
         g_low = torch.zeros((L, max(n_low, 1)), **f32)
         P = 3 * K - 1
         per = 9 if lower else 6
         grads = [None] * ctx.n_params
-        gw2p = torch.empty((rows.numel(), H), **f32)
-        gb2p = torch.empty((rows.numel(),), **f32)
         for l in range(L):
+            si = l % len(sets)
+            bufs = sets[si]
+            if overlap and done[si] is not None:
+                main.wait_event(done[si])  # this set's previous dW reads are over
             ops.coupling_bwd_layer(d, ctx.packed, ctx.pbwd, ctx.flat, l, states[l + 1], context, g, g_lp, bufs, g_next,
                                    g_low[l] if lower else None)
             gW0, gb0 = torch.empty((H, C + S), **f32), torch.empty((H,), **f32)
             gW1, gb1 = torch.empty((H, H), **f32), torch.empty((H,), **f32)
-            ops.gemm(bufs["dp1"].t(), bufs["x0"], out=gW0, rowsum=gb0)
-            ops.gemm(bufs["dp2"].t(), bufs["h1"], out=gW1, rowsum=gb1)
-            ops.gemm(bufs["dp3"].t(), bufs["h2"], out=gw2p, rowsum=gb2p)
-            gW2 = torch.zeros(((D - S) * P, H), **f32).index_copy_(0, orow, gw2p.index_select(0, cols))
-            gb2 = torch.zeros(((D - S) * P,), **f32).index_copy_(0, orow, gb2p.index_select(0, cols))
+            gW2 = torch.zeros(((D - S) * P, H), **f32)
+            gb2 = torch.zeros(((D - S) * P,), **f32)
+            gw2p = torch.empty((rows.numel(), H), **f32)
+            gb2p = torch.empty((rows.numel(),), **f32)
+            if overlap:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                for t in (gW0, gb0, gW1, gb1, gW2, gb2, gw2p, gb2p, *bufs.values()):
+                    t.record_stream(side)
+            with torch.cuda.stream(side) if overlap else _nullcontext():
+                ops.gemm(bufs["dp1"].t(), bufs["x0"], out=gW0, rowsum=gb0)
+                ops.gemm(bufs["dp2"].t(), bufs["h1"], out=gW1, rowsum=gb1)
+                ops.gemm(bufs["dp3"].t(), bufs["h2"], out=gw2p, rowsum=gb2p)
+                gW2.index_copy_(0, orow, gw2p.index_select(0, cols))
+                gb2.index_copy_(0, orow, gb2p.index_select(0, cols))
+            if overlap:
+                done[si] = torch.cuda.Event()
+                done[si].record(side)
             out = [gW0, gb0, gW1, gb1, gW2, gb2]
             if lower:
                 gl = g_low[l]
                 out += [gl[:S * K].view(S, K), gl[S * K:2 * S * K].view(S, K), gl[2 * S * K:].view(S, K - 1)]
             grads[l * per:(l + 1) * per] = out
             g, g_next = g_next, g
+        if overlap:
+            for e in done:
+                if e is not None:
+                    main.wait_event(e)  # the gradients are read on the main stream
         return (None, None, None, None, *grads)
 
 

@@ -280,6 +280,35 @@ def test_fused_train_path_vs_oracle_and_walk(monkeypatch, shape):
         assert rel < 5e-3, f"{k}: fused vs walk {rel:.2e}"
 
 
+@pytest.mark.parametrize("shape", [(16, 32, 8, 8), (8, 0, 4, 6)])
+def test_fused_train_dw_side_stream_matches(monkeypatch, shape):
+    """NAZ_TRAIN_DW_STREAM: layer l's dW reductions on a side stream while layer l + 1's backward
+    runs (two operand sets, event fork / join) give the gradients of the one-stream backward (to the
+    dW kernels' atomic-order rounding), on a batch large enough for the kernels to overlap."""
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import flow as flow_mod
+    from naz_amd.flows import io as fio
+    D, C, S, L = shape
+    spec = dict(flow_type="nsc", D=D, C=C, hidden=[128, 128], L=L, K=8, split=S)
+    state = {k: v.numpy() for k, v in O.random_state(spec, seed=23).items()}
+    x = torch.as_tensor(O.gaussian_mixture(1 << 16, D, seed=4), device=DEV)
+    c = torch.as_tensor(O.context_normal(1 << 16, C, seed=5), device=DEV) if C else None
+    res = {}
+    for side in (False, True):
+        monkeypatch.setattr(flow_mod, "_DW_STREAM", side)
+        f = NormalizingFlow("nsc", None, D, C, [128, 128], L, 8, S)
+        fio.load_state(f, state)
+        assert f._plan.train_ready(x, c)
+        lp = f.log_prob(x, condition=c)
+        (-lp.mean()).backward()
+        torch.cuda.synchronize()
+        res[side] = {k: p.grad.detach().clone() for k, p in fio.named_state_params(f).items()}
+    for k, a in res[False].items():
+        b = res[True][k]
+        rel = float((a - b).norm() / a.norm().clamp_min(1e-30))
+        assert rel < 1e-5, f"{k}: side-stream dW vs one stream {rel:.2e}"
+
+
 def test_fused_train_full_size_properties():
     """The training forward (coupling_r16_kernel VAR=1, the ring protocol of the metric kernel)
     and the fused backward at BASELINE's 2^20 rows: finite, deterministic and chunk-invariant

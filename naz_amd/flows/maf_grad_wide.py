@@ -49,6 +49,9 @@ from .. import ops
 # dW: one strided GEMM per block (measured faster than the batch-reduction kernel on these strided
 # views: 222 vs 254 ms per 2^16-row maf4 step, profiles/r04_s10_*); NAZ_MAF_WIDE_WGRAD=1 = the latter
 _ONE_DW_GEMM = os.environ.get("NAZ_MAF_WIDE_WGRAD", "0") != "1"
+# the dW reductions on a side stream beside the chain's next transposed product (NAZ_MAF_WIDE_DW_STREAM)
+_DW_STREAM = os.environ.get("NAZ_MAF_WIDE_DW_STREAM", "1") == "1"
+_SIDE = {}
 
 
 class WideMafGrad:
@@ -81,6 +84,8 @@ class WideMafGrad:
             raise ValueError("WideMafGrad: mask does not match the flow's flat parameter count")
         self.ws = torch.zeros(L * o, device=dev, dtype=torch.float32)
         self._bufs = {}
+        self._main = self._side = None  # streams of the running backward (side: dW reductions)
+        self._evs = []                   # side-stream events, one per submitted reduction
         # unit blocks [a, b) on 4-unit boundaries (the GEMMs store 16-byte row pieces): one per
         # degree class, a class start rounded down; the units past the last class of degree < D are
         # dropped (rounded up).  Per block: fwd_k = the inputs its forward product reads, k0 = the
@@ -197,6 +202,25 @@ class WideMafGrad:
                 ops.gemm(gv[:, r0:r1].t(), xv[:, c0:c1], out=out[r0:r1, c0:c1], accumulate=True,
                          rowsum=rowsum[r0:r1] if (last and rowsum is not None) else None)
 
+    def _wg(self, gv: Tensor, xv: Tensor, out: Tensor, rowsum: Optional[Tensor]) -> None:
+        """_wgrad on the side stream (after everything the main stream has queued), or inline."""
+        if self._side is None:
+            self._wgrad(gv, xv, out, rowsum)
+            return
+        ev = torch.cuda.Event()
+        ev.record(self._main)
+        self._side.wait_event(ev)
+        with torch.cuda.stream(self._side):
+            self._wgrad(gv, xv, out, rowsum)
+        done = torch.cuda.Event()
+        done.record(self._side)
+        self._evs.append(done)
+
+    def _after(self, k: int) -> None:
+        """The main stream waits for the side stream's first k reductions (in order: the k-th)."""
+        if self._side is not None and 0 < k <= len(self._evs):
+            self._main.wait_event(self._evs[k - 1])
+
     def _chain(self, a: Tensor, W, h, P: int, b: dict, dw=None) -> Tensor:
         """The transposed products of one chain, output layer first, over the units [0, P): a = dL/d
         (MADE output) [B, 2D] -> dL/d(first hidden pre-activation) [B, :P].  ``dw``: the layer's dW
@@ -204,11 +228,16 @@ class WideMafGrad:
         NH = self.desc.n_hidden
         blks = [(a0, min(b0, P), fk, k0) for (a0, b0, fk, k0) in self.blocks if a0 < P]
         dl = ops.gemm_dact(a, W[NH][0][:, :P], h[NH - 1][:, :P], "tanh", out=b["da"][:, :P])
+        prev = len(self._evs)  # reductions submitted before the previous step's
         for i in range(NH - 1, 0, -1):
             if dw is not None:
+                # (reads dl and h[i - 1]; dl's buffer is written again two steps on)
                 for (a0, b0, fk, _) in blks:
-                    self._wgrad(dl[:, a0:b0], h[i - 1][:, :fk], dw[i][0][a0:b0, :fk], dw[i][1][a0:b0])
+                    self._wg(dl[:, a0:b0], h[i - 1][:, :fk], dw[i][0][a0:b0, :fk], dw[i][1][a0:b0])
             nxt = b["db"] if dl.data_ptr() == b["da"].data_ptr() else b["da"]
+            if dw is not None:  # nxt was the previous step's dl: its reductions must be over
+                self._after(prev)
+                prev = len(self._evs)
             for (a0, b0, _, k0) in blks:
                 ops.gemm_dact(dl[:, k0:P], W[i][0][k0:P, a0:b0], h[i - 1][:, a0:b0], "tanh", out=nxt[:, a0:b0])
             dl = nxt[:, :P]
@@ -226,6 +255,14 @@ class WideMafGrad:
         if B == 0:
             return self.ws * self.mask, torch.zeros((0, D), device=self.dev)
         g_lp = b["ones"] if g_lp is None else g_lp.to(self.dev).contiguous()  # fp32 (checked by the kernels)
+        if _DW_STREAM and self.dev.type == "cuda":
+            self._main = torch.cuda.current_stream(self.dev)
+            i = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+            if i not in _SIDE:
+                _SIDE[i] = torch.cuda.Stream(self.dev)
+            self._side, self._evs = _SIDE[i], []
+        else:
+            self._main = self._side = None
         g, g_next = b["g"], b["g_next"]
         g.copy_(ops.base_log_prob_bwd(states[0], g_lp))  # d/dz of the Normal(0, I) base log-density
         h, raw, tot, chain = b["h"], b["raw"], b["tot"], b["chain"]
@@ -234,6 +271,7 @@ class WideMafGrad:
         if ctx is not None and C > 0:
             cb = ctx.reshape(1, C).expand(B, C) if ctx.dim() == 1 or ctx.shape[0] == 1 else ctx
         for l in range(L):
+            self._after(len(self._evs))  # the previous layer's reductions read h, tot and da / db
             s = states[l]
             W = self._views(wflat, l)
             G = self._views(self.ws, l)
@@ -258,12 +296,14 @@ class WideMafGrad:
             ops.maf_dim_vjp(raw, s, g, g_lp, int(self.perms[l, 0]), g_next, tot, chain=None,
                             clip_zero=self.clip_zero)
             # 3. the total δ's and this layer's dW / db
-            self._wgrad(tot, h[NH - 1][:, :A], G[NH][0][:, :A], G[NH][1])
+            self._wg(tot, h[NH - 1][:, :A], G[NH][0][:, :A], G[NH][1])
             dl = self._chain(tot, W, h, A, b, dw=G)
             if cb is not None:
-                self._wgrad(dl, cb, G[0][0][:A, :C], None)
-            self._wgrad(dl, s, G[0][0][:A, C:], G[0][1][:A])
+                self._wg(dl, cb, G[0][0][:A, :C], None)
+            self._wg(dl, s, G[0][0][:A, C:], G[0][1][:A])
             g, g_next = g_next, g
+        self._after(len(self._evs))  # the workspace is read on the main stream
+        self._main = self._side = None
         return self.ws * self.mask, g
 
     def __call__(self, flat: Tensor, x: Tensor, ctx: Optional[Tensor]) -> Tuple[Tensor, Tensor]:

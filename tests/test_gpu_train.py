@@ -415,6 +415,38 @@ def test_config3_ar_maf_train_path_vs_oracle_and_walk(monkeypatch, ctx_rows, B):
     _maf_train_vs_oracle_and_walk(monkeypatch, 16, 32, [128, 128], 3, B, ctx_rows, "composed maf D16C32")
 
 
+def test_wide_maf_dw_side_stream_matches():
+    """NAZ_MAF_WIDE_DW_STREAM: the composed wide-maf backward's dW reductions on a side stream beside
+    the chain's next transposed product (event-ordered reuse of the two delta buffers and of the layer's
+    activations) give the one-stream gradients, to the reductions' atomic-order rounding."""
+    from naz_amd.flows import maf_grad_wide as mgw
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    spec = dict(flow_type="maf", D=4, C=2, hidden=[512] * 5, L=3)
+    state = {k: v.numpy() for k, v in O.random_state(spec, seed=33).items()}
+    B = 10752
+    x = torch.as_tensor(O.gaussian_mixture(B, 4, seed=6), device=DEV)
+    c = torch.as_tensor(O.context_normal(B, 2, seed=7), device=DEV)
+    res = {}
+    prev = mgw._DW_STREAM
+    try:
+        for side in (False, True):
+            mgw._DW_STREAM = side
+            f = NormalizingFlow("maf", None, 4, 2, [512] * 5, 3)
+            fio.load_state(f, state)
+            f = f.to(DEV)
+            lp = f.log_prob(x, condition=c)
+            (-lp.mean()).backward()
+            torch.cuda.synchronize()
+            res[side] = {k: p.grad.detach().clone() for k, p in fio.named_state_params(f).items()}
+    finally:
+        mgw._DW_STREAM = prev
+    for k, a in res[False].items():
+        b = res[True][k]
+        rel = float((a - b).norm() / a.norm().clamp_min(1e-30))
+        assert rel < 1e-5, f"{k}: side-stream dW vs one stream {rel:.2e}"
+
+
 def test_graphed_nll_step_matches_eager_steps():
     """trainers.GraphedNllStep (the whole NLL step -- wide maf forward kernel, the GEMM-composed
     backward, clip, capturable Adam -- replayed as one captured HIP graph) takes the same steps as

@@ -51,6 +51,8 @@ from .. import ops
 _ONE_DW_GEMM = os.environ.get("NAZ_MAF_WIDE_WGRAD", "0") != "1"
 # the dW reductions on a side stream beside the chain's next transposed product (NAZ_MAF_WIDE_DW_STREAM)
 _DW_STREAM = os.environ.get("NAZ_MAF_WIDE_DW_STREAM", "1") == "1"
+# ... and the next layer's dense pass on a second stream (NAZ_MAF_WIDE_DENSE_STREAM; needs the first)
+_DENSE_STREAM = os.environ.get("NAZ_MAF_WIDE_DENSE_STREAM", "1") == "1"
 _SIDE = {}
 
 
@@ -84,7 +86,8 @@ class WideMafGrad:
             raise ValueError("WideMafGrad: mask does not match the flow's flat parameter count")
         self.ws = torch.zeros(L * o, device=dev, dtype=torch.float32)
         self._bufs = {}
-        self._main = self._side = None  # streams of the running backward (side: dW reductions)
+        self._main = self._side = self._dense = None  # streams of the running backward (side: dW
+        # reductions; dense: the next layer's dense pass)
         self._evs = []                   # side-stream events, one per submitted reduction
         # unit blocks [a, b) on 4-unit boundaries (the GEMMs store 16-byte row pieces): one per
         # degree class, a class start rounded down; the units past the last class of degree < D are
@@ -167,6 +170,8 @@ class WideMafGrad:
             b = dict(states=torch.empty((d.L, B, d.D), **f32), lp=torch.empty((B,), **f32),
                      g=torch.empty((B, d.D), **f32), g_next=torch.empty((B, d.D), **f32),
                      h=[torch.zeros((B, d.H), **f32) for _ in range(d.n_hidden)],
+                     h2=[torch.zeros((B, d.H), **f32) for _ in range(d.n_hidden)] if _DW_STREAM else None,
+                     raw2=torch.empty((B, 2 * d.D), **f32) if _DW_STREAM else None,
                      da=torch.empty((B, d.H), **f32), db=torch.empty((B, d.H), **f32),
                      raw=torch.empty((B, 2 * d.D), **f32), tot=torch.empty((B, 2 * d.D), **f32),
                      chain=torch.empty((B, 2 * d.D), **f32), ones=torch.ones((B,), **f32))
@@ -260,7 +265,9 @@ class WideMafGrad:
             i = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
             if i not in _SIDE:
                 _SIDE[i] = torch.cuda.Stream(self.dev)
-            self._side, self._evs = _SIDE[i], []
+            if (i, 1) not in _SIDE:
+                _SIDE[(i, 1)] = torch.cuda.Stream(self.dev)
+            self._side, self._dense, self._evs = _SIDE[i], _SIDE[(i, 1)], []
         else:
             self._main = self._side = None
         g, g_next = b["g"], b["g_next"]
@@ -270,20 +277,46 @@ class WideMafGrad:
         cb = None
         if ctx is not None and C > 0:
             cb = ctx.reshape(1, C).expand(B, C) if ctx.dim() == 1 or ctx.shape[0] == 1 else ctx
-        for l in range(L):
-            self._after(len(self._evs))  # the previous layer's reductions read h, tot and da / db
-            s = states[l]
-            W = self._views(wflat, l)
-            G = self._views(self.ws, l)
-            fo = self.foff[l]
+        def dense(l, h, raw):
             # 1. the dense MADE pass on (ctx, s_l), the units that reach an output only
-            ops.linear_act(s, W[0][0][:A], W[0][1][:A], "tanh", context=ctx if C > 0 else None, out=h[0][:, :A])
+            W, fo = self._views(wflat, l), self.foff[l]
+            ops.linear_act(states[l], W[0][0][:A], W[0][1][:A], "tanh", context=ctx if C > 0 else None, out=h[0][:, :A])
             for i in range(1, NH):
                 for (a0, b0, fk, _), o0 in zip(self.blocks, fo[i - 1]):
                     ops.linear_act(h[i - 1][:, :fk], fimg[o0:o0 + (b0 - a0) * fk].view(b0 - a0, fk), W[i][1][a0:b0],
                                    "tanh", out=h[i][:, a0:b0])
             o0 = fo[NH - 1][0]
             ops.linear_act(h[NH - 1][:, :A], fimg[o0:o0 + 2 * D * A].view(2 * D, A), W[NH][1], "identity", out=raw)
+
+        # with the side streams: layer l + 1's dense pass (it reads only s_{l+1} and the weights) runs on
+        # a second stream into the other activation set while layer l's chains run
+        two = _DENSE_STREAM and self._side is not None and b["h2"] is not None
+        sets = [(h, raw), (b["h2"], b["raw2"])] if two else [(h, raw)]
+        dense_ev = {}
+
+        def submit_dense(l):
+            ev = torch.cuda.Event()
+            ev.record(self._main)
+            self._dense.wait_event(ev)
+            with torch.cuda.stream(self._dense):
+                dense(l, *sets[l % 2])
+            dense_ev[l] = torch.cuda.Event()
+            dense_ev[l].record(self._dense)
+
+        if len(sets) == 2:
+            submit_dense(0)
+        for l in range(L):
+            self._after(len(self._evs))  # the previous layer's reductions read h, tot and da / db
+            s = states[l]
+            W = self._views(wflat, l)
+            G = self._views(self.ws, l)
+            h, raw = sets[l % len(sets)]
+            if len(sets) == 2:
+                self._main.wait_event(dense_ev.pop(l))
+                if l + 1 < L:  # (its set's readers: layer l - 1's chains and reductions, all behind us)
+                    submit_dense(l + 1)
+            else:
+                dense(l, h, raw)
             # 2. the inverse's sequential dependence, last order first: dim d_p's outputs reach the
             #    units of degree <= p only
             for p in range(D - 1, 0, -1):

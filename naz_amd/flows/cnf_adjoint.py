@@ -31,6 +31,7 @@ RK4 combinations.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -45,6 +46,40 @@ def _pairs(B: int, N: int, like: torch.Tensor) -> torch.Tensor:
     npad = (N + 3) // 4 * 4
     t = torch.empty((2 * B, npad), device=like.device, dtype=like.dtype)
     return t[:, :N] if npad != N else t
+
+
+# The weight / bias gradient reductions of a VJP only read its adjoints and saved activations, so they
+# run on a side stream beside the next layer's input-adjoint GEMM (NAZ_CNF_DW_STREAM, default on); the
+# caller joins with _join_reductions before reading the gradients.
+_DW_STREAM = os.environ.get("NAZ_CNF_DW_STREAM", "1") == "1"
+_SIDE = {}
+
+
+def _reductions(dev):
+    """fn(fn, *tensors_read): run fn on the device's reduction stream after everything the current
+    stream has queued (the tensors it reads are kept from the allocator until it is done), or inline."""
+    if not (_DW_STREAM and dev.type == "cuda"):
+        return lambda fn, *ts: fn()
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _SIDE:
+        _SIDE[i] = torch.cuda.Stream(dev)
+    side, main = _SIDE[i], torch.cuda.current_stream(dev)
+
+    def run(fn, *ts):
+        ev = torch.cuda.Event()
+        ev.record(main)
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            fn()
+        for t in ts:
+            t.record_stream(side)
+    return run
+
+
+def _join_reductions(dev) -> None:
+    i = dev.index if dev.index is not None else (torch.cuda.current_device() if dev.type == "cuda" else None)
+    if dev.type == "cuda" and i in _SIDE:
+        torch.cuda.current_stream(dev).wait_stream(_SIDE[i])
 
 
 class CnfWalk:
@@ -97,16 +132,18 @@ class CnfWalk:
         G = _pairs(B, D, g_k)  # output adjoints in row pairs: (g_f, g_(J eps)) = (g_k, -g_t eps)
         G[0::2] = g_k
         G[1::2] = -g_t[:, None] * eps
-        ops.gemm(G.t(), saved[-1], out=gW[-1], accumulate=True)
-        ops.colsum(g_k, out=gb[-1])
+        red = _reductions(g_k.device)
+        red(lambda G=G: (ops.gemm(G.t(), saved[-1], out=gW[-1], accumulate=True), ops.colsum(g_k, out=gb[-1])),
+            G, g_k, saved[-1])
         W_next = self.W[-1]
         for i in reversed(range(n - 1)):
             GP = ops.gemm_jvp_bwd(G, W_next, saved[i + 1], self.act)  # pre-activation adjoints, pairs
-            ops.colsum(GP[0::2], out=gb[i])
             if i > 0:
-                ops.gemm(GP.t(), saved[i], out=gW[i], accumulate=True)
+                red(lambda GP=GP, i=i: (ops.colsum(GP[0::2], out=gb[i]),
+                                        ops.gemm(GP.t(), saved[i], out=gW[i], accumulate=True)), GP, saved[i])
                 G, W_next = GP, self.W[i]
                 continue
+            ops.colsum(GP[0::2], out=gb[i])
             S0 = torch.zeros((2 * B, D + C), device=z.device, dtype=z.dtype)  # pairs ([z, ctx], [eps, 0])
             S0[0::2, :D] = z
             S0[1::2, :D] = eps
@@ -327,6 +364,7 @@ class CnfSolveFn(Function):
                 h = (t1 - t0) / ctx.checkpoints
                 for n in reversed(range(ctx.checkpoints)):
                     lam = _rk4_step_adjoint(walk, xs[n], context, eps, h, lam, mu, gW, gb, g_ctx)
+        _join_reductions(dev)
         if g_ctx is not None:
             g_ctx = g_ctx.reshape(context.shape)
         grads = [t for pair in zip(gW, gb) for t in pair]

@@ -110,6 +110,28 @@ def test_cnf_rk4_gradient_vs_oracle_autograd(D, C, hidden, L, act):
         assert_parity(_np(g[k]), ref64, ref32, what=f"cnf d/d{k}", floor=grad_floor(ref64), count_factor=None)
 
 
+def test_cnf_reductions_side_stream_match():
+    """NAZ_CNF_DW_STREAM: the VJP's weight / bias reductions on a side stream beside the next layer's
+    input-adjoint GEMM (joined before the gradients are read) give the one-stream gradients, to the
+    reductions' atomic-order rounding, at a batch where the kernels overlap."""
+    from naz_amd.flows import cnf_adjoint as adj
+    res = {}
+    prev = adj._DW_STREAM
+    try:
+        for side in (False, True):
+            adj._DW_STREAM = side
+            spec, state, f, x, c, eps, w = _setup(16, 0, [128, 128, 128], 1, "softplus", B=1 << 15, seed=3)
+            res[side] = _product_grads(f, x, c, eps, w)
+            torch.cuda.synchronize()
+    finally:
+        adj._DW_STREAM = prev
+    assert torch.equal(res[False][0], res[True][0])
+    for k, a in res[False][1].items():
+        b = res[True][1][k]
+        rel = float((a - b).norm() / a.norm().clamp_min(1e-30))
+        assert rel < 1e-5, f"{k}: side-stream reductions vs one stream {rel:.2e}"
+
+
 def test_cnf_broadcast_context_gradient():
     """One context row for the whole batch (naz sample/log_prob with condition=[C]): its gradient
     is the sum over rows."""

@@ -76,6 +76,18 @@ def _reductions(dev):
     return run
 
 
+_PREFETCH = os.environ.get("NAZ_CNF_PREFETCH", "1") == "1"
+
+
+def _prefetch_stream(dev):
+    if not (_PREFETCH and dev.type == "cuda"):
+        return None
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if (i, 1) not in _SIDE:
+        _SIDE[(i, 1)] = torch.cuda.Stream(dev)
+    return _SIDE[(i, 1)]
+
+
 def _join_reductions(dev) -> None:
     i = dev.index if dev.index is not None else (torch.cuda.current_device() if dev.type == "cuda" else None)
     if dev.type == "cuda" and i in _SIDE:
@@ -256,13 +268,20 @@ def walk_dopri5(walk: CnfWalk, x: torch.Tensor, ctx, eps: torch.Tensor, t0: floa
     return y, a, (nfe if t == t1 else -nfe)
 
 
-def _rk4_step_adjoint(walk, x, ctx, eps, h, lam, mu, gW, gb, g_ctx):
-    """Discrete adjoint of one classical RK4 step from checkpoint x (naz odeint.py:46-52)."""
+def _rk4_stages(walk, x, ctx, eps, h):
+    """The four RK4 stages' saved activations of one step from checkpoint x (naz odeint.py:46-52)."""
     k1, _, s1 = walk.rhs(x, ctx, eps)
     k2, _, s2 = walk.rhs(x + 0.5 * h * k1, ctx, eps)
     k3, _, s3 = walk.rhs(x + 0.5 * h * k2, ctx, eps)
     _, _, s4 = walk.rhs(x + h * k3, ctx, eps)
-    del k1, k2, k3
+    return s1, s2, s3, s4
+
+
+def _rk4_step_adjoint(walk, x, ctx, eps, h, lam, mu, gW, gb, g_ctx, stages=None):
+    """Discrete adjoint of one classical RK4 step from checkpoint x (naz odeint.py:46-52); ``stages``:
+    the step's recomputed stages when the caller already has them."""
+    s1, s2, s3, s4 = _rk4_stages(walk, x, ctx, eps, h) if stages is None else stages
+    del stages
     w1, w2 = h / 6.0, h / 3.0
     gz4 = walk.vjp(s4, ctx, eps, w1 * lam, w1 * mu, gW, gb, g_ctx)
     del s4
@@ -362,8 +381,27 @@ class CnfSolveFn(Function):
                 lam = _continuous_adjoint(walk, y1, context, eps, t0, t1, core.adjoint_steps, lam, mu, gW, gb, g_ctx)
             else:
                 h = (t1 - t0) / ctx.checkpoints
+                # the next (earlier) step's forward recompute on its own stream while this step's
+                # VJPs run: the recompute reads only its checkpoint (NAZ_CNF_PREFETCH, default on)
+                rec = _prefetch_stream(dev)
+                main = torch.cuda.current_stream(dev) if rec is not None else None
+                nxt = None
                 for n in reversed(range(ctx.checkpoints)):
-                    lam = _rk4_step_adjoint(walk, xs[n], context, eps, h, lam, mu, gW, gb, g_ctx)
+                    stages, nxt = nxt, None
+                    if rec is not None and n > 0:
+                        ev = torch.cuda.Event()
+                        ev.record(main)
+                        rec.wait_event(ev)
+                        with torch.cuda.stream(rec):
+                            nxt = _rk4_stages(walk, xs[n - 1], context, eps, h)
+                        done = torch.cuda.Event()
+                        done.record(rec)
+                    lam = _rk4_step_adjoint(walk, xs[n], context, eps, h, lam, mu, gW, gb, g_ctx, stages=stages)
+                    if nxt is not None:
+                        main.wait_event(done)
+                        for sv in nxt:  # made on the prefetch stream, read on this one
+                            for t in sv:
+                                t.record_stream(main)
         _join_reductions(dev)
         if g_ctx is not None:
             g_ctx = g_ctx.reshape(context.shape)

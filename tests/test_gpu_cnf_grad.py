@@ -111,20 +111,21 @@ def test_cnf_rk4_gradient_vs_oracle_autograd(D, C, hidden, L, act):
 
 
 def test_cnf_reductions_side_stream_match():
-    """NAZ_CNF_DW_STREAM: the VJP's weight / bias reductions on a side stream beside the next layer's
-    input-adjoint GEMM (joined before the gradients are read) give the one-stream gradients, to the
-    reductions' atomic-order rounding, at a batch where the kernels overlap."""
+    """NAZ_CNF_DW_STREAM / NAZ_CNF_PREFETCH: the VJP's weight / bias reductions on a side stream beside
+    the next layer's input-adjoint GEMM, and the next RK4 step's forward recompute on another beside
+    this step's VJPs (joined before use) give the one-stream gradients, to the reductions' atomic-order
+    rounding, at a batch where the kernels overlap."""
     from naz_amd.flows import cnf_adjoint as adj
     res = {}
-    prev = adj._DW_STREAM
+    prev = adj._DW_STREAM, adj._PREFETCH
     try:
-        for side in (False, True):
-            adj._DW_STREAM = side
+        for side in (False, True):  # (with it: the next RK4 step's recompute on its own stream too)
+            adj._DW_STREAM = adj._PREFETCH = side
             spec, state, f, x, c, eps, w = _setup(16, 0, [128, 128, 128], 1, "softplus", B=1 << 15, seed=3)
             res[side] = _product_grads(f, x, c, eps, w)
             torch.cuda.synchronize()
     finally:
-        adj._DW_STREAM = prev
+        adj._DW_STREAM, adj._PREFETCH = prev
     assert torch.equal(res[False][0], res[True][0])
     for k, a in res[False][1].items():
         b = res[True][1][k]

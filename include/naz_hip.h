@@ -75,7 +75,7 @@ int naz_image_attach(const void* image, int64_t bytes, void* stream);
  * naz_gemm_jvp_bwd, naz_gemm's dX shape) runs outputs wider than 128 columns as balanced panels of at
  * most 128 (1, default; NAZ_RG_SPLIT in the environment sets the initial value) or as one (0).  "rowgemm_fill":
  * for short batches it narrows the column panels until the grid holds this many workgroups per CU
- * (0 = off, at most 16; default 4, NAZ_RG_FILL).  Neither changes a result.  "rowgemm_x6": its
+ * (0 = off, at most 16; default 2, NAZ_RG_FILL).  Neither changes a result.  "rowgemm_x6": its
  * arithmetic, exact FP32 MFMA (0, default; NAZ_RG_X6) or the bf16x6 split (1: fp32-grade, other
  * rounding).  value >= 0 sets one; returns the value before the call (-1 and an error for an unknown
  * key). */

@@ -360,10 +360,12 @@ int rowgemm_h3_setting(int v) {
 }
 
 int rowgemm_fill_setting(int v) {
-  // NAZ_RG_FILL at first use, else 4 workgroups (= waves per SIMD) per CU
+  // NAZ_RG_FILL at first use, else 2 workgroups (= waves per SIMD) per CU (with the wide-maf step's
+  // side streams: 163.5 ms at 2^16 rows vs 168.5 at 4 and 179.5 at 8; 10,752 rows 49.3 vs 48.7 / 48.9;
+  // profiles/r05_g25_*)
   static std::atomic<int> cur{[] {
     const char* e = getenv("NAZ_RG_FILL");
-    const int f = e ? atoi(e) : 4;
+    const int f = e ? atoi(e) : 2;
     return f < 0 ? 0 : (f > 16 ? 16 : f);
   }()};
   return v >= 0 ? cur.exchange(v > 16 ? 16 : v) : cur.load();

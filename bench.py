@@ -228,6 +228,21 @@ def load_traffic(mode: str, rows: int = None):
     return None, None
 
 
+def check_step_losses(losses, args, rank: int, what: str) -> None:
+    """Every warm-up and timed step's loss must be finite (VERDICT r05 Next #1: a non-finite NLL step
+    must not yield a bench line).  The losses stay on the device during the timed loop; this one
+    read-back runs after it.  On the first non-finite loss: one JSON line naming the step, exit 3."""
+    t = torch.stack([l.detach().reshape(()).float() for l in losses])
+    bad = torch.nonzero(~torch.isfinite(t)).reshape(-1)
+    if bad.numel():
+        k = int(bad[0])
+        if rank == 0:
+            print(json.dumps({"error": f"non-finite loss in {what}", "first_nonfinite_step": k,
+                              "phase": "warmup" if k < args.warmup else "timed", "loss": float(t[k]),
+                              "previous_loss": float(t[k - 1]) if k else None}), flush=True)
+        sys.exit(3)
+
+
 def run_train(args, dev, rank, world, dist):
     """configs[3]: the NLL step of naz's train (train_flows.py:194-213) on one global batch of
     2^23 rows (strong scaling, the default: split over the ranks) or --batch rows per rank
@@ -253,8 +268,7 @@ def run_train(args, dev, rank, world, dist):
     def step():
         return nll_step(flow, x, c, opt, params, dp, G, clip_val=1.0, micro_batch=mb)
 
-    for _ in range(args.warmup):
-        step()
+    losses = [step() for _ in range(args.warmup)]  # every step's loss is checked after the timed region
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -262,6 +276,7 @@ def run_train(args, dev, rank, world, dist):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+        losses.append(loss)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -271,6 +286,7 @@ def run_train(args, dev, rank, world, dist):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
+    check_step_losses(losses, args, rank, "bench --train")
     if rank == 0:
         step_s = elapsed / args.steps
         flop = 3 * flops_per_row() * B  # per rank: fwd GEMMs + dX + dW
@@ -301,7 +317,7 @@ def run_train(args, dev, rank, world, dist):
                          "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
                          "peak_note": peak_note,
                          "kernel": "whole step", "flop_per_row": 3 * flops_per_row()},
-            "final_loss": float(loss),
+            "final_loss": float(loss), "losses_checked_finite": len(losses),
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = train_cpu_baseline(flow)
@@ -347,8 +363,7 @@ def run_train_flow(args, dev, rank, world, dist):
             return graphed(x, c)
         return nll_step(f, x, c, opt, params, dp, G, clip_val=1.0, micro_batch=args.micro_batch)
 
-    for _ in range(args.warmup):
-        step()
+    losses = [step() for _ in range(args.warmup)]  # every step's loss is checked after the timed region
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -356,6 +371,7 @@ def run_train_flow(args, dev, rank, world, dist):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+        losses.append(loss)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -365,6 +381,7 @@ def run_train_flow(args, dev, rank, world, dist):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
+    check_step_losses(losses, args, rank, "bench --train --flow")
     if rank == 0:
         step_s = elapsed / args.steps
         dims = [Dd + Cd] + list(hid) + [2 * Dd]
@@ -409,7 +426,7 @@ def run_train_flow(args, dev, rank, world, dist):
                        "micro_batch": args.micro_batch, "path": path,
                        "hip_graph": bool(args.graph) and graphed.replays >= args.steps,
                        "parallelism": f"dp{world} (RCCL all-reduce, one flat bucket)"},
-            "roofline": roof, "final_loss": float(loss),
+            "roofline": roof, "final_loss": float(loss), "losses_checked_finite": len(losses),
         }
         if world == 1 and not args.no_cpu_baseline:
             spec = dict(flow_type=ftype, D=Dd, C=Cd, hidden=list(hid), L=Ld)
@@ -619,8 +636,7 @@ def run_cnf_train(args, dev, rank, world, dist):
     def step():
         return nll_step(f, x, None, opt, params, dp, G, clip_val=1.0, micro_batch=args.micro_batch)
 
-    for _ in range(args.warmup):
-        step()
+    losses = [step() for _ in range(args.warmup)]  # every step's loss is checked after the timed region
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -628,6 +644,7 @@ def run_cnf_train(args, dev, rank, world, dist):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+        losses.append(loss)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -637,6 +654,7 @@ def run_cnf_train(args, dev, rank, world, dist):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
+    check_step_losses(losses, args, rank, "bench --cnf-train")
     if rank == 0:
         step_s = elapsed / args.steps
         # per RHS evaluation: forward value + JVP (2 MLP passes, fused kernel), backward recompute (2),
@@ -659,7 +677,7 @@ def run_cnf_train(args, dev, rank, world, dist):
                          "flop_per_row": flop_row,
                          "peak_note": "exact-FP32 MFMA peak (the backward walk's GEMMs; the fused forward, "
                                       "1/4 of the FLOPs, runs on the f16x3 pipe)"},
-            "final_loss": float(loss),
+            "final_loss": float(loss), "losses_checked_finite": len(losses),
         }
         if world == 1 and not args.no_cpu_baseline:
             from oracle import naz_oracle as O  # baseline only

@@ -823,6 +823,9 @@ def run_flow_case(args, dev, rank, world, dist):
         step_s = elapsed / args.steps
         achieved = fl_row * B / step_s / 1e12
         fused = ar_fused or (ftype == "nsc" and getattr(f, "fused", False))
+        # HBM bytes per call from rocprofv3 PMC passes over every dispatch of the call
+        # (scripts/pmc_step_traffic.py -> profiles/traffic_<flow>[_sample].json), scaled to B rows
+        traffic, traffic_src = load_traffic(f"traffic_{args.flow}{'_sample' if args.sample else ''}.json", rows=B)
         rec = {
             "metric": (f"samples/sec through sample (forward transform + log|detJ|), naz {ftype} flow (NormalizingFlow "
                        "API)" if args.sample else
@@ -839,7 +842,8 @@ def run_flow_case(args, dev, rank, world, dist):
             "roofline": {"bound": "mfma", "achieved": achieved,
                          "peak": FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3, "unit": "TFLOP/s",
                          "frac": achieved / (FP32_PEAK_TFLOPS if not fused else BF16_PEAK_TFLOPS / 3),
-                         "traffic": None, "kernel": "whole sample call" if args.sample else "whole log_prob call",
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "whole sample call" if args.sample else "whole log_prob call",
                          "flop_per_row": fl_row,
                          "reference_flop_per_row": fl_ref},
         }

@@ -519,6 +519,8 @@ int naz_coupling_bwd_layer(const naz_coupling_desc* d, const void* packed, const
                            const float* g_lp, float* h1, float* h2, float* dp1, float* dp2, float* dp3, float* x0,
                            float* g_out, float* g_low, int64_t B, void* stream) {
   if (d != nullptr && d->C > 0 && ctx == nullptr) return set_error("naz_coupling_bwd_layer: conditional flow needs ctx");
+  if (B < 0) return set_error("naz_coupling_bwd_layer: negative batch");
+  if (B == 0) return 0;  // an empty batch is a no-op, as in every other entry (no image is read)
   NAZ_IMG("naz_coupling_bwd_layer", spec_coupling(d, IMG_COUPLING), packed, 1, 0, 0, body);
   NAZ_IMG("naz_coupling_bwd_layer", spec_coupling(d, IMG_COUPLING_BWD), packed_bwd, 1, 0, 0, body_bwd);
   return coupling_bwd_layer(d, body, body_bwd, flat, layer, state, ctx, ldc, g_in, g_lp, h1, h2, dp1, dp2, dp3,
@@ -534,6 +536,7 @@ static int coupling_layer_api(const char* what, const naz_coupling_desc* d, int 
   if (B > 0 && (packed == nullptr || x == nullptr || y == nullptr || ld == nullptr))
     return set_error("%s: null pointer", what);
   if (d != nullptr && d->C > 0 && B > 0 && ctx == nullptr) return set_error("%s: conditional flow needs ctx", what);
+  if (B == 0) return 0;  // an empty batch is a no-op, as in every other entry (no image is read)
   NAZ_IMG(what, spec_coupling(d, IMG_COUPLING), packed, 1, 0, 0, body);
   return coupling_layer(d, inv, body, layer, x, ldx, ctx, ldc, y, ldy, ld, ld_mode, B, as_stream(stream));
 }

@@ -94,7 +94,10 @@ class _FusedCoupling:
         sig = tuple((p.data_ptr(), p._version) for p in ps) + (cache_epoch(),)
         if sig != self._sig or self._packed is None:
             D, C, S, K, H, act, lower, bound = self.shape
-            self.mode = self._resolve_mode()
+            if self._packed is None or not _capturing(ps[0].device):
+                # (a capture keeps the mode its eager warm-up step resolved: reading the weights back
+                # is a host sync; the graph's packer kernel re-packs every replay in that mode)
+                self.mode = self._resolve_mode()
             self.desc = ops.coupling_desc(D, C, S, K, len(self.layers), H, act, lower, bound, self.mode)
             flat = torch.cat([p.detach().reshape(-1) for p in ps])
             # a fresh image per repack: a training forward's backward (_CouplingTrainFn) still
@@ -116,10 +119,9 @@ class _FusedCoupling:
         self.packed()
         if self.mode != "f16x3r16":
             return False
-        m = x.detach().abs().amax()
-        if context is not None and context.numel():
-            m = torch.maximum(m, context.detach().abs().amax())
-        return float(m) < self.F16_DATA_LIMIT
+        if _RANGE_CHECKED.get():  # a HIP-graph capture whose caller checks the range before every replay
+            return True
+        return ops.absmax(x, context) < self.F16_DATA_LIMIT
 
     def packed_bwd(self) -> torch.Tensor:
         packed = self.packed()
@@ -208,12 +210,9 @@ class _FusedAR:
     def log_prob_ready(self, x, context) -> bool:
         if not self.inverse or x.dim() != 2:
             return False
-        if _RANGE_CHECKED:  # a HIP-graph capture whose caller checks the range before every replay
+        if _RANGE_CHECKED.get():  # a HIP-graph capture whose caller checks the range before every replay
             return True
-        m = x.detach().abs().amax() if x.numel() else torch.zeros((), device=x.device)
-        if context is not None and context.numel():
-            m = torch.maximum(m, context.detach().abs().amax())
-        return float(m) < self.F16_DATA_LIMIT
+        return ops.absmax(x, context) < self.F16_DATA_LIMIT
 
     def train_ready(self, x, context) -> bool:
         """The maf NLL step on the fused backward (made_ar_bwd.h, flows/maf_grad.py): an affine flow
@@ -298,7 +297,7 @@ class _FusedAR:
         if z.dim() != 2:
             return False
         if context is not None and context.numel():
-            return float(context.detach().abs().amax()) < self.F16_DATA_LIMIT
+            return ops.absmax(context) < self.F16_DATA_LIMIT
         return True
 
     def sample(self, z, context=None, bounds=None, with_logdet=False):
@@ -358,10 +357,15 @@ class _FusedAR:
 
 
 _TRAIN_FUSED = __import__("os").environ.get("NAZ_TRAIN_FUSED", "1")
-# set by trainers.GraphedNllStep while it captures a step: the fused AR paths' f16-range check reads
-# the data back to the host (no sync is allowed in a capture), so the graph's owner checks each
-# replay's rows itself before replaying (and runs an out-of-range minibatch eagerly)
-_RANGE_CHECKED = False
+# set by trainers.GraphedNllStep around the capture of a step (a context variable: only the capturing
+# thread's calls skip the check): the fused paths' f16-range check reads the data back to the host
+# (no sync is allowed in a capture), so the graph's owner checks each replay's rows itself before
+# replaying (and runs an out-of-range minibatch eagerly)
+_RANGE_CHECKED = __import__("contextvars").ContextVar("naz_range_checked", default=False)
+
+
+def _capturing(dev) -> bool:
+    return dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
 _TRAIN_WIDE = __import__("os").environ.get("NAZ_TRAIN_WIDE", "1")  # the GEMM-composed maf backward
 _AR_FUSED = __import__("os").environ.get("NAZ_AR_FUSED", "1")
 _AR_PASS0 = __import__("os").environ.get("NAZ_AR_PASS0", "1") != "0"  # one-context-vector first-pass folding
@@ -399,6 +403,8 @@ class _MafTrainFn(torch.autograd.Function):
 # layer l's dW reductions on a side stream while layer l + 1's backward kernel runs (default on:
 # 164.4 / 165.5 -> 156.6 / 158.6 ms per 2^23-row step, profiles/r05_g17_*; NAZ_TRAIN_DW_STREAM=0 off)
 _DW_STREAM = os.environ.get("NAZ_TRAIN_DW_STREAM", "1") == "1"
+# operand sets the backward kernels rotate through (a set is rewritten once its dW reductions are done)
+_DW_SETS = max(2, int(os.environ.get("NAZ_TRAIN_DW_SETS", "2")))
 _SIDE: Dict[int, "torch.cuda.Stream"] = {}
 
 
@@ -455,25 +461,40 @@ class _CouplingTrainFn(torch.autograd.Function):
         if rows is None or rows.device != dev:
             rows = ops.coupling_dp3_columns(d).to(dev)
             plan._dp3_rows = rows
-        valid = rows >= 0
-        cols, orow = torch.nonzero(valid).flatten(), rows[valid]
+            valid = rows >= 0
+            perm = torch.empty((int(valid.sum()),), dtype=torch.int64, device=dev)
+            perm[rows[valid]] = torch.nonzero(valid).flatten()  # DenseNN output row -> its dp3 column
+            plan._dp3_perm = perm
+        perm = plan._dp3_perm
+        NC = rows.numel()
         f32 = dict(device=dev, dtype=torch.float32)
 
         def operand_set():
             return {"h1": torch.empty((B, H), **f32), "h2": torch.empty((B, H), **f32),
                     "dp1": torch.empty((B, H), **f32), "dp2": torch.empty((B, H), **f32),
-                    "dp3": torch.empty((B, rows.numel()), **f32), "x0": torch.empty((B, C + S), **f32)}
+                    "dp3": torch.empty((B, NC), **f32), "x0": torch.empty((B, C + S), **f32)}
 
-        # layer l's dW reductions on a side stream, overlapping layer l + 1's backward kernel (two
-        # operand sets; fork / join by events, capture-safe; NAZ_TRAIN_DW_STREAM=0: one stream)
-        overlap = _DW_STREAM and dev.type == "cuda"
-        sets = [operand_set(), operand_set()] if overlap else [operand_set()]
+        # every layer's dW / db in ONE zeroed buffer (one fill on the main stream before the loop): the
+        # reductions accumulate into it, so the side stream launches only the three dW kernels per
+        # layer — r06 trace (profiles/r06_g3_*): the per-call zero fills queued behind the concurrent
+        # backward kernel and took ~2 ms per layer on the side stream, its critical path
+        sizes = [H * (C + S), H, H * H, H, NC * H, NC]
+        offs = np.concatenate([[0], np.cumsum(sizes)]).tolist()
+        gall = torch.zeros((L, offs[-1]), **f32)
+        # layer l's dW reductions on a side stream, overlapping layer l + 1's backward kernel
+        # (_DW_SETS operand sets; fork / join by events, capture-safe; NAZ_TRAIN_DW_STREAM=0: one stream)
+        overlap = _DW_STREAM and dev.type == "cuda" and not _capturing(dev)  # (a captured step: one stream)
+        sets = [operand_set() for _ in range(_DW_SETS if overlap else 1)]
         main = torch.cuda.current_stream(dev) if overlap else None
         side = _side_stream(dev) if overlap else None
-        done = [None, None]  # the side stream's event after the dW of the last layer that used set i
+        if overlap:
+            gall.record_stream(side)
+            for bufs in sets:
+                for t in bufs.values():
+                    t.record_stream(side)
+        done = [None] * len(sets)  # the side stream's event after the dW of the last layer that used set i
         n_low = S * (3 * K - 1) if lower else 0
         g_low = torch.zeros((L, max(n_low, 1)), **f32)
-        P = 3 * K - 1
         per = 9 if lower else 6
         grads = [None] * ctx.n_params
         for l in range(L):
@@ -483,37 +504,33 @@ class _CouplingTrainFn(torch.autograd.Function):
                 main.wait_event(done[si])  # this set's previous dW reads are over
             ops.coupling_bwd_layer(d, ctx.packed, ctx.pbwd, ctx.flat, l, states[l + 1], context, g, g_lp, bufs, g_next,
                                    g_low[l] if lower else None)
-            gW0, gb0 = torch.empty((H, C + S), **f32), torch.empty((H,), **f32)
-            gW1, gb1 = torch.empty((H, H), **f32), torch.empty((H,), **f32)
-            gW2 = torch.zeros(((D - S) * P, H), **f32)
-            gb2 = torch.zeros(((D - S) * P,), **f32)
-            gw2p = torch.empty((rows.numel(), H), **f32)
-            gb2p = torch.empty((rows.numel(),), **f32)
+            gw = [gall[l, offs[i]:offs[i + 1]] for i in range(6)]
             if overlap:
                 ev = torch.cuda.Event()
                 ev.record(main)
                 side.wait_event(ev)
-                for t in (gW0, gb0, gW1, gb1, gW2, gb2, gw2p, gb2p, *bufs.values()):
-                    t.record_stream(side)
             with torch.cuda.stream(side) if overlap else _nullcontext():
-                ops.gemm(bufs["dp1"].t(), bufs["x0"], out=gW0, rowsum=gb0)
-                ops.gemm(bufs["dp2"].t(), bufs["h1"], out=gW1, rowsum=gb1)
-                ops.gemm(bufs["dp3"].t(), bufs["h2"], out=gw2p, rowsum=gb2p)
-                gW2.index_copy_(0, orow, gw2p.index_select(0, cols))
-                gb2.index_copy_(0, orow, gb2p.index_select(0, cols))
+                ops.gemm(bufs["dp1"].t(), bufs["x0"], out=gw[0].view(H, C + S), rowsum=gw[1], accumulate=True)
+                ops.gemm(bufs["dp2"].t(), bufs["h1"], out=gw[2].view(H, H), rowsum=gw[3], accumulate=True)
+                ops.gemm(bufs["dp3"].t(), bufs["h2"], out=gw[4].view(NC, H), rowsum=gw[5], accumulate=True)
             if overlap:
                 done[si] = torch.cuda.Event()
                 done[si].record(side)
-            out = [gW0, gb0, gW1, gb1, gW2, gb2]
-            if lower:
-                gl = g_low[l]
-                out += [gl[:S * K].view(S, K), gl[S * K:2 * S * K].view(S, K), gl[2 * S * K:].view(S, K - 1)]
-            grads[l * per:(l + 1) * per] = out
             g, g_next = g_next, g
         if overlap:
             for e in done:
                 if e is not None:
                     main.wait_event(e)  # the gradients are read on the main stream
+        # dp3 columns (lane-slot order, padding included) -> DenseNN output rows, all layers at once
+        w2 = gall[:, offs[4]:offs[5]].view(L, NC, H).index_select(1, perm)
+        b2 = gall[:, offs[5]:offs[6]].index_select(1, perm)
+        for l in range(L):
+            out = [gall[l, offs[0]:offs[1]].view(H, C + S), gall[l, offs[1]:offs[2]],
+                   gall[l, offs[2]:offs[3]].view(H, H), gall[l, offs[3]:offs[4]], w2[l], b2[l]]
+            if lower:
+                gl = g_low[l]
+                out += [gl[:S * K].view(S, K), gl[S * K:2 * S * K].view(S, K), gl[2 * S * K:].view(S, K - 1)]
+            grads[l * per:(l + 1) * per] = out
         return (None, None, None, None, *grads)
 
 

@@ -62,20 +62,44 @@ def _p(t: Optional[Tensor]) -> Optional[int]:
 
 
 _WS: dict = {}
+_WS_PER_DEVICE = 4  # streams whose workspace is kept per device (least recently used dropped first)
 
 
 def workspace(dev: torch.device, nbytes: int) -> Tuple[Optional[int], int]:
     """Caller-owned device workspace of the autoregressive log_prob entries (include/naz_hip.h
     naz_ar_flow_workspace_bytes: the wide MAF inverse's per-wave hidden layers; no entry allocates):
     one buffer per (device, stream), grown on demand and kept, so a captured HIP graph replays one
-    fixed address.  Returns (pointer, bytes) for the call."""
+    fixed address.  Returns (pointer, bytes) for the call.
+
+    The key is the device INDEX ('cuda' and 'cuda:0' are one device) and the stream; at most
+    _WS_PER_DEVICE streams keep a buffer per device.  Dropping the least recently used one is safe:
+    the caching allocator reuses a freed block only for allocations on the stream it was allocated
+    on (here: the stream it served), so later work is ordered after the dropped buffer's last use."""
     if nbytes <= 0:
         return None, 0
-    key = (str(dev), _stream(dev))
-    buf = _WS.get(key)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, _stream(dev))
+    buf = _WS.pop(key, None)  # re-inserted below: dict order = recency
     if buf is None or buf.numel() < nbytes:
-        buf = _WS[key] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", idx))
+    _WS[key] = buf
+    mine = [k for k in _WS if k[0] == idx]
+    for k in mine[:max(0, len(mine) - _WS_PER_DEVICE)]:
+        del _WS[k]
     return buf.data_ptr(), buf.numel()
+
+
+def absmax(*ts: Optional[Tensor]) -> float:
+    """max |t| over the given tensors (None / empty skipped) as a host float: the fused kernels'
+    f16-split range check.  One reduction pass per tensor (an inf-norm) with no |t| temporary —
+    r06 PMC: x.abs().amax() wrote and re-read a full |x| copy, 100 of the 348 MB per nsa16 call."""
+    m = None
+    for t in ts:
+        if t is None or t.numel() == 0:
+            continue
+        v = torch.linalg.vector_norm(t.detach(), float("inf"))
+        m = v if m is None else torch.maximum(m, v)
+    return 0.0 if m is None else float(m)
 
 
 def rowgemm_split(value: Optional[bool] = None) -> bool:

@@ -174,22 +174,44 @@ class GraphedNllStep:
     The rows are copied into static buffers and the graph replays; the first call for a shape is
     an eager step on a side stream (it creates the gradients, the optimizer state and the paths'
     caches: schedules, packs, buffers) after which one step is captured without running, so every
-    call is exactly one optimizer step.  The optimizer must be
-    capturable (``torch.optim.Adam(..., capturable=True)``; set here before its first step).  The
-    fused autoregressive paths check that the rows fit their f16 input split (|x|, |ctx| < 2^15)
-    with a host read-back, which a capture cannot do: the check runs eagerly before every replay,
-    and an out-of-range minibatch takes the eager step instead."""
+    call is exactly one optimizer step.  The fused paths check that the rows fit their f16 input
+    split (|x|, |ctx| < 2^15) with a host read-back, which a capture cannot do: the check runs
+    eagerly before every replay, and an out-of-range minibatch takes the eager step instead.
+
+    Captured: the fused maf paths and the fused nsc step (the weights are re-packed by a device
+    kernel inside the graph, in the MFMA mode the eager step resolved).  A flow whose step reads
+    device values back on the host (a CNF's adaptive solver, the per-layer walk's checks) cannot be
+    captured: the first failed capture is reported once and every later call runs the eager step
+    (``self.eager_only``), still exactly one optimizer step per call.
+
+    Limits (fixed at capture time): the optimizer must be capturable — ``torch.optim.Adam(...,
+    capturable=True)``, set here when the optimizer has no state yet (an optimizer that already
+    stepped keeps its host-side step counters and is refused); the learning rate and the other
+    hyper-parameters are baked into the graph (changing ``param_groups[i]['lr']`` later, e.g. naz
+    train's ``lr_decay``, needs ``recapture()``); the gradients must not be set to None outside the
+    step (``zero_grad(set_to_none=True)`` would free the buffers the graph writes); the naz_tuning
+    launch choices and the fused / walk path choice are those of the capture."""
 
     def __init__(self, flow, optimizer, params: List[torch.Tensor], dp: "DataParallel", global_batch: int,
                  clip_val: Optional[float] = 1.0, micro_batch: Optional[int] = None):
         self.flow, self.opt, self.params, self.dp = flow, optimizer, params, dp
         self.global_batch, self.clip_val, self.micro_batch = global_batch, clip_val, micro_batch
+        if any(len(st) for st in optimizer.state.values()):
+            raise ValueError("GraphedNllStep: the optimizer has already stepped (its state is not capturable); "
+                             "pass a fresh optimizer")
         for g in optimizer.param_groups:
             if "capturable" in g:
                 g["capturable"] = True
         self._key, self._graph = None, None
+        self._stream = None
         self.replays = 0
         self.eager_steps = 0
+        self.eager_only = False
+        self.capture_error = None
+
+    def recapture(self) -> None:
+        """Drop the graph: the next call captures again (after a hyper-parameter change)."""
+        self._key, self._graph = None, None
 
     def _eager(self, x_b, y_b):
         self.eager_steps += 1
@@ -197,33 +219,44 @@ class GraphedNllStep:
                         micro_batch=self.micro_batch)
 
     def _in_range(self, x_b, y_b) -> bool:
-        m = x_b.detach().abs().amax() if x_b.numel() else torch.zeros((), device=x_b.device)
-        if y_b is not None and y_b.numel():
-            m = torch.maximum(m, y_b.detach().abs().amax())
-        return float(m) < 32768.0
+        from .. import ops
+        return ops.absmax(x_b, y_b) < 32768.0
 
     def __call__(self, x_b: torch.Tensor, y_b: Optional[torch.Tensor]) -> torch.Tensor:
         from ..flows import flow as flow_mod
         key = (tuple(x_b.shape), None if y_b is None else tuple(y_b.shape), x_b.device)
-        if not self._in_range(x_b, y_b):
+        if self.eager_only or not self._in_range(x_b, y_b):
             return self._eager(x_b, y_b)
         if key != self._key:
             dev = x_b.device
             self._x = x_b.detach().clone()
             self._y = None if y_b is None else y_b.detach().clone()
-            side = torch.cuda.Stream(dev)
+            if self._stream is None:  # one warm-up stream for every (re)capture
+                self._stream = torch.cuda.Stream(dev)
+            side = self._stream
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 loss = self._eager(self._x, self._y).clone()  # this call's step
             torch.cuda.current_stream(dev).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            flow_mod._RANGE_CHECKED = True
+            tok = flow_mod._RANGE_CHECKED.set(True)
             try:
                 with torch.cuda.graph(graph):  # recorded, not run
                     self._loss = nll_step(self.flow, self._x, self._y, self.opt, self.params, self.dp,
                                           self.global_batch, self.clip_val, micro_batch=self.micro_batch)
+            except RuntimeError as e:  # a host read-back inside the step: eager from now on
+                import warnings
+                self.eager_only, self.capture_error = True, str(e)[:300]
+                warnings.warn(f"GraphedNllStep: this flow's step cannot be captured ({self.capture_error}); "
+                              "running it eagerly", RuntimeWarning)
+                # caches (packed images, plans) touched inside the aborted capture were never filled:
+                # a new cache epoch makes every path re-pack eagerly
+                from ..nn import invalidate_caches
+                invalidate_caches()
+                torch.cuda.synchronize(dev)
+                return loss
             finally:
-                flow_mod._RANGE_CHECKED = False
+                flow_mod._RANGE_CHECKED.reset(tok)
             self._graph, self._key = graph, key
             return loss
         self._x.copy_(x_b)

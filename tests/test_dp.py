@@ -47,7 +47,7 @@ def _data(n=203, D=3, C=2):
     return x, y
 
 
-def _steps(flow, x, y, dp, steps=5, batch=37):
+def _steps(flow, x, y, dp, steps=5, batch=37, micro_batch=None):
     params = T._flow_parameters(flow)
     opt = torch.optim.Adam(params, lr=1e-2)
     losses = []
@@ -55,7 +55,8 @@ def _steps(flow, x, y, dp, steps=5, batch=37):
         idx = torch.arange(s * batch, (s + 1) * batch) % x.shape[0]
         lo, hi = dp.shard(len(idx))
         mine = idx[lo:hi]
-        losses.append(float(T.nll_step(flow, x[mine], y[mine], opt, params, dp, len(idx), 1.0, lambda_l1=1e-3)))
+        losses.append(float(T.nll_step(flow, x[mine], y[mine], opt, params, dp, len(idx), 1.0, lambda_l1=1e-3,
+                                       micro_batch=micro_batch)))
     return losses, [p.detach().clone() for p in params]
 
 
@@ -71,10 +72,11 @@ def _worker(rank, world, port, q, mode):
     try:
         torch.manual_seed(100 + rank)  # replicas start different: train() must broadcast rank 0
         x, y = _data()
-        if mode == "steps":
+        if mode.startswith("steps"):
             flow = _TinyFlow(seed=0)
             dp = T.DataParallel()
-            losses, params = _steps(flow, x, y, dp)
+            mb = None if mode == "steps" else int(mode.split(":")[1])
+            losses, params = _steps(flow, x, y, dp, micro_batch=mb)
             q.put((rank, losses, [p.numpy() for p in params]))
         else:
             flow = _TinyFlow(seed=rank)
@@ -100,11 +102,14 @@ def _run(world, mode):
     return sorted(res, key=lambda r: r[0])
 
 
-def test_dp_step_matches_single_process():
-    """2 ranks on ragged slices of each global minibatch == one process on the whole batch."""
+@pytest.mark.parametrize("micro_batch", [None, 64, 7])
+def test_dp_step_matches_single_process(micro_batch):
+    """2 ranks on ragged slices of each global minibatch == one process on the whole batch; with
+    a micro-batch larger than a rank's 18-19-row slice (64: one chunk, what 8 ranks of bench --train
+    run) and smaller (7: chunks accumulated before the one all-reduce)."""
     x, y = _data()
-    ref_losses, ref_params = _steps(_TinyFlow(seed=0), x, y, T.DataParallel())
-    res = _run(2, "steps")
+    ref_losses, ref_params = _steps(_TinyFlow(seed=0), x, y, T.DataParallel(), micro_batch=micro_batch)
+    res = _run(2, "steps" if micro_batch is None else f"steps:{micro_batch}")
     for _, losses, params in res:
         assert losses == pytest.approx(ref_losses, rel=1e-5, abs=1e-6)
         for a, b in zip(params, ref_params):

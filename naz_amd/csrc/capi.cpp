@@ -228,6 +228,7 @@ int naz_tuning(const char* key, int value) {
   if (key != nullptr && strcmp(key, "rowgemm_x6") == 0) return rowgemm_x6_setting(value);
   if (key != nullptr && strcmp(key, "rowgemm_fill") == 0) return rowgemm_fill_setting(value);
   if (key != nullptr && strcmp(key, "rowgemm_h3") == 0) return rowgemm_h3_setting(value);
+  if (key != nullptr && strcmp(key, "rowgemm_bres") == 0) return rowgemm_bres_setting(value);
   return set_error("naz_tuning: unknown key '%s'", key ? key : "(null)");
 }
 

@@ -18,6 +18,7 @@
 //   * wgrad: a workgroup reduces a contiguous slice of rows into the full (small) output in
 //     registers — each wave owns a set of 32×32 output blocks — and adds it to C with one fp32
 //     atomic per element at the end (split-K over workgroups, no partial buffers).
+#include <algorithm>
 #include <atomic>
 
 #include "naz_device.h"
@@ -96,6 +97,9 @@ struct RowGemmArgs {
   // small batches: narrow the column panels until the grid holds this many workgroups per CU
   // (0: off, -1: the library's setting, naz_tuning "rowgemm_fill")
   int fill = -1;
+  // ... or the B-resident f16x3 kernel (1: rowgemm_bres_kernel), or the library's setting (-1:
+  // naz_tuning "rowgemm_bres"); tried before x6 / h3
+  int bres = -1;
 };
 
 // A(m, k) of the concatenated row [a0 | a1]
@@ -359,6 +363,15 @@ int rowgemm_h3_setting(int v) {
   return v >= 0 ? cur.exchange(v != 0 ? 1 : 0) : cur.load();
 }
 
+int rowgemm_bres_setting(int v) {
+  // NAZ_RG_BRES at first use, else off until a same-box A/B sets the default
+  static std::atomic<int> cur{[] {
+    const char* e = getenv("NAZ_RG_BRES");
+    return e ? (atoi(e) != 0 ? 1 : 0) : 0;
+  }()};
+  return v >= 0 ? cur.exchange(v != 0 ? 1 : 0) : cur.load();
+}
+
 int rowgemm_fill_setting(int v) {
   // NAZ_RG_FILL at first use, else 2 workgroups (= waves per SIMD) per CU (with the wide-maf step's
   // side streams: 163.5 ms at 2^16 rows vs 168.5 at 4 and 179.5 at 8; 10,752 rows 49.3 vs 48.7 / 48.9;
@@ -383,6 +396,8 @@ namespace {
 
 int rowgemm_x6_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s);  // below
 int rowgemm_h3_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s);
+int rowgemm_bres_nb(const RowGemmArgs& p, int nz);
+int rowgemm_bres_dispatch(const RowGemmArgs& p, int nb, hipStream_t s);
 
 int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   if (p.M <= 0 || p.N <= 0 || nz <= 0) return 0;
@@ -401,6 +416,12 @@ int rowgemm(RowGemmArgs p, hipStream_t s, int nz = 1) {
   if (nz > 1) {  // every problem's base keeps the alignment
     p.vec = p.vec && p.za0 % 4 == 0 && p.za1 % 4 == 0;
     p.vst = p.vst && p.zc % 4 == 0;
+  }
+  // the B-resident f16x3 form (naz_tuning "rowgemm_bres") where a panel of B fits the LDS
+  const int bres = p.bres >= 0 ? p.bres : rowgemm_bres_setting(-1);
+  if (bres && K >= 16) {
+    const int bnb = rowgemm_bres_nb(p, nz);
+    if (bnb > 0) return rowgemm_bres_dispatch(p, bnb, s);
   }
   int nb = (p.N + 31) / 32;
   // panel split: outputs of more than 4 column blocks in balanced panels of at most 4 blocks (4 waves
@@ -1257,6 +1278,272 @@ int rowgemm_h3_dispatch(const RowGemmArgs& p, int nz, int nb, hipStream_t s) {
     default: rowgemm_h3_launch<8>(p, nz, s); break;
   }
   return check_launch("rowgemm_h3_kernel");
+}
+
+// rowgemm_bres_kernel: the batch-row GEMM on the f16 matrix pipe with the B panel RESIDENT in LDS
+// (naz_tuning "rowgemm_bres").  rowgemm_h3 streamed and split every 16-k B chunk per 128-row
+// workgroup behind a barrier: the B split cost as much VALU as the A split and the barrier held the
+// waves in step (CNF training 94 vs 83 ms, r05).  Here a persistent workgroup owns one column panel
+// of 32 NB columns for the whole call: it splits B (times its mask) ONCE into f16 hi / lo fragments
+// in the MFMA's B layout ([k-step][block][piece][lane][8 f16], K x 32 NB x 4 bytes of LDS) at a
+// power-of-two panel scale (its largest |B| into [2^13, 2^14)), then every wave walks 32-row tiles
+// on its own — no barrier after the panel load.  Per tile: a pre-pass over the wave's A rows finds
+// each row's power-of-two scale (the gradients' range is unbounded; f16's lo pieces must stay clear
+// of subnormals), then C += Ah·Bh + Ah·Bl + Al·Bh on v_mfma_f32_32x32x16_f16 (the dropped Al·Bl
+// term <= 2^-22 relative) with A read straight into registers two k-steps ahead, and the
+// accumulators unscaled exactly in a register epilogue (bias, activation, chained act', accumulate;
+// the CNF pair VJP stays on the other kernels).  Panels of one row range are mapped to one XCD
+// (workgroup w runs on XCD w mod 8), so their A rows are fetched into one L2.
+// KSR > 0: K <= 16 KSR, and a wave's whole 32-row A tile is loaded into registers at once (all loads in
+// flight together; the row maxima from those registers: A is read once), for the CNF's 128-wide layers
+template <int NB, int KSR>
+__global__ void __launch_bounds__(256, (NB <= 3 && KSR == 0) ? 4 : 2) rowgemm_bres_kernel(RowGemmArgs p, int npanels,
+                                                                                         int per_panel) {
+  extern __shared__ __attribute__((aligned(16))) float bres_lds[];
+  __shared__ unsigned bmax_bits;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kh = lane >> 5;
+  const int K = p.ka0 + p.ka1, KSP = (K + 15) / 16;
+  // workgroup -> (panel, slot): the npanels workgroups sharing a slot sit on one XCD (w mod 8 = XCD)
+  const int w = blockIdx.x;
+  const int xcd = w & 7, wq = w >> 3;
+  const int panel = wq % npanels, slot = (wq / npanels) * 8 + xcd;
+  const int nslots = per_panel;
+  if (slot >= nslots) return;  // (the grid is rounded to whole XCD groups)
+  const int n0 = panel * 32 * NB;
+  unsigned* const bsm = reinterpret_cast<unsigned*>(bres_lds);
+
+  // ---- the panel's B: max |B|, then the split fragments
+  const auto bsrd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.b), (short)0, p.bbytes, 0x00020000);
+  const auto msrd =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.mask ? p.mask : p.b), (short)0, p.mbytes, 0x00020000);
+  const int sbk = (int)p.sbk, sbn = (int)p.sbn, smk = (int)p.smk, smn = (int)p.smn;
+  auto bval = [&](int k, int n) -> float {
+    const bool in = k < K && n < p.N;
+    float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(bsrd, in ? 4 * (k * sbk + n * sbn) : p.bbytes, 0, 0));
+    if (p.mask != nullptr)
+      v *= __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(msrd, in ? 4 * (k * smk + n * smn) : p.mbytes, 0, 0));
+    return v;
+  };
+  if (tid == 0) bmax_bits = 0u;
+  __syncthreads();
+  const int nfl = KSP * NB * 64;  // fragment lanes: (k-step t, block o, lane l)
+  {
+    float mx = 0.f;
+    for (int fl = tid; fl < nfl; fl += 256) {
+      const int l = fl & 63, o = (fl >> 6) % NB, t = (fl >> 6) / NB;
+      const int kb = 16 * t + 8 * (l >> 5), n = n0 + 32 * o + (l & 31);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(bval(kb + e, n)));
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d));
+    if (lane == 0) atomicMax(&bmax_bits, __float_as_uint(mx));  // |B| >= 0: the bits order as the values
+  }
+  __syncthreads();
+  const float bmx = __uint_as_float(bmax_bits);
+  int bex = bmx > 0.f ? __builtin_amdgcn_frexp_expf(bmx) : 14;
+  bex = bex < -100 ? -100 : (bex > 100 ? 100 : bex);
+  const float bsc = __builtin_amdgcn_ldexpf(1.f, 14 - bex);
+  for (int fl = tid; fl < nfl; fl += 256) {
+    const int l = fl & 63, fo = fl >> 6;  // fo = t NB + o
+    const int o = fo % NB, t = fo / NB;
+    const int kb = 16 * t + 8 * (l >> 5), n = n0 + 32 * o + (l & 31);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bval(kb + e, n);
+    const RgH2 q = rg_split8_f16(v, bsc);
+    rg_u32x4* d = reinterpret_cast<rg_u32x4*>(bsm) + (fo * 2) * 64 + l;
+    d[0] = __builtin_bit_cast(rg_u32x4, q.h);
+    d[64] = __builtin_bit_cast(rg_u32x4, q.l);
+  }
+  __syncthreads();
+  const float binv = __builtin_amdgcn_ldexpf(1.f, bex - 14);
+
+  // ---- 32-row tiles: wave (slot, wave) takes tiles slot 4 + wave, + 4 nslots, ...
+  const int64_t ntiles = (p.M + 31) / 32;
+  const rg_u32x4* bfr = reinterpret_cast<const rg_u32x4*>(bsm) + lane;
+  for (int64_t tile = (int64_t)slot * 4 + wave; tile < ntiles; tile += (int64_t)nslots * 4) {
+    const int64_t am = tile * 32 + (lane & 31);
+    const bool arow = am < p.M;
+    // (p.vec: 16-byte aligned rows, ka0 % 8 == 0, so an 8-k group never straddles the two segments)
+    const float* const row0 = p.a0 + (arow ? am : 0) * p.lda0;
+    const float* const row1 = p.a1 + (arow ? am : 0) * p.lda1;
+    auto load_a = [&](int t, float (&v)[8]) {
+      const int kb = 16 * t + 8 * kh;
+      const bool s0 = kb < p.ka0;
+      const float* seg = s0 ? row0 + kb : row1 + (kb - p.ka0);
+      const int lim = arow ? (s0 ? p.ka0 - kb : K - kb) : 0;  // valid k of this group
+      if (lim >= 8) {
+        const float4 v0 = *reinterpret_cast<const float4*>(seg);
+        const float4 v1 = *reinterpret_cast<const float4*>(seg + 4);
+        v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+        v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = e < lim ? seg[e] : 0.f;
+      }
+    };
+    // the row's scale (both lanes of a row agree): its largest |A| into [2^13, 2^14); zero rows 1
+    float sc, rinv;
+    auto row_scale = [&](float mx) {
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      int ex = mx > 0.f ? __builtin_amdgcn_frexp_expf(mx) : 14;  // mx < 2^ex (a non-finite row: 0)
+      ex = ex < -100 ? -100 : ex;
+      sc = __builtin_amdgcn_ldexpf(1.f, 14 - ex);
+      rinv = __builtin_amdgcn_ldexpf(1.f, ex - 14) * binv;
+    };
+    floatx16 acc[NB];
+#pragma unroll
+    for (int o = 0; o < NB; ++o)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[o][r] = 0.f;
+    if constexpr (KSR > 0) {
+      float areg[KSR][8];
+      if (p.ka1 == 0 && K == 16 * KSR && arow) {  // one segment of exactly KSR k-steps: plain 16-byte loads
+#pragma unroll
+        for (int t = 0; t < KSR; ++t) {
+          const float4 v0 = *reinterpret_cast<const float4*>(row0 + 16 * t + 8 * kh);
+          const float4 v1 = *reinterpret_cast<const float4*>(row0 + 16 * t + 8 * kh + 4);
+          areg[t][0] = v0.x; areg[t][1] = v0.y; areg[t][2] = v0.z; areg[t][3] = v0.w;
+          areg[t][4] = v1.x; areg[t][5] = v1.y; areg[t][6] = v1.z; areg[t][7] = v1.w;
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < KSR; ++t) load_a(t, areg[t]);
+      }
+      float mx = 0.f;
+#pragma unroll
+      for (int t = 0; t < KSR; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(areg[t][e]));
+      row_scale(mx);
+#pragma unroll
+      for (int t = 0; t < KSR; ++t) {
+        const RgH2 a = rg_split8_f16(areg[t], sc);
+#pragma unroll
+        for (int o = 0; o < NB; ++o) {
+          const int f = (t * NB + o) * 2 * 64;
+          const RgH2 b{__builtin_bit_cast(rg_half8, bfr[f]), __builtin_bit_cast(rg_half8, bfr[f + 64])};
+          acc[o] = rg_mfma3(a, b, acc[o]);
+        }
+      }
+    } else {
+      {
+        float mx = 0.f;
+        for (int t = 0; t < KSP; ++t) {
+          float v[8];
+          load_a(t, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(v[e]));
+        }
+        row_scale(mx);
+      }
+      float va[8], vb[8];
+      load_a(0, va);
+      if (KSP > 1) load_a(1, vb);
+      for (int t = 0; t < KSP; ++t) {
+        float vc[8];
+        if (t + 2 < KSP) load_a(t + 2, vc);  // two k-steps ahead
+        const RgH2 a = rg_split8_f16(va, sc);
+#pragma unroll
+        for (int o = 0; o < NB; ++o) {
+          const int f = (t * NB + o) * 2 * 64;
+          const RgH2 b{__builtin_bit_cast(rg_half8, bfr[f]), __builtin_bit_cast(rg_half8, bfr[f + 64])};
+          acc[o] = rg_mfma3(a, b, acc[o]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          va[e] = vb[e];
+          vb[e] = vc[e];
+        }
+      }
+    }
+    // register epilogue: accumulator register r of a block = row (r & 3) + 8 (r >> 2) + 4 kh of the tile
+    // (its scale from the lane that loaded that row), column 32 o + (lane & 31) of the panel.  Rows are
+    // addressed by 32-bit offsets from the tile's first row (a wave-uniform base: SGPRs), so the
+    // unrolled stores do not each hold a 64-bit address
+    const int64_t tb = (int64_t)__builtin_amdgcn_readfirstlane((int)(tile >> 5)) * 1024 +
+                       __builtin_amdgcn_readfirstlane((int)(tile & 31)) * 32;
+    float* const cb = p.c + tb * p.ldc;
+    const float* const dyb = p.dy != nullptr ? p.dy + tb * p.lddy : nullptr;
+    // (the row offsets below are the same for every tile: made opaque per tile, or the compiler hoists
+    // all 16 of them out of the tile loop as 64-bit values and spills)
+    int ldc = (int)p.ldc, lddy = (int)p.lddy, lc = lane & 31, kh4 = 4 * kh;
+    asm volatile("" : "+v"(lc), "+v"(kh4), "+s"(ldc), "+s"(lddy));
+    float bn[NB];
+#pragma unroll
+    for (int o = 0; o < NB; ++o) {
+      const int n = n0 + 32 * o + (lane & 31);
+      bn[o] = (p.bias != nullptr && n < p.N) ? p.bias[n] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = (r & 3) + 8 * (r >> 2) + kh4;
+      const float u = __shfl(rinv, rr);
+      if (tb + rr >= p.M) continue;
+#pragma unroll
+      for (int o = 0; o < NB; ++o) {
+        const int n = n0 + 32 * o + lc;
+        if (n >= p.N) continue;
+        float v = activate_rt(p.act, acc[o][r] * u + bn[o]);
+        if (dyb != nullptr) v *= activate_grad_from_out(p.dact, dyb[(uint32_t)(rr * lddy + n)]);
+        float* dst = cb + (uint32_t)(rr * ldc + n);
+        *dst = p.accumulate ? *dst + v : v;
+      }
+    }
+  }
+}
+
+// LDS bytes of a B-resident panel of NB blocks over K
+static int64_t bres_lds_bytes(int K, int nb) { return (int64_t)((K + 15) / 16) * nb * 2048; }
+
+template <int NB, int KSR>
+int rowgemm_bres_launch(const RowGemmArgs& p, hipStream_t s) {
+  const int npanels = (p.N + 32 * NB - 1) / (32 * NB);
+  const int64_t lds = bres_lds_bytes(p.ka0 + p.ka1, NB);
+  const int per_cu = (int)std::min<int64_t>(4, (160 * 1024) / (lds + 64));
+  const int64_t ntiles = (p.M + 31) / 32;
+  // slots per panel: enough workgroups to hold per_cu per CU, no more than the tiles need, whole XCD groups
+  int64_t slots = std::max<int64_t>(1, (int64_t)per_cu * device_cus() / npanels);
+  slots = std::min<int64_t>(slots, (ntiles + 3) / 4);
+  slots = (slots + 7) / 8 * 8;
+  const int64_t grid = slots / 8 * npanels * 8;
+  hipLaunchKernelGGL((rowgemm_bres_kernel<NB, KSR>), dim3((unsigned)grid), dim3(256), (size_t)lds, s, p, npanels,
+                     (int)slots);
+  return check_launch("rowgemm_bres_kernel");
+}
+
+// the B-resident form applies: one problem, no CNF pair VJP, a panel of >= 2 blocks (or the whole
+// output) fits the LDS.  Returns the blocks per panel, or 0.
+int rowgemm_bres_nb(const RowGemmArgs& p, int nz) {
+  if (nz != 1 || p.jvp != nullptr || p.M < 1024 || !p.vec) return 0;
+  if (p.ldc * 32 + p.N >= (1ll << 31) || (p.dy != nullptr && p.lddy * 32 + p.N >= (1ll << 31))) return 0;
+  const int K = p.ka0 + p.ka1, nball = (p.N + 31) / 32;
+  for (int nb = 4; nb >= 1; --nb) {
+    if (bres_lds_bytes(K, nb) > 144 * 1024) continue;
+    if (nb >= 2 || nball == 1) {
+      const int panels = (nball + nb - 1) / nb;
+      return (nball + panels - 1) / panels;  // balanced panels
+    }
+  }
+  return 0;
+}
+
+int rowgemm_bres_dispatch(const RowGemmArgs& p, int nb, hipStream_t s) {
+  if (p.ka0 + p.ka1 <= 128) {  // the whole A tile in registers
+    switch (nb) {
+      case 1: return rowgemm_bres_launch<1, 8>(p, s);
+      case 2: return rowgemm_bres_launch<2, 8>(p, s);
+      case 3: return rowgemm_bres_launch<3, 8>(p, s);
+      default: return rowgemm_bres_launch<4, 8>(p, s);
+    }
+  }
+  switch (nb) {
+    case 1: return rowgemm_bres_launch<1, 0>(p, s);
+    case 2: return rowgemm_bres_launch<2, 0>(p, s);
+    case 3: return rowgemm_bres_launch<3, 0>(p, s);
+    default: return rowgemm_bres_launch<4, 0>(p, s);
+  }
 }
 
 template <int NOW, int NB2, int JS>

@@ -150,6 +150,7 @@ int rowgemm_x6_setting(int v);
 int rowgemm_fill_setting(int v);
 // ... and its f16x3 form (rowgemm_h3_kernel: the caller keeps |B| < 2^9)
 int rowgemm_h3_setting(int v);
+int rowgemm_bres_setting(int v);
 // elementwise.hip: compute units of the current device (cached per device)
 int device_cus();
 int rowgemm_jvp_bwd(const float* A, int64_t lda, int K, const float* W, int64_t ldw, float* C, int64_t ldc,

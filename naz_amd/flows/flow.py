@@ -400,9 +400,12 @@ class _MafTrainFn(torch.autograd.Function):
         return (None, None, None, *outs)
 
 
-# layer l's dW reductions on a side stream while layer l + 1's backward kernel runs (default on:
-# 164.4 / 165.5 -> 156.6 / 158.6 ms per 2^23-row step, profiles/r05_g17_*; NAZ_TRAIN_DW_STREAM=0 off)
-_DW_STREAM = os.environ.get("NAZ_TRAIN_DW_STREAM", "1") == "1"
+# layer l's dW reductions on a side stream while layer l + 1's backward kernel runs (NAZ_TRAIN_DW_STREAM=1).
+# Off by default since r06: the r05 gain (164-165 -> 157-159 ms per 2^23-row step) was measured on runs
+# whose loss went NaN; on the fixed step, same box, interleaved (profiles/r06_g7_*): 158.5 / 159.1 / 158.9
+# ms with it vs 157.4 / 158.2 / 158.5 without.  The two kernels share the CUs (the backward kernel holds
+# every register slot), so the overlap buys nothing, and one stream needs half the operand memory.
+_DW_STREAM = os.environ.get("NAZ_TRAIN_DW_STREAM", "0") == "1"
 # operand sets the backward kernels rotate through (a set is rewritten once its dW reductions are done)
 _DW_SETS = max(2, int(os.environ.get("NAZ_TRAIN_DW_SETS", "2")))
 _SIDE: Dict[int, "torch.cuda.Stream"] = {}

@@ -122,6 +122,16 @@ def rowgemm_h3(value: Optional[bool] = None) -> bool:
     return bool(r)
 
 
+def rowgemm_bres(value: Optional[bool] = None) -> bool:
+    """The batch-row GEMM's B-resident f16x3 form (naz_tuning "rowgemm_bres": a persistent workgroup
+    keeps its column panel of B split into f16 pieces in LDS, A rows split at per-row power-of-two
+    scales; fp32-grade, other rounding).  ``value`` sets it; returns the setting before."""
+    r = int(lib().naz_tuning(b"rowgemm_bres", -1 if value is None else int(bool(value))))
+    if r < 0:
+        check(r, "rowgemm_bres")
+    return bool(r)
+
+
 def rowgemm_fill(value: Optional[int] = None) -> int:
     """The batch-row GEMM's small-batch grid fill (naz_tuning "rowgemm_fill": column panels narrowed
     until the grid holds ``value`` workgroups per CU, 0 = off; no result changes).  Returns the

@@ -169,7 +169,7 @@ def test_rowgemm_config3_shapes():
 
 @pytest.mark.parametrize("N", [168, 172, 300])
 @pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("arith", ["fp32", "x6", "h3"])
+@pytest.mark.parametrize("arith", ["fp32", "x6", "h3", "bres"])
 def test_rowgemm_panel_split(N, split, arith):
     """The batch-row kernel with the panel split on and off (naz_tuning "rowgemm_split"; default on):
     widths of 6 / 6 / 10 column blocks (an odd half-panel at 168 / 172 runs the paired epilogue's
@@ -181,6 +181,7 @@ def test_rowgemm_panel_split(N, split, arith):
     prev = ops.rowgemm_split(split)
     prev6 = ops.rowgemm_x6(arith == "x6")
     prevh = ops.rowgemm_h3(arith == "h3")
+    prevb = ops.rowgemm_bres(arith == "bres")  # (B-resident f16x3: the masked dX and chained act' here)
     prevf = ops.rowgemm_fill(0)  # the panels as the split sets them (4098 rows would be narrowed)
     try:
         g = torch.Generator().manual_seed(N + 11 * split)
@@ -218,6 +219,7 @@ def test_rowgemm_panel_split(N, split, arith):
         ops.rowgemm_split(prev)
         ops.rowgemm_x6(prev6)
         ops.rowgemm_h3(prevh)
+        ops.rowgemm_bres(prevb)
         ops.rowgemm_fill(prevf)
 
 

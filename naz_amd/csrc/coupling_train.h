@@ -235,6 +235,15 @@ constexpr bool kBwdPF = false;
 constexpr bool kBwdPF = true;
 #endif
 
+// NAZ_ABL_BWD_NOSTORE (timing ablation only, wrong gradients): the six dW operand stores skipped, so a
+// run measures what the operand writes (their bandwidth and the ring barriers' vmcnt(0) on their
+// acknowledgements) cost the kernel
+#ifdef NAZ_ABL_BWD_NOSTORE
+constexpr bool kBwdStore = false;
+#else
+constexpr bool kBwdStore = true;
+#endif
+
 template <class CF>
 struct BwdSlot {  // LDS ring slot: the largest forward or backward stage
   static constexpr int v = std::max({CF::A_SIZE, CF::B_SIZE, CF::C_SIZE, BwdR16<CF>::S3, BwdR16<CF>::S2,
@@ -400,7 +409,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
 #endif
             }
             in[8 * t + jj] = v;
-            if (valid && col >= 0) o.x0[row * (C + S) + col] = v;
+            if (kBwdStore && valid && col >= 0) o.x0[row * (C + S) + col] = v;
           }
         const float4* b4 = reinterpret_cast<const float4*>(cur + CF::A_BIAS);
 #pragma unroll
@@ -432,7 +441,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
           // weight-gradient operand stores go out at the HEAD of the stage after the one that
           // produced them: the next barrier's vmcnt(0) then waits on stores that drained under a
           // whole stage of compute, not on stores issued just before it
-          if (valid)
+          if (kBwdStore && valid)
 #pragma unroll
             for (int b = 0; b < CF::HB; ++b)
               *reinterpret_cast<float4*>(o.h1 + row * H + 16 * b + 4 * q) =
@@ -455,7 +464,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
       } else if constexpr (j < NSTG_F) {
         constexpr int s = j - 1 - CF::NB2;
         if constexpr (s == 0) {
-          if (valid)
+          if (kBwdStore && valid)
 #pragma unroll
             for (int b = 0; b < CF::HB; ++b)
               *reinterpret_cast<float4*>(o.h2 + row * H + 16 * b + 4 * q) =
@@ -499,7 +508,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         // ---- dH2 = dPre3 · W2, k-steps of stage sb
         constexpr int sb = j - NSTG_F;
         if constexpr (sb == 0) {
-          if (valid) {
+          if (kBwdStore && valid) {
             float* dst = o.dp3 + row * (4 * BW::NS3) + q * BW::NS3;
 #pragma unroll
             for (int b = 0; b < CF::NO; ++b)
@@ -517,7 +526,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         // ---- dH1 = dPre2 · W1
         constexpr int sb = j - NSTG_F - BW::NB3;
         if constexpr (sb == 0) {
-          if (valid)
+          if (kBwdStore && valid)
 #pragma unroll
             for (int b = 0; b < CF::HB; ++b)
               *reinterpret_cast<float4*>(o.dp2 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
@@ -528,7 +537,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         if constexpr (!kEpiEarly && sb == BW::NB2 - 1) epi_dh1();
       } else {
         // ---- dx1 = dPre1 · W0[:, C:], lower spline VJP, g(P[l + 1])
-        if (valid)
+        if (kBwdStore && valid)
 #pragma unroll
           for (int b = 0; b < CF::HB; ++b)
             *reinterpret_cast<float4*>(o.dp1 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};

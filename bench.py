@@ -1158,10 +1158,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # NAZ_BENCH_BACKEND=gloo: a REHEARSAL of the N-rank path on a box with fewer GPUs (ranks share
+    # devices round-robin, gradients / timings all-reduced over gloo); the driver's runs use RCCL
+    rehearsal = os.environ.get("NAZ_BENCH_BACKEND", "nccl") == "gloo"
+    if rehearsal and world > 1:
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         world = dist.get_world_size()  # n_gpus = the ranks RCCL actually formed
         rank = dist.get_rank()
     if world != args.gpus and rank == 0:

@@ -303,7 +303,11 @@ template <int NFLOATS, int NW>
 NAZ_DEV void stage_issue_lim(float* lds, const float* __restrict__ src, int nch) {
   static_assert(NFLOATS % 256 == 0, "stage must be whole 1 KB chunks");
   constexpr int CHUNKS = NFLOATS / 256;
-  const int lane = threadIdx.x & 63;
+  // (the lane offset is formed here, per issue: hoisted out of the layer loop as a 64-bit per-lane
+  // source base it was one of the three pointers the nsa16 inverse spilled, and its scratch reload
+  // sat right before a stage's DMA issue)
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   nch = nch < CHUNKS ? nch : CHUNKS;
 #pragma unroll
@@ -1439,7 +1443,10 @@ struct CouplingOps {
       if (B == 0) return 0;
       const int64_t ntiles = (B + 16 * kBwdWaves - 1) / (16 * kBwdWaves);
       const int64_t grid = std::min<int64_t>(ntiles, 2048);
-      const size_t lds = (size_t)(2 * BwdSlot<CR>::v + 2 * CR::S * (3 * CR::K - 1)) * 4;  // ring, glow, lowp
+      size_t lds = (size_t)(2 * BwdSlot<CR>::v + 2 * CR::S * (3 * CR::K - 1)) * 4;  // ring, glow, lowp
+#ifdef NAZ_ABL_BWD_ONEWG  // timing ablation: 64 KB of unused LDS, so one workgroup (one wave per SIMD) per CU
+      lds += 64 * 1024;
+#endif
       hipLaunchKernelGGL((coupling_bwd_r16_kernel<CR>), dim3((unsigned)grid), dim3(kBwdWaves * 64), lds, s,
                          reinterpret_cast<const float*>(packed), reinterpret_cast<const float*>(bwd), flat, l, state,
                          ctx, ldc, g_in, g_lp, o, B, bound);

@@ -627,15 +627,25 @@ __global__ void __launch_bounds__(64 * CF::NW, CF::WPE_INV) made_ar_r16_kernel(
     // the training forward (naz_ar_flow_log_prob_train, one draw): layer l's output s_l for the
     // backward (made_ar_bwd.h)
     if (states != nullptr && q == 0 && valid) {
+      // (row re-formed at the store from an opaque thread index: a 64-bit per-lane address held across
+      // the layer loop is what the nsa16 instance spilled)
+      unsigned tid = threadIdx.x;
+      asm volatile("" : "+v"(tid));
+      const int64_t r2 = (int64_t)blockIdx.x * (16 * NW) + (tid >> 6) * 16 + (tid & 15);
+      float* const sp = states + ((int64_t)l * B + r2) * D;
 #pragma unroll
-      for (int d = 0; d < D; ++d) states[((int64_t)l * B + row) * D + d] = v[d];
+      for (int d = 0; d < D; ++d) sp[d] = v[d];
     }
   }
   constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
   float base = 0.f;
 #pragma unroll
   for (int d = 0; d < D; ++d) base += -(v[d] * v[d]) / 2.f - kLogSqrt2Pi;
-  if (q == 0 && valid) out_lp[row] = base - ldsum + logjac;
+  if (q == 0 && valid) {
+    unsigned tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    out_lp[(int64_t)blockIdx.x * (16 * NW) + (tid >> 6) * 16 + (tid & 15)] = base - ldsum + logjac;
+  }
 }
 
 // ================================================================ forward (sample) direction

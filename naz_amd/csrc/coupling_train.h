@@ -244,6 +244,18 @@ constexpr bool kBwdStore = false;
 constexpr bool kBwdStore = true;
 #endif
 
+// NAZ_BWD_NT_STORES (A/B): the operands nothing in this kernel re-reads (dPre3, dPre2, dPre1, X0) stored
+// non-temporally, so 9 GB of them per 2^22 rows and layer do not push the weight images and the H1 / H2
+// rows this kernel re-reads out of L2
+template <class T>
+NAZ_DEV void bwd_store_stream(T* p, T v) {
+#ifdef NAZ_BWD_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 template <class CF>
 struct BwdSlot {  // LDS ring slot: the largest forward or backward stage
   static constexpr int v = std::max({CF::A_SIZE, CF::B_SIZE, CF::C_SIZE, BwdR16<CF>::S3, BwdR16<CF>::S2,
@@ -409,7 +421,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
 #endif
             }
             in[8 * t + jj] = v;
-            if (kBwdStore && valid && col >= 0) o.x0[row * (C + S) + col] = v;
+            if (kBwdStore && valid && col >= 0) bwd_store_stream(o.x0 + row * (C + S) + col, v);
           }
         const float4* b4 = reinterpret_cast<const float4*>(cur + CF::A_BIAS);
 #pragma unroll
@@ -512,7 +524,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
             float* dst = o.dp3 + row * (4 * BW::NS3) + q * BW::NS3;
 #pragma unroll
             for (int b = 0; b < CF::NO; ++b)
-              *reinterpret_cast<float4*>(dst + 4 * b) = float4{a3[b][0], a3[b][1], a3[b][2], a3[b][3]};
+              bwd_store_stream(reinterpret_cast<floatx4*>(dst + 4 * b), floatx4{a3[b][0], a3[b][1], a3[b][2], a3[b][3]});
           }
         }
         if constexpr (kBwdF16) {
@@ -529,7 +541,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
           if (kBwdStore && valid)
 #pragma unroll
             for (int b = 0; b < CF::HB; ++b)
-              *reinterpret_cast<float4*>(o.dp2 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
+              bwd_store_stream(reinterpret_cast<floatx4*>(o.dp2 + row * H + 16 * b + 4 * q), dp2[b]);
           if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         }
         if constexpr (kBwdF16) gemm_r16_lazy<CF::HB, BW::KB2, sb * BW::KB2, false, CF::HB, kBwdPF>(dacc, cur, lane, dp2);
@@ -540,7 +552,7 @@ __global__ void __launch_bounds__(kBwdWaves * 64, 2) coupling_bwd_r16_kernel(
         if (kBwdStore && valid)
 #pragma unroll
           for (int b = 0; b < CF::HB; ++b)
-            *reinterpret_cast<float4*>(o.dp1 + row * H + 16 * b + 4 * q) = float4{dp2[b][0], dp2[b][1], dp2[b][2], dp2[b][3]};
+            bwd_store_stream(reinterpret_cast<floatx4*>(o.dp1 + row * H + 16 * b + 4 * q), dp2[b]);
         if constexpr (kBwdF16) gscale = bwd_row_scale(dp2);
         floatx4 a1[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
         if constexpr (kBwdF16) {

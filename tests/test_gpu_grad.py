@@ -346,6 +346,26 @@ def test_wgrad_t16_shapes(N1, N2, M):
     _check(rs, a.double().sum(0), a.sum(0), f"wgrad {N1}x{N2} M={M} row sums")
 
 
+@pytest.mark.parametrize("N1,N2", [(128, 40), (128, 128), (192, 128)])
+@pytest.mark.parametrize("M", [1, 31, 32, 33, 257 * 32 + 5, (1 << 19) + 3])
+def test_wgrad_nsc_shapes_masked_accumulate(N1, N2, M):
+    """The nsc backward's three per-layer reductions (dPre1 x [ctx | x1], dPre2 x H1, dPre3 x H2 at
+    config 3) on wgrad_x6: fewer chunks than workgroups, one partial chunk, a ragged tail, half a
+    million rows; an output mask and accumulation into existing dW / db, vs fp64 (and the fp32
+    reference's own error, tests/parity.py's criterion)."""
+    from naz_amd import ops
+    g = torch.Generator().manual_seed(N1 + 7 * N2 + M)
+    a = torch.randn(M, N1, generator=g) * 1e-3  # dPre-like magnitudes
+    b = torch.tanh(torch.randn(M, N2, generator=g))
+    mask = (torch.rand(N1, N2, generator=g) > 0.25).float()
+    c0, r0 = torch.randn(N1, N2, generator=g), torch.randn(N1, generator=g)
+    out, rs = _cuda(c0).clone(), _cuda(r0).clone()
+    ops.gemm(_cuda(a).t(), _cuda(b), out=out, mask=_cuda(mask), accumulate=True, rowsum=rs)
+    _check(out, (a.double().t() @ b.double()) * mask.double() + c0.double(), (a.t() @ b) * mask + c0,
+           f"wgrad nsc {N1}x{N2} M={M}")
+    _check(rs, a.double().sum(0) + r0.double(), a.sum(0) + r0, f"wgrad nsc {N1}x{N2} M={M} row sums")
+
+
 # ------------------------------------------------------------------ a5 affine step VJP
 @pytest.mark.parametrize("N1,N2,M,nb", [(160, 160, 65536, 3), (160, 8, 3000, 3), (8, 160, 4097, 5), (160, 144, 517, 2),
                                         (128, 128, 70001, 1)])

@@ -1116,7 +1116,7 @@ def main():
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="strong (default, north_star's '>=6x strong scaling at 8 GPUs'): one global batch split "
                          "over the ranks; weak: --batch rows on every rank")
-    ap.add_argument("--micro-batch", type=int, default=1 << 22,  # (2^20: 166-171 ms per step, 2^22: 140-156, r05_g26/27)
+    ap.add_argument("--micro-batch", type=int, default=1 << 22,  # (2^20: 170-174 ms per step, 2^22: 157-164, r06_g3/g7)
                     help="--train: rows per forward+backward chunk (gradients accumulate before the all-reduce)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true",

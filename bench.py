@@ -243,6 +243,28 @@ def check_step_losses(losses, args, rank: int, what: str) -> None:
         sys.exit(3)
 
 
+WARM_MIN_S = 0.05  # an inference line's untimed warm-up: at least --warmup steps and at least 50 ms
+
+
+def warm_up(step, args, dev):
+    """--warmup untimed steps, repeated in rounds of --warmup until WARM_MIN_S of wall time has
+    passed.  A step of a few hundred microseconds (a rank's 2^17-row slice of the headline batch
+    at N = 8) otherwise enters the timed region before the GPU's clocks have left the idle state:
+    r06_g16 measured 0.340 ms per launch over 20 steps after 10 warm-up steps (3 ms of work) and
+    0.301 ms over 100 steps.  Returns the number of warm-up steps run (reported in the JSON line)."""
+    if args.warmup <= 0:
+        return 0
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        for _ in range(args.warmup):
+            step()
+        n += args.warmup
+        torch.cuda.synchronize(dev)
+        if time.perf_counter() - t0 >= WARM_MIN_S:
+            return n
+
+
 def run_train(args, dev, rank, world, dist):
     """configs[3]: the NLL step of naz's train (train_flows.py:194-213) on one global batch of
     2^23 rows (strong scaling, the default: split over the ranks) or --batch rows per rank
@@ -800,8 +822,7 @@ def run_flow_case(args, dev, rank, world, dist):
         def run():
             return f.log_prob(x, condition=c)
     with torch.no_grad():
-        for _ in range(args.warmup):
-            run()
+        warm_steps = warm_up(run, args, dev)
         torch.cuda.synchronize(dev)
         if dist is not None:
             dist.barrier()
@@ -831,7 +852,8 @@ def run_flow_case(args, dev, rank, world, dist):
                        "API)" if args.sample else
                        f"samples/sec through log_prob+log|detJ|, naz {ftype} flow (NormalizingFlow API)"),
             "value": G / step_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": args.scaling,
+            "warmup": args.warmup, "warmup_steps_run": warm_steps, "ms_per_step": step_s * 1e3,
+            "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I); random-init weights",
             "config": {"workload": desc, "batch_per_gpu": B, "global_batch": G,
@@ -1214,8 +1236,7 @@ def run_log_prob(args, dev, rank, world, dist):
     def step():
         ops.coupling_log_prob(plan.desc, packed, x, c, out=out)
 
-    for _ in range(args.warmup):
-        step()
+    warm_steps = warm_up(step, args, dev)
     # per-launch kernel time with HIP events on the launch stream (the current stream)
     stream = torch.cuda.current_stream(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -1284,7 +1305,8 @@ def run_log_prob(args, dev, rank, world, dist):
         traffic, traffic_src = load_traffic(mode)
         rec = {
             "metric": METRIC, "value": total_rows / elapsed, "unit": "samples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "steps": args.steps, "warmup": args.warmup, "warmup_steps_run": warm_steps,
+            "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: x ~ 8-component Gaussian mixture, context ~ N(0, I) (one global batch, 2^16-row "
                     "seeded chunks); "

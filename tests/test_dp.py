@@ -72,11 +72,11 @@ def _worker(rank, world, port, q, mode):
     try:
         torch.manual_seed(100 + rank)  # replicas start different: train() must broadcast rank 0
         x, y = _data()
-        if mode.startswith("steps"):
+        if mode.startswith("steps") or mode == "tiny":
             flow = _TinyFlow(seed=0)
             dp = T.DataParallel()
-            mb = None if mode == "steps" else int(mode.split(":")[1])
-            losses, params = _steps(flow, x, y, dp, micro_batch=mb)
+            mb = None if mode in ("steps", "tiny") else int(mode.split(":")[1])
+            losses, params = _steps(flow, x, y, dp, micro_batch=mb, batch=2 if mode == "tiny" else 37)
             q.put((rank, losses, [p.numpy() for p in params]))
         else:
             flow = _TinyFlow(seed=rank)
@@ -116,6 +116,22 @@ def test_dp_step_matches_single_process(micro_batch):
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
     for a, b in zip(res[0][2], res[1][2]):
         assert torch.equal(a, b), "replicas diverged"
+
+
+def test_dp_step_with_an_empty_rank_matches_single_process():
+    """3 ranks over 2-row global minibatches: one rank's slice is empty every step (what 8 ranks
+    see on a minibatch smaller than 8 rows).  It adds zero gradients to the flat all-reduce (its
+    .grad is materialised as zeros, so every rank posts the same bucket) and steps identically."""
+    x, y = _data()
+    ref_losses, ref_params = _steps(_TinyFlow(seed=0), x, y, T.DataParallel(), batch=2)
+    res = _run(3, "tiny")
+    for _, losses, params in res:
+        assert losses == pytest.approx(ref_losses, rel=1e-5, abs=1e-6)
+        for a, b in zip(params, ref_params):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    for r in res[1:]:
+        for a, b in zip(res[0][2], r[2]):
+            assert torch.equal(a, b), "replicas diverged"
 
 
 def test_dp_train_replicas_agree():

@@ -174,6 +174,28 @@ def test_dp_two_ranks_on_one_gpu_match_single_process(micro_batch, side):
         assert np.array_equal(a, b), "replicas diverged"
 
 
+@pytest.mark.parametrize("micro_batch", [None, 4096])
+def test_nll_step_empty_rank_slice(micro_batch):
+    """A rank whose slice of the global batch is empty (8 ranks over a batch smaller than 8 rows, or
+    the ragged tail of DataParallel.shard): the fused nsc step contributes a zero loss and zero
+    gradients to the all-reduce, takes no NaN from 0 / 0, and leaves the weights as SGD on a zero
+    gradient does."""
+    from naz_amd.trainers import DataParallel, nll_step
+    from naz_amd.trainers.train_flows import _flow_parameters
+    state = {k: v.numpy() for k, v in O.random_state(CFG3, seed=99).items()}
+    f = _cfg3_flow(state)
+    ps = _flow_parameters(f)
+    before = [p.detach().clone() for p in ps]
+    opt = torch.optim.SGD(ps, lr=1e-2)
+    x = torch.as_tensor(O.gaussian_mixture(4, 16, seed=5), device=DEV)[:0]
+    c = torch.as_tensor(O.context_normal(4, 32, seed=6), device=DEV)[:0]
+    loss = nll_step(f, x, c, opt, ps, DataParallel(), 4, clip_val=1.0, micro_batch=micro_batch)
+    assert float(loss) == 0.0
+    for p, b in zip(ps, before):
+        assert p.grad is None or (torch.isfinite(p.grad).all() and float(p.grad.abs().max()) == 0.0)
+        assert torch.equal(p.detach(), b)
+
+
 def test_naz_compat_front_end_runs_unchanged():
     """The import paths and calls of examples/papers/2506.05657/train_mle_all_data.py:1-20,
     62-89 (at a toy size): construction, train(), sample(), log_prob; train_lightning too."""

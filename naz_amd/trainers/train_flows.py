@@ -219,8 +219,16 @@ class GraphedNllStep:
                         micro_batch=self.micro_batch)
 
     def _in_range(self, x_b, y_b) -> bool:
+        """The rows and the context the fused kernels will see: with an embedding net that is the
+        net's output (flow.py NormalizingFlow._pdf conditions on embedding_net(condition)), formed
+        here once more, eagerly (a dropout embedding net's draw differs from the graph's)."""
         from .. import ops
-        return ops.absmax(x_b, y_b) < 32768.0
+        emb = getattr(self.flow, "embedding_net", None)
+        ctx = None
+        if y_b is not None and emb is not None and not isinstance(emb, nn.Identity):
+            with torch.no_grad():
+                ctx = emb(y_b)
+        return ops.absmax(x_b, y_b, ctx) < 32768.0
 
     def __call__(self, x_b: torch.Tensor, y_b: Optional[torch.Tensor]) -> torch.Tensor:
         from ..flows import flow as flow_mod

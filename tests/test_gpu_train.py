@@ -696,6 +696,40 @@ def test_graphed_nll_step_nsc_matches_eager_steps():
         assert rel < 1e-4, rel
 
 
+@pytest.mark.parametrize("scale", [1.0, 1e5])
+def test_graphed_nll_step_range_checks_the_embedded_context(scale):
+    """with an embedding net the fused step's f16 range applies to the net's output,
+    not to the raw condition.  A net that maps in-range conditions past 2^15 must send every call to
+    the eager step (no replay of a graph captured without the check); an in-range net captures."""
+    from torch import nn
+    from naz_amd.flows import NormalizingFlow
+    from naz_amd.flows import io as fio
+    from naz_amd.trainers import DataParallel, GraphedNllStep
+    from naz_amd.trainers.train_flows import _flow_parameters
+    spec = dict(CFG3, L=2)
+    state = {k: v.numpy() for k, v in O.random_state(spec, seed=33).items()}
+    B = 1024
+    emb = nn.Linear(32, 32)
+    with torch.no_grad():
+        emb.weight.copy_(torch.eye(32) * scale)
+        emb.bias.zero_()
+    f = NormalizingFlow("nsc", None, 16, 32, [128, 128], 2, 8, 8, embedding_net=emb)
+    fio.load_state(f, state)
+    f.to(DEV)
+    params = _flow_parameters(f)
+    opt = torch.optim.Adam(params, lr=1e-4, capturable=True)
+    g = GraphedNllStep(f, opt, params, DataParallel(), B)
+    xs = [torch.as_tensor(O.gaussian_mixture(B, 16, seed=80 + i), device=DEV) for i in range(3)]
+    cs = [torch.as_tensor(O.context_normal(B, 32, seed=90 + i), device=DEV) for i in range(3)]
+    losses = [float(g(x, c)) for x, c in zip(xs, cs)]
+    assert all(np.isfinite(losses)), losses
+    if scale > 1.0:
+        assert g.replays == 0 and g.eager_steps == 3
+    else:
+        assert not g.eager_only, g.capture_error
+        assert g.eager_steps == 1 and g.replays == 2
+
+
 @pytest.mark.parametrize("solver", ["rk4", "dopri5"])
 def test_graphed_nll_step_cnf_captures_or_runs_eagerly(solver):
     """GraphedNllStep on a CNF.  The RK4 step (fused solve, discrete adjoint) captures
